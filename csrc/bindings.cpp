@@ -1,0 +1,180 @@
+// Python bindings for the gfx950 kernels (operator_amd._C).
+//
+// Every binding validates dtype / device / contiguity / shape on the host
+// BEFORE launching, so a hand-written kernel never runs with operands whose
+// shapes differ from what its grid assumes. Kernels are launched on PyTorch's
+// current HIP stream, so they are captured by torch.cuda.CUDAGraph (hipGraph).
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+
+#include "kernels/kernels.h"
+#include "kernels/scan.h"
+
+namespace {
+
+using oamd::bf16_t;
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+
+#define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
+#define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
+#define CHECK_DT(t, dt) TORCH_CHECK((t).scalar_type() == (dt), #t " has wrong dtype ", (t).scalar_type())
+#define CHECK_BF16(t) CHECK_DT(t, at::kBFloat16)
+#define ROWMAJOR_VEC(t) \
+  TORCH_CHECK((t).dim() == 2 && (t).stride(1) == 1 && (t).stride(0) % 8 == 0, #t " must be [rows, cols] row-major with 16-B aligned rows")
+#define RC(call)                                                           \
+  do {                                                                     \
+    int rc__ = (call);                                                     \
+    TORCH_CHECK(rc__ == 0, "kernel launch failed: " #call " rc=", rc__);   \
+  } while (0)
+
+template <typename T>
+T* ptr(const at::Tensor& t) { return reinterpret_cast<T*>(t.data_ptr()); }
+template <typename T>
+T* optr(const c10::optional<at::Tensor>& t) { return t.has_value() ? reinterpret_cast<T*>(t->data_ptr()) : nullptr; }
+
+void rmsnorm(const at::Tensor& x, const c10::optional<at::Tensor>& residual, const at::Tensor& w,
+             at::Tensor& y, double eps) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(y); ROWMAJOR_VEC(x); ROWMAJOR_VEC(y);
+  CHECK_CONTIG(w);
+  const int64_t rows = x.size(0), hidden = x.size(1);
+  TORCH_CHECK(hidden % 8 == 0 && hidden <= 256 * 8 * 8, "hidden must be a multiple of 8 and <= 16384");
+  TORCH_CHECK(w.numel() == hidden && y.size(0) == rows && y.size(1) == hidden, "rmsnorm shape mismatch");
+  int64_t rstride = 0;
+  if (residual.has_value()) {
+    CHECK_BF16(*residual); ROWMAJOR_VEC(*residual);
+    TORCH_CHECK(residual->size(0) == rows && residual->size(1) == hidden, "residual shape mismatch");
+    rstride = residual->stride(0);
+  }
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  RC(oamd::rmsnorm(ptr<bf16_t>(x), optr<bf16_t>(residual), ptr<bf16_t>(w), ptr<bf16_t>(y), (int)rows,
+                   (int)hidden, x.stride(0), rstride, y.stride(0), (float)eps, cur_stream()));
+}
+
+void silu_mul(const at::Tensor& gu, at::Tensor& out) {
+  CHECK_DEV(gu); CHECK_BF16(gu); CHECK_BF16(out); ROWMAJOR_VEC(gu); ROWMAJOR_VEC(out);
+  const int64_t rows = gu.size(0), inter = out.size(1);
+  TORCH_CHECK(gu.size(1) == 2 * inter && out.size(0) == rows && inter % 8 == 0, "silu_mul shape mismatch");
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(gu.device());
+  RC(oamd::silu_mul(ptr<bf16_t>(gu), ptr<bf16_t>(out), rows, (int)inter, gu.stride(0), out.stride(0),
+                    cur_stream()));
+}
+
+void embedding(const at::Tensor& ids, const at::Tensor& table, at::Tensor& out) {
+  CHECK_DEV(ids); CHECK_DT(ids, at::kLong); CHECK_BF16(table); CHECK_BF16(out);
+  CHECK_CONTIG(ids); CHECK_CONTIG(table); CHECK_CONTIG(out);
+  TORCH_CHECK(table.dim() == 2 && table.size(1) % 8 == 0, "table must be [vocab, hidden%8==0]");
+  TORCH_CHECK(out.dim() == 2 && out.size(0) == ids.numel() && out.size(1) == table.size(1), "embedding out shape");
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(ids.device());
+  RC(oamd::embedding(ptr<int64_t>(ids), ptr<bf16_t>(table), ptr<bf16_t>(out), (int)ids.numel(),
+                     (int)table.size(1), table.size(0), cur_stream()));
+}
+
+void rope_kv(const at::Tensor& qkv, const at::Tensor& pos, const at::Tensor& cos_t, const at::Tensor& sin_t,
+             int64_t Hq, int64_t Hkv, at::Tensor& q_out, const c10::optional<at::Tensor>& k_out,
+             const c10::optional<at::Tensor>& v_out, const c10::optional<at::Tensor>& k_cache,
+             const c10::optional<at::Tensor>& v_cache, const c10::optional<at::Tensor>& slots) {
+  CHECK_DEV(qkv); CHECK_BF16(qkv); ROWMAJOR_VEC(qkv);
+  CHECK_DT(pos, at::kLong); CHECK_CONTIG(pos);
+  CHECK_DT(cos_t, at::kFloat); CHECK_DT(sin_t, at::kFloat); CHECK_CONTIG(cos_t); CHECK_CONTIG(sin_t);
+  const int64_t T = qkv.size(0);
+  const int64_t D = cos_t.size(1) * 2;
+  TORCH_CHECK(D == 128, "only head_dim 128 is supported");
+  TORCH_CHECK(qkv.size(1) == (Hq + 2 * Hkv) * D, "qkv width != (Hq+2Hkv)*D");
+  TORCH_CHECK(pos.numel() == T && sin_t.sizes() == cos_t.sizes(), "pos/cos/sin shape");
+  CHECK_BF16(q_out); CHECK_CONTIG(q_out);
+  TORCH_CHECK(q_out.numel() == T * Hq * D, "q_out shape");
+  if (k_out.has_value()) { CHECK_BF16(*k_out); CHECK_CONTIG(*k_out); TORCH_CHECK(k_out->numel() == T * Hkv * D, "k_out shape"); }
+  if (v_out.has_value()) { CHECK_BF16(*v_out); CHECK_CONTIG(*v_out); TORCH_CHECK(v_out->numel() == T * Hkv * D, "v_out shape"); }
+  int page = 1;
+  if (k_cache.has_value()) {
+    TORCH_CHECK(v_cache.has_value() && slots.has_value(), "k_cache needs v_cache and slots");
+    CHECK_BF16(*k_cache); CHECK_BF16(*v_cache); CHECK_CONTIG(*k_cache); CHECK_CONTIG(*v_cache);
+    CHECK_DT(*slots, at::kLong); CHECK_CONTIG(*slots);
+    TORCH_CHECK(k_cache->dim() == 4 && k_cache->size(1) == Hkv && k_cache->size(3) == D &&
+                    k_cache->sizes() == v_cache->sizes(), "cache must be [pages, Hkv, page, D]");
+    TORCH_CHECK(slots->numel() == T, "slots shape");
+    page = (int)k_cache->size(2);
+  }
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(qkv.device());
+  RC(oamd::rope_kv(ptr<bf16_t>(qkv), qkv.stride(0), ptr<int64_t>(pos), ptr<float>(cos_t), ptr<float>(sin_t),
+                   (int)T, (int)Hq, (int)Hkv, (int)D, ptr<bf16_t>(q_out), optr<bf16_t>(k_out), optr<bf16_t>(v_out),
+                   optr<bf16_t>(k_cache), optr<bf16_t>(v_cache), optr<int64_t>(slots), page, cos_t.size(0),
+                   cur_stream()));
+}
+
+void attn_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
+                 const at::Tensor& block_tables, const at::Tensor& seq_lens, at::Tensor& out,
+                 at::Tensor& o_part, at::Tensor& ml_part, int64_t num_splits, double scale) {
+  CHECK_DEV(q); CHECK_BF16(q); CHECK_CONTIG(q); CHECK_BF16(out); CHECK_CONTIG(out);
+  CHECK_BF16(k_cache); CHECK_BF16(v_cache); CHECK_CONTIG(k_cache); CHECK_CONTIG(v_cache);
+  CHECK_DT(block_tables, at::kInt); CHECK_CONTIG(block_tables); CHECK_DT(seq_lens, at::kInt); CHECK_CONTIG(seq_lens);
+  CHECK_DT(o_part, at::kFloat); CHECK_DT(ml_part, at::kFloat); CHECK_CONTIG(o_part); CHECK_CONTIG(ml_part);
+  TORCH_CHECK(q.dim() == 3, "q must be [B, Hq, D]");
+  const int64_t B = q.size(0), Hq = q.size(1), D = q.size(2);
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.sizes() == v_cache.sizes() && k_cache.size(3) == D, "cache shape");
+  const int64_t Hkv = k_cache.size(1), page = k_cache.size(2);
+  TORCH_CHECK(D == 128 && Hq % Hkv == 0, "head_dim must be 128 and Hq % Hkv == 0");
+  TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) == B && seq_lens.numel() == B, "tables shape");
+  TORCH_CHECK(out.numel() == B * Hq * D, "out shape");
+  TORCH_CHECK(num_splits >= 1, "num_splits >= 1");
+  if (num_splits > 1) {
+    TORCH_CHECK(o_part.numel() >= B * Hq * num_splits * D && ml_part.numel() >= B * Hq * num_splits * 2,
+                "partial buffers too small");
+  }
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
+  RC(oamd::attn_decode(ptr<bf16_t>(q), ptr<bf16_t>(k_cache), ptr<bf16_t>(v_cache), ptr<int>(block_tables),
+                       ptr<int>(seq_lens), ptr<bf16_t>(out), ptr<float>(o_part), ptr<float>(ml_part), (int)B,
+                       (int)Hq, (int)Hkv, (int)D, (int)page, (int)block_tables.size(1), (int)num_splits,
+                       (float)scale, cur_stream()));
+}
+
+void attn_prefill(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor& o,
+                  const at::Tensor& cu_seqlens, const at::Tensor& work_seq, const at::Tensor& work_q0,
+                  double scale) {
+  CHECK_DEV(q); for (auto* t : {&q, &k, &v}) { CHECK_BF16(*t); CHECK_CONTIG(*t); }
+  CHECK_BF16(o); CHECK_CONTIG(o);
+  for (auto* t : {&cu_seqlens, &work_seq, &work_q0}) { CHECK_DT(*t, at::kInt); CHECK_CONTIG(*t); }
+  TORCH_CHECK(q.dim() == 3 && k.dim() == 3 && v.sizes() == k.sizes() && o.sizes() == q.sizes(), "qkvo shapes");
+  TORCH_CHECK(q.size(0) == k.size(0) && q.size(2) == 128 && k.size(2) == 128, "T / head_dim mismatch");
+  TORCH_CHECK(q.size(1) % k.size(1) == 0, "Hq % Hkv");
+  TORCH_CHECK(work_seq.numel() == work_q0.numel(), "work list shape");
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
+  RC(oamd::attn_prefill(ptr<bf16_t>(q), ptr<bf16_t>(k), ptr<bf16_t>(v), ptr<bf16_t>(o), ptr<int>(cu_seqlens),
+                        ptr<int>(work_seq), ptr<int>(work_q0), (int)work_seq.numel(), (int)q.size(1),
+                        (int)k.size(1), 128, (float)scale, cur_stream()));
+}
+
+void sample(const at::Tensor& logits, const at::Tensor& temperature, const at::Tensor& seeds,
+            const at::Tensor& positions, at::Tensor& out) {
+  CHECK_DEV(logits);
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits must be [rows, vocab] row-major");
+  TORCH_CHECK(logits.scalar_type() == at::kFloat || logits.scalar_type() == at::kBFloat16, "logits dtype");
+  const int64_t rows = logits.size(0);
+  CHECK_DT(temperature, at::kFloat); CHECK_DT(seeds, at::kLong); CHECK_DT(positions, at::kLong); CHECK_DT(out, at::kLong);
+  TORCH_CHECK(temperature.numel() == rows && seeds.numel() == rows && positions.numel() == rows && out.numel() == rows,
+              "sampler per-row tensor shape");
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
+  RC(oamd::sample_tokens(logits.data_ptr(), logits.scalar_type() == at::kBFloat16, logits.stride(0), (int)rows,
+                         (int)logits.size(1), ptr<float>(temperature), ptr<int64_t>(seeds), ptr<int64_t>(positions),
+                         ptr<int64_t>(out), cur_stream()));
+}
+
+}  // namespace
+
+void register_scan_bindings(pybind11::module_& m);
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "operator_amd gfx950 kernels";
+  m.def("rmsnorm", &rmsnorm, "RMSNorm with optional fused residual add");
+  m.def("silu_mul", &silu_mul);
+  m.def("embedding", &embedding);
+  m.def("rope_kv", &rope_kv);
+  m.def("attn_decode", &attn_decode);
+  m.def("attn_prefill", &attn_prefill);
+  m.def("sample", &sample);
+  register_scan_bindings(m);
+  m.attr("ARCH") = "gfx950";
+}

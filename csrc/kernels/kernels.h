@@ -1,0 +1,34 @@
+// Host-side launcher declarations for every HIP kernel in csrc/kernels.
+// Launchers return 0 on success, a hipError_t (>0) on a launch failure, or a
+// negative code for an unsupported shape. They never allocate or synchronise,
+// so callers may capture them into a hipGraph.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace oamd {
+typedef uint16_t bf16_t;
+
+// ---- explanation-model ops ----
+int rmsnorm(const bf16_t* x, bf16_t* residual, const bf16_t* w, bf16_t* y, int rows, int hidden,
+            int64_t x_stride, int64_t r_stride, int64_t y_stride, float eps, hipStream_t stream);
+int silu_mul(const bf16_t* gu, bf16_t* out, int64_t rows, int inter, int64_t in_stride,
+             int64_t out_stride, hipStream_t stream);
+int embedding(const int64_t* ids, const bf16_t* table, bf16_t* out, int tokens, int hidden,
+              int64_t vocab, hipStream_t stream);
+int rope_kv(const bf16_t* qkv, int64_t qkv_stride, const int64_t* pos, const float* cos_t,
+            const float* sin_t, int tokens, int Hq, int Hkv, int head_dim, bf16_t* q_out,
+            bf16_t* k_out, bf16_t* v_out, bf16_t* k_cache, bf16_t* v_cache, const int64_t* slots,
+            int page_size, int64_t max_pos, hipStream_t stream);
+int attn_decode(const bf16_t* q, const bf16_t* k_cache, const bf16_t* v_cache, const int* block_tables,
+                const int* seq_lens, bf16_t* out, float* o_part, float* ml_part, int B, int Hq, int Hkv,
+                int head_dim, int page_size, int max_pages, int num_splits, float scale,
+                hipStream_t stream);
+int attn_prefill(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, const int* cu_seqlens,
+                 const int* work_seq, const int* work_q0, int num_work, int Hq, int Hkv, int head_dim,
+                 float scale, hipStream_t stream);
+int sample_tokens(const void* logits, bool logits_bf16, int64_t stride, int rows, int vocab,
+                  const float* temperature, const int64_t* seeds, const int64_t* positions,
+                  int64_t* out_tokens, hipStream_t stream);
+
+}  // namespace oamd

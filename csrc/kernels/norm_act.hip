@@ -1,0 +1,139 @@
+// RMSNorm (+ fused residual add), SiLU-and-mul, embedding gather.
+//
+// These are the memory-bound elementwise/normalisation ops of the explanation
+// model. All bf16 traffic is 16 B per lane.
+#include "common.h"
+#include "kernels.h"
+
+namespace oamd {
+
+// One 256-thread block per row. Each thread owns up to MAXV vectors of 8 bf16
+// kept in registers between the reduction and the scaling pass, so the row is
+// read from HBM exactly once (x, and residual when fused).
+template <int NT, int MAXV>
+__global__ void __launch_bounds__(NT) rmsnorm_kernel(
+    const bf16_t* __restrict__ x, bf16_t* __restrict__ residual,
+    const bf16_t* __restrict__ w, bf16_t* __restrict__ y, int hidden,
+    int64_t x_stride, int64_t r_stride, int64_t y_stride, float eps) {
+  __shared__ float scratch[NT / 64];
+  const int row = blockIdx.x;
+  const int nvec = hidden >> 3;
+  const u16x8* xr = reinterpret_cast<const u16x8*>(x + row * x_stride);
+  u16x8* rr = residual ? reinterpret_cast<u16x8*>(residual + row * r_stride) : nullptr;
+  float v[MAXV][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int vi = threadIdx.x + i * NT;
+    if (vi < nvec) {
+      u16x8 a = xr[vi];
+      if (rr) {
+        u16x8 b = rr[vi];
+        u16x8 s;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          // residual stream is bf16: round the sum before normalising it
+          s[j] = f2bf(bf2f(a[j]) + bf2f(b[j]));
+        }
+        rr[vi] = s;
+        a = s;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        v[i][j] = bf2f(a[j]);
+        ss += v[i][j] * v[i][j];
+      }
+    }
+  }
+  const float tot = block_sum<NT>(ss, scratch);
+  const float rs = rsqrtf(tot / static_cast<float>(hidden) + eps);
+  const u16x8* wr = reinterpret_cast<const u16x8*>(w);
+  u16x8* yr = reinterpret_cast<u16x8*>(y + row * y_stride);
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int vi = threadIdx.x + i * NT;
+    if (vi < nvec) {
+      u16x8 wv = wr[vi];
+      u16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        // HF semantics: normalised value is rounded to bf16, then scaled by w
+        o[j] = f2bf(bf2f(f2bf(v[i][j] * rs)) * bf2f(wv[j]));
+      }
+      yr[vi] = o;
+    }
+  }
+}
+
+int rmsnorm(const bf16_t* x, bf16_t* residual, const bf16_t* w, bf16_t* y,
+            int rows, int hidden, int64_t x_stride, int64_t r_stride,
+            int64_t y_stride, float eps, hipStream_t stream) {
+  if (rows == 0) return 0;
+  constexpr int NT = 256;
+  const int nvec = hidden / 8;
+  if (nvec <= NT * 2) {
+    rmsnorm_kernel<NT, 2><<<rows, NT, 0, stream>>>(x, residual, w, y, hidden, x_stride, r_stride, y_stride, eps);
+  } else if (nvec <= NT * 4) {
+    rmsnorm_kernel<NT, 4><<<rows, NT, 0, stream>>>(x, residual, w, y, hidden, x_stride, r_stride, y_stride, eps);
+  } else {
+    rmsnorm_kernel<NT, 8><<<rows, NT, 0, stream>>>(x, residual, w, y, hidden, x_stride, r_stride, y_stride, eps);
+  }
+  OAMD_LAUNCH_CHECK();
+  return 0;
+}
+
+// out[m, i] = silu(gu[m, i]) * gu[m, I + i]; grid-stride over 8-element vectors.
+__global__ void silu_mul_kernel(const bf16_t* __restrict__ gu, bf16_t* __restrict__ out,
+                                int64_t rows, int inter, int64_t in_stride, int64_t out_stride) {
+  const int vpr = inter >> 3;
+  const int64_t total = rows * vpr;
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = idx / vpr;
+    const int c = static_cast<int>(idx - m * vpr) << 3;
+    const u16x8 g = *reinterpret_cast<const u16x8*>(gu + m * in_stride + c);
+    const u16x8 u = *reinterpret_cast<const u16x8*>(gu + m * in_stride + inter + c);
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float gf = bf2f(g[j]);
+      // HF: act(gate) rounded to bf16, then multiplied by up in bf16
+      const float s = bf2f(f2bf(gf / (1.f + __expf(-gf))));
+      o[j] = f2bf(s * bf2f(u[j]));
+    }
+    *reinterpret_cast<u16x8*>(out + m * out_stride + c) = o;
+  }
+}
+
+int silu_mul(const bf16_t* gu, bf16_t* out, int64_t rows, int inter,
+             int64_t in_stride, int64_t out_stride, hipStream_t stream) {
+  if (rows == 0) return 0;
+  const int64_t total = rows * (inter / 8);
+  const int nt = 256;
+  int64_t blocks = (total + nt - 1) / nt;
+  if (blocks > 256 * 16) blocks = 256 * 16;
+  silu_mul_kernel<<<static_cast<int>(blocks), nt, 0, stream>>>(gu, out, rows, inter, in_stride, out_stride);
+  OAMD_LAUNCH_CHECK();
+  return 0;
+}
+
+// Row gather: out[t, :] = table[ids[t], :]. One block per token, 16 B per lane.
+__global__ void embedding_kernel(const int64_t* __restrict__ ids, const bf16_t* __restrict__ table,
+                                 bf16_t* __restrict__ out, int hidden, int64_t vocab) {
+  const int t = blockIdx.x;
+  int64_t id = ids[t];
+  if (id < 0 || id >= vocab) id = 0;  // out-of-range ids are clamped, never read OOB
+  const u16x8* src = reinterpret_cast<const u16x8*>(table + id * hidden);
+  u16x8* dst = reinterpret_cast<u16x8*>(out + (int64_t)t * hidden);
+  for (int i = threadIdx.x; i < (hidden >> 3); i += blockDim.x) dst[i] = src[i];
+}
+
+int embedding(const int64_t* ids, const bf16_t* table, bf16_t* out, int tokens,
+              int hidden, int64_t vocab, hipStream_t stream) {
+  if (tokens == 0) return 0;
+  embedding_kernel<<<tokens, 256, 0, stream>>>(ids, table, out, hidden, vocab);
+  OAMD_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace oamd

@@ -1,0 +1,99 @@
+// Fused RoPE + paged KV-cache write.
+//
+// Input is the packed output of the fused QKV projection, one row per token:
+//   qkv[t] = [ q(Hq*D) | k(Hkv*D) | v(Hkv*D) ]  (bf16)
+// Rotary embedding (neox / rotate-half form, as HF Llama) is applied to q and
+// k using a host-precomputed fp32 cos/sin table [max_pos, D/2] (no on-device
+// trig: cdna_hip_programming.md App. B "Element-wise"). Outputs:
+//   q_out  [T, Hq, D]            rotated q (always)
+//   k_out/v_out [T, Hkv, D]      rotated k / copied v (optional, prefill path)
+//   k_cache/v_cache [pages, Hkv, P, D] at slot_mapping[t] (optional; slot<0 skips)
+#include "common.h"
+#include "kernels.h"
+
+namespace oamd {
+
+template <int D>
+__global__ void __launch_bounds__(256) rope_kv_kernel(
+    const bf16_t* __restrict__ qkv, int64_t qkv_stride, const int64_t* __restrict__ pos,
+    const float* __restrict__ cos_t, const float* __restrict__ sin_t, int Hq, int Hkv,
+    bf16_t* __restrict__ q_out, bf16_t* __restrict__ k_out, bf16_t* __restrict__ v_out,
+    bf16_t* __restrict__ k_cache, bf16_t* __restrict__ v_cache,
+    const int64_t* __restrict__ slots, int page_size, int64_t max_pos) {
+  constexpr int HALF = D / 2;
+  constexpr int GPH = HALF / 8;  // 8-element groups per half-head
+  const int t = blockIdx.x;
+  const bf16_t* row = qkv + t * qkv_stride;
+  int64_t p = pos[t];
+  if (p < 0) p = 0;
+  if (p >= max_pos) p = max_pos - 1;
+  const float* cr = cos_t + p * HALF;
+  const float* sr = sin_t + p * HALF;
+  int64_t slot = slots ? slots[t] : -1;
+  int64_t cache_base_k = -1;
+  if (slot >= 0) {
+    const int64_t page = slot / page_size, off = slot % page_size;
+    cache_base_k = (page * Hkv * page_size + off) * D;  // + h*page_size*D
+  }
+  const int rot_items = (Hq + Hkv) * GPH;
+  const int copy_items = Hkv * (D / 8);
+  for (int it = threadIdx.x; it < rot_items + copy_items; it += blockDim.x) {
+    if (it < rot_items) {
+      const int h = it / GPH, g = (it % GPH) * 8;
+      const bf16_t* src = row + h * D;
+      const u16x8 x1 = *reinterpret_cast<const u16x8*>(src + g);
+      const u16x8 x2 = *reinterpret_cast<const u16x8*>(src + HALF + g);
+      const f32x4 c0 = *reinterpret_cast<const f32x4*>(cr + g);
+      const f32x4 c1 = *reinterpret_cast<const f32x4*>(cr + g + 4);
+      const f32x4 s0 = *reinterpret_cast<const f32x4*>(sr + g);
+      const f32x4 s1 = *reinterpret_cast<const f32x4*>(sr + g + 4);
+      u16x8 o1, o2;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float c = j < 4 ? c0[j & 3] : c1[j & 3];
+        const float s = j < 4 ? s0[j & 3] : s1[j & 3];
+        const float a = bf2f(x1[j]), b = bf2f(x2[j]);
+        o1[j] = f2bf(a * c - b * s);
+        o2[j] = f2bf(b * c + a * s);
+      }
+      if (h < Hq) {
+        bf16_t* dst = q_out + ((int64_t)t * Hq + h) * D;
+        *reinterpret_cast<u16x8*>(dst + g) = o1;
+        *reinterpret_cast<u16x8*>(dst + HALF + g) = o2;
+      } else {
+        const int kh = h - Hq;
+        if (k_out) {
+          bf16_t* dst = k_out + ((int64_t)t * Hkv + kh) * D;
+          *reinterpret_cast<u16x8*>(dst + g) = o1;
+          *reinterpret_cast<u16x8*>(dst + HALF + g) = o2;
+        }
+        if (cache_base_k >= 0) {
+          bf16_t* dst = k_cache + cache_base_k + (int64_t)kh * page_size * D;
+          *reinterpret_cast<u16x8*>(dst + g) = o1;
+          *reinterpret_cast<u16x8*>(dst + HALF + g) = o2;
+        }
+      }
+    } else {
+      const int ci = it - rot_items;
+      const int kh = ci / (D / 8), g = (ci % (D / 8)) * 8;
+      const u16x8 v = *reinterpret_cast<const u16x8*>(row + (Hq + Hkv + kh) * D + g);
+      if (v_out) *reinterpret_cast<u16x8*>(v_out + ((int64_t)t * Hkv + kh) * D + g) = v;
+      if (cache_base_k >= 0)
+        *reinterpret_cast<u16x8*>(v_cache + cache_base_k + (int64_t)kh * page_size * D + g) = v;
+    }
+  }
+}
+
+int rope_kv(const bf16_t* qkv, int64_t qkv_stride, const int64_t* pos, const float* cos_t,
+            const float* sin_t, int tokens, int Hq, int Hkv, int head_dim, bf16_t* q_out,
+            bf16_t* k_out, bf16_t* v_out, bf16_t* k_cache, bf16_t* v_cache,
+            const int64_t* slots, int page_size, int64_t max_pos, hipStream_t stream) {
+  if (tokens == 0) return 0;
+  if (head_dim != 128) return -1;
+  rope_kv_kernel<128><<<tokens, 256, 0, stream>>>(qkv, qkv_stride, pos, cos_t, sin_t, Hq, Hkv, q_out, k_out,
+                                                 v_out, k_cache, v_cache, slots, page_size, max_pos);
+  OAMD_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace oamd

@@ -1,0 +1,79 @@
+// Token sampler: temperature + Gumbel-max over the full
+// vocabulary, greedy when temperature <= 0. One 1024-thread block per row;
+// each thread keeps a (value, index) pair over a grid-stride of the vocab with
+// 16-B loads, then a wave + LDS argmax. The noise is a counter-based hash of
+// (seed[row], position[row], column), so a captured hipGraph replays to the
+// same tokens and the kernel needs no RNG state on the device.
+#include "common.h"
+#include "kernels.h"
+
+namespace oamd {
+
+template <typename T>
+__device__ __forceinline__ float load_logit(const T* p, int64_t i);
+template <>
+__device__ __forceinline__ float load_logit<float>(const float* p, int64_t i) { return p[i]; }
+template <>
+__device__ __forceinline__ float load_logit<bf16_t>(const bf16_t* p, int64_t i) { return bf2f(p[i]); }
+
+__device__ __forceinline__ void argmax_merge(float& bv, int& bi, float v, int i) {
+  if (v > bv || (v == bv && i < bi)) { bv = v; bi = i; }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(1024) sample_kernel(const T* __restrict__ logits, int64_t stride, int vocab,
+                                                      const float* __restrict__ temperature,
+                                                      const int64_t* __restrict__ seeds,
+                                                      const int64_t* __restrict__ positions,
+                                                      int64_t* __restrict__ out_tokens) {
+  __shared__ float sv[16];
+  __shared__ int si[16];
+  const int row = blockIdx.x;
+  const T* lr = logits + row * stride;
+  const float temp = temperature[row];
+  const bool greedy = !(temp > 0.f);
+  const float inv_t = greedy ? 1.f : 1.f / temp;
+  const uint64_t key = (static_cast<uint64_t>(seeds[row]) * 0x9E3779B97F4A7C15ULL) ^
+                       (static_cast<uint64_t>(positions[row]) << 32);
+  float bv = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int i = threadIdx.x; i < vocab; i += blockDim.x) {
+    float x = load_logit<T>(lr, i);
+    if (!greedy) {
+      const float u = uniform01(key + static_cast<uint64_t>(i));
+      x = x * inv_t - __logf(-__logf(u));
+    }
+    argmax_merge(bv, bi, x, i);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(bv, o, kWave);
+    const int oi = __shfl_xor(bi, o, kWave);
+    argmax_merge(bv, bi, ov, oi);
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) { sv[w] = bv; si[w] = bi; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float v = sv[0];
+    int id = si[0];
+    for (int j = 1; j < (int)(blockDim.x >> 6); ++j) argmax_merge(v, id, sv[j], si[j]);
+    out_tokens[row] = (id == 0x7fffffff) ? 0 : id;
+  }
+}
+
+int sample_tokens(const void* logits, bool logits_bf16, int64_t stride, int rows, int vocab,
+                  const float* temperature, const int64_t* seeds, const int64_t* positions,
+                  int64_t* out_tokens, hipStream_t stream) {
+  if (rows == 0) return 0;
+  if (logits_bf16)
+    sample_kernel<bf16_t><<<rows, 1024, 0, stream>>>(static_cast<const bf16_t*>(logits), stride, vocab,
+                                                     temperature, seeds, positions, out_tokens);
+  else
+    sample_kernel<float><<<rows, 1024, 0, stream>>>(static_cast<const float*>(logits), stride, vocab,
+                                                    temperature, seeds, positions, out_tokens);
+  OAMD_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace oamd

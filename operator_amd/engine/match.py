@@ -1,0 +1,315 @@
+"""Pattern-match engine: batched pod logs -> AnalysisResult (replaces the
+reference's log-parser REST hop, J/service/LogParserClient.java:36-55 /
+LogParserRestClient.java:37-39).
+
+GPU path (one call per batch of failures):
+  host  : plan + pack logs into a pinned staging buffer (native, threaded)
+  H2D   : one contiguous async copy
+  device: ac_scan (DFA walk, LDS hot states) -> per-segment newline counts
+          -> exclusive prefix (cumsum) -> scan_fixup (doc, factor, line, offset)
+  D2H   : the (small) match list
+  host  : factor -> matcher expansion, regex verification of candidate lines
+          only, native event scoring, result assembly with context lines.
+CPU path: the same post-processing fed by the pure-Python oracle.
+"""
+from __future__ import annotations
+
+import threading
+import time
+import uuid
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from operator_amd.api.models import AnalysisEvent, AnalysisResult, AnalysisSummary, MatchedPattern
+from operator_amd.patterns import oracle
+from operator_amd.patterns.compiler import CompiledPatterns, compile_patterns
+from operator_amd.patterns.schema import SEVERITIES, SEVERITY_RANK, PatternSet
+
+
+@dataclass
+class ScanStats:
+    bytes_scanned: int = 0
+    docs: int = 0
+    raw_matches: int = 0
+    verified_hits: int = 0
+    scan_ms: float = 0.0
+    host_ms: float = 0.0
+
+
+def _line_bounds(doc: bytes, off: int) -> tuple[int, int]:
+    s = doc.rfind(b"\n", 0, off) + 1
+    e = doc.find(b"\n", off)
+    return s, (len(doc) if e < 0 else e)
+
+
+def _context(doc: bytes, off: int, k: int) -> tuple[list[str], str]:
+    s, e = _line_bounds(doc, off)
+    line = doc[s:e]
+    before = []
+    ps = s
+    for _ in range(k):
+        if ps <= 0:
+            break
+        pe = ps - 1
+        ps = doc.rfind(b"\n", 0, pe) + 1
+        before.append(doc[ps:pe])
+    after = []
+    ne = e
+    for _ in range(k):
+        if ne >= len(doc):
+            break
+        ns = ne + 1
+        if ns >= len(doc):
+            break
+        ne = doc.find(b"\n", ns)
+        ne = len(doc) if ne < 0 else ne
+        after.append(doc[ns:ne])
+    ctx = [b.decode("utf-8", "replace") for b in reversed(before)] + [line.decode("utf-8", "replace")] + \
+          [a.decode("utf-8", "replace") for a in after]
+    return ctx, line.decode("utf-8", "replace")
+
+
+def _line_offsets(doc: bytes) -> list[int]:
+    offs = [0]
+    i = doc.find(b"\n")
+    while i >= 0:
+        offs.append(i + 1)
+        i = doc.find(b"\n", i + 1)
+    return offs
+
+
+class MatchEngine:
+    """Compile a PatternSet once, then analyze batches of logs on one device."""
+
+    def __init__(self, patterns: PatternSet | CompiledPatterns, device: str | torch.device = "cuda",
+                 seg_bytes: int = 1024, max_events: int = 50, significance: float = 0.5,
+                 match_cap: int = 1 << 20, grid_blocks: int = 0, use_native_scorer: bool = True):
+        self.cp = patterns if isinstance(patterns, CompiledPatterns) else compile_patterns(patterns)
+        self.device = torch.device(device)
+        self.seg_bytes = int(seg_bytes)
+        self.max_events = max_events
+        self.significance = significance
+        self.match_cap = int(match_cap)
+        self.grid_blocks = grid_blocks
+        self.use_native_scorer = use_native_scorer
+        self.stats = ScanStats()
+        self._lock = threading.Lock()
+        self._pinned: torch.Tensor | None = None
+        self._text: torch.Tensor | None = None
+        self._seg_nl: torch.Tensor | None = None
+        self._matches: torch.Tensor | None = None
+        self._count: torch.Tensor | None = None
+        # matcher -> list of (pattern) where it is primary, for quick checks
+        self._nm = self.cp.num_matchers
+        fm_ptr = [0]
+        fm_ids: list[int] = []
+        for ms in self.cp.factor_matchers:
+            fm_ids.extend(ms)
+            fm_ptr.append(len(fm_ids))
+        self._fm_ptr = np.asarray(fm_ptr, dtype=np.int64)
+        self._fm_ids = np.asarray(fm_ids if fm_ids else [0], dtype=np.int64)
+        self._verify = np.asarray(self.cp.matcher_verify + [False], dtype=bool)
+        if self.device.type == "cuda" and self.cp.factors:
+            self._upload_dfa()
+
+    # ------------------------------------------------------------------ DFA upload
+    def _upload_dfa(self) -> None:
+        from operator_amd.ops import kernels
+
+        d = self.cp.dfa
+        dev = self.device
+        S, log2c = int(d["num_states"]), int(d["log2_classes"])
+        self.dfa_states, self.log2c = S, log2c
+        self.cls_map = torch.frombuffer(bytearray(d["cls_map"]), dtype=torch.uint8).to(dev)
+        self.table = torch.frombuffer(bytearray(d["table"]), dtype=torch.int16).reshape(S, 1 << log2c).to(dev)
+        self.out_off = torch.frombuffer(bytearray(d["out_off"]), dtype=torch.int32).to(dev)
+        self.out_ids = torch.frombuffer(bytearray(d["out_ids"]), dtype=torch.int32).to(dev)
+        self.hot_states = int(min(S, kernels().max_hot_states(log2c)))
+
+    # ------------------------------------------------------------------ GPU scan
+    def _ensure(self, name: str, numel: int, dtype, pinned: bool = False, device=None) -> torch.Tensor:
+        t = getattr(self, name)
+        if t is None or t.numel() < numel:
+            cap = max(numel, int((t.numel() if t is not None else 0) * 1.5))
+            if pinned:
+                t = torch.empty(cap, dtype=dtype, pin_memory=True)
+            else:
+                t = torch.empty(cap, dtype=dtype, device=device or self.device)
+            setattr(self, name, t)
+        return t
+
+    def scan_gpu(self, docs: list[bytes]) -> np.ndarray:
+        """Raw factor hits as int64 array [n, 4] = (doc, factor, line, end_offset_in_doc)."""
+        from operator_amd.ops import kernels, patterns
+
+        P = patterns()
+        seg = self.seg_bytes
+        total, first = P.plan_docs([len(d) for d in docs], seg)
+        n_segs = total // seg
+        pinned = self._ensure("_pinned", total, torch.uint8, pinned=True)
+        P.pack_docs(docs, first, seg, pinned.data_ptr(), 8)
+        text = self._ensure("_text", total, torch.uint8)
+        text[:total].copy_(pinned[:total], non_blocking=True)
+        seg_nl = self._ensure("_seg_nl", n_segs, torch.int32)
+        C = kernels()
+        first_t = torch.tensor(first, dtype=torch.int64).to(self.device, non_blocking=True)
+        while True:
+            if self._matches is None or self._matches.shape[0] < self.match_cap:
+                self._matches = torch.empty(self.match_cap, 4, dtype=torch.int32, device=self.device)
+            if self._count is None:
+                self._count = torch.zeros(1, dtype=torch.int32, device=self.device)
+            self._count.zero_()
+            C.ac_scan(text[:total], seg, self.cls_map, self.table, self.log2c, self.hot_states, self.out_off,
+                      self.out_ids, self._matches, self._count, seg_nl, self.grid_blocks)
+            nl = seg_nl[:n_segs].to(torch.int64)
+            excl = torch.cumsum(nl, 0) - nl
+            C.scan_fixup(self._matches, self._count, excl, first_t, seg)
+            cnt = int(self._count.item())
+            if cnt <= self._matches.shape[0]:
+                break
+            self.match_cap = int(cnt * 1.25) + 1024  # overflow: grow and rescan (rare)
+            self._matches = None
+        self.stats.raw_matches += cnt
+        self.stats.bytes_scanned += sum(len(d) for d in docs)
+        return self._matches[:cnt].cpu().numpy().astype(np.int64) if cnt else np.zeros((0, 4), np.int64)
+
+    def scan_cpu(self, docs: list[bytes]) -> np.ndarray:
+        """Same contract as scan_gpu, computed with Python (used without a GPU)."""
+        rows = []
+        lows = [f for f in self.cp.factors]
+        for di, d in enumerate(docs):
+            dl = d.lower()
+            for fi, f in enumerate(lows):
+                start = 0
+                while True:
+                    i = dl.find(f, start)
+                    if i < 0:
+                        break
+                    end = i + len(f) - 1
+                    line = dl.count(b"\n", 0, end)
+                    rows.append((di, fi, line, end))
+                    start = i + 1
+        return np.asarray(rows, dtype=np.int64).reshape(-1, 4)
+
+    # ------------------------------------------------------------------ analysis
+    def hits(self, docs: list[bytes]) -> tuple[np.ndarray, dict]:
+        """Verified, de-duplicated matcher hits [n, 3] = (doc, matcher, line) + offsets."""
+        t0 = time.perf_counter()
+        raw = self.scan_gpu(docs) if (self.device.type == "cuda" and self.cp.factors) else (
+            self.scan_cpu(docs) if self.cp.factors else np.zeros((0, 4), np.int64))
+        t1 = time.perf_counter()
+        offs: dict[tuple[int, int, int], int] = {}
+        out: set[tuple[int, int, int]] = set()
+        if raw.shape[0]:
+            f = raw[:, 1]
+            cnt = self._fm_ptr[f + 1] - self._fm_ptr[f]
+            rep = np.repeat(np.arange(raw.shape[0]), cnt)
+            starts = np.repeat(self._fm_ptr[f], cnt)
+            within = np.arange(rep.shape[0]) - np.repeat(np.cumsum(cnt) - cnt, cnt)
+            mat = self._fm_ids[starts + within]
+            doc, line, off = raw[rep, 0], raw[rep, 2], raw[rep, 3]
+            need = self._verify[mat]
+            # fast path: exact factors
+            for d_, m_, l_, o_ in zip(doc[~need].tolist(), mat[~need].tolist(), line[~need].tolist(),
+                                      off[~need].tolist()):
+                k = (d_, m_, l_)
+                if k not in out:
+                    out.add(k)
+                    offs[k] = o_
+            # verify path: regex / case-sensitive on the candidate line only
+            checked: dict[tuple[int, int, int], bool] = {}
+            for d_, m_, l_, o_ in zip(doc[need].tolist(), mat[need].tolist(), line[need].tolist(),
+                                      off[need].tolist()):
+                k = (d_, m_, l_)
+                if k in checked:
+                    continue
+                s, e = _line_bounds(docs[d_], o_)
+                ok = self.cp.regexes[m_].search(docs[d_][s:e]) is not None
+                checked[k] = ok
+                if ok:
+                    out.add(k)
+                    offs[k] = o_
+        # matchers with no usable factor: evaluated on every line on the CPU
+        for m_ in self.cp.unfiltered:
+            rx = self.cp.regexes[m_]
+            for d_, doc_b in enumerate(docs):
+                lo = _line_offsets(doc_b)
+                for li, ls in enumerate(lo):
+                    le = lo[li + 1] - 1 if li + 1 < len(lo) else len(doc_b)
+                    if rx.search(doc_b[ls:le]):
+                        k = (d_, m_, li)
+                        out.add(k)
+                        offs[k] = max(ls, le - 1) if le > ls else ls
+        arr = np.asarray(sorted(out), dtype=np.int64).reshape(-1, 3)
+        self.stats.verified_hits += arr.shape[0]
+        self.stats.scan_ms += (t1 - t0) * 1e3
+        self.stats.host_ms += (time.perf_counter() - t1) * 1e3
+        return arr, offs
+
+    def events(self, docs: list[bytes]) -> tuple[list[list[oracle.Event]], dict]:
+        hits, offs = self.hits(docs)
+        cp = self.cp
+        if self.use_native_scorer:
+            from operator_amd.ops import patterns
+
+            pats = cp.patset.patterns
+            res = patterns().score_events(
+                hits[:, 0].tolist(), hits[:, 1].tolist(), hits[:, 2].tolist(), len(docs),
+                cp.pattern_primary, [p.primary.confidence for p in pats], [p.severity_rank for p in pats],
+                cp.pattern_secondary, [[s.weight for s in p.secondary] for p in pats],
+                [[s.window for s in p.secondary] for p in pats], cp.num_matchers)
+            evs = [[oracle.Event(int(p), int(l), float(s)) for (p, l, s) in d] for d in res]
+        else:
+            per: list[set] = [set() for _ in docs]
+            for d_, m_, l_ in hits.tolist():
+                per[d_].add((m_, l_))
+            evs = [oracle.score_doc(cp, h) for h in per]
+        return evs, offs
+
+    def analyze(self, docs: list[bytes], pods: list[tuple[str, str]] | None = None) -> list[AnalysisResult]:
+        """Full AnalysisResult per doc (pods = [(name, namespace)] for labelling)."""
+        with self._lock:
+            t0 = time.perf_counter()
+            evs, offs = self.events(docs)
+            out = []
+            for di, (doc, ev) in enumerate(zip(docs, evs)):
+                out.append(self._result(di, doc, ev, offs, pods[di] if pods else (None, None),
+                                        (time.perf_counter() - t0) * 1e3))
+            self.stats.docs += len(docs)
+            return out
+
+    def _result(self, di: int, doc: bytes, ev: list[oracle.Event], offs: dict, pod, ms: float) -> AnalysisResult:
+        cp = self.cp
+        pats = cp.patset.patterns
+        dist = {s: 0 for s in SEVERITIES}
+        sig = 0
+        hi = -1
+        for e in ev:
+            p = pats[e.pattern]
+            dist[p.severity] += 1
+            hi = max(hi, p.severity_rank)
+            if e.score >= self.significance:
+                sig += 1
+        events = []
+        for e in ev[: self.max_events]:
+            p = pats[e.pattern]
+            off = offs.get((di, cp.pattern_primary[e.pattern], e.line))
+            if off is None:
+                lo = _line_offsets(doc)
+                off = lo[e.line] if e.line < len(lo) else 0
+            ctx, line = _context(doc, off, p.context_lines)
+            events.append(AnalysisEvent(
+                line_number=e.line + 1,
+                matched_pattern=MatchedPattern(id=p.id, name=p.name, severity=p.severity, category=p.category or None,
+                                               library=p.library or None),
+                score=round(e.score, 6), context=ctx, matched_line=line,
+                remediation=p.remediation or None))
+        summary = AnalysisSummary(highest_severity=SEVERITIES[hi] if hi >= 0 else None, significant_events=sig,
+                                  total_events=len(ev), severity_distribution={k: v for k, v in dist.items() if v})
+        return AnalysisResult(analysis_id=str(uuid.uuid4()), pod_name=pod[0], pod_namespace=pod[1], events=events,
+                              summary=summary,
+                              metadata={"engine": "gpu-ac" if self.device.type == "cuda" else "cpu-oracle",
+                                        "patternsChecked": len(pats), "totalLines": doc.count(b"\n") + 1,
+                                        "bytes": len(doc), "processingTimeMs": round(ms, 3)})

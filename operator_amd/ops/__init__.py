@@ -1,0 +1,154 @@
+"""Device ops of the explanation model and the log scanner.
+
+GPU tensors always go to the hand-written gfx950 kernels in ``operator_amd._C``
+(loading fails loudly if the extension is missing); CPU tensors use the fp32
+reference implementations in :mod:`operator_amd.ops.reference`.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import reference
+from ._native import kernels, native_available, patterns
+
+__all__ = [
+    "rmsnorm", "silu_mul", "embedding", "rope_kv", "attn_prefill", "attn_decode", "sample",
+    "kernels", "patterns", "native_available", "reference", "prefill_work_list", "decode_splits",
+]
+
+DECODE_SPLIT_TOKENS = 256  # must match kSplit in csrc/kernels/attn_decode.hip
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: torch.Tensor | None = None,
+            out: torch.Tensor | None = None) -> torch.Tensor:
+    """RMSNorm; if ``residual`` is given it is updated in place to x + residual first."""
+    if not x.is_cuda:
+        y, r = reference.rmsnorm(x, w, eps, residual)
+        if residual is not None:
+            residual.copy_(r)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+    y = out if out is not None else torch.empty_like(x)
+    kernels().rmsnorm(x, residual, w, y, eps)
+    return y
+
+
+def silu_mul(gu: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    if not gu.is_cuda:
+        r = reference.silu_mul(gu)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    inter = gu.shape[1] // 2
+    o = out if out is not None else torch.empty(gu.shape[0], inter, dtype=gu.dtype, device=gu.device)
+    kernels().silu_mul(gu, o)
+    return o
+
+
+def embedding(ids: torch.Tensor, table: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    if not ids.is_cuda:
+        r = reference.embedding(ids, table)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    o = out if out is not None else torch.empty(ids.numel(), table.shape[1], dtype=table.dtype, device=ids.device)
+    kernels().embedding(ids, table, o)
+    return o
+
+
+def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, Hq: int, Hkv: int,
+            k_cache: torch.Tensor | None = None, v_cache: torch.Tensor | None = None,
+            slots: torch.Tensor | None = None, want_kv: bool = True,
+            q_out: torch.Tensor | None = None):
+    """Rotate q/k of the packed qkv rows and scatter k/v into the paged cache.
+
+    Returns (q [T,Hq,D], k [T,Hkv,D] | None, v [T,Hkv,D] | None).
+    """
+    if not qkv.is_cuda:
+        q, k, v = reference.rope_kv(qkv, pos, cos, sin, Hq, Hkv, k_cache, v_cache, slots)
+        if q_out is not None:
+            q_out.copy_(q.reshape(q_out.shape))
+            q = q_out
+        return q, (k if want_kv else None), (v if want_kv else None)
+    T = qkv.shape[0]
+    D = cos.shape[1] * 2
+    q = q_out if q_out is not None else torch.empty(T, Hq, D, dtype=qkv.dtype, device=qkv.device)
+    k = torch.empty(T, Hkv, D, dtype=qkv.dtype, device=qkv.device) if want_kv else None
+    v = torch.empty(T, Hkv, D, dtype=qkv.dtype, device=qkv.device) if want_kv else None
+    kernels().rope_kv(qkv, pos, cos, sin, Hq, Hkv, q, k, v, k_cache, v_cache, slots)
+    return q, k, v
+
+
+def prefill_work_list(seq_lens: list[int], block_q: int = 64) -> tuple[list[int], list[int]]:
+    """(work_seq, work_q0) for attn_prefill: one item per 64-row query block; longest first."""
+    items = []
+    for s, L in enumerate(seq_lens):
+        for q0 in range(0, L, block_q):
+            items.append((q0, s))
+    items.sort(key=lambda t: -t[0])  # heavy (late, long-causal) blocks first
+    return [s for _, s in items], [q0 for q0, _ in items]
+
+
+def attn_prefill(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, seq_lens: list[int], scale: float,
+                 out: torch.Tensor | None = None, work: tuple[torch.Tensor, torch.Tensor, torch.Tensor] | None = None):
+    """Causal attention over packed sequences (q [T,Hq,D], k/v [T,Hkv,D])."""
+    cu = [0]
+    for L in seq_lens:
+        cu.append(cu[-1] + int(L))
+    if not q.is_cuda:
+        r = reference.attn_prefill(q, k, v, cu, scale)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    o = out if out is not None else torch.empty_like(q)
+    if work is None:
+        ws, wq = prefill_work_list([int(x) for x in seq_lens])
+        dev = q.device
+        work = (torch.tensor(cu, dtype=torch.int32, device=dev), torch.tensor(ws, dtype=torch.int32, device=dev),
+                torch.tensor(wq, dtype=torch.int32, device=dev))
+    kernels().attn_prefill(q, k, v, o, work[0], work[1], work[2], scale)
+    return o
+
+
+def decode_splits(max_context: int) -> int:
+    return max(1, (int(max_context) + DECODE_SPLIT_TOKENS - 1) // DECODE_SPLIT_TOKENS)
+
+
+def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
+                seq_lens: torch.Tensor, scale: float, num_splits: int, out: torch.Tensor | None = None,
+                workspace: tuple[torch.Tensor, torch.Tensor] | None = None) -> torch.Tensor:
+    """Paged split-KV decode attention. ``num_splits`` * 256 must cover the longest context."""
+    if not q.is_cuda:
+        r = reference.attn_decode(q, k_cache, v_cache, block_tables, seq_lens, scale)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    B, Hq, D = q.shape
+    o = out if out is not None else torch.empty_like(q)
+    if workspace is None:
+        n = max(1, B * Hq * num_splits)
+        workspace = (torch.empty(n * D, dtype=torch.float32, device=q.device),
+                     torch.empty(n * 2, dtype=torch.float32, device=q.device))
+    kernels().attn_decode(q, k_cache, v_cache, block_tables, seq_lens, o, workspace[0], workspace[1],
+                          num_splits, scale)
+    return o
+
+
+def sample(logits: torch.Tensor, temperature: torch.Tensor, seeds: torch.Tensor, positions: torch.Tensor,
+           out: torch.Tensor | None = None) -> torch.Tensor:
+    """Temperature / Gumbel-max sampling (greedy rows where temperature <= 0)."""
+    if not logits.is_cuda:
+        r = reference.sample(logits, temperature, seeds, positions)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    o = out if out is not None else torch.empty(logits.shape[0], dtype=torch.long, device=logits.device)
+    kernels().sample(logits, temperature, seeds, positions, o)
+    return o

@@ -1,0 +1,167 @@
+"""Plain-PyTorch fp32 reference implementations of every HIP kernel.
+
+These define the numerics each gfx950 kernel is tested against (tests/test_kernels_gpu.py)
+and are what runs when a model is executed on CPU (the CPU test tier, gloo
+multi-process TP tests). They are intentionally simple and unfused.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: torch.Tensor | None = None):
+    """y = rmsnorm(x [+ residual]); returns (y, new_residual). HF Llama numerics."""
+    if residual is not None:
+        x = (x.float() + residual.float()).to(x.dtype)
+        new_res = x
+    else:
+        new_res = None
+    xf = x.float()
+    var = xf.pow(2).mean(-1, keepdim=True)
+    y = (xf * torch.rsqrt(var + eps)).to(x.dtype)
+    return (y.float() * w.float()).to(x.dtype), new_res
+
+
+def silu_mul(gu: torch.Tensor) -> torch.Tensor:
+    inter = gu.shape[-1] // 2
+    g, u = gu[..., :inter], gu[..., inter:]
+    s = torch.nn.functional.silu(g.float()).to(gu.dtype)
+    return (s.float() * u.float()).to(gu.dtype)
+
+
+def embedding(ids: torch.Tensor, table: torch.Tensor) -> torch.Tensor:
+    return table[ids.clamp(0, table.shape[0] - 1)]
+
+
+def rope_tables(max_pos: int, head_dim: int, theta: float, scaling: dict | None = None,
+                device=None) -> tuple[torch.Tensor, torch.Tensor]:
+    """fp32 cos/sin tables [max_pos, head_dim/2]; supports Llama-3.1 'llama3' scaling."""
+    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+    if scaling and scaling.get("rope_type", scaling.get("type")) == "llama3":
+        factor = scaling["factor"]
+        lo, hi = scaling.get("low_freq_factor", 1.0), scaling.get("high_freq_factor", 4.0)
+        old = scaling.get("original_max_position_embeddings", 8192)
+        lo_wl, hi_wl = old / lo, old / hi
+        wl = 2 * math.pi / inv
+        smooth = (old / wl - lo) / (hi - lo)
+        scaled = torch.where(wl > lo_wl, inv / factor, inv)
+        mid = (wl <= lo_wl) & (wl >= hi_wl)
+        inv = torch.where(mid, (1 - smooth) * inv / factor + smooth * inv, scaled)
+    t = torch.arange(max_pos, dtype=torch.float64)
+    f = torch.outer(t, inv)
+    return f.cos().float().to(device), f.sin().float().to(device)
+
+
+def apply_rope(x: torch.Tensor, pos: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+    """x: [T, H, D] -> rotate-half RoPE at positions pos [T]."""
+    half = x.shape[-1] // 2
+    c = cos[pos].unsqueeze(1)
+    s = sin[pos].unsqueeze(1)
+    xf = x.float()
+    x1, x2 = xf[..., :half], xf[..., half:]
+    return torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], dim=-1).to(x.dtype)
+
+
+def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, Hq: int, Hkv: int,
+            k_cache: torch.Tensor | None = None, v_cache: torch.Tensor | None = None,
+            slots: torch.Tensor | None = None):
+    """Split packed qkv, rotate q/k, optionally scatter k/v into the paged cache.
+
+    Cache layout [pages, Hkv, page, D]; slot = page*page_size + offset; slot < 0 skips.
+    Returns (q [T,Hq,D], k [T,Hkv,D], v [T,Hkv,D]).
+    """
+    T = qkv.shape[0]
+    D = cos.shape[1] * 2
+    q = qkv[:, : Hq * D].reshape(T, Hq, D)
+    k = qkv[:, Hq * D: (Hq + Hkv) * D].reshape(T, Hkv, D)
+    v = qkv[:, (Hq + Hkv) * D:].reshape(T, Hkv, D)
+    q = apply_rope(q, pos, cos, sin)
+    k = apply_rope(k, pos, cos, sin)
+    if k_cache is not None:
+        P = k_cache.shape[2]
+        for t in range(T):
+            s = int(slots[t])
+            if s < 0:
+                continue
+            k_cache[s // P, :, s % P] = k[t]
+            v_cache[s // P, :, s % P] = v[t]
+    return q, k.contiguous(), v.contiguous()
+
+
+def attn_prefill(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cu_seqlens: list[int] | torch.Tensor,
+                 scale: float) -> torch.Tensor:
+    """Causal GQA attention over packed variable-length sequences. q [T,Hq,D], k/v [T,Hkv,D]."""
+    cu = [int(x) for x in cu_seqlens]
+    Hq, Hkv = q.shape[1], k.shape[1]
+    G = Hq // Hkv
+    out = torch.empty_like(q)
+    for i in range(len(cu) - 1):
+        a, b = cu[i], cu[i + 1]
+        if b == a:
+            continue
+        qs = q[a:b].float().transpose(0, 1)                      # [Hq, L, D]
+        ks = k[a:b].float().transpose(0, 1).repeat_interleave(G, 0)
+        vs = v[a:b].float().transpose(0, 1).repeat_interleave(G, 0)
+        s = torch.matmul(qs, ks.transpose(1, 2)) * scale
+        L = b - a
+        mask = torch.ones(L, L, dtype=torch.bool, device=q.device).triu(1)
+        s.masked_fill_(mask, float("-inf"))
+        p = torch.softmax(s, -1)
+        out[a:b] = torch.matmul(p, vs).transpose(0, 1).to(q.dtype)
+    return out
+
+
+def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
+                seq_lens: torch.Tensor, scale: float) -> torch.Tensor:
+    """One query token per sequence over a paged cache [pages, Hkv, page, D]."""
+    B, Hq, D = q.shape
+    Hkv, P = k_cache.shape[1], k_cache.shape[2]
+    G = Hq // Hkv
+    out = torch.zeros_like(q)
+    for b in range(B):
+        L = int(seq_lens[b])
+        if L == 0:
+            continue
+        npg = (L + P - 1) // P
+        pages = block_tables[b, :npg].long()
+        ks = k_cache[pages].permute(1, 0, 2, 3).reshape(Hkv, npg * P, D)[:, :L].float()
+        vs = v_cache[pages].permute(1, 0, 2, 3).reshape(Hkv, npg * P, D)[:, :L].float()
+        ks = ks.repeat_interleave(G, 0)
+        vs = vs.repeat_interleave(G, 0)
+        s = torch.einsum("hd,hld->hl", q[b].float(), ks) * scale
+        p = torch.softmax(s, -1)
+        out[b] = torch.einsum("hl,hld->hd", p, vs).to(q.dtype)
+    return out
+
+
+def gumbel_noise_ref(seed: int, position: int, vocab: int) -> torch.Tensor:
+    """Host mirror of the device counter hash (common.h hash_u32/uniform01)."""
+    M = (1 << 64) - 1
+    key = ((seed * 0x9E3779B97F4A7C15) & M) ^ ((position << 32) & M)
+    xs = [(key + i) & M for i in range(vocab)]
+    out = []
+    for x in xs:
+        x ^= x >> 33
+        x = (x * 0xFF51AFD7ED558CCD) & M
+        x ^= x >> 33
+        x = (x * 0xC4CEB9FE1A85EC53) & M
+        x ^= x >> 33
+        u = ((x & 0xFFFFFFFF) >> 8) + 0.5
+        out.append(u / 16777216.0)
+    u = torch.tensor(out, dtype=torch.float64)
+    return -torch.log(-torch.log(u))
+
+
+def sample(logits: torch.Tensor, temperature: torch.Tensor, seeds: torch.Tensor,
+           positions: torch.Tensor) -> torch.Tensor:
+    """Greedy when T<=0 else Gumbel-max with the same counter hash as the kernel."""
+    out = torch.empty(logits.shape[0], dtype=torch.long)
+    for r in range(logits.shape[0]):
+        x = logits[r].double().cpu()
+        t = float(temperature[r])
+        if t > 0:
+            x = x / t + gumbel_noise_ref(int(seeds[r]), int(positions[r]), x.numel())
+        out[r] = int(torch.argmax(x))
+    return out.to(logits.device)

@@ -1,0 +1,142 @@
+"""Numerics of every gfx950 HIP kernel against the plain-PyTorch fp32 reference."""
+import math
+
+import pytest
+import torch
+
+from operator_amd import ops
+from operator_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rand(*shape, dtype=torch.bfloat16, scale=1.0):
+    return (torch.randn(*shape, device=DEV) * scale).to(dtype)
+
+
+def test_native_module_is_loaded():
+    C = ops.kernels()
+    assert C.ARCH == "gfx950"
+    maps = open("/proc/self/maps").read()
+    assert "_C.cpython" in maps
+    hip_libs = {l.split()[-1] for l in maps.splitlines() if "libamdhip64" in l}
+    assert len(hip_libs) == 1, f"two HIP runtimes mapped: {hip_libs}"
+
+
+@pytest.mark.parametrize("rows,hidden", [(1, 4096), (7, 4096), (64, 8192), (3, 128)])
+@pytest.mark.parametrize("fused", [False, True])
+def test_rmsnorm(rows, hidden, fused):
+    torch.manual_seed(0)
+    x = _rand(rows, hidden)
+    w = _rand(hidden) * 0.5 + 1
+    r = _rand(rows, hidden) if fused else None
+    r_ref = r.clone() if fused else None
+    y = ops.rmsnorm(x, w, 1e-5, residual=r)
+    y_ref, nr = ref.rmsnorm(x.cpu(), w.cpu(), 1e-5, r_ref.cpu() if fused else None)
+    torch.testing.assert_close(y.cpu().float(), y_ref.float(), atol=2e-2, rtol=2e-2)
+    if fused:
+        torch.testing.assert_close(r.cpu().float(), nr.float(), atol=0, rtol=0)
+
+
+def test_silu_mul():
+    gu = _rand(37, 2 * 1408)
+    out = ops.silu_mul(gu)
+    torch.testing.assert_close(out.cpu().float(), ref.silu_mul(gu.cpu()).float(), atol=2e-2, rtol=2e-2)
+
+
+def test_embedding():
+    table = _rand(1000, 512)
+    ids = torch.randint(0, 1000, (33,), device=DEV)
+    torch.testing.assert_close(ops.embedding(ids, table).cpu(), table.cpu()[ids.cpu()])
+
+
+@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (16, 16)])
+def test_rope_kv_and_cache(Hq, Hkv):
+    torch.manual_seed(1)
+    T, D, P, pages = 19, 128, 16, 8
+    cos, sin = ref.rope_tables(4096, D, 500000.0, device=DEV)
+    qkv = _rand(T, (Hq + 2 * Hkv) * D)
+    pos = torch.randint(0, 4000, (T,), device=DEV)
+    kc = torch.zeros(pages, Hkv, P, D, dtype=torch.bfloat16, device=DEV)
+    vc = torch.zeros_like(kc)
+    slots = torch.randperm(pages * P, device=DEV)[:T]
+    slots[3] = -1
+    q, k, v = ops.rope_kv(qkv, pos, cos, sin, Hq, Hkv, kc, vc, slots)
+    kc_r, vc_r = torch.zeros_like(kc).cpu(), torch.zeros_like(vc).cpu()
+    q_r, k_r, v_r = ref.rope_kv(qkv.cpu(), pos.cpu(), cos.cpu(), sin.cpu(), Hq, Hkv, kc_r, vc_r, slots.cpu())
+    torch.testing.assert_close(q.cpu().float(), q_r.float(), atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(k.cpu().float(), k_r.float(), atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(v.cpu(), v_r)
+    torch.testing.assert_close(kc.cpu().float(), kc_r.float(), atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(vc.cpu(), vc_r)
+
+
+@pytest.mark.parametrize("lens", [[1], [17, 64, 130], [300, 5, 64]])
+@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 8), (16, 2)])
+def test_attn_prefill(lens, Hq, Hkv):
+    torch.manual_seed(2)
+    T, D = sum(lens), 128
+    q, k, v = _rand(T, Hq, D), _rand(T, Hkv, D), _rand(T, Hkv, D)
+    scale = 1 / math.sqrt(D)
+    o = ops.attn_prefill(q, k, v, lens, scale)
+    cu = [0]
+    for L in lens:
+        cu.append(cu[-1] + L)
+    o_r = ref.attn_prefill(q.cpu(), k.cpu(), v.cpu(), cu, scale)
+    torch.testing.assert_close(o.cpu().float(), o_r.float(), atol=2e-2, rtol=3e-2)
+
+
+def test_attn_prefill_large_scores():
+    """Spike one key so the running max jumps mid-sequence (forces the rescale path)."""
+    torch.manual_seed(3)
+    lens, Hq, Hkv, D = [256], 8, 8, 128
+    q, k, v = _rand(256, Hq, D), _rand(256, Hkv, D), _rand(256, Hkv, D)
+    k[200] = (q[220].float() * 6).to(torch.bfloat16)[: Hkv]
+    o = ops.attn_prefill(q, k, v, lens, 1 / math.sqrt(D))
+    o_r = ref.attn_prefill(q.cpu(), k.cpu(), v.cpu(), [0, 256], 1 / math.sqrt(D))
+    torch.testing.assert_close(o.cpu().float(), o_r.float(), atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("lens", [[1, 5, 300], [1000, 0, 2049], [4096]])
+@pytest.mark.parametrize("Hq,Hkv,P", [(32, 8, 64), (8, 1, 16), (16, 16, 32)])
+def test_attn_decode(lens, Hq, Hkv, P):
+    torch.manual_seed(4)
+    B, D = len(lens), 128
+    maxp = (max(lens) + P - 1) // P + 1
+    pages = B * maxp + 3
+    kc, vc = _rand(pages, Hkv, P, D), _rand(pages, Hkv, P, D)
+    bt = torch.randperm(pages, device=DEV)[: B * maxp].reshape(B, maxp).int()
+    sl = torch.tensor(lens, dtype=torch.int32, device=DEV)
+    q = _rand(B, Hq, D)
+    scale = 1 / math.sqrt(D)
+    ns = ops.decode_splits(max(lens))
+    o = ops.attn_decode(q, kc, vc, bt, sl, scale, ns)
+    o_r = ref.attn_decode(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), sl.cpu(), scale)
+    torch.testing.assert_close(o.cpu().float(), o_r.float(), atol=2e-2, rtol=3e-2)
+    # the same call with more splits than needed (graph-capture mode) must agree
+    o2 = ops.attn_decode(q, kc, vc, bt, sl, scale, ns + 3)
+    torch.testing.assert_close(o2.cpu().float(), o_r.float(), atol=2e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_sample(dtype):
+    torch.manual_seed(5)
+    B, V = 6, 5000
+    logits = (torch.randn(B, V, device=DEV) * 3).to(dtype)
+    temp = torch.tensor([0.0, 0.3, 1.0, 0.0, 0.7, 2.0], device=DEV)
+    seeds = torch.arange(B, device=DEV) * 7 + 1
+    pos = torch.arange(B, device=DEV) + 100
+    tok = ops.sample(logits, temp, seeds, pos).cpu()
+    tok_r = ref.sample(logits.cpu().float(), temp.cpu(), seeds.cpu(), pos.cpu())
+    for r in range(B):
+        if tok[r] != tok_r[r]:
+            # accept fp32-vs-fp64 near-ties only
+            x = logits[r].double().cpu()
+            t = float(temp[r])
+            if t > 0:
+                x = x / t + ref.gumbel_noise_ref(int(seeds[r]), int(pos[r]), V)
+            assert abs(float(x[tok[r]] - x[tok_r[r]])) < 1e-3
+    assert tok[0] == int(torch.argmax(logits[0].float()))
+    # deterministic replay
+    assert torch.equal(ops.sample(logits, temp, seeds, pos).cpu(), tok)

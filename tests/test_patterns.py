@@ -1,0 +1,150 @@
+"""Pattern schema / compiler / DFA / scorer (CPU tier)."""
+import re
+
+import numpy as np
+import pytest
+
+from operator_amd.engine.match import MatchEngine
+from operator_amd.ops import patterns as native_patterns
+from operator_amd.patterns import oracle
+from operator_amd.patterns.compiler import compile_patterns, required_cover
+from operator_amd.patterns.schema import PatternError, PatternSet
+from operator_amd.patterns.synth import LogFactory, catalog_library, library_yaml, synthetic_library
+
+
+def _dfa_scan(d, text: bytes):
+    """Python walk of the native DFA table (what ac_scan does on the device)."""
+    C = 1 << d["log2_classes"]
+    tab = np.frombuffer(d["table"], dtype=np.uint16).reshape(-1, C)
+    cls = np.frombuffer(d["cls_map"], dtype=np.uint8)
+    off = np.frombuffer(d["out_off"], dtype=np.uint32)
+    ids = np.frombuffer(d["out_ids"], dtype=np.uint32)
+    s = 0
+    out = []
+    for i, b in enumerate(text):
+        e = int(tab[s, cls[b]])
+        s = e & 0x7FFF
+        if e & 0x8000:
+            for k in range(off[s], off[s + 1]):
+                out.append((i, int(ids[k])))
+    return out
+
+
+def test_dfa_matches_naive_find():
+    facs = [b"he", b"she", b"his", b"hers", b"connection refused", b"refused", b"a"]
+    d = native_patterns().compile_dfa(facs)
+    text = b"ushers Connection REFUSED: a his"
+    got = sorted(_dfa_scan(d, text))
+    want = []
+    low = text.lower()
+    for fi, f in enumerate(facs):
+        i = low.find(f)
+        while i >= 0:
+            want.append((i + len(f) - 1, fi))
+            i = low.find(f, i + 1)
+    assert got == sorted(want)
+    # BFS numbering: depth is non-decreasing
+    assert d["depth"] == sorted(d["depth"])
+
+
+def test_dfa_rejects_bad_factors():
+    P = native_patterns()
+    with pytest.raises(ValueError):
+        P.compile_dfa([b"a\nb"])
+    with pytest.raises(ValueError):
+        P.compile_dfa([b""])
+    with pytest.raises(ValueError):
+        P.compile_dfa([b"x" * 65])
+
+
+def test_nul_resets_dfa():
+    d = native_patterns().compile_dfa([b"abcd"])
+    assert _dfa_scan(d, b"ab\0cd") == []
+    assert _dfa_scan(d, b"ab\0abcd") == [(6, 0)]
+
+
+def test_required_cover():
+    assert required_cover(rb"java\.lang\.OutOfMemoryError: (a|b)") == [b"java.lang.OutOfMemoryError: "]
+    assert sorted(required_cover(rb"foo bar|baz qux")) == [b"baz qux", b"foo bar"]
+    assert required_cover(rb"a.b") is None
+    assert required_cover(rb"(abc)+def") in ([b"abc"], [b"def"])
+
+
+def test_schema_validation():
+    with pytest.raises(PatternError):
+        PatternSet.from_dicts([{"id": "x", "severity": "BAD", "primary_pattern": {"literal": "a"}}])
+    with pytest.raises(PatternError):
+        PatternSet.from_dicts([{"id": "x", "primary_pattern": {"literal": "a", "regex": "b"}}])
+    with pytest.raises(PatternError):
+        PatternSet.from_dicts([{"id": "x", "primary_pattern": {"regex": "("}}])
+    ps = PatternSet.from_dicts([{"id": "x", "primaryPattern": {"literal": "boom", "confidence": 0.7},
+                                 "secondaryPatterns": [{"literal": "bang", "weight": 0.2, "proximityWindow": 3}]}])
+    assert ps.patterns[0].secondary[0].window == 3
+    ys = PatternSet.from_yaml_text(library_yaml(20))
+    assert len(ys) == 20 and ys.libraries == ["synthetic"]
+
+
+def test_load_dir_enabled_filter(tmp_path):
+    (tmp_path / "a").mkdir()
+    (tmp_path / "a" / "one.yaml").write_text(library_yaml(3, library_id="one"))
+    (tmp_path / "two.yml").write_text(library_yaml(4, seed=1, library_id="two"))
+    assert len(PatternSet.load_dir(tmp_path)) == 7
+    assert len(PatternSet.load_dir(tmp_path, enabled=["two"])) == 4
+
+
+def _compare_engine_to_oracle(eng, docs):
+    cp = eng.cp
+    evs, _ = eng.events(docs)
+    ref = oracle.analyze_docs(cp, docs)
+    assert len(evs) == len(ref)
+    for a, b in zip(evs, ref):
+        assert [(e.pattern, e.line) for e in a] == [(e.pattern, e.line) for e in b]
+        assert np.allclose([e.score for e in a], [e.score for e in b])
+
+
+def test_cpu_engine_matches_oracle_catalog():
+    ps = catalog_library()
+    fac = LogFactory(n_patterns=len(ps), seed=3, pool_lines=256)
+    docs, truth = fac.batch(6, 6000, n_failures=4)
+    docs.append(b"")
+    docs.append(b"no newline at end: Connection refused")
+    eng = MatchEngine(ps, device="cpu")
+    _compare_engine_to_oracle(eng, docs)
+    res = eng.analyze(docs)
+    for r, t in zip(res, truth):
+        found = {e.matched_pattern.id for e in r.events}
+        for pid in t:
+            assert pid in found, (pid, found)
+    assert res[-2].summary.highest_severity is None and res[-2].summary.total_events == 0
+    assert res[-1].events[0].matched_pattern.id == "conn-refused"
+    assert res[-1].events[0].line_number == 1
+
+
+def test_native_scorer_equals_python_scorer():
+    ps = synthetic_library(120, seed=5)
+    fac = LogFactory(n_patterns=120, seed=5, pool_lines=256)
+    docs, _ = fac.batch(5, 20000, n_failures=8)
+    a = MatchEngine(ps, device="cpu", use_native_scorer=True)
+    b = MatchEngine(ps, device="cpu", use_native_scorer=False)
+    ea, _ = a.events(docs)
+    eb, _ = b.events(docs)
+    assert [[(e.pattern, e.line, round(e.score, 12)) for e in d] for d in ea] == \
+           [[(e.pattern, e.line, round(e.score, 12)) for e in d] for d in eb]
+
+
+def test_scoring_proximity():
+    ps = PatternSet.from_dicts([{
+        "id": "p", "severity": "HIGH", "primary_pattern": {"literal": "boom", "confidence": 0.8},
+        "secondary_patterns": [{"literal": "bang", "weight": 1.0, "proximity_window": 3}]}])
+    cp = compile_patterns(ps)
+    doc = b"boom\nx\nbang\nx\nx\nx\nx\nx\nboom\n"
+    ev = oracle.score_doc(cp, oracle.doc_hits(cp, doc))
+    # line 0: bang at distance 2 -> bonus 1*(1-2/4)=0.5 -> 0.8*1.5/2 = 0.6 ; line 8: distance 6 > 3 -> 0.4
+    assert [(e.line, round(e.score, 6)) for e in ev] == [(0, 0.6), (8, 0.4)]
+
+
+def test_case_sensitive_literal_is_verified():
+    ps = PatternSet.from_dicts([{"id": "cs", "primary_pattern": {"literal": "FATAL", "ignore_case": False}}])
+    eng = MatchEngine(ps, device="cpu")
+    evs, _ = eng.events([b"fatal\nFATAL\nFaTaL"])
+    assert [e.line for e in evs[0]] == [1]
