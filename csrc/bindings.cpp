@@ -148,7 +148,8 @@ void attn_prefill(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
 }
 
 void sample(const at::Tensor& logits, const at::Tensor& temperature, const at::Tensor& seeds,
-            const at::Tensor& positions, at::Tensor& out) {
+            const at::Tensor& positions, at::Tensor& out, int64_t col_offset,
+            const c10::optional<at::Tensor>& out_val) {
   CHECK_DEV(logits);
   TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits must be [rows, vocab] row-major");
   TORCH_CHECK(logits.scalar_type() == at::kFloat || logits.scalar_type() == at::kBFloat16, "logits dtype");
@@ -156,10 +157,14 @@ void sample(const at::Tensor& logits, const at::Tensor& temperature, const at::T
   CHECK_DT(temperature, at::kFloat); CHECK_DT(seeds, at::kLong); CHECK_DT(positions, at::kLong); CHECK_DT(out, at::kLong);
   TORCH_CHECK(temperature.numel() == rows && seeds.numel() == rows && positions.numel() == rows && out.numel() == rows,
               "sampler per-row tensor shape");
+  if (out_val.has_value()) {
+    CHECK_DT(*out_val, at::kFloat);
+    TORCH_CHECK(out_val->numel() == rows, "out_val shape");
+  }
   const c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
   RC(oamd::sample_tokens(logits.data_ptr(), logits.scalar_type() == at::kBFloat16, logits.stride(0), (int)rows,
                          (int)logits.size(1), ptr<float>(temperature), ptr<int64_t>(seeds), ptr<int64_t>(positions),
-                         ptr<int64_t>(out), cur_stream()));
+                         ptr<int64_t>(out), col_offset, optr<float>(out_val), cur_stream()));
 }
 
 }  // namespace
@@ -174,7 +179,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("rope_kv", &rope_kv);
   m.def("attn_decode", &attn_decode);
   m.def("attn_prefill", &attn_prefill);
-  m.def("sample", &sample);
+  m.def("sample", &sample, pybind11::arg("logits"), pybind11::arg("temperature"), pybind11::arg("seeds"),
+        pybind11::arg("positions"), pybind11::arg("out"), pybind11::arg("col_offset") = 0,
+        pybind11::arg("out_val") = pybind11::none());
   register_scan_bindings(m);
   m.attr("ARCH") = "gfx950";
 }

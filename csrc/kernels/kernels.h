@@ -29,6 +29,6 @@ int attn_prefill(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, c
                  float scale, hipStream_t stream);
 int sample_tokens(const void* logits, bool logits_bf16, int64_t stride, int rows, int vocab,
                   const float* temperature, const int64_t* seeds, const int64_t* positions,
-                  int64_t* out_tokens, hipStream_t stream);
+                  int64_t* out_tokens, int64_t col_offset, float* out_val, hipStream_t stream);
 
 }  // namespace oamd

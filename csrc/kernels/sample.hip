@@ -1,5 +1,6 @@
-// Token sampler: temperature + Gumbel-max over the full
-// vocabulary, greedy when temperature <= 0. One 1024-thread block per row;
+// Token sampler: temperature + Gumbel-max over the
+// vocabulary (or one tensor-parallel vocab shard: col_offset + out_val let the
+// caller take the max over shards, Gumbel-max being decomposable), greedy when temperature <= 0. One 1024-thread block per row;
 // each thread keeps a (value, index) pair over a grid-stride of the vocab with
 // 16-B loads, then a wave + LDS argmax. The noise is a counter-based hash of
 // (seed[row], position[row], column), so a captured hipGraph replays to the
@@ -25,7 +26,8 @@ __global__ void __launch_bounds__(1024) sample_kernel(const T* __restrict__ logi
                                                       const float* __restrict__ temperature,
                                                       const int64_t* __restrict__ seeds,
                                                       const int64_t* __restrict__ positions,
-                                                      int64_t* __restrict__ out_tokens) {
+                                                      int64_t* __restrict__ out_tokens, int64_t col_offset,
+                                                      float* __restrict__ out_val) {
   __shared__ float sv[16];
   __shared__ int si[16];
   const int row = blockIdx.x;
@@ -40,7 +42,7 @@ __global__ void __launch_bounds__(1024) sample_kernel(const T* __restrict__ logi
   for (int i = threadIdx.x; i < vocab; i += blockDim.x) {
     float x = load_logit<T>(lr, i);
     if (!greedy) {
-      const float u = uniform01(key + static_cast<uint64_t>(i));
+      const float u = uniform01(key + static_cast<uint64_t>(i + col_offset));
       x = x * inv_t - __logf(-__logf(u));
     }
     argmax_merge(bv, bi, x, i);
@@ -58,20 +60,21 @@ __global__ void __launch_bounds__(1024) sample_kernel(const T* __restrict__ logi
     float v = sv[0];
     int id = si[0];
     for (int j = 1; j < (int)(blockDim.x >> 6); ++j) argmax_merge(v, id, sv[j], si[j]);
-    out_tokens[row] = (id == 0x7fffffff) ? 0 : id;
+    out_tokens[row] = ((id == 0x7fffffff) ? 0 : id) + col_offset;
+    if (out_val) out_val[row] = v;
   }
 }
 
 int sample_tokens(const void* logits, bool logits_bf16, int64_t stride, int rows, int vocab,
                   const float* temperature, const int64_t* seeds, const int64_t* positions,
-                  int64_t* out_tokens, hipStream_t stream) {
+                  int64_t* out_tokens, int64_t col_offset, float* out_val, hipStream_t stream) {
   if (rows == 0) return 0;
   if (logits_bf16)
     sample_kernel<bf16_t><<<rows, 1024, 0, stream>>>(static_cast<const bf16_t*>(logits), stride, vocab,
-                                                     temperature, seeds, positions, out_tokens);
+                                                     temperature, seeds, positions, out_tokens, col_offset, out_val);
   else
     sample_kernel<float><<<rows, 1024, 0, stream>>>(static_cast<const float*>(logits), stride, vocab,
-                                                    temperature, seeds, positions, out_tokens);
+                                                    temperature, seeds, positions, out_tokens, col_offset, out_val);
   OAMD_LAUNCH_CHECK();
   return 0;
 }

@@ -1,0 +1,226 @@
+"""Llama-architecture explanation model on the gfx950 kernels.
+
+This is the on-node replacement for the reference's external LLM hop
+(ai-interface -> provider, J/service/AIInterfaceClient.java:45-59 and
+AIInterfaceRestClient.java:37-39). Per layer:
+
+    x   = rmsnorm(h)                          HIP  (fused residual add)
+    qkv = x @ Wqkv^T                          GEMM (fused QKV projection)
+    q,k,v = rope_kv(qkv) -> paged KV write    HIP  (fused RoPE + cache scatter)
+    o   = attn(q, K, V)                       HIP  (MFMA flash prefill | split-KV paged decode)
+    a   = o @ Wo^T        [TP: all-reduce]    GEMM
+    x   = rmsnorm(a + h)                      HIP
+    gu  = x @ Wgu^T                           GEMM (fused gate|up)
+    m   = silu(g) * u                         HIP
+    d   = m @ Wd^T        [TP: all-reduce]    GEMM
+logits = rmsnorm(h) @ Wlm^T (vocab-parallel under TP); tokens = Gumbel-max
+sampler on each vocab shard + a max over shards.
+
+Tensor parallelism is Megatron-style: QKV and gate|up column-parallel (whole
+heads / whole FFN columns per rank), O and down row-parallel followed by one
+all-reduce each (2 per layer), embeddings replicated (2.1 GB at 70B, fits the
+288 GB HBM trivially), lm_head vocab-parallel.
+Plain GEMMs go to hipBLASLt through torch (F.linear); everything else is a
+hand-written HIP kernel (operator_amd.ops).
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import math
+import os
+from dataclasses import dataclass, field
+
+import torch
+import torch.nn.functional as F
+
+from operator_amd import ops
+from operator_amd.ops import reference as ref
+from operator_amd.parallel.comm import Group
+
+from .config import LlamaConfig
+from .kv_cache import PagedKVCache
+
+
+@dataclass
+class ForwardBatch:
+    """Flattened tokens of one engine step (prefill or decode, never mixed)."""
+    input_ids: torch.Tensor            # [T] int64
+    positions: torch.Tensor            # [T] int64
+    slots: torch.Tensor                # [T] int64 (cache slot, -1 = do not write)
+    is_prefill: bool
+    logits_index: torch.Tensor | None  # [n_out] int64 rows to produce logits for (None = all)
+    # prefill
+    seq_lens: list[int] = field(default_factory=list)
+    prefill_work: tuple | None = None
+    # decode
+    block_tables: torch.Tensor | None = None   # [B, max_pages] int32
+    context_lens: torch.Tensor | None = None   # [B] int32 (including the new token)
+    num_splits: int = 1
+
+
+@dataclass
+class LayerWeights:
+    wqkv: torch.Tensor
+    wo: torch.Tensor
+    wgu: torch.Tensor
+    wd: torch.Tensor
+    attn_norm: torch.Tensor
+    mlp_norm: torch.Tensor
+
+
+def _seed_for(seed: int, name: str) -> int:
+    return int.from_bytes(hashlib.sha256(f"{seed}:{name}".encode()).digest()[:8], "little") & ((1 << 63) - 1)
+
+
+class LlamaModel:
+    def __init__(self, cfg: LlamaConfig, device: str | torch.device = "cuda", tp: Group | None = None,
+                 dtype: torch.dtype = torch.bfloat16):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.tp = tp or Group.single()
+        self.dtype = dtype
+        W = self.tp.world
+        if cfg.heads % W or cfg.kv_heads % W or cfg.intermediate % W or cfg.vocab_size % W:
+            raise ValueError(f"{cfg.name}: heads/kv_heads/intermediate/vocab must divide by tp={W}")
+        self.hq = cfg.heads // W
+        self.hkv = cfg.kv_heads // W
+        self.inter = cfg.intermediate // W
+        self.vocab_local = cfg.vocab_size // W
+        self.vocab_offset = self.tp.rank * self.vocab_local
+        self.scale = 1.0 / math.sqrt(cfg.head_dim)
+        cos, sin = ref.rope_tables(cfg.max_position, cfg.head_dim, cfg.rope_theta, cfg.rope_scaling)
+        self.cos, self.sin = cos.to(self.device), sin.to(self.device)
+        self.layers: list[LayerWeights] = []
+        self.embed = self.final_norm = self.lm_head = None
+
+    # ------------------------------------------------------------------ weights
+    def _randn(self, seed: int, name: str, shape, std: float) -> torch.Tensor:
+        g = torch.Generator(device=self.device)
+        g.manual_seed(_seed_for(seed, name))
+        t = torch.randn(shape, generator=g, device=self.device, dtype=self.dtype)
+        return t.mul_(std)
+
+    def init_random(self, seed: int = 0) -> "LlamaModel":
+        """Random weights of the exact architecture. Each full tensor is generated from a
+        name-derived seed and then sharded, so every TP degree sees the same global model."""
+        c, r = self.cfg, self.tp.rank
+        D, H = c.head_dim, c.hidden
+        std_in = 1.0 / math.sqrt(H)
+        self.embed = self._randn(seed, "embed", (c.vocab_size, H), 1.0)
+        self.layers = []
+        for i in range(c.layers):
+            wq = self._randn(seed, f"l{i}.wq", (c.heads * D, H), std_in)
+            wk = self._randn(seed, f"l{i}.wk", (c.kv_heads * D, H), std_in)
+            wv = self._randn(seed, f"l{i}.wv", (c.kv_heads * D, H), std_in)
+            wo = self._randn(seed, f"l{i}.wo", (H, c.heads * D), 1.0 / math.sqrt(c.heads * D))
+            wg = self._randn(seed, f"l{i}.wg", (c.intermediate, H), std_in)
+            wu = self._randn(seed, f"l{i}.wu", (c.intermediate, H), std_in)
+            wd = self._randn(seed, f"l{i}.wd", (H, c.intermediate), 1.0 / math.sqrt(c.intermediate))
+            self.layers.append(self._shard_layer(wq, wk, wv, wo, wg, wu, wd,
+                                                 torch.ones(H, dtype=self.dtype, device=self.device),
+                                                 torch.ones(H, dtype=self.dtype, device=self.device)))
+            del wq, wk, wv, wo, wg, wu, wd
+        self.final_norm = torch.ones(H, dtype=self.dtype, device=self.device)
+        lm = self.embed if c.tie_embeddings else self._randn(seed, "lm_head", (c.vocab_size, H), std_in)
+        self.lm_head = lm[r * self.vocab_local:(r + 1) * self.vocab_local].contiguous()
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        return self
+
+    def _shard_layer(self, wq, wk, wv, wo, wg, wu, wd, an, mn) -> LayerWeights:
+        r, D = self.tp.rank, self.cfg.head_dim
+        q = wq[r * self.hq * D:(r + 1) * self.hq * D]
+        k = wk[r * self.hkv * D:(r + 1) * self.hkv * D]
+        v = wv[r * self.hkv * D:(r + 1) * self.hkv * D]
+        g = wg[r * self.inter:(r + 1) * self.inter]
+        u = wu[r * self.inter:(r + 1) * self.inter]
+        return LayerWeights(
+            wqkv=torch.cat([q, k, v], 0).contiguous(),
+            wo=wo[:, r * self.hq * D:(r + 1) * self.hq * D].contiguous(),
+            wgu=torch.cat([g, u], 0).contiguous(),
+            wd=wd[:, r * self.inter:(r + 1) * self.inter].contiguous(),
+            attn_norm=an.contiguous(), mlp_norm=mn.contiguous())
+
+    def load_hf(self, path: str) -> "LlamaModel":
+        """Load a HuggingFace Llama checkpoint directory (safetensors) and shard it."""
+        from safetensors import safe_open
+
+        files = sorted(f for f in os.listdir(path) if f.endswith(".safetensors"))
+        if not files:
+            raise FileNotFoundError(f"no *.safetensors in {path}")
+        tensors: dict[str, str] = {}
+        for f in files:
+            with safe_open(os.path.join(path, f), framework="pt") as sf:
+                for k in sf.keys():
+                    tensors[k] = f
+
+        def get(name):
+            with safe_open(os.path.join(path, tensors[name]), framework="pt", device="cpu") as sf:
+                return sf.get_tensor(name).to(self.device, self.dtype)
+
+        c, r = self.cfg, self.tp.rank
+        self.embed = get("model.embed_tokens.weight")
+        self.layers = []
+        for i in range(c.layers):
+            p = f"model.layers.{i}."
+            self.layers.append(self._shard_layer(
+                get(p + "self_attn.q_proj.weight"), get(p + "self_attn.k_proj.weight"),
+                get(p + "self_attn.v_proj.weight"), get(p + "self_attn.o_proj.weight"),
+                get(p + "mlp.gate_proj.weight"), get(p + "mlp.up_proj.weight"), get(p + "mlp.down_proj.weight"),
+                get(p + "input_layernorm.weight"), get(p + "post_attention_layernorm.weight")))
+        self.final_norm = get("model.norm.weight")
+        lm = get("lm_head.weight") if "lm_head.weight" in tensors else self.embed
+        self.lm_head = lm[r * self.vocab_local:(r + 1) * self.vocab_local].contiguous()
+        return self
+
+    def weight_bytes(self) -> int:
+        n = self.embed.numel() + self.final_norm.numel() + self.lm_head.numel()
+        for lw in self.layers:
+            n += sum(t.numel() for t in (lw.wqkv, lw.wo, lw.wgu, lw.wd, lw.attn_norm, lw.mlp_norm))
+        return n * self.embed.element_size()
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, fb: ForwardBatch, kv: PagedKVCache) -> torch.Tensor:
+        """Run all layers; returns logits [n_out, vocab_local] for fb.logits_index rows."""
+        c = self.cfg
+        h = ops.embedding(fb.input_ids, self.embed)          # residual stream [T, H]
+        x = ops.rmsnorm(h, self.layers[0].attn_norm, c.rms_eps)
+        T = h.shape[0]
+        for i, lw in enumerate(self.layers):
+            kc, vc = kv.layer(i)
+            qkv = F.linear(x, lw.wqkv)
+            q, k, v = ops.rope_kv(qkv, fb.positions, self.cos, self.sin, self.hq, self.hkv, kc, vc, fb.slots,
+                                  want_kv=fb.is_prefill)
+            if fb.is_prefill:
+                o = ops.attn_prefill(q, k, v, fb.seq_lens, self.scale, work=fb.prefill_work)
+            else:
+                o = ops.attn_decode(q, kc, vc, fb.block_tables, fb.context_lens, self.scale, fb.num_splits)
+            a = F.linear(o.view(T, self.hq * c.head_dim), lw.wo)
+            self.tp.all_reduce_(a)
+            x = ops.rmsnorm(a, lw.mlp_norm, c.rms_eps, residual=h)
+            gu = F.linear(x, lw.wgu)
+            m = ops.silu_mul(gu)
+            d = F.linear(m, lw.wd)
+            self.tp.all_reduce_(d)
+            nw = self.layers[i + 1].attn_norm if i + 1 < len(self.layers) else self.final_norm
+            x = ops.rmsnorm(d, nw, c.rms_eps, residual=h)
+        if fb.logits_index is not None:
+            x = x.index_select(0, fb.logits_index)
+        return F.linear(x, self.lm_head)
+
+    def sample(self, logits: torch.Tensor, temperature: torch.Tensor, seeds: torch.Tensor,
+               positions: torch.Tensor) -> torch.Tensor:
+        """Sample one token per row; under TP each rank samples its vocab shard and the
+        global winner is the max perturbed value (ties -> smaller token id)."""
+        if self.tp.world == 1:
+            return ops.sample(logits, temperature, seeds, positions)
+        n = logits.shape[0]
+        val = torch.empty(n, dtype=torch.float32, device=logits.device)
+        tok = ops.sample(logits, temperature, seeds, positions, col_offset=self.vocab_offset, out_val=val)
+        pair = torch.stack([val, tok.to(torch.float32)], 1)             # exact for ids < 2^24
+        allp = self.tp.all_gather_into(pair)                             # [W, n, 2]
+        vals, toks = allp[..., 0], allp[..., 1]
+        best = vals.max(0).values
+        cand = torch.where(vals == best.unsqueeze(0), toks, torch.full_like(toks, float("inf")))
+        return cand.min(0).values.to(torch.long)

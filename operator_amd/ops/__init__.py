@@ -141,14 +141,20 @@ def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, b
 
 
 def sample(logits: torch.Tensor, temperature: torch.Tensor, seeds: torch.Tensor, positions: torch.Tensor,
-           out: torch.Tensor | None = None) -> torch.Tensor:
-    """Temperature / Gumbel-max sampling (greedy rows where temperature <= 0)."""
+           out: torch.Tensor | None = None, col_offset: int = 0, out_val: torch.Tensor | None = None) -> torch.Tensor:
+    """Temperature / Gumbel-max sampling (greedy rows where temperature <= 0).
+
+    For a vocab shard pass ``col_offset`` (global id of column 0) and ``out_val``
+    (receives each row's winning perturbed value) and take the max over shards.
+    """
     if not logits.is_cuda:
-        r = reference.sample(logits, temperature, seeds, positions)
+        tok, val = reference.sample_shard(logits, temperature, seeds, positions, col_offset)
+        if out_val is not None:
+            out_val.copy_(val)
         if out is not None:
-            out.copy_(r)
+            out.copy_(tok)
             return out
-        return r
+        return tok
     o = out if out is not None else torch.empty(logits.shape[0], dtype=torch.long, device=logits.device)
-    kernels().sample(logits, temperature, seeds, positions, o)
+    kernels().sample(logits, temperature, seeds, positions, o, col_offset, out_val)
     return o

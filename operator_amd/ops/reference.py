@@ -136,32 +136,43 @@ def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, b
     return out
 
 
-def gumbel_noise_ref(seed: int, position: int, vocab: int) -> torch.Tensor:
-    """Host mirror of the device counter hash (common.h hash_u32/uniform01)."""
+def gumbel_noise_ref(seed: int, position: int, vocab: int, col_offset: int = 0) -> torch.Tensor:
+    """Host mirror of the device counter hash (common.h hash_u32/uniform01), vectorised."""
+    import numpy as np
+
     M = (1 << 64) - 1
     key = ((seed * 0x9E3779B97F4A7C15) & M) ^ ((position << 32) & M)
-    xs = [(key + i) & M for i in range(vocab)]
-    out = []
-    for x in xs:
-        x ^= x >> 33
-        x = (x * 0xFF51AFD7ED558CCD) & M
-        x ^= x >> 33
-        x = (x * 0xC4CEB9FE1A85EC53) & M
-        x ^= x >> 33
-        u = ((x & 0xFFFFFFFF) >> 8) + 0.5
-        out.append(u / 16777216.0)
-    u = torch.tensor(out, dtype=torch.float64)
+    with np.errstate(over="ignore"):
+        x = (np.arange(vocab, dtype=np.uint64) + np.uint64((key + col_offset) & M))
+        x ^= x >> np.uint64(33)
+        x *= np.uint64(0xFF51AFD7ED558CCD)
+        x ^= x >> np.uint64(33)
+        x *= np.uint64(0xC4CEB9FE1A85EC53)
+        x ^= x >> np.uint64(33)
+    u = ((x & np.uint64(0xFFFFFFFF)) >> np.uint64(8)).astype(np.float64) + 0.5
+    u = torch.from_numpy(u / 16777216.0)
     return -torch.log(-torch.log(u))
 
 
-def sample(logits: torch.Tensor, temperature: torch.Tensor, seeds: torch.Tensor,
-           positions: torch.Tensor) -> torch.Tensor:
-    """Greedy when T<=0 else Gumbel-max with the same counter hash as the kernel."""
+def sample_shard(logits: torch.Tensor, temperature: torch.Tensor, seeds: torch.Tensor, positions: torch.Tensor,
+                 col_offset: int = 0) -> tuple[torch.Tensor, torch.Tensor]:
+    """Greedy when T<=0 else Gumbel-max with the same counter hash as the kernel.
+
+    Returns (global token ids, winning perturbed values) for a vocab shard.
+    """
     out = torch.empty(logits.shape[0], dtype=torch.long)
+    val = torch.empty(logits.shape[0], dtype=torch.float32)
     for r in range(logits.shape[0]):
         x = logits[r].double().cpu()
         t = float(temperature[r])
         if t > 0:
-            x = x / t + gumbel_noise_ref(int(seeds[r]), int(positions[r]), x.numel())
-        out[r] = int(torch.argmax(x))
-    return out.to(logits.device)
+            x = x / t + gumbel_noise_ref(int(seeds[r]), int(positions[r]), x.numel(), col_offset)
+        i = int(torch.argmax(x))
+        out[r] = i + col_offset
+        val[r] = float(x[i])
+    return out.to(logits.device), val.to(logits.device)
+
+
+def sample(logits: torch.Tensor, temperature: torch.Tensor, seeds: torch.Tensor,
+           positions: torch.Tensor) -> torch.Tensor:
+    return sample_shard(logits, temperature, seeds, positions)[0]

@@ -1,0 +1,124 @@
+"""Collective layer over torch.distributed (backend "nccl" == RCCL on ROCm,
+"gloo" for the CPU test tier). SURVEY.md §2.4 X1 / §5.8.
+
+* ``init_from_env()`` — torchrun-style env:// rendezvous (RANK, WORLD_SIZE,
+  LOCAL_RANK, MASTER_ADDR=127.0.0.1), one process per GPU.
+* ``Group`` — a thin handle used by the model: rank/world, in-place
+  all-reduce, all-gather, broadcast; a world-1 group is a no-op so the same
+  model code runs TP=1 without any communication.
+* ``split_groups(tp)`` — carve the world into DP replicas of TP groups
+  (TP ranks are consecutive = same xGMI-fully-connected node).
+
+Sizing notes for MI355X xGMI (7 point-to-point links / GPU, ~153 GB/s each):
+TP decode all-reduces are tiny (M x hidden x 2 B, e.g. 16 KB/token at 70B),
+i.e. latency-bound; RCCL's LL/LL128 protocols cover them. DP needs no
+collective on the hot path (per-rank engines, host-side result gathering).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistInfo:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    backend: str = "none"
+
+
+def init_from_env(backend: str | None = None, timeout_s: int = 600) -> DistInfo:
+    """Initialise the default process group from torchrun env vars (no-op when WORLD_SIZE<=1)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if world <= 1:
+        return DistInfo(0, 1, 0, "none")
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29500")
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend == "nccl":
+        torch.cuda.set_device(local)
+    if not dist.is_initialized():
+        kw = {}
+        if backend == "nccl":
+            kw["device_id"] = torch.device("cuda", local)
+        dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    return DistInfo(rank, world, local, backend)
+
+
+class Group:
+    """Process-group handle; world==1 makes every collective a no-op."""
+
+    def __init__(self, pg=None, ranks: list[int] | None = None):
+        self.pg = pg
+        if pg is None and not (dist.is_available() and dist.is_initialized()):
+            self.rank, self.world, self.ranks = 0, 1, [0]
+        else:
+            self.rank = dist.get_rank(pg)
+            self.world = dist.get_world_size(pg)
+            self.ranks = ranks if ranks is not None else list(range(self.world))
+
+    @staticmethod
+    def single() -> "Group":
+        g = Group.__new__(Group)
+        g.pg, g.rank, g.world, g.ranks = None, 0, 1, [0]
+        return g
+
+    def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
+        if self.world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.pg)
+        return t
+
+    def all_gather(self, t: torch.Tensor, dim: int = 0) -> torch.Tensor:
+        if self.world == 1:
+            return t
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(out, t.contiguous(), group=self.pg)
+        return torch.cat(out, dim=dim)
+
+    def all_gather_into(self, t: torch.Tensor) -> torch.Tensor:
+        """Gather equal-shaped tensors along a new leading dim: [world, *t.shape]."""
+        if self.world == 1:
+            return t.unsqueeze(0)
+        out = torch.empty((self.world, *t.shape), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t.contiguous(), group=self.pg)
+        return out
+
+    def broadcast_(self, t: torch.Tensor, src_local: int = 0) -> torch.Tensor:
+        if self.world > 1:
+            dist.broadcast(t, src=self.ranks[src_local], group=self.pg)
+        return t
+
+    def barrier(self) -> None:
+        if self.world > 1:
+            dist.barrier(group=self.pg)
+
+
+def split_groups(tp: int) -> tuple[Group, Group]:
+    """Return (tp_group, dp_group) for this rank. World must be a multiple of tp."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return Group.single(), Group.single()
+    world, rank = dist.get_world_size(), dist.get_rank()
+    if world % tp:
+        raise ValueError(f"world {world} not divisible by tp {tp}")
+    tp_g = dp_g = None
+    tp_ranks = dp_ranks = None
+    for i in range(world // tp):
+        ranks = list(range(i * tp, (i + 1) * tp))
+        g = dist.new_group(ranks)
+        if rank in ranks:
+            tp_g, tp_ranks = g, ranks
+    for j in range(tp):
+        ranks = list(range(j, world, tp))
+        g = dist.new_group(ranks)
+        if rank in ranks:
+            dp_g, dp_ranks = g, ranks
+    return Group(tp_g, tp_ranks), Group(dp_g, dp_ranks)
