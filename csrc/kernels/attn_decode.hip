@@ -1,28 +1,37 @@
 // Paged decode attention, split-KV ("flash-decoding"), GQA.
 //
 // One query token per sequence. Workgroup = (split of 256 cached tokens,
-// kv-head, sequence); the G = Hq/Hkv query heads that share the kv-head are
-// processed together so each K/V row is read from HBM once for all of them.
-// With G <= 8 query rows per kv head this is a streaming, memory-bound op, so
-// K/V go straight to VGPRs with 16-B loads (cdna_hip_programming.md App. B
-// "Attention decode": GEMV-like, no LDS round trip for the stream) and the
-// dot products run on the VALU; the VALU budget per token (~40 SIMD cycles
-// for G = 4) is well under the ~200 SIMD cycles per 512 B of K+V that the
-// HBM rate allows per CU.
-//
-// Two phases per split, so there is no online-softmax rescaling at all:
-//   1. s[h][t] = q_h . k_t for all tokens of the split -> LDS (4 KB at G = 4)
-//   2. block max/sum per head, p = exp2(s - m), o_h = sum_t p[h][t] v_t
-// Lane mapping (both phases): token sub-slot = lane >> 4 (4 tokens per wave
-// step), dims 8*(lane & 15) .. +8 (one 16-B load per lane per token).
-// KV cache layout: [pages, Hkv, page_size, D] bf16 (a kv-head's tokens of one
-// page are contiguous: 4 consecutive tokens = 1 KiB per wave load).
+// kv-head, sequence); the G = Hq/Hkv query heads sharing the kv-head are
+// processed together so every K/V row is read from HBM exactly once.
+// This op is HBM-bound (B x ctx x Hkv x 512 B per layer), so the structure is
+// built around bytes in flight, not arithmetic:
+//   * every lane issues ALL of its K loads (16 x 16 B) and V loads (16 x 16 B)
+//     at kernel entry — 64 KiB of K+V per workgroup in flight — and the
+//     QK^T, softmax and PV work then runs under that traffic;
+//   * S = K Q^T runs on MFMA (v_mfma_f32_16x16x32_bf16, K tile = A operand,
+//     the G query heads zero-padded to 16 columns = B operand), so no
+//     cross-lane reduction is needed for the dot products;
+//   * softmax is two-pass over the split (max, then exp2/sum) in LDS — no
+//     online rescaling; PV runs on the VALU (16 B V rows per lane, P read as
+//     one ds_read_b128 per token for G = 4) and reduces over the 4 token
+//     sub-slots with 2 xor-shuffles.
+// Fragment maps (cdna_hip_programming.md §3): A lane l -> A[l&15][8(l>>4)+j];
+// B lane l -> B[8(l>>4)+j][l&15]; C col = l&15, row = 4(l>>4)+r. The dims of a
+// k-step are permuted so lane group g covers dims 32g..32g+31 over the 4
+// k-steps (Q uses the same permutation, so the contraction is unchanged).
+// KV cache layout: [pages, Hkv, page_size, D] bf16.
 #include "common.h"
 #include "kernels.h"
 
 namespace oamd {
 
 constexpr int kSplit = 256;  // tokens per split == threads per block
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ u16x8 ld16(const bf16_t* p) {
+  return __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(p));
+}
 
 template <int G>
 __global__ void __launch_bounds__(256) attn_decode_kernel(
@@ -31,7 +40,8 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(
     bf16_t* __restrict__ out, float* __restrict__ o_part, float* __restrict__ ml_part, int Hkv,
     int page_size, int log2_page, int max_pages, int num_splits, float scale_log2) {
   constexpr int D = 128;
-  __shared__ __attribute__((aligned(16))) float sc[G * kSplit];
+  constexpr int GP = (G < 4) ? 4 : G;  // score row stride (float4-aligned)
+  __shared__ __attribute__((aligned(16))) float sc[kSplit * GP];   // [token][head]
   __shared__ __attribute__((aligned(16))) float red[4 * G * D];
   __shared__ float wred[4][G];
 
@@ -41,52 +51,71 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(
   const int start = s * kSplit;
   if (start >= len && !(num_splits == 1 && len == 0)) return;  // empty split: combine skips it
   const int n = min(len - start, kSplit);
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, sub = lane >> 4;
-  const int dl = (lane & 15) * 8;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int l15 = lane & 15, lg = lane >> 4;
   const int* bt = block_tables + (int64_t)b * max_pages;
 
-  // q for the G heads of this kv head, this lane's 8 dims, pre-scaled into log2 domain
-  float qf[G][8];
-#pragma unroll
-  for (int h = 0; h < G; ++h) {
-    const u16x8 qv = *reinterpret_cast<const u16x8*>(q + ((int64_t)b * Hq + kvh * G + h) * D + dl);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) qf[h][j] = bf2f(qv[j]) * scale_log2;
-  }
-
-  auto row_off = [&](int t) -> int64_t {
+  auto row_ptr = [&](const bf16_t* base, int t) -> const bf16_t* {
     const int tok = start + t;
     const int64_t page = bt[tok >> log2_page];
-    return ((page * Hkv + kvh) * page_size + (tok & (page_size - 1))) * (int64_t)D + dl;
+    return base + ((page * Hkv + kvh) * page_size + (tok & (page_size - 1))) * (int64_t)D;
   };
 
-  // ---- phase 1: scores ----
-#pragma unroll 4
-  for (int it = 0; it < kSplit / 16; ++it) {
-    const int t = it * 16 + w * 4 + sub;
+  // ---- issue every K and V load of this lane up front ----
+  u16x8 kf[4][4];  // [tile][kstep]: token w*64 + 16*i + l15, dims 32*lg + 8*ks
+  u16x8 vf[16];    // token w*64 + 4*it + lg, dims 8*l15
+  const u16x8 z8 = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int t = w * 64 + 16 * i + l15;
     if (t < n) {
-      const u16x8 kv = *reinterpret_cast<const u16x8*>(kc + row_off(t));
-      float kf[8];
+      const bf16_t* p = row_ptr(kc, t) + 32 * lg;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) kf[j] = bf2f(kv[j]);
+      for (int ks = 0; ks < 4; ++ks) kf[i][ks] = ld16(p + 8 * ks);
+    } else {
 #pragma unroll
-      for (int h = 0; h < G; ++h) {
-        float d = 0.f;
+      for (int ks = 0; ks < 4; ++ks) kf[i][ks] = z8;
+    }
+  }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) d += qf[h][j] * kf[j];
-        d = group_sum<16>(d);
-        if ((lane & 15) == 0) sc[h * kSplit + t] = d;
+  for (int it = 0; it < 16; ++it) {
+    const int t = w * 64 + 4 * it + lg;
+    vf[it] = (t < n) ? ld16(row_ptr(vc, t) + 8 * l15) : z8;
+  }
+
+  // ---- q as the MFMA B operand: column = head (l15 < G), same dim permutation ----
+  u16x8 qb[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    if (l15 < G)
+      qb[ks] = *reinterpret_cast<const u16x8*>(q + ((int64_t)b * Hq + kvh * G + l15) * D + 32 * lg + 8 * ks);
+    else
+      qb[ks] = z8;
+  }
+
+  // ---- S = K Q^T on MFMA, scaled scores -> LDS [token][head] ----
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, kf[i][ks]),
+                                                    __builtin_bit_cast(bf16x8_t, qb[ks]), acc, 0, 0, 0);
+    if (l15 < G) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int t = w * 64 + 16 * i + 4 * lg + r;
+        sc[t * GP + l15] = (t < n) ? acc[r] * scale_log2 : -INFINITY;
       }
     }
   }
   __syncthreads();
 
-  // ---- block softmax per head (thread tid <-> token tid) ----
+  // ---- two-pass softmax over the split: thread tid <-> token tid ----
   float mh[G], lh[G];
 #pragma unroll
   for (int h = 0; h < G; ++h) {
-    const float v = tid < n ? sc[h * kSplit + tid] : -INFINITY;
-    const float m = wave_max(v);
+    const float m = wave_max(sc[tid * GP + h]);
     if (lane == 0) wred[w][h] = m;
   }
   __syncthreads();
@@ -95,8 +124,9 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(
   __syncthreads();
 #pragma unroll
   for (int h = 0; h < G; ++h) {
-    const float p = tid < n ? exp2f(sc[h * kSplit + tid] - mh[h]) : 0.f;
-    if (tid < n) sc[h * kSplit + tid] = p;
+    const float sv = sc[tid * GP + h];
+    const float p = (tid < n) ? exp2f(sv - mh[h]) : 0.f;
+    sc[tid * GP + h] = p;
     const float ls = wave_sum(p);
     if (lane == 0) wred[w][h] = ls;
   }
@@ -104,24 +134,33 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(
 #pragma unroll
   for (int h = 0; h < G; ++h) lh[h] = wred[0][h] + wred[1][h] + wred[2][h] + wred[3][h];
 
-  // ---- phase 2: o = P V ----
+  // ---- O = P V on the VALU (V already in registers) ----
   float acc[G][8];
 #pragma unroll
   for (int h = 0; h < G; ++h)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[h][j] = 0.f;
-#pragma unroll 4
-  for (int it = 0; it < kSplit / 16; ++it) {
-    const int t = it * 16 + w * 4 + sub;
-    if (t < n) {
-      const u16x8 vv = *reinterpret_cast<const u16x8*>(vc + row_off(t));
 #pragma unroll
-      for (int h = 0; h < G; ++h) {
-        const float p = sc[h * kSplit + t];
+  for (int it = 0; it < 16; ++it) {
+    const int t = w * 64 + 4 * it + lg;
+    float p[G];
+    if constexpr (G % 4 == 0) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[h][j] += p * bf2f(vv[j]);
+      for (int h4 = 0; h4 < G; h4 += 4) {
+        const f32x4 pv = *reinterpret_cast<const f32x4*>(&sc[t * GP + h4]);
+        p[h4] = pv[0]; p[h4 + 1] = pv[1]; p[h4 + 2] = pv[2]; p[h4 + 3] = pv[3];
       }
+    } else {
+#pragma unroll
+      for (int h = 0; h < G; ++h) p[h] = sc[t * GP + h];
     }
+    float vv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) vv[j] = bf2f(vf[it][j]);
+#pragma unroll
+    for (int h = 0; h < G; ++h)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[h][j] += p[h] * vv[j];
   }
   // reduce over the 4 token sub-slots of the wave (lanes l, l^16, l^32, l^48)
 #pragma unroll
@@ -133,10 +172,10 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(
       a += __shfl_xor(a, 32, kWave);
       acc[h][j] = a;
     }
-  if (sub == 0) {
+  if (lg == 0) {
 #pragma unroll
     for (int h = 0; h < G; ++h) {
-      float* r = red + (w * G + h) * D + dl;
+      float* r = red + (w * G + h) * D + 8 * l15;
       *reinterpret_cast<f32x4*>(r) = f32x4{acc[h][0], acc[h][1], acc[h][2], acc[h][3]};
       *reinterpret_cast<f32x4*>(r + 4) = f32x4{acc[h][4], acc[h][5], acc[h][6], acc[h][7]};
     }
@@ -164,10 +203,10 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(
 // Combine the per-split partials: grid (B*Hq), block D threads.
 __global__ void attn_decode_combine_kernel(const float* __restrict__ o_part, const float* __restrict__ ml_part,
                                            const int* __restrict__ seq_lens, bf16_t* __restrict__ out, int Hq,
-                                           int num_splits) {
+                                           int num_splits, int max_tokens) {
   constexpr int D = 128;
   const int bh = blockIdx.x, b = bh / Hq, d = threadIdx.x;
-  const int len = seq_lens[b];
+  const int len = min(seq_lens[b], max_tokens);
   const int ns = min(num_splits, (len + kSplit - 1) / kSplit);
   const float* ml = ml_part + (int64_t)bh * num_splits * 2;
   float M = -INFINITY;
@@ -207,7 +246,8 @@ int attn_decode(const bf16_t* q, const bf16_t* k_cache, const bf16_t* v_cache, c
 #undef OAMD_DEC
   OAMD_LAUNCH_CHECK();
   if (num_splits > 1) {
-    attn_decode_combine_kernel<<<B * Hq, 128, 0, stream>>>(o_part, ml_part, seq_lens, out, Hq, num_splits);
+    attn_decode_combine_kernel<<<B * Hq, 128, 0, stream>>>(o_part, ml_part, seq_lens, out, Hq, num_splits,
+                                                           max_pages * page_size);
     OAMD_LAUNCH_CHECK();
   }
   return 0;

@@ -1,0 +1,193 @@
+"""Result sinks: pod annotations and the Podmortem status (recentFailures ring).
+
+Mirrors J/service/AnalysisStorageService.java:
+* annotations ``podmortem.io/{analysis,severity,analyzed-at,monitor}`` on the pod
+  (:42-46), full AI text or a pattern-only one-line summary (:145-155);
+* ``status.recentFailures`` — newest first, capped at 10 (:48, :329-333), each
+  entry {podName, podNamespace, failureTime, analysisStatus="Completed",
+  explanation} with a multi-line pattern-only fallback (:295-326);
+* every write is GET-latest -> modify -> PATCH with the fresh resourceVersion,
+  retried on 409 up to 5 times with 100 ms doubling backoff (:75-76, :179-187);
+  403 on the pod gives up immediately (:188-193).
+
+Race fix: all status writes for one Podmortem go through
+one ``StatusWriter`` lock, and the phase/message update is a merge patch of
+just those two fields on a fresh object, so it can never clobber
+``recentFailures`` (the reference patches the whole status from a stale list).
+"""
+from __future__ import annotations
+
+import logging
+import threading
+import time
+from collections import defaultdict
+from concurrent.futures import Executor
+
+from operator_amd.api.models import AnalysisResult
+from operator_amd.kube.resources import PODMORTEMS, PODS, ApiError
+from operator_amd.utils.javafmt import fmt2, is_blank, jstr
+from operator_amd.utils.timefmt import instant_str
+
+log = logging.getLogger(__name__)
+
+ANNOTATION_PREFIX = "podmortem.io/"
+ANALYSIS_ANNOTATION = ANNOTATION_PREFIX + "analysis"
+SEVERITY_ANNOTATION = ANNOTATION_PREFIX + "severity"
+TIMESTAMP_ANNOTATION = ANNOTATION_PREFIX + "analyzed-at"
+MONITOR_ANNOTATION = ANNOTATION_PREFIX + "monitor"
+MAX_RECENT_FAILURES = 10
+
+
+def pattern_annotation(result: AnalysisResult) -> str:
+    s = result.summary
+    return "Pattern Analysis: Severity=%s, SignificantEvents=%d, TotalMatches=%d" % (
+        jstr(s.highest_severity) if s is not None else "UNKNOWN",
+        s.significant_events if s is not None else 0,
+        len(result.events) if result.events is not None else 0)
+
+
+def pattern_explanation(result: AnalysisResult) -> str:
+    out = ["Pattern Analysis Results:\n", "========================\n"]
+    s = result.summary
+    if s is not None:
+        out.append(f"Highest Severity: {jstr(s.highest_severity)}\n")
+        out.append(f"Significant Events: {s.significant_events}\n")
+    if result.events:
+        out.append("\nTop Matches:\n")
+        for e in result.events[:5]:
+            if e.matched_pattern is not None:
+                out.append(f"- {jstr(e.matched_pattern.name)} (Severity: {jstr(e.matched_pattern.severity)}, "
+                           f"Score: {fmt2(e.score)})\n")
+    return "".join(out)
+
+
+class Retrier:
+    def __init__(self, max_retries: int = 5, initial_delay_s: float = 0.1, sleep=time.sleep):
+        self.max_retries, self.initial_delay_s, self.sleep = max_retries, initial_delay_s, sleep
+
+
+class StatusWriter:
+    """Single writer per Podmortem (per-key lock)."""
+
+    def __init__(self, kube, retrier: Retrier | None = None, use_finished_at: bool = False):
+        self.kube = kube
+        self.retrier = retrier or Retrier()
+        self.use_finished_at = use_finished_at
+        self._locks: dict[tuple[str, str], threading.Lock] = defaultdict(threading.Lock)
+        self._guard = threading.Lock()
+
+    def _lock(self, monitor: dict) -> threading.Lock:
+        md = monitor.get("metadata") or {}
+        with self._guard:
+            return self._locks[(md.get("namespace") or "", md.get("name") or "")]
+
+    def _with_retry(self, what: str, fn) -> bool:
+        delay = self.retrier.initial_delay_s
+        for attempt in range(self.retrier.max_retries + 1):
+            if attempt:
+                self.retrier.sleep(delay)
+                delay *= 2
+            try:
+                return fn()
+            except ApiError as e:
+                if e.code == 409 and attempt < self.retrier.max_retries:
+                    log.debug("conflict on %s, retry %d/%d", what, attempt + 1, self.retrier.max_retries)
+                    continue
+                if e.code == 403:
+                    log.warning("Forbidden to update %s - check RBAC permissions: %s", what, e)
+                else:
+                    log.warning("Failed to store %s after %d attempts: %s", what, attempt + 1, e)
+                return False
+            except Exception as e:  # noqa: BLE001
+                log.warning("Unexpected error storing %s: %s", what, e)
+                return False
+        return False
+
+    # ------------------------------------------------------------------ phase/message
+    def set_phase(self, monitor: dict, phase: str, message: str, observed_generation: bool = False) -> bool:
+        md = monitor.get("metadata") or {}
+
+        def do():
+            patch = {"phase": phase, "message": message, "lastUpdate": instant_str()}
+            if observed_generation and md.get("generation") is not None:
+                patch["observedGeneration"] = md.get("generation")
+            self.kube.patch_status(PODMORTEMS, md["name"], md.get("namespace"), patch)
+            return True
+
+        with self._lock(monitor):
+            return self._with_retry(f"Podmortem {md.get('name')} status", do)
+
+    def update_pod_failure(self, monitor: dict, pod: dict, message: str) -> bool:
+        """PodFailureWatcher.updatePodFailureStatusAsync (:452-502): phase Processing,
+        message "<msg> (Pod: <name>)"."""
+        return self.set_phase(monitor, "Processing", f"{message} (Pod: {(pod.get('metadata') or {}).get('name')})")
+
+    # ------------------------------------------------------------------ recentFailures ring
+    def append_failure(self, pod: dict, monitor: dict, result: AnalysisResult, ai_analysis: str | None) -> bool:
+        md = monitor.get("metadata") or {}
+        pmd = pod.get("metadata") or {}
+
+        def do():
+            latest = self.kube.get(PODMORTEMS, md["name"], md.get("namespace"))
+            if latest is None:
+                log.warning("Podmortem not found: %s", md.get("name"))
+                return False
+            status = dict(latest.get("status") or {})
+            recent = list(status.get("recentFailures") or [])
+            when = instant_str()
+            if self.use_finished_at:
+                for cs in (pod.get("status") or {}).get("containerStatuses") or []:
+                    t = ((cs or {}).get("state") or {}).get("terminated") or {}
+                    if t.get("finishedAt"):
+                        when = t["finishedAt"]
+                        break
+            entry = {"podName": pmd.get("name"), "podNamespace": pmd.get("namespace"), "failureTime": when,
+                     "analysisStatus": "Completed",
+                     "explanation": ai_analysis if not is_blank(ai_analysis) else pattern_explanation(result)}
+            recent.insert(0, entry)
+            recent = recent[:MAX_RECENT_FAILURES]
+            self.kube.patch_status(PODMORTEMS, md["name"], md.get("namespace"),
+                                   {"recentFailures": recent, "lastUpdate": instant_str()},
+                                   resource_version=latest["metadata"]["resourceVersion"])
+            return True
+
+        with self._lock(monitor):
+            return self._with_retry(f"Podmortem {md.get('name')} status", do)
+
+
+class AnalysisStorage:
+    """storeAnalysisResults: annotations + status ring, both on the worker pool."""
+
+    def __init__(self, kube, status: StatusWriter, executor: Executor | None = None, retrier: Retrier | None = None):
+        self.kube, self.status, self.executor = kube, status, executor
+        self.retrier = retrier or status.retrier
+
+    def store(self, pod: dict, monitor: dict, result: AnalysisResult, ai_analysis: str | None):
+        futs = []
+        for fn in (self.store_annotations, self.status.append_failure):
+            if self.executor is None:
+                fn(pod, monitor, result, ai_analysis)
+            else:
+                futs.append(self.executor.submit(fn, pod, monitor, result, ai_analysis))
+        return futs
+
+    def store_annotations(self, pod: dict, monitor: dict, result: AnalysisResult, ai_analysis: str | None) -> bool:
+        pmd = pod.get("metadata") or {}
+        name, ns = pmd.get("name"), pmd.get("namespace")
+
+        def do():
+            latest = self.kube.get(PODS, name, ns)
+            if latest is None:
+                log.warning("Pod not found: %s", name)
+                return False
+            ann = dict((latest.get("metadata") or {}).get("annotations") or {})
+            ann[ANALYSIS_ANNOTATION] = ai_analysis if not is_blank(ai_analysis) else pattern_annotation(result)
+            if result.summary is not None and result.summary.highest_severity is not None:
+                ann[SEVERITY_ANNOTATION] = result.summary.highest_severity
+            ann[TIMESTAMP_ANNOTATION] = instant_str()
+            ann[MONITOR_ANNOTATION] = (monitor.get("metadata") or {}).get("name")
+            self.kube.patch(PODS, name, ns, {"metadata": {"annotations": ann}},
+                            resource_version=latest["metadata"]["resourceVersion"])
+            return True
+
+        return self.status._with_retry(f"pod annotations for {name}", do)

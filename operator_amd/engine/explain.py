@@ -1,0 +1,183 @@
+"""Explanation service: AnalysisResult + AIProviderConfig -> AIResponse.
+
+On-node replacement for the reference's ai-interface hop
+(POST /api/v1/analysis/analyze, J/service/AIInterfaceRestClient.java:37-39;
+request built in J/service/AIInterfaceClient.java:45-59). Semantics kept from
+the AIProvider contract (aiprovider-crd.yaml; defaults 30 s / 3 retries /
+caching on / 500 tokens / T=0.3 per AIInterfaceClient.java:78-84):
+
+* ``maxTokens``      -> generation length cap
+* ``temperature``    -> sampler temperature (0 = greedy)
+* ``timeoutSeconds`` -> per-attempt deadline; the request is cancelled (its KV
+                        pages freed) and retried up to ``maxRetries`` times
+* ``cachingEnabled`` -> LRU of responses keyed by (model, prompt, T, maxTokens)
+* ``promptTemplate`` -> operator_amd.engine.prompt.render
+
+Requests from any number of threads are batched continuously by one engine
+loop thread that owns the GPU (LLMEngine.step).
+"""
+from __future__ import annotations
+
+import hashlib
+import threading
+import time
+from collections import OrderedDict
+from dataclasses import dataclass
+
+import torch
+
+from operator_amd.api.models import AIProviderConfig, AIResponse, AnalysisResult
+
+from . import prompt as prompt_mod
+from .llm import GenRequest, LLMEngine
+
+
+class ExplainError(RuntimeError):
+    pass
+
+
+class EngineLoop(threading.Thread):
+    """Owns the LLMEngine; steps it whenever requests are pending."""
+
+    def __init__(self, llm: LLMEngine):
+        super().__init__(name="llm-engine-loop", daemon=True)
+        self.llm = llm
+        self._cv = threading.Condition()
+        self._stop = False
+        self.error: BaseException | None = None
+
+    def notify(self) -> None:
+        with self._cv:
+            self._cv.notify()
+
+    def stop(self) -> None:
+        with self._cv:
+            self._stop = True
+            self._cv.notify()
+
+    def run(self) -> None:
+        if self.llm.device.type == "cuda":
+            torch.cuda.set_device(self.llm.device)
+        while True:
+            with self._cv:
+                while not self._stop and not self.llm.has_work():
+                    self._cv.wait(timeout=0.5)
+                if self._stop:
+                    return
+            try:
+                self.llm.step()
+            except BaseException as e:  # surface to every waiter
+                self.error = e
+                for r in list(self.llm.running) + list(self.llm.waiting):
+                    r.error = f"engine failure: {e}"
+                    r.done = True
+                    r.event.set()
+                self.llm.running.clear()
+                self.llm.waiting.clear()
+
+
+@dataclass
+class _Pending:
+    req: GenRequest
+    key: str | None
+    cfg: AIProviderConfig
+    t0: float
+    attempt: int = 0
+
+
+class ExplainEngine:
+    def __init__(self, llm: LLMEngine, tokenizer, model_id: str = "local", max_prompt_tokens: int = 1024,
+                 cache_size: int = 4096, ignore_eos: bool = False, start_loop: bool = True):
+        self.llm, self.tok = llm, tokenizer
+        self.model_id = model_id
+        self.max_prompt_tokens = max_prompt_tokens
+        self.ignore_eos = ignore_eos
+        self._cache: OrderedDict[str, AIResponse] = OrderedDict()
+        self._cache_size = cache_size
+        self._lock = threading.Lock()
+        self.loop = EngineLoop(llm)
+        if start_loop:
+            self.loop.start()
+
+    def close(self) -> None:
+        self.loop.stop()
+
+    # ------------------------------------------------------------------ helpers
+    def build_prompt(self, result: AnalysisResult, cfg: AIProviderConfig) -> list[int]:
+        return prompt_mod.render_bounded(result, self.tok, self.max_prompt_tokens, cfg.prompt_template)
+
+    def _key(self, ids: list[int], cfg: AIProviderConfig) -> str:
+        h = hashlib.sha256()
+        h.update(f"{cfg.model_id}|{cfg.temperature}|{cfg.max_tokens}|".encode())
+        h.update(bytes(str(ids), "ascii"))
+        return h.hexdigest()
+
+    def _seed(self, ids: list[int]) -> int:
+        return int(hashlib.sha1(bytes(str(ids), "ascii")).hexdigest()[:8], 16)
+
+    def _start(self, p: _Pending, ids: list[int]) -> None:
+        cfg = p.cfg
+        p.req = GenRequest(ids, max_tokens=max(1, int(cfg.max_tokens)), temperature=float(cfg.temperature),
+                           seed=self._seed(ids) + p.attempt, ignore_eos=self.ignore_eos)
+        self.llm.submit(p.req)
+        self.loop.notify()
+
+    # ------------------------------------------------------------------ API
+    def explain_many(self, items: list[tuple[AnalysisResult, AIProviderConfig]]) -> list[AIResponse | ExplainError]:
+        """Explain a batch concurrently (continuous batching); per-item errors are returned, not raised."""
+        pend: list[_Pending | AIResponse | ExplainError] = []
+        for res, cfg in items:
+            ids = self.build_prompt(res, cfg)
+            key = self._key(ids, cfg) if cfg.caching_enabled else None
+            if key is not None:
+                with self._lock:
+                    hit = self._cache.get(key)
+                    if hit is not None:
+                        self._cache.move_to_end(key)
+                        pend.append(hit.model_copy(update={"cached": True}))
+                        continue
+            p = _Pending(None, key, cfg, time.perf_counter())  # type: ignore[arg-type]
+            p.ids = ids  # type: ignore[attr-defined]
+            self._start(p, ids)
+            pend.append(p)
+        out: list[AIResponse | ExplainError] = []
+        for p in pend:
+            if not isinstance(p, _Pending):
+                out.append(p)
+                continue
+            out.append(self._wait(p))
+        return out
+
+    def explain(self, result: AnalysisResult, cfg: AIProviderConfig) -> AIResponse:
+        r = self.explain_many([(result, cfg)])[0]
+        if isinstance(r, ExplainError):
+            raise r
+        return r
+
+    def _wait(self, p: _Pending) -> AIResponse | ExplainError:
+        cfg = p.cfg
+        while True:
+            deadline = max(0.001, float(cfg.timeout_seconds or 30))
+            ok = p.req.event.wait(timeout=deadline)
+            err = None
+            if not ok:
+                self.llm.cancel(p.req)
+                err = f"explanation timed out after {cfg.timeout_seconds}s"
+            elif p.req.error:
+                err = p.req.error
+            if err is None:
+                break
+            if p.attempt >= int(cfg.max_retries or 0):
+                return ExplainError(f"{err} (after {p.attempt + 1} attempt(s))")
+            p.attempt += 1
+            self._start(p, p.ids)  # type: ignore[attr-defined]
+        r = p.req
+        text = self.tok.decode(r.output)
+        resp = AIResponse(explanation=text, provider_id=cfg.provider_id or "local", model_id=cfg.model_id or self.model_id,
+                          tokens_generated=len(r.output), latency_ms=round((r.t_done - p.t0) * 1e3, 3), cached=False)
+        if p.key is not None:
+            with self._lock:
+                self._cache[p.key] = resp
+                while len(self._cache) > self._cache_size:
+                    self._cache.popitem(last=False)
+        return resp

@@ -43,6 +43,8 @@ class GenRequest:
     pages: list[int] = field(default_factory=list)
     output: list[int] = field(default_factory=list)
     done: bool = False
+    cancelled: bool = False
+    done_pending: bool = False     # EOS seen inside a multi-step window
     error: str | None = None
     t_submit: float = 0.0
     t_first: float = 0.0
@@ -74,50 +76,93 @@ def _buckets(max_batch: int) -> list[int]:
 
 
 class _DecodeGraph:
+    """Device-resident decode state for one batch bucket + its captured step.
+
+    One replay = forward + sample + state advance (ids <- sampled token,
+    pos/ctx += 1 on active rows, token appended to ``hist[:, step]``), so the
+    host can replay several steps back-to-back and read ``hist`` once.
+    Rows with ctx == 0 are padding: slot -1 (no KV write), zero attention.
+    """
+
     def __init__(self, eng: "LLMEngine", bp: int):
-        dev, m = eng.device, eng.model
+        dev = eng.device
         self.bp = bp
         self.ids = torch.zeros(bp, dtype=torch.long, device=dev)
         self.pos = torch.zeros(bp, dtype=torch.long, device=dev)
-        self.slots = torch.full((bp,), -1, dtype=torch.long, device=dev)
         self.bt = torch.zeros(bp, eng.max_pages, dtype=torch.int32, device=dev)
         self.ctx = torch.zeros(bp, dtype=torch.int32, device=dev)
         self.temp = torch.zeros(bp, dtype=torch.float32, device=dev)
         self.seeds = torch.zeros(bp, dtype=torch.long, device=dev)
-        self.spos = torch.zeros(bp, dtype=torch.long, device=dev)
+        self.hist = torch.zeros(bp, eng.multi_step, dtype=torch.long, device=dev)
+        self.step = torch.zeros(1, dtype=torch.long, device=dev)
         self.graph: torch.cuda.CUDAGraph | None = None
-        self.out: torch.Tensor | None = None
         self.eng = eng
 
-    def _run(self) -> torch.Tensor:
+    def _run(self) -> None:
         e = self.eng
-        fb = ForwardBatch(self.ids, self.pos, self.slots, False, None, block_tables=self.bt, context_lens=self.ctx,
+        P = e.kv.page_size
+        act = self.ctx > 0
+        pg = torch.gather(self.bt, 1, torch.clamp(self.pos // P, max=e.max_pages - 1).unsqueeze(1)).squeeze(1)
+        slots = torch.where(act, pg.to(torch.long) * P + self.pos % P, torch.full_like(self.pos, -1))
+        fb = ForwardBatch(self.ids, self.pos, slots, False, None, block_tables=self.bt, context_lens=self.ctx,
                           num_splits=e.num_splits)
         logits = e.model.forward(fb, e.kv)
-        return e.model.sample(logits, self.temp, self.seeds, self.spos)
+        tok = e.model.sample(logits, self.temp, self.seeds, self.pos + 1)
+        self.ids.copy_(tok)
+        self.hist.index_copy_(1, self.step, tok.unsqueeze(1))
+        self.pos.add_(act.to(torch.long))
+        self.ctx.add_(act.to(torch.int32))
+        self.step.add_(1)
 
     def capture(self, pool) -> None:
+        # warm up on a side stream (allocator + hipBLASLt heuristics), then capture
+        snap = [t.clone() for t in (self.ids, self.pos, self.ctx)]
         s = torch.cuda.Stream(device=self.eng.device)
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(2):
+                self.step.zero_()
                 self._run()
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, pool=pool):
-            self.out = self._run()
+            self._run()
         self.graph = g
+        for t, v in zip((self.ids, self.pos, self.ctx), snap):
+            t.copy_(v)
+        self.step.zero_()
 
-    def run(self, use_graph: bool) -> torch.Tensor:
+    def load(self, reqs: list[GenRequest], max_pages: int) -> None:
+        """Write the per-row state of ``reqs`` (rows beyond are padding)."""
+        bp = self.bp
+        ids = torch.zeros(bp, dtype=torch.long)
+        pos = torch.zeros(bp, dtype=torch.long)
+        ctx = torch.zeros(bp, dtype=torch.int32)
+        bt = torch.zeros(bp, max_pages, dtype=torch.int32)
+        temp = torch.zeros(bp, dtype=torch.float32)
+        seeds = torch.zeros(bp, dtype=torch.long)
+        for i, r in enumerate(reqs):
+            ids[i] = r.output[-1]
+            pos[i] = r.length - 1
+            ctx[i] = r.length
+            bt[i, :len(r.pages)] = torch.as_tensor(r.pages, dtype=torch.int32)
+            temp[i] = r.temperature
+            seeds[i] = r.seed
+        nb = self.ids.is_cuda
+        for dst, src in ((self.ids, ids), (self.pos, pos), (self.ctx, ctx), (self.bt, bt), (self.temp, temp),
+                         (self.seeds, seeds)):
+            dst.copy_(src.pin_memory() if nb else src, non_blocking=nb)
+
+    def run(self, use_graph: bool) -> None:
         if use_graph and self.graph is not None:
             self.graph.replay()
-            return self.out
-        return self._run()
+        else:
+            self._run()
 
 
 class LLMEngine:
     def __init__(self, model: LlamaModel, kv: PagedKVCache, max_batch: int = 256, max_prefill_tokens: int = 16384,
-                 max_context: int | None = None, use_graphs: bool = True):
+                 max_context: int | None = None, use_graphs: bool = True, multi_step: int = 8):
         self.model, self.kv = model, kv
         self.device = model.device
         self.max_batch = max_batch
@@ -126,6 +171,8 @@ class LLMEngine:
         self.max_pages = kv.pages_needed(self.max_context)
         self.num_splits = ops.decode_splits(self.max_context)
         self.use_graphs = use_graphs and self.device.type == "cuda"
+        self.multi_step = max(1, multi_step)
+        self._active: _DecodeGraph | None = None   # bucket whose device state matches self.running
         self.waiting: deque[GenRequest] = deque()
         self.running: list[GenRequest] = []
         self.stats = EngineStats()
@@ -149,6 +196,16 @@ class LLMEngine:
             req.t_submit = time.perf_counter()
             self.waiting.append(req)
         return req
+
+    def cancel(self, req: GenRequest) -> None:
+        """Cancel from any thread; the engine loop frees the pages at its next reap."""
+        req.cancelled = True
+        with self._lock:
+            if req in self.waiting:
+                self.waiting.remove(req)
+                req.done = True
+                req.error = "cancelled"
+                req.event.set()
 
     def has_work(self) -> bool:
         return bool(self.waiting or self.running)
@@ -183,6 +240,9 @@ class LLMEngine:
         with self._lock:
             while self.waiting and len(self.running) + len(out) < self.max_batch:
                 r = self.waiting[0]
+                if r.cancelled:
+                    self.waiting.popleft()
+                    continue
                 if out and toks + len(r.prompt) > self.max_prefill_tokens:
                     break
                 need = self.kv.pages_needed(len(r.prompt) + r.max_tokens)
@@ -227,6 +287,7 @@ class LLMEngine:
             r.output.append(int(tk))
             r.t_first = now
             self.running.append(r)
+        self._active = None  # new rows joined
         self.stats.prefill_tokens += len(ids)
         self.stats.prefill_s += now - t0
 
@@ -242,44 +303,40 @@ class LLMEngine:
         return g
 
     def _decode(self) -> None:
+        """Up to ``multi_step`` decode steps with no host round trip in between."""
         t0 = time.perf_counter()
         B = len(self.running)
-        bp = next(b for b in self.buckets if b >= B)
-        g = self._graph(bp)
-        P = self.kv.page_size
-        ids = [r.output[-1] for r in self.running] + [0] * (bp - B)
-        pos = [r.length - 1 for r in self.running] + [0] * (bp - B)
-        slots = [r.pages[(p // P)] * P + p % P for r, p in zip(self.running, pos)] + [-1] * (bp - B)
-        ctx = [r.length for r in self.running] + [0] * (bp - B)
-        bt = torch.zeros(bp, self.max_pages, dtype=torch.int32)
-        for i, r in enumerate(self.running):
-            bt[i, :len(r.pages)] = torch.tensor(r.pages, dtype=torch.int32)
-        temp = [r.temperature for r in self.running] + [0.0] * (bp - B)
-        seeds = [r.seed for r in self.running] + [0] * (bp - B)
-        spos = [r.length for r in self.running] + [0] * (bp - B)
-        nb = self.device.type == "cuda"
-        g.ids.copy_(torch.tensor(ids), non_blocking=nb)
-        g.pos.copy_(torch.tensor(pos), non_blocking=nb)
-        g.slots.copy_(torch.tensor(slots), non_blocking=nb)
-        g.ctx.copy_(torch.tensor(ctx, dtype=torch.int32), non_blocking=nb)
-        g.bt.copy_(bt, non_blocking=nb)
-        g.temp.copy_(torch.tensor(temp, dtype=torch.float32), non_blocking=nb)
-        g.seeds.copy_(torch.tensor(seeds), non_blocking=nb)
-        g.spos.copy_(torch.tensor(spos), non_blocking=nb)
-        out = g.run(self.use_graphs)
-        toks = out[:B].tolist()
-        for r, tk in zip(self.running, toks):
-            r.output.append(int(tk))
-        self.stats.graph_replays += int(self.use_graphs)
-        self.stats.decode_tokens += B
+        g = self._active
+        if g is None:
+            bp = next(b for b in self.buckets if b >= B)
+            g = self._graph(bp)
+            g.load(self.running, self.max_pages)
+            self._active = g
+        k = min(self.multi_step, min(r.max_tokens - len(r.output) for r in self.running))
+        k = max(1, k)
+        g.step.zero_()
+        for _ in range(k):
+            g.run(self.use_graphs)
+        toks = g.hist[:B, :k].tolist()
+        for r, row in zip(self.running, toks):
+            for tk in row:
+                if r.done_pending:
+                    break
+                r.output.append(int(tk))
+                if (not r.ignore_eos) and int(tk) in self.eos:
+                    r.done_pending = True
+        self.stats.graph_replays += k if self.use_graphs else 0
+        self.stats.decode_tokens += B * k
         self.stats.decode_s += time.perf_counter() - t0
 
     def _reap(self) -> list[GenRequest]:
         fin, keep = [], []
         now = time.perf_counter()
         for r in self.running:
-            hit_eos = (not r.ignore_eos) and r.output and r.output[-1] in self.eos
-            if len(r.output) >= r.max_tokens or hit_eos:
+            hit_eos = r.done_pending or ((not r.ignore_eos) and r.output and r.output[-1] in self.eos)
+            if r.cancelled:
+                r.error = r.error or "cancelled"
+            if len(r.output) >= r.max_tokens or hit_eos or r.cancelled:
                 r.done = True
                 r.t_done = now
                 self.kv.allocator.release(r.pages)
@@ -288,5 +345,7 @@ class LLMEngine:
                 r.event.set()
             else:
                 keep.append(r)
+        if fin:
+            self._active = None  # batch composition changed: reload device state next step
         self.running = keep
         return fin

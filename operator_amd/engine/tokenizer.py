@@ -1,0 +1,96 @@
+"""Tokenizer for the explanation model.
+
+If a HuggingFace ``tokenizer.json`` is available (model directory or
+``OAMD_TOKENIZER``) it is used as-is. Otherwise — the normal case offline,
+where no Llama-3 vocabulary files exist — a byte-level BPE is trained
+deterministically on a synthetic corpus of pod-log lines and failure
+explanations (``tokenizers`` library, Rust core) and cached on disk, so token
+counts per log line are realistic (~3-4 bytes/token) instead of the 1 byte/token
+of a raw byte fallback. Special ids (BOS/EOS) come from the model config, and
+ids the trained vocabulary does not cover (a random-weight model can sample
+any id < vocab_size) are folded into range for decoding.
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+import threading
+from pathlib import Path
+
+_CACHE = Path(os.environ.get("OAMD_CACHE_DIR", Path(__file__).resolve().parent.parent / ".cache"))
+_lock = threading.Lock()
+
+_EXPLAIN_TEXT = """Root Cause: the container was terminated because it exceeded its memory limit.
+Evidence: the log shows OOMKilled shortly after the heap grew past the configured maximum.
+Fix: raise resources.limits.memory or reduce the JVM heap with -Xmx so the process fits the cgroup.
+Root Cause: the application could not reach its database; connections were refused.
+Evidence: repeated Connection refused errors followed by retrying in 5 seconds.
+Fix: verify the database service, its endpoints and network policies, and add a readiness dependency.
+Root Cause: a required configuration value or secret is missing.
+Fix: define the environment variable in the Deployment or mount the referenced Secret.
+The pod entered CrashLoopBackOff after the liveness probe failed repeatedly.
+Consider increasing initialDelaySeconds, checking the probe path, and reviewing recent deployments.
+"""
+
+
+def _corpus(n_lines: int = 40000):
+    from operator_amd.patterns.synth import CATALOG, LogFactory
+
+    fac = LogFactory(n_patterns=200, seed=123, pool_lines=4096)
+    for line in fac.pool:
+        yield line.decode()
+    for c in CATALOG:
+        yield c[6]
+    for pid, ex in list(fac.examples.items())[:2000]:
+        for e in ex:
+            yield e
+    for _ in range(50):
+        for line in _EXPLAIN_TEXT.splitlines():
+            yield line
+
+
+class Tokenizer:
+    def __init__(self, vocab_limit: int, bos_id: int, eos_id: int, path: str | None = None):
+        import tokenizers
+
+        self.bos_id, self.eos_id = bos_id, eos_id
+        path = path or os.environ.get("OAMD_TOKENIZER")
+        if path and os.path.exists(path):
+            self.tk = tokenizers.Tokenizer.from_file(path)
+        else:
+            self.tk = self._trained(min(32000, max(256 + 8, vocab_limit - 16)))
+        self.n_vocab = self.tk.get_vocab_size()
+
+    @staticmethod
+    def _trained(vocab: int):
+        import tokenizers
+        from tokenizers import decoders, models, pre_tokenizers, trainers
+
+        key = hashlib.sha1(f"bpe-v1-{vocab}".encode()).hexdigest()[:12]
+        f = _CACHE / f"tokenizer-{key}.json"
+        with _lock:
+            if f.exists():
+                return tokenizers.Tokenizer.from_file(str(f))
+            tk = tokenizers.Tokenizer(models.BPE())
+            tk.pre_tokenizer = pre_tokenizers.ByteLevel(add_prefix_space=False)
+            tk.decoder = decoders.ByteLevel()
+            tr = trainers.BpeTrainer(vocab_size=vocab, show_progress=False,
+                                     initial_alphabet=pre_tokenizers.ByteLevel.alphabet())
+            tk.train_from_iterator(_corpus(), trainer=tr)
+            _CACHE.mkdir(parents=True, exist_ok=True)
+            tmp = f.with_suffix(f".{os.getpid()}.tmp")
+            tk.save(str(tmp))
+            os.replace(tmp, f)
+            return tk
+
+    def encode(self, text: str, bos: bool = True) -> list[int]:
+        ids = self.tk.encode(text).ids
+        return ([self.bos_id] if bos else []) + ids
+
+    def encode_batch(self, texts: list[str], bos: bool = True) -> list[list[int]]:
+        return [([self.bos_id] if bos else []) + e.ids for e in self.tk.encode_batch(texts)]
+
+    def decode(self, ids: list[int]) -> str:
+        n = self.n_vocab
+        keep = [i % n for i in ids if i != self.bos_id and i != self.eos_id]
+        return self.tk.decode(keep)

@@ -1,0 +1,349 @@
+"""FakeKube: an in-memory Kubernetes API server for tests and the plumbing
+benchmark (SURVEY.md §4.2 "Controller integration, CPU"; BASELINE config 1).
+
+The reference has no test double at all. FakeKube models the
+behaviour the controllers depend on:
+
+* namespaced objects with uid / resourceVersion / generation / creationTimestamp;
+  optimistic concurrency: a write carrying a stale resourceVersion -> 409;
+* JSON merge patch (RFC 7386) on objects and on the ``status`` subresource
+  (status writes never touch spec and do not bump generation);
+* list with label + field selectors; ``pods/log`` subresource;
+* watches (ADDED / MODIFIED / DELETED) with resourceVersion resume and
+  close-with-error injection;
+* a fault matrix: ``inject(verb, plural, code, times)`` makes the next N
+  matching calls raise ApiError(code) (409 / 403 / 500 ...);
+* a call journal (``calls``) so tests can assert on the exact verbs issued.
+
+Thread-safe; every read returns a deep copy.
+"""
+from __future__ import annotations
+
+import copy
+import itertools
+import queue
+import threading
+import uuid
+from collections import defaultdict
+from typing import Any, Iterator
+
+from operator_amd.utils.timefmt import instant_str
+
+from .resources import (ALL, PODS, ApiError, Resource, WatchClosed, match_fields, match_selector, parse_selector)
+
+
+def merge_patch(target: Any, patch: Any) -> Any:
+    """RFC 7386 JSON merge patch."""
+    if not isinstance(patch, dict):
+        return copy.deepcopy(patch)
+    out = copy.deepcopy(target) if isinstance(target, dict) else {}
+    for k, v in patch.items():
+        if v is None:
+            out.pop(k, None)
+        else:
+            out[k] = merge_patch(out.get(k), v)
+    return out
+
+
+class FakeWatch:
+    """Iterator of (type, obj) events; ``close()`` ends it normally."""
+
+    _END = object()
+
+    def __init__(self, fk: "FakeKube", res: Resource, namespace: str | None):
+        self.fk, self.res, self.namespace = fk, res, namespace
+        self.q: queue.Queue = queue.Queue()
+        self.closed = False
+
+    def push(self, typ: str, obj: dict) -> None:
+        if not self.closed:
+            self.q.put((typ, obj))
+
+    def fail(self, message: str = "watch stream error") -> None:
+        self.q.put(WatchClosed(message))
+
+    def close(self) -> None:
+        if not self.closed:
+            self.closed = True
+            self.q.put(self._END)
+            self.fk._drop_watch(self)
+
+    def __iter__(self) -> Iterator[tuple[str, dict]]:
+        return self
+
+    def __next__(self) -> tuple[str, dict]:
+        item = self.q.get()
+        if item is self._END:
+            raise StopIteration
+        if isinstance(item, WatchClosed):
+            self.closed = True
+            self.fk._drop_watch(self)
+            raise item
+        return item
+
+
+class FakeKube:
+    def __init__(self):
+        self._lock = threading.RLock()
+        self._objs: dict[tuple[str, str, str], dict] = {}  # (plural-key, ns, name) -> obj
+        self._rv = itertools.count(1)
+        self._history: list[tuple[int, str, str, dict]] = []  # (rv, plural-key, type, obj)
+        self._watches: list[FakeWatch] = []
+        self._faults: dict[tuple[str, str], list[int]] = defaultdict(list)
+        self._logs: dict[tuple[str, str, str | None], str] = {}
+        self.calls: list[tuple[str, str, str | None, str | None]] = []
+
+    # ------------------------------------------------------------------ faults
+    def inject(self, verb: str, plural: str, code: int, times: int = 1) -> None:
+        """Next ``times`` calls of verb ('get','list','create','patch','patch_status','delete','watch','log')
+        on ``plural`` raise ApiError(code)."""
+        with self._lock:
+            self._faults[(verb, plural)].extend([code] * times)
+
+    def _fault(self, verb: str, res: Resource) -> None:
+        with self._lock:
+            lst = self._faults.get((verb, res.plural))
+            if lst:
+                code = lst.pop(0)
+                raise ApiError(code, f"injected {verb} {res.plural} failure", {409: "Conflict", 403: "Forbidden",
+                                                                                404: "NotFound"}.get(code, "Error"))
+
+    def _log_call(self, verb, res, ns, name) -> None:
+        self.calls.append((verb, res.plural, ns, name))
+
+    # ------------------------------------------------------------------ helpers
+    @staticmethod
+    def _key(res: Resource) -> str:
+        return f"{res.api_version}/{res.plural}"
+
+    def _emit(self, res: Resource, typ: str, obj: dict) -> None:
+        rv = int(obj["metadata"]["resourceVersion"])
+        self._history.append((rv, self._key(res), typ, copy.deepcopy(obj)))
+        for w in list(self._watches):
+            if w.res == res and (w.namespace is None or w.namespace == obj["metadata"].get("namespace")):
+                w.push(typ, copy.deepcopy(obj))
+
+    def _drop_watch(self, w: FakeWatch) -> None:
+        with self._lock:
+            if w in self._watches:
+                self._watches.remove(w)
+
+    def current_resource_version(self) -> str:
+        with self._lock:
+            return str(max((int(o["metadata"]["resourceVersion"]) for o in self._objs.values()), default=0))
+
+    # ------------------------------------------------------------------ verbs
+    def get(self, res: Resource, name: str, namespace: str | None = None) -> dict | None:
+        self._log_call("get", res, namespace, name)
+        self._fault("get", res)
+        with self._lock:
+            o = self._objs.get((self._key(res), namespace or "", name))
+            return copy.deepcopy(o) if o is not None else None
+
+    def list(self, res: Resource, namespace: str | None = None, label_selector: dict | str | None = None,
+             field_selector: str | None = None) -> list[dict]:
+        self._log_call("list", res, namespace, None)
+        self._fault("list", res)
+        sel = parse_selector(label_selector) if isinstance(label_selector, str) else label_selector
+        key = self._key(res)
+        with self._lock:
+            out = []
+            for (k, ns, _), o in sorted(self._objs.items()):
+                if k != key or (namespace is not None and ns != namespace):
+                    continue
+                if sel is not None and not match_selector(sel, o["metadata"].get("labels")):
+                    continue
+                if not match_fields(field_selector, o):
+                    continue
+                out.append(copy.deepcopy(o))
+            return out
+
+    def create(self, res: Resource, obj: dict, namespace: str | None = None) -> dict:
+        ns = namespace or obj.get("metadata", {}).get("namespace") or ("default" if res.namespaced else "")
+        name = obj.get("metadata", {}).get("name")
+        self._log_call("create", res, ns, name)
+        self._fault("create", res)
+        if not name:
+            gen = obj.get("metadata", {}).get("generateName")
+            if not gen:
+                raise ApiError(422, "metadata.name is required", "Invalid")
+            name = gen + uuid.uuid4().hex[:5]
+        with self._lock:
+            k = (self._key(res), ns if res.namespaced else "", name)
+            if k in self._objs:
+                raise ApiError(409, f"{res.plural} {name} already exists", "AlreadyExists")
+            o = copy.deepcopy(obj)
+            md = o.setdefault("metadata", {})
+            md["name"] = name
+            if res.namespaced:
+                md["namespace"] = ns
+            md["uid"] = str(uuid.uuid4())
+            md["resourceVersion"] = str(next(self._rv))
+            md["generation"] = 1
+            md.setdefault("creationTimestamp", instant_str())
+            o.setdefault("apiVersion", res.api_version)
+            o.setdefault("kind", res.kind)
+            self._objs[k] = o
+            self._emit(res, "ADDED", o)
+            return copy.deepcopy(o)
+
+    def _update(self, res: Resource, name: str, namespace: str | None, fn, resource_version: str | None,
+                status: bool) -> dict:
+        with self._lock:
+            k = (self._key(res), namespace or "", name)
+            cur = self._objs.get(k)
+            if cur is None:
+                raise ApiError(404, f"{res.plural} {name} not found", "NotFound")
+            if resource_version is not None and str(resource_version) != cur["metadata"]["resourceVersion"]:
+                raise ApiError(409, f"the object has been modified; resourceVersion {resource_version} is stale",
+                               "Conflict")
+            new = fn(copy.deepcopy(cur))
+            new["metadata"]["uid"] = cur["metadata"]["uid"]
+            new["metadata"]["name"] = name
+            if res.namespaced:
+                new["metadata"]["namespace"] = namespace
+            if status:
+                # status subresource: only status may change
+                kept = copy.deepcopy(cur)
+                kept["status"] = new.get("status")
+                if kept["status"] is None:
+                    kept.pop("status", None)
+                new = kept
+            elif new.get("spec") != cur.get("spec"):
+                new["metadata"]["generation"] = int(cur["metadata"].get("generation", 1)) + 1
+            else:
+                new["metadata"]["generation"] = cur["metadata"].get("generation", 1)
+            new["metadata"]["resourceVersion"] = str(next(self._rv))
+            self._objs[k] = new
+            self._emit(res, "MODIFIED", new)
+            return copy.deepcopy(new)
+
+    def patch(self, res: Resource, name: str, namespace: str | None, patch: dict,
+              resource_version: str | None = None) -> dict:
+        self._log_call("patch", res, namespace, name)
+        self._fault("patch", res)
+        rv = resource_version or (patch.get("metadata") or {}).get("resourceVersion")
+        return self._update(res, name, namespace, lambda o: merge_patch(o, patch), rv, status=False)
+
+    def replace(self, res: Resource, obj: dict, namespace: str | None = None) -> dict:
+        name = obj["metadata"]["name"]
+        ns = namespace or obj["metadata"].get("namespace")
+        self._log_call("replace", res, ns, name)
+        self._fault("replace", res)
+        rv = obj["metadata"].get("resourceVersion")
+        return self._update(res, name, ns, lambda o: copy.deepcopy(obj), rv, status=False)
+
+    def patch_status(self, res: Resource, name: str, namespace: str | None, status_patch: dict,
+                     resource_version: str | None = None) -> dict:
+        self._log_call("patch_status", res, namespace, name)
+        self._fault("patch_status", res)
+        return self._update(res, name, namespace, lambda o: merge_patch(o, {"status": status_patch}),
+                            resource_version, status=True)
+
+    def replace_status(self, res: Resource, obj: dict, namespace: str | None = None) -> dict:
+        name = obj["metadata"]["name"]
+        ns = namespace or obj["metadata"].get("namespace")
+        self._log_call("replace_status", res, ns, name)
+        self._fault("patch_status", res)
+        rv = obj["metadata"].get("resourceVersion")
+
+        def fn(o):
+            o["status"] = copy.deepcopy(obj.get("status"))
+            return o
+
+        return self._update(res, name, ns, fn, rv, status=True)
+
+    def delete(self, res: Resource, name: str, namespace: str | None = None) -> bool:
+        self._log_call("delete", res, namespace, name)
+        self._fault("delete", res)
+        with self._lock:
+            o = self._objs.pop((self._key(res), namespace or "", name), None)
+            if o is None:
+                return False
+            o["metadata"]["resourceVersion"] = str(next(self._rv))
+            self._emit(res, "DELETED", o)
+            return True
+
+    def watch(self, res: Resource, namespace: str | None = None, resource_version: str | None = None) -> FakeWatch:
+        self._log_call("watch", res, namespace, None)
+        self._fault("watch", res)
+        with self._lock:
+            w = FakeWatch(self, res, namespace)
+            if resource_version:
+                key = self._key(res)
+                for rv, k, typ, o in self._history:
+                    if k == key and rv > int(resource_version) and \
+                            (namespace is None or o["metadata"].get("namespace") == namespace):
+                        w.push(typ, copy.deepcopy(o))
+            self._watches.append(w)
+            return w
+
+    def fail_watches(self, message: str = "injected watch failure", res: Resource | None = None) -> int:
+        """Close every open watch (optionally of one resource) with an error."""
+        with self._lock:
+            ws = [w for w in self._watches if res is None or w.res == res]
+        for w in ws:
+            w.fail(message)
+        return len(ws)
+
+    def open_watches(self, res: Resource | None = None) -> int:
+        with self._lock:
+            return sum(1 for w in self._watches if res is None or w.res == res)
+
+    # ------------------------------------------------------------------ pods/log
+    def set_log(self, namespace: str, pod: str, text: str | bytes, container: str | None = None) -> None:
+        if isinstance(text, bytes):
+            text = text.decode("utf-8", "replace")
+        with self._lock:
+            self._logs[(namespace, pod, container)] = text
+
+    def pod_log(self, name: str, namespace: str, container: str | None = None, previous: bool = False,
+                tail_lines: int | None = None, limit_bytes: int | None = None) -> str:
+        self._log_call("log", PODS, namespace, name)
+        self._fault("log", PODS)
+        with self._lock:
+            if (self._key(PODS), namespace, name) not in self._objs:
+                raise ApiError(404, f"pod {name} not found", "NotFound")
+            text = self._logs.get((namespace, name, container))
+            if text is None:
+                text = self._logs.get((namespace, name, None), "")
+        if tail_lines is not None:
+            text = "\n".join(text.split("\n")[-tail_lines:])
+        if limit_bytes is not None:
+            text = text.encode()[:limit_bytes].decode("utf-8", "ignore")
+        return text
+
+    # ------------------------------------------------------------------ conveniences for tests
+    def objects(self, res: Resource) -> list[dict]:
+        return self.list(res)
+
+    def reset_calls(self) -> None:
+        self.calls.clear()
+
+
+def failed_pod(name: str, namespace: str = "default", labels: dict | None = None, exit_code: int = 1,
+               finished_at: str | None = None, reason: str = "Error", owner_rs: str | None = None) -> dict:
+    """A pod whose single container terminated with ``exit_code``."""
+    md: dict[str, Any] = {"name": name, "namespace": namespace, "labels": labels or {}}
+    if owner_rs:
+        md["ownerReferences"] = [{"apiVersion": "apps/v1", "kind": "ReplicaSet", "name": owner_rs,
+                                  "uid": str(uuid.uuid4()), "controller": True}]
+    return {
+        "apiVersion": "v1", "kind": "Pod", "metadata": md,
+        "spec": {"containers": [{"name": "app", "image": "registry.example/app:1.0"}]},
+        "status": {"phase": "Running", "containerStatuses": [{
+            "name": "app", "ready": False, "restartCount": 1,
+            "state": {"terminated": {"exitCode": exit_code, "reason": reason,
+                                     "finishedAt": finished_at or instant_str().split(".")[0] + "Z"}}}]},
+    }
+
+
+def running_pod(name: str, namespace: str = "default", labels: dict | None = None) -> dict:
+    return {"apiVersion": "v1", "kind": "Pod",
+            "metadata": {"name": name, "namespace": namespace, "labels": labels or {}},
+            "spec": {"containers": [{"name": "app", "image": "registry.example/app:1.0"}]},
+            "status": {"phase": "Running", "containerStatuses": [{"name": "app", "ready": True,
+                                                                  "state": {"running": {"startedAt": instant_str()}}}]}}
+
+
+__all__ = ["FakeKube", "FakeWatch", "merge_patch", "failed_pod", "running_pod", "ALL"]
