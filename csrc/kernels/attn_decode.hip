@@ -45,6 +45,8 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(
   __shared__ __attribute__((aligned(16))) float red[4 * G * D];
   __shared__ float wred[4][G];
 
+  __shared__ int pg_lds[kSplit / 16 + 2];
+
   const int s = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
   const int Hq = Hkv * G;
   const int len = min(seq_lens[b], max_pages * page_size);  // never index past the block table
@@ -53,44 +55,47 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(
   const int n = min(len - start, kSplit);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int l15 = lane & 15, lg = lane >> 4;
-  const int* bt = block_tables + (int64_t)b * max_pages;
-
-  auto row_ptr = [&](const bf16_t* base, int t) -> const bf16_t* {
+  if (n <= 0) {  // empty sequence (single split): zero output
+    for (int e = tid; e < G * D; e += 256) out[((int64_t)b * Hq + kvh * G) * D + e] = 0;
+    return;
+  }
+  // Stage this split's page ids in LDS. The data loads below then depend only on
+  // LDS (lgkmcnt), so hipcc can issue all of them back to back; a per-token
+  // global block-table load would share vmcnt with the data loads and force a
+  // vmcnt(0) before every one of them.
+  const int page0 = start >> log2_page;
+  const int npg = min(((start + n - 1) >> log2_page) - page0 + 1, kSplit / 16 + 2);
+  if (tid < npg) pg_lds[tid] = block_tables[(int64_t)b * max_pages + page0 + tid];
+  __syncthreads();
+  auto row_off = [&](int t) -> int64_t {  // t already clamped to [0, n)
     const int tok = start + t;
-    const int64_t page = bt[tok >> log2_page];
-    return base + ((page * Hkv + kvh) * page_size + (tok & (page_size - 1))) * (int64_t)D;
+    const int64_t page = pg_lds[(tok >> log2_page) - page0];
+    return ((page * Hkv + kvh) * page_size + (tok & (page_size - 1))) * (int64_t)D;
   };
 
-  // ---- issue every K and V load of this lane up front ----
+  // ---- q first (the first MFMA needs it), as the B operand: column = head ----
+  u16x8 qb[4];
+  {
+    const int hq = kvh * G + (l15 < G ? l15 : 0);
+    const bf16_t* qp = q + ((int64_t)b * Hq + hq) * D + 32 * lg;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) qb[ks] = *reinterpret_cast<const u16x8*>(qp + 8 * ks);
+  }
+  // ---- then every K and V load of this lane, branch-free (rows past n are clamped
+  // duplicates; their scores are masked to -inf and their P to 0) ----
   u16x8 kf[4][4];  // [tile][kstep]: token w*64 + 16*i + l15, dims 32*lg + 8*ks
   u16x8 vf[16];    // token w*64 + 4*it + lg, dims 8*l15
-  const u16x8 z8 = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int t = w * 64 + 16 * i + l15;
-    if (t < n) {
-      const bf16_t* p = row_ptr(kc, t) + 32 * lg;
+    const bf16_t* p = kc + row_off(min(w * 64 + 16 * i + l15, n - 1)) + 32 * lg;
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) kf[i][ks] = ld16(p + 8 * ks);
-    } else {
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) kf[i][ks] = z8;
-    }
+    for (int ks = 0; ks < 4; ++ks) kf[i][ks] = ld16(p + 8 * ks);
   }
 #pragma unroll
-  for (int it = 0; it < 16; ++it) {
-    const int t = w * 64 + 4 * it + lg;
-    vf[it] = (t < n) ? ld16(row_ptr(vc, t) + 8 * l15) : z8;
-  }
-
-  // ---- q as the MFMA B operand: column = head (l15 < G), same dim permutation ----
-  u16x8 qb[4];
+  for (int it = 0; it < 16; ++it) vf[it] = ld16(vc + row_off(min(w * 64 + 4 * it + lg, n - 1)) + 8 * l15);
+  if (l15 >= G) {
 #pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    if (l15 < G)
-      qb[ks] = *reinterpret_cast<const u16x8*>(q + ((int64_t)b * Hq + kvh * G + l15) * D + 32 * lg + 8 * ks);
-    else
-      qb[ks] = z8;
+    for (int ks = 0; ks < 4; ++ks) qb[ks] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
   }
 
   // ---- S = K Q^T on MFMA, scaled scores -> LDS [token][head] ----
@@ -226,7 +231,7 @@ int attn_decode(const bf16_t* q, const bf16_t* k_cache, const bf16_t* v_cache, c
                 hipStream_t stream) {
   if (B == 0) return 0;
   if (head_dim != 128) return -1;
-  if (page_size <= 0 || (page_size & (page_size - 1)) != 0) return -2;
+  if (page_size < 16 || (page_size & (page_size - 1)) != 0) return -2;  // pg_lds holds <= 18 pages
   int log2p = 0;
   while ((1 << log2p) < page_size) ++log2p;
   const int G = Hq / Hkv;

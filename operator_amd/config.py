@@ -1,0 +1,151 @@
+"""Typed configuration.
+
+Precedence: defaults < YAML file (``--config`` / ``PODMORTEM_CONFIG``) <
+environment ``PODMORTEM_<SECTION>__<KEY>`` < explicit overrides.
+Every reference config key / hard-coded constant has a home here, with the
+reference's default:
+
+reference                                             here
+----------------------------------------------------  ---------------------------------------
+quarkus.application.name=podmortem-operator           operator.name
+pattern.cache.directory=/shared/patterns (ignored!)   patterns.cache_dir (honoured: Q10)
+quarkus.rest-client.log-parser.url / timeouts 30/10s  services.log_parser_url / *_timeout_s
+quarkus.rest-client.ai-interface.url / 180/120s       services.ai_interface_url / *_timeout_s
+podmortem.watch.namespaces                            watch.namespaces
+quarkus.kubernetes-client.namespace=default           kube.namespace
+MAX_RECENT_FAILURES=10 (AnalysisStorageService:48)    storage.max_recent_failures
+5 retries / 100 ms backoff (:75-76)                   storage.max_retries / initial_backoff_s
+watch restart 5 s (PodFailureWatcher:574)             watch.restart_delay_s
+readiness grace 5 min (ReadinessCheck:26)             health.grace_s
+event caps 850 / 900 (EventService:87,117)            (constants, controller/events.py)
+refresh default 1h (PatternLibraryReconciler)         (grammar default, controller/patternlibrary.py)
+AIProvider defaults 30s/3/true/500/0.3                (controller/ai_client.py DEFAULTS)
+"""
+from __future__ import annotations
+
+import os
+from typing import Any, Optional
+
+import yaml
+from pydantic import BaseModel, Field
+
+
+class OperatorCfg(BaseModel):
+    name: str = "podmortem-operator"
+    workers: int = 16                 # analysis pipeline thread pool
+    io_workers: int = 8               # kube write pool (annotations, status, events)
+
+
+class KubeCfg(BaseModel):
+    mode: str = "auto"                # auto | incluster | kubeconfig | fake
+    kubeconfig: Optional[str] = None
+    namespace: str = "default"
+    request_timeout_s: float = 30.0
+
+
+class WatchCfg(BaseModel):
+    namespaces: str = ""
+    restart_delay_s: float = 5.0
+    include_last_state: bool = False  # treat lastState.terminated (CrashLoopBackOff) as a failure
+    include_init_containers: bool = False
+    dedupe_max_entries: int = 100_000
+    dedupe_ttl_s: float = 7 * 24 * 3600
+
+
+class StorageCfg(BaseModel):
+    max_recent_failures: int = 10
+    max_retries: int = 5
+    initial_backoff_s: float = 0.1
+    failure_time_from_pod: bool = False  # Q5: reference records now(); true = container finishedAt
+
+
+class PatternsCfg(BaseModel):
+    cache_dir: str = "/shared/patterns"
+    builtin_catalog: bool = True      # ship the built-in failure catalog beside synced libraries
+    seg_bytes: int = 1024
+    max_events: int = 50
+    significance_threshold: float = 0.5
+
+
+class ServicesCfg(BaseModel):
+    match: str = "local"              # local | remote | cpu
+    explain: str = "local"            # local | remote | echo | none
+    log_parser_url: str = "http://podmortem-log-parser-service.podmortem-system.svc.cluster.local:8080"
+    log_parser_read_timeout_s: float = 30.0
+    log_parser_connect_timeout_s: float = 10.0
+    ai_interface_url: str = "http://podmortem-ai-interface-service.podmortem-system.svc.cluster.local:8080"
+    ai_interface_read_timeout_s: float = 180.0
+    ai_interface_connect_timeout_s: float = 120.0
+    match_batch_wait_ms: float = 2.0
+    match_max_batch: int = 1024
+
+
+class EngineCfg(BaseModel):
+    model: str = "llama3-8b"
+    model_path: Optional[str] = None  # HF safetensors dir; random init when absent
+    seed: int = 0
+    dtype: str = "bfloat16"
+    device: str = "cuda"
+    tp: int = 1
+    max_batch: int = 256
+    max_prefill_tokens: int = 16384
+    max_context: int = 4096
+    max_prompt_tokens: int = 1536
+    kv_cache_gb: float = 64.0
+    page_size: int = 64
+    use_graphs: bool = True
+    multi_step: int = 8
+    ignore_eos: bool = False
+
+
+class HealthCfg(BaseModel):
+    port: int = 8080
+    host: str = "0.0.0.0"
+    grace_s: float = 300.0
+    enabled: bool = True
+
+
+class Settings(BaseModel):
+    operator: OperatorCfg = Field(default_factory=OperatorCfg)
+    kube: KubeCfg = Field(default_factory=KubeCfg)
+    watch: WatchCfg = Field(default_factory=WatchCfg)
+    storage: StorageCfg = Field(default_factory=StorageCfg)
+    patterns: PatternsCfg = Field(default_factory=PatternsCfg)
+    services: ServicesCfg = Field(default_factory=ServicesCfg)
+    engine: EngineCfg = Field(default_factory=EngineCfg)
+    health: HealthCfg = Field(default_factory=HealthCfg)
+
+
+def _set_path(d: dict, path: list[str], value: Any) -> None:
+    for p in path[:-1]:
+        d = d.setdefault(p, {})
+    d[path[-1]] = value
+
+
+def _coerce(v: str) -> Any:
+    try:
+        return yaml.safe_load(v)
+    except yaml.YAMLError:
+        return v
+
+
+def load_settings(path: str | None = None, env: dict[str, str] | None = None,
+                  overrides: dict[str, Any] | None = None) -> Settings:
+    env = dict(os.environ if env is None else env)
+    data: dict = {}
+    path = path or env.get("PODMORTEM_CONFIG")
+    if path:
+        with open(path) as f:
+            data = yaml.safe_load(f) or {}
+    for k, v in env.items():
+        if not k.startswith("PODMORTEM_") or k == "PODMORTEM_CONFIG":
+            continue
+        parts = [p.lower() for p in k[len("PODMORTEM_"):].split("__")]
+        if len(parts) == 2:
+            _set_path(data, parts, _coerce(v))
+    # the reference's own property name keeps working (PodFailureWatcher.java:52)
+    if "PODMORTEM_WATCH_NAMESPACES" in env:
+        _set_path(data, ["watch", "namespaces"], env["PODMORTEM_WATCH_NAMESPACES"])
+    for k, v in (overrides or {}).items():
+        _set_path(data, k.split("."), v)
+    return Settings.model_validate(data)

@@ -1,0 +1,53 @@
+"""AIProvider reconciler — an extension: the reference has no
+controller for AIProvider, so its status (phase Pending/Ready/Failed,
+message, lastValidated, observedGeneration; K/aiprovider-crd.yaml:64-77) is
+never written. Here the provider is validated against the on-node engine:
+
+* the referenced auth Secret (if any) must exist and contain the key;
+* the explain service must be ready (model weights loaded / engine loop alive);
+* ``modelId`` is informational (the local engine serves its configured model);
+  a mismatch is reported in the message, not treated as a failure.
+"""
+from __future__ import annotations
+
+import logging
+
+from operator_amd.kube.resources import SECRETS, ApiError
+from operator_amd.utils.timefmt import instant_str
+
+from .runtime import UpdateControl
+
+log = logging.getLogger(__name__)
+
+
+class AIProviderReconciler:
+    def __init__(self, kube, explainer, engine_model: str = "local"):
+        self.kube, self.explainer, self.engine_model = kube, explainer, engine_model
+
+    def reconcile(self, provider: dict) -> UpdateControl:
+        md = provider.get("metadata") or {}
+        spec = provider.get("spec") or {}
+        problems = []
+        auth = spec.get("authenticationRef")
+        if auth:
+            try:
+                sec = self.kube.get(SECRETS, auth.get("secretName"), md.get("namespace"))
+                if sec is None:
+                    problems.append(f"secret {auth.get('secretName')} not found")
+                elif auth.get("secretKey") not in (sec.get("data") or {}):
+                    problems.append(f"key {auth.get('secretKey')} missing in secret {auth.get('secretName')}")
+            except ApiError as e:
+                problems.append(f"secret lookup failed: {e}")
+        ready = self.explainer is not None and getattr(self.explainer, "ready", lambda: True)()
+        if not ready:
+            problems.append("explanation engine not ready")
+        if problems:
+            phase, msg = "Failed", "; ".join(problems)
+        else:
+            phase = "Ready"
+            mid = spec.get("modelId")
+            msg = f"Served by on-node engine ({self.engine_model})"
+            if mid and mid != self.engine_model:
+                msg += f"; requested modelId {mid} is mapped to {self.engine_model}"
+        return UpdateControl.patch_status({"phase": phase, "message": msg, "lastValidated": instant_str(),
+                                           "observedGeneration": md.get("generation")})

@@ -1,0 +1,79 @@
+"""Construct the on-node engines from Settings (one process per GPU)."""
+from __future__ import annotations
+
+import logging
+
+import torch
+
+from operator_amd.config import Settings
+from operator_amd.patterns.schema import PatternSet
+
+log = logging.getLogger(__name__)
+
+
+def build_llm(s: Settings, device: str | torch.device | None = None, tp=None):
+    """(model, kv, LLMEngine, Tokenizer) for the configured explanation model."""
+    from operator_amd.engine.llm import LLMEngine
+    from operator_amd.engine.tokenizer import Tokenizer
+    from operator_amd.models.config import get_config
+    from operator_amd.models.kv_cache import PagedKVCache
+    from operator_amd.models.llama import LlamaModel
+
+    e = s.engine
+    dev = torch.device(device or e.device)
+    cfg = get_config(e.model)
+    dtype = getattr(torch, e.dtype)
+    model = LlamaModel(cfg, device=dev, tp=tp, dtype=dtype)
+    if e.model_path:
+        model.load_hf(e.model_path)
+    else:
+        model.init_random(e.seed)
+    pages = PagedKVCache.pages_for_budget(int(e.kv_cache_gb * 1e9), cfg.layers, model.hkv, cfg.head_dim,
+                                          e.page_size, torch.finfo(dtype).bits // 8)
+    kv = PagedKVCache(cfg.layers, pages, model.hkv, cfg.head_dim, e.page_size, device=dev, dtype=dtype)
+    llm = LLMEngine(model, kv, max_batch=e.max_batch, max_prefill_tokens=e.max_prefill_tokens,
+                    max_context=e.max_context, use_graphs=e.use_graphs, multi_step=e.multi_step)
+    tok = Tokenizer(cfg.vocab_size, cfg.bos_id, cfg.eos_ids[0],
+                    path=(f"{e.model_path}/tokenizer.json" if e.model_path else None))
+    log.info("explanation model %s: %.1f GB weights, %d KV pages (%d tokens)", cfg.name,
+             model.weight_bytes() / 1e9, pages, pages * e.page_size)
+    return model, kv, llm, tok
+
+
+def build_explain_service(s: Settings, metrics=None, tp=None):
+    from operator_amd.engine import service
+
+    kind = s.services.explain
+    if kind == "none":
+        return None
+    if kind == "echo":
+        return service.EchoExplainService()
+    if kind == "remote":
+        return service.RemoteAIInterface(s.services.ai_interface_url, s.services.ai_interface_read_timeout_s,
+                                         s.services.ai_interface_connect_timeout_s)
+    from operator_amd.engine.explain import ExplainEngine
+
+    _, _, llm, tok = build_llm(s, tp=tp)
+    ee = ExplainEngine(llm, tok, model_id=s.engine.model, max_prompt_tokens=s.engine.max_prompt_tokens,
+                       ignore_eos=s.engine.ignore_eos)
+    return service.LocalExplainService(ee, metrics)
+
+
+def build_match_engine(s: Settings, patterns: PatternSet, device: str | None = None):
+    from operator_amd.engine.match import MatchEngine
+
+    dev = device or (s.engine.device if s.services.match == "local" else "cpu")
+    if dev.startswith("cuda") and not torch.cuda.is_available():
+        raise RuntimeError("services.match=local needs a GPU; use services.match=cpu without one")
+    return MatchEngine(patterns, device=dev, seg_bytes=s.patterns.seg_bytes, max_events=s.patterns.max_events,
+                       significance=s.patterns.significance_threshold)
+
+
+def build_match_service(s: Settings, patterns: PatternSet, metrics=None):
+    from operator_amd.engine import service
+
+    if s.services.match == "remote":
+        return service.RemoteLogParser(s.services.log_parser_url, s.services.log_parser_read_timeout_s,
+                                       s.services.log_parser_connect_timeout_s)
+    return service.LocalMatchService(build_match_engine(s, patterns), s.services.match_max_batch,
+                                     s.services.match_batch_wait_ms, metrics)

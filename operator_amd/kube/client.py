@@ -1,0 +1,254 @@
+"""HTTPS Kubernetes client (the role fabric8's KubernetesClient plays for the
+reference; the ``kubernetes`` Python package is not available offline).
+
+Same interface as FakeKube: get / list / create / replace / patch /
+patch_status / replace_status / delete / watch / pod_log.
+* config: in-cluster service account (token + CA + KUBERNETES_SERVICE_*), or a
+  kubeconfig (current-context; token, client cert, or CA data/file);
+* writes use JSON merge patch (``application/merge-patch+json``) and carry
+  ``metadata.resourceVersion`` when given, so a stale write gets 409 exactly
+  like fabric8's ``patch(latest)`` did;
+* watches stream newline-delimited JSON and surface a ``WatchClosed`` on
+  error / 410 Gone so callers restart (with resourceVersion resume).
+"""
+from __future__ import annotations
+
+import base64
+import json
+import logging
+import os
+import tempfile
+from typing import Any, Iterator
+from urllib.parse import urlencode
+
+import httpx
+import yaml
+
+from .resources import ApiError, Resource, WatchClosed, selector_to_string
+
+log = logging.getLogger(__name__)
+
+SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
+
+
+class KubeConfig:
+    def __init__(self, server: str, token: str | None = None, ca: str | bool | None = None,
+                 cert: tuple[str, str] | None = None, namespace: str = "default"):
+        self.server, self.token, self.ca, self.cert, self.namespace = server.rstrip("/"), token, ca, cert, namespace
+
+    @staticmethod
+    def in_cluster() -> "KubeConfig":
+        host, port = os.environ["KUBERNETES_SERVICE_HOST"], os.environ.get("KUBERNETES_SERVICE_PORT", "443")
+        with open(os.path.join(SA_DIR, "token")) as f:
+            token = f.read().strip()
+        ns = "default"
+        if os.path.exists(os.path.join(SA_DIR, "namespace")):
+            with open(os.path.join(SA_DIR, "namespace")) as f:
+                ns = f.read().strip()
+        if ":" in host:
+            host = f"[{host}]"
+        return KubeConfig(f"https://{host}:{port}", token, os.path.join(SA_DIR, "ca.crt"), None, ns)
+
+    @staticmethod
+    def from_kubeconfig(path: str | None = None, context: str | None = None) -> "KubeConfig":
+        path = path or os.environ.get("KUBECONFIG", os.path.expanduser("~/.kube/config"))
+        with open(path) as f:
+            kc = yaml.safe_load(f)
+        ctx_name = context or kc.get("current-context")
+        ctx = next(c["context"] for c in kc["contexts"] if c["name"] == ctx_name)
+        cluster = next(c["cluster"] for c in kc["clusters"] if c["name"] == ctx["cluster"])
+        user = next((u["user"] for u in kc.get("users", []) if u["name"] == ctx.get("user")), {}) or {}
+
+        def materialise(data_key: str, file_key: str, src: dict) -> str | None:
+            if src.get(data_key):
+                fd, p = tempfile.mkstemp(prefix="oamd-kube-")
+                with os.fdopen(fd, "wb") as f:
+                    f.write(base64.b64decode(src[data_key]))
+                return p
+            return src.get(file_key)
+
+        ca: str | bool | None = materialise("certificate-authority-data", "certificate-authority", cluster)
+        if cluster.get("insecure-skip-tls-verify"):
+            ca = False
+        cert = None
+        c, k = materialise("client-certificate-data", "client-certificate", user), \
+            materialise("client-key-data", "client-key", user)
+        if c and k:
+            cert = (c, k)
+        token = user.get("token")
+        if not token and user.get("tokenFile"):
+            with open(user["tokenFile"]) as f:
+                token = f.read().strip()
+        return KubeConfig(cluster["server"], token, ca, cert, ctx.get("namespace", "default"))
+
+
+class HttpWatch:
+    def __init__(self, client: "KubeClient", url: str, res: Resource):
+        self.client, self.url, self.res = client, url, res
+        self._cm = client.http.stream("GET", url, timeout=httpx.Timeout(None, connect=10.0))
+        self._resp = self._cm.__enter__()
+        if self._resp.status_code >= 400:
+            body = self._resp.read()
+            self._cm.__exit__(None, None, None)
+            raise _error(self._resp.status_code, body)
+        self._lines = self._resp.iter_lines()
+        self.closed = False
+
+    def __iter__(self) -> Iterator[tuple[str, dict]]:
+        return self
+
+    def __next__(self) -> tuple[str, dict]:
+        try:
+            while True:
+                line = next(self._lines)
+                if not line.strip():
+                    continue
+                ev = json.loads(line)
+                typ, obj = ev.get("type"), ev.get("object") or {}
+                if typ == "ERROR":
+                    raise WatchClosed(f"watch error: {obj.get('code')} {obj.get('message')}")
+                if typ == "BOOKMARK":
+                    continue
+                obj.setdefault("apiVersion", self.res.api_version)
+                obj.setdefault("kind", self.res.kind)
+                return typ, obj
+        except StopIteration:
+            self.close()
+            raise
+        except WatchClosed:
+            self.close()
+            raise
+        except (httpx.HTTPError, OSError) as e:
+            if self.closed:
+                raise StopIteration
+            self.close()
+            raise WatchClosed(str(e)) from e
+
+    def close(self) -> None:
+        if not self.closed:
+            self.closed = True
+            try:
+                self._cm.__exit__(None, None, None)
+            except Exception:  # noqa: BLE001
+                pass
+
+
+def _error(code: int, body: bytes | str) -> ApiError:
+    try:
+        j = json.loads(body)
+        return ApiError(code, j.get("message", ""), j.get("reason", ""))
+    except Exception:  # noqa: BLE001
+        return ApiError(code, body.decode() if isinstance(body, bytes) else str(body))
+
+
+class KubeClient:
+    def __init__(self, cfg: KubeConfig, timeout_s: float = 30.0):
+        self.cfg = cfg
+        headers = {"Accept": "application/json"}
+        if cfg.token:
+            headers["Authorization"] = f"Bearer {cfg.token}"
+        verify: Any = cfg.ca if cfg.ca is not None else True
+        self.http = httpx.Client(base_url=cfg.server, headers=headers, verify=verify, cert=cfg.cert,
+                                 timeout=timeout_s)
+
+    @staticmethod
+    def auto(mode: str = "auto", kubeconfig: str | None = None, timeout_s: float = 30.0) -> "KubeClient":
+        if mode in ("auto", "incluster") and os.environ.get("KUBERNETES_SERVICE_HOST") and \
+                os.path.exists(os.path.join(SA_DIR, "token")):
+            return KubeClient(KubeConfig.in_cluster(), timeout_s)
+        return KubeClient(KubeConfig.from_kubeconfig(kubeconfig), timeout_s)
+
+    # ------------------------------------------------------------------ helpers
+    def _req(self, method: str, url: str, **kw) -> Any:
+        r = self.http.request(method, url, **kw)
+        if r.status_code >= 400:
+            raise _error(r.status_code, r.content)
+        if not r.content:
+            return None
+        ctype = r.headers.get("content-type", "")
+        return r.json() if "json" in ctype else r.text
+
+    @staticmethod
+    def _with_kind(o: dict, res: Resource) -> dict:
+        o.setdefault("apiVersion", res.api_version)
+        o.setdefault("kind", res.kind)
+        return o
+
+    # ------------------------------------------------------------------ verbs
+    def get(self, res: Resource, name: str, namespace: str | None = None) -> dict | None:
+        try:
+            return self._with_kind(self._req("GET", f"{res.base_path(namespace)}/{name}"), res)
+        except ApiError as e:
+            if e.code == 404:
+                return None
+            raise
+
+    def list(self, res: Resource, namespace: str | None = None, label_selector: dict | str | None = None,
+             field_selector: str | None = None) -> list[dict]:
+        q = {}
+        if label_selector:
+            q["labelSelector"] = label_selector if isinstance(label_selector, str) else selector_to_string(label_selector)
+        if field_selector:
+            q["fieldSelector"] = field_selector
+        url = res.base_path(namespace) + (f"?{urlencode(q)}" if q else "")
+        items = (self._req("GET", url) or {}).get("items") or []
+        return [self._with_kind(o, res) for o in items]
+
+    def create(self, res: Resource, obj: dict, namespace: str | None = None) -> dict:
+        ns = namespace or (obj.get("metadata") or {}).get("namespace")
+        return self._req("POST", res.base_path(ns), json=self._with_kind(dict(obj), res))
+
+    def replace(self, res: Resource, obj: dict, namespace: str | None = None) -> dict:
+        ns = namespace or obj["metadata"].get("namespace")
+        return self._req("PUT", f"{res.base_path(ns)}/{obj['metadata']['name']}", json=obj)
+
+    def _merge(self, url: str, patch: dict, rv: str | None) -> dict:
+        if rv is not None:
+            patch = dict(patch)
+            patch["metadata"] = dict(patch.get("metadata") or {}, resourceVersion=str(rv))
+        return self._req("PATCH", url, content=json.dumps(patch),
+                         headers={"Content-Type": "application/merge-patch+json"})
+
+    def patch(self, res: Resource, name: str, namespace: str | None, patch: dict,
+              resource_version: str | None = None) -> dict:
+        return self._merge(f"{res.base_path(namespace)}/{name}", patch, resource_version)
+
+    def patch_status(self, res: Resource, name: str, namespace: str | None, status_patch: dict,
+                     resource_version: str | None = None) -> dict:
+        return self._merge(f"{res.base_path(namespace)}/{name}/status", {"status": status_patch}, resource_version)
+
+    def replace_status(self, res: Resource, obj: dict, namespace: str | None = None) -> dict:
+        ns = namespace or obj["metadata"].get("namespace")
+        return self._req("PUT", f"{res.base_path(ns)}/{obj['metadata']['name']}/status", json=obj)
+
+    def delete(self, res: Resource, name: str, namespace: str | None = None) -> bool:
+        try:
+            self._req("DELETE", f"{res.base_path(namespace)}/{name}")
+            return True
+        except ApiError as e:
+            if e.code == 404:
+                return False
+            raise
+
+    def watch(self, res: Resource, namespace: str | None = None, resource_version: str | None = None) -> HttpWatch:
+        q = {"watch": "1", "allowWatchBookmarks": "true"}
+        if resource_version:
+            q["resourceVersion"] = str(resource_version)
+        return HttpWatch(self, f"{res.base_path(namespace)}?{urlencode(q)}", res)
+
+    def pod_log(self, name: str, namespace: str, container: str | None = None, previous: bool = False,
+                tail_lines: int | None = None, limit_bytes: int | None = None) -> str:
+        q: dict[str, Any] = {}
+        if container:
+            q["container"] = container
+        if previous:
+            q["previous"] = "true"
+        if tail_lines is not None:
+            q["tailLines"] = tail_lines
+        if limit_bytes is not None:
+            q["limitBytes"] = limit_bytes
+        url = f"/api/v1/namespaces/{namespace}/pods/{name}/log" + (f"?{urlencode(q)}" if q else "")
+        r = self.http.get(url)
+        if r.status_code >= 400:
+            raise _error(r.status_code, r.content)
+        return r.text

@@ -16,8 +16,10 @@ def jstr(v) -> str:
 
 
 def fmt2(x: float) -> str:
-    """String.format("%.2f", double): exact binary value, HALF_UP (Java Formatter)."""
-    return str(Decimal(x).quantize(Decimal("0.01"), rounding=ROUND_HALF_UP))
+    """String.format("%.2f", double). Java's Formatter rounds HALF_UP starting from the
+    shortest round-trip decimal of the double (FormattedFloatingDecimal), so
+    0.675 -> "0.68" and 0.125 -> "0.13" (C printf would give 0.67 / 0.12)."""
+    return str(Decimal(repr(float(x))).quantize(Decimal("0.01"), rounding=ROUND_HALF_UP))
 
 
 def jtrim(s: str) -> str:
