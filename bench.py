@@ -1,0 +1,229 @@
+#!/usr/bin/env python3
+"""Flagship benchmark: pod-failure analyses/sec (whole node) + p50 explanation
+latency, Llama-3-8B explanation model at TP=1 per GPU, data-parallel over GPUs
+(BASELINE.json metric; config 4 "End-to-end: synthetic pod failures -> pattern
+match + 8B explanation, DP across 8xMI355X").
+
+One process per GPU (torchrun / ``python -m torch.distributed.run``), RCCL
+process group for the barrier + max-over-ranks timing. Each rank runs the
+full operator — FakeKube (in-memory API server) + pod watcher + analysis
+pipeline + GPU log scan (1k-pattern Aho-Corasick DFA) + Llama-3-8B bf16
+explanation on the gfx950 kernels (continuous batching, hipGraph decode) +
+result sinks (pod annotations, Podmortem status ring, Events).
+
+A *step* is one wave of ``--batch`` failures per GPU: the failed pods are
+written to FakeKube (MODIFIED events), the watcher picks them up, and the step
+ends when every failure's analysis + explanation is stored. Weak scaling:
+per-GPU work is fixed as N grows. Work per failure: one synthetic ~``--log-kb``
+KiB pod log scanned against the pattern library, a <= ``--prompt-tokens``
+prompt, ``--max-tokens`` (AIProvider default 500) generated tokens at
+temperature 0.3. Random-init weights (no checkpoints offline) => EOS is not
+meaningful, so generation always runs to maxTokens (``ignore_eos``).
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+METRIC = "pod-failure analyses/sec (whole node) + p50 explanation latency, 8B TP=1"
+
+
+def parse_args():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=256, help="failures per GPU per step")
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--max-tokens", type=int, default=500)
+    ap.add_argument("--prompt-tokens", type=int, default=1024, help="prompt budget (tokens)")
+    ap.add_argument("--log-kb", type=int, default=64)
+    ap.add_argument("--patterns", type=int, default=1000)
+    ap.add_argument("--max-batch", type=int, default=256, help="LLM continuous-batching width")
+    ap.add_argument("--mode", choices=["pipeline", "engine"], default="pipeline")
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--kv-gb", type=float, default=None, help="KV-cache budget (default 96 GB on GPU, 1 GB on CPU)")
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args()
+
+
+def main() -> int:
+    a = parse_args()
+    import torch
+    import torch.distributed as dist
+
+    from operator_amd.parallel.comm import init_from_env
+
+    info = init_from_env()
+    rank, world, local = info.rank, info.world, info.local_rank
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)
+    dev = f"cuda:{local}" if torch.cuda.is_available() else "cpu"
+
+    from operator_amd.config import load_settings
+    from operator_amd.controller.operator import Operator
+    from operator_amd.engine.explain import ExplainEngine
+    from operator_amd.engine.factory import build_llm
+    from operator_amd.engine.match import MatchEngine
+    from operator_amd.engine.service import LocalExplainService, LocalMatchService
+    from operator_amd.kube.fake import FakeKube, failed_pod, running_pod
+    from operator_amd.kube.resources import AIPROVIDERS, PODMORTEMS, PODS
+    from operator_amd.patterns.synth import LogFactory, synthetic_library
+
+    s = load_settings(env={}, overrides={
+        "engine.model": a.model, "engine.device": dev, "engine.max_batch": a.max_batch,
+        "engine.max_context": a.prompt_tokens + a.max_tokens + 64, "engine.max_prompt_tokens": a.prompt_tokens,
+        "engine.kv_cache_gb": a.kv_gb or (96.0 if dev != "cpu" else 1.0), "engine.use_graphs": not a.no_graphs, "engine.ignore_eos": True,
+        "engine.seed": 0, "health.enabled": False, "operator.workers": a.batch + 16, "operator.io_workers": 16,
+        "patterns.cache_dir": f"/tmp/oamd-bench-{os.getpid()}", "services.match_max_batch": max(a.batch, 64),
+        "services.match_batch_wait_ms": 5.0})
+
+    # ---- engines (weights, DFA, graphs) : not timed ----
+    t_init = time.perf_counter()
+    patset = synthetic_library(a.patterns, seed=0)
+    meng = MatchEngine(patset, device=dev, seg_bytes=s.patterns.seg_bytes)
+    model, kv, llm, tok = build_llm(s, device=dev)
+    llm.warmup([b for b in llm.buckets if b <= a.max_batch])
+    ee = ExplainEngine(llm, tok, model_id=a.model, max_prompt_tokens=a.prompt_tokens, ignore_eos=True)
+    explainer = LocalExplainService(ee)
+    init_s = time.perf_counter() - t_init
+
+    fac = LogFactory(n_patterns=a.patterns, seed=rank)
+    waves = a.warmup + a.steps
+    logs = [fac.batch(a.batch, a.log_kb * 1024, n_failures=3, seed=1000 * rank + w)[0] for w in range(waves)]
+
+    lat: list[float] = []
+    t_inject: dict[str, float] = {}
+    done_ev = threading.Event()
+    counter = {"n": 0, "target": 0, "outcomes": {}}
+    lock = threading.Lock()
+
+    if a.mode == "pipeline":
+        fk = FakeKube()
+        matcher = LocalMatchService(meng, max_batch=max(a.batch, 64), max_wait_ms=5.0)
+        op = Operator(fk, s, match_service=matcher, explain_service=explainer)
+        fk.create(AIPROVIDERS, {"metadata": {"name": "local-llm", "namespace": "default"},
+                                "spec": {"providerId": "local", "modelId": a.model, "maxTokens": a.max_tokens,
+                                         "temperature": 0.3, "cachingEnabled": False,
+                                         "timeoutSeconds": 3600}})
+        fk.create(PODMORTEMS, {"metadata": {"name": "bench-monitor", "namespace": "default"},
+                               "spec": {"podSelector": {"matchLabels": {"app": "bench"}}, "aiAnalysisEnabled": True,
+                                        "aiProviderRef": {"name": "local-llm"}}})
+
+        def on_done(monitor, pod, outcome):
+            name = pod["metadata"]["name"]
+            with lock:
+                lat.append(time.perf_counter() - t_inject.get(name, time.perf_counter()))
+                counter["n"] += 1
+                counter["outcomes"][outcome] = counter["outcomes"].get(outcome, 0) + 1
+                if counter["n"] >= counter["target"]:
+                    done_ev.set()
+
+        op.pipeline.listeners.append(on_done)
+        op.start(http=False)
+        while not op.monitors.list():
+            time.sleep(0.01)
+
+        def run_wave(w: int) -> None:
+            with lock:
+                counter["n"], counter["target"] = 0, a.batch
+                done_ev.clear()
+            names = [f"app-r{rank}-w{w}-{i}" for i in range(a.batch)]
+            for name, log in zip(names, logs[w]):
+                fk.create(PODS, running_pod(name, labels={"app": "bench"}))
+                fk.set_log("default", name, log)
+            now = time.perf_counter()
+            for name in names:
+                cur = fk.get(PODS, name, "default")
+                cur["status"] = failed_pod(name, finished_at=f"2025-08-29T10:{w % 60:02d}:00Z")["status"]
+                t_inject[name] = time.perf_counter()
+                fk.replace(PODS, cur)
+            done_ev.wait()
+            op.drain(600)
+    else:
+        from operator_amd.api.models import AIProviderConfig
+        from operator_amd.controller.storage import pattern_annotation
+
+        cfg = AIProviderConfig(provider_id="local", model_id=a.model, max_tokens=a.max_tokens, temperature=0.3,
+                               caching_enabled=False, timeout_seconds=3600)
+
+        def run_wave(w: int) -> None:
+            t0 = time.perf_counter()
+            res = meng.analyze(logs[w], [(f"app-{w}-{i}", "default") for i in range(a.batch)])
+            outs = ee.explain_many([(r, cfg) for r in res])
+            for r, o in zip(res, outs):
+                _ = pattern_annotation(r) if isinstance(o, Exception) else o.explanation
+                lat.append(time.perf_counter() - t0)
+            counter["outcomes"]["ai-complete"] = counter["outcomes"].get("ai-complete", 0) + len(outs)
+
+    for w in range(a.warmup):
+        run_wave(w)
+    lat.clear()
+    counter["outcomes"] = {}
+    stats0 = (llm.stats.prefill_tokens, llm.stats.decode_tokens)
+
+    def sync():
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    sync()
+    t0 = time.perf_counter()
+    for w in range(a.warmup, waves):
+        run_wave(w)
+    sync()
+    elapsed = time.perf_counter() - t0
+
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev if info.backend == "nccl" else "cpu")
+    p50_local = statistics.median(lat) if lat else float("nan")
+    p50 = torch.tensor([p50_local], dtype=torch.float64, device=el.device)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        dist.all_reduce(p50, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    total = a.batch * a.steps * world
+    value = total / elapsed
+    ptoks = llm.stats.prefill_tokens - stats0[0]
+    dtoks = llm.stats.decode_tokens - stats0[1]
+    out = {
+        "metric": METRIC, "value": round(value, 3), "unit": "analyses/s", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 2), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic pod logs (LogFactory) + random-init weights",
+        "p50_explanation_latency_ms": round(float(p50.item()) * 1e3, 1),
+        "config": {"model": a.model, "global_batch": a.batch * world, "seq_len": a.prompt_tokens + a.max_tokens,
+                   "parallelism": f"dp{world}", "tp": 1, "max_tokens": a.max_tokens,
+                   "prompt_tokens_cap": a.prompt_tokens, "log_kib": a.log_kb, "patterns": a.patterns,
+                   "mode": a.mode, "hipgraph": not a.no_graphs},
+        "detail": {"init_s": round(init_s, 1), "prefill_tokens_per_gpu": ptoks, "decode_tokens_per_gpu": dtoks,
+                   "decode_tok_s_per_gpu": round(dtoks / elapsed, 1), "outcomes": counter["outcomes"],
+                   "dfa_states": getattr(meng, "dfa_states", None)},
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                json.dump(out, f, indent=1)
+    if a.mode == "pipeline":
+        op.stop()
+    ee.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -46,6 +46,7 @@ class AnalysisPipeline:
         self.log_container, self.log_previous, self.log_limit_bytes = log_container, log_previous, log_limit_bytes
         self.completed = 0
         self.failed = 0
+        self.listeners: list = []  # callables (monitor, pod, outcome) after each finished analysis
 
     # ------------------------------------------------------------------ entry points
     def submit(self, monitor: dict, pod: dict) -> Future | None:
@@ -88,7 +89,15 @@ class AnalysisPipeline:
             self.metrics.stage_seconds.labels(stage="total").observe(time.perf_counter() - t0)
             self.metrics.analyses.labels(outcome=out).inc()
         self.completed += 1
+        self._notify(monitor, pod, out)
         return out
+
+    def _notify(self, monitor: dict, pod: dict, outcome: str) -> None:
+        for fn in self.listeners:
+            try:
+                fn(monitor, pod, outcome)
+            except Exception as e:  # noqa: BLE001
+                log.warning("pipeline listener failed: %s", e)
 
     def _fail(self, monitor: dict, pod: dict, message: str) -> None:
         self.failed += 1
@@ -96,6 +105,7 @@ class AnalysisPipeline:
         self.events.emit_analysis_error(pod, monitor, message)
         if self.metrics:
             self.metrics.analyses.labels(outcome="error").inc()
+        self._notify(monitor, pod, "error")
 
     # ------------------------------------------------------------------ branching (PodFailureWatcher.java:347-443)
     def handle_result(self, monitor: dict, pod: dict, result: AnalysisResult) -> str:
