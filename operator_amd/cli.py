@@ -1,0 +1,199 @@
+"""Command line: ``python -m operator_amd <command>``.
+
+  run            start the operator (kube watch + reconcilers + GPU engines + health)
+  manifests      print / write CRDs, RBAC and the Deployment (kubectl apply -f -)
+  scan           pattern-analyse log files -> AnalysisResult JSON
+  explain        scan + explain log files with the local LLM -> AIResponse JSON
+  serve-compat   REST server speaking the reference's log-parser / ai-interface contracts
+  bench          run bench.py (flagship benchmark)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import logging
+import os
+import signal
+import sys
+import threading
+
+
+def _settings(args):
+    from operator_amd.config import load_settings
+
+    ov = {}
+    for kv in args.set or []:
+        k, _, v = kv.partition("=")
+        import yaml
+
+        ov[k] = yaml.safe_load(v)
+    return load_settings(getattr(args, "config", None), overrides=ov)
+
+
+def _patterns(s, paths: list[str] | None):
+    from operator_amd.patterns.schema import PatternSet
+    from operator_amd.patterns.synth import catalog_library
+
+    ps = catalog_library() if s.patterns.builtin_catalog else PatternSet([], [])
+    for p in paths or []:
+        ps = ps.merged(PatternSet.load_dir(p) if os.path.isdir(p) else PatternSet.from_yaml_text(open(p).read()))
+    return ps
+
+
+def cmd_manifests(args) -> int:
+    from operator_amd.api.crds import render_all
+
+    text = render_all(namespace=args.namespace, image=args.image, gpus=args.gpus)
+    if args.out:
+        with open(args.out, "w") as f:
+            f.write(text)
+    else:
+        sys.stdout.write(text)
+    return 0
+
+
+def cmd_scan(args) -> int:
+    from operator_amd.engine.factory import build_match_engine
+
+    s = _settings(args)
+    if args.device:
+        s.engine.device = args.device
+        s.services.match = "cpu" if args.device == "cpu" else "local"
+    eng = build_match_engine(s, _patterns(s, args.patterns), device=args.device)
+    docs = [open(p, "rb").read() for p in args.logs]
+    res = eng.analyze(docs, [(os.path.basename(p), None) for p in args.logs])
+    print(json.dumps([r.to_obj() for r in res], indent=1))
+    return 0
+
+
+def cmd_explain(args) -> int:
+    from operator_amd.api.models import AIProviderConfig
+    from operator_amd.engine.explain import ExplainEngine
+    from operator_amd.engine.factory import build_llm, build_match_engine
+
+    s = _settings(args)
+    eng = build_match_engine(s, _patterns(s, args.patterns))
+    _, _, llm, tok = build_llm(s)
+    ee = ExplainEngine(llm, tok, model_id=s.engine.model, max_prompt_tokens=s.engine.max_prompt_tokens)
+    docs = [open(p, "rb").read() for p in args.logs]
+    res = eng.analyze(docs, [(os.path.basename(p), None) for p in args.logs])
+    cfg = AIProviderConfig(max_tokens=args.max_tokens, temperature=args.temperature)
+    outs = ee.explain_many([(r, cfg) for r in res])
+    print(json.dumps([o.to_obj() if hasattr(o, "to_obj") else {"error": str(o)} for o in outs], indent=1))
+    ee.close()
+    return 0
+
+
+def _build_services(s, metrics):
+    from operator_amd.engine.factory import build_explain_service, build_match_engine
+    from operator_amd.engine.service import LocalMatchService, RemoteLogParser
+
+    if s.services.match == "remote":
+        matcher = RemoteLogParser(s.services.log_parser_url, s.services.log_parser_read_timeout_s,
+                                  s.services.log_parser_connect_timeout_s)
+        factory = None
+    else:
+        factory = lambda ps: build_match_engine(s, ps)  # noqa: E731
+        matcher = None
+    explainer = build_explain_service(s, metrics)
+    return matcher, factory, explainer
+
+
+def cmd_run(args) -> int:
+    from operator_amd.controller.operator import Operator
+    from operator_amd.kube.client import KubeClient
+    from operator_amd.kube.fake import FakeKube
+    from operator_amd.utils.metrics import Metrics
+
+    s = _settings(args)
+    if s.kube.mode == "fake" or args.fake:
+        kube = FakeKube()
+    else:
+        kube = KubeClient.auto(s.kube.mode, s.kube.kubeconfig, s.kube.request_timeout_s)
+    metrics = Metrics()
+    matcher, factory, explainer = _build_services(s, metrics)
+    op = Operator(kube, s, match_service=matcher, explain_service=explainer, metrics=metrics,
+                  match_engine_factory=factory)
+    op.start()
+    stop = threading.Event()
+    signal.signal(signal.SIGTERM, lambda *_: stop.set())
+    signal.signal(signal.SIGINT, lambda *_: stop.set())
+    logging.getLogger(__name__).info("running; health on :%d", s.health.port)
+    stop.wait()
+    op.stop()
+    return 0
+
+
+def cmd_serve_compat(args) -> int:
+    from operator_amd.engine.server import CompatServer
+    from operator_amd.engine.service import LocalMatchService
+    from operator_amd.utils.metrics import Metrics
+
+    s = _settings(args)
+    metrics = Metrics()
+    matcher, factory, explainer = _build_services(s, metrics)
+    if matcher is None:
+        matcher = LocalMatchService(factory(_patterns(s, args.patterns)), metrics=metrics)
+    srv = CompatServer(matcher, explainer, s.health.host, args.port or s.health.port, metrics).start()
+    stop = threading.Event()
+    signal.signal(signal.SIGTERM, lambda *_: stop.set())
+    signal.signal(signal.SIGINT, lambda *_: stop.set())
+    stop.wait()
+    srv.stop()
+    return 0
+
+
+def cmd_bench(args, rest) -> int:
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    return subprocess.call([sys.executable, os.path.join(root, "bench.py"), *rest])
+
+
+def main(argv: list[str] | None = None) -> int:
+    logging.basicConfig(level=os.environ.get("PODMORTEM_LOG_LEVEL", "INFO"),
+                        format="%(asctime)s %(levelname)s %(name)s: %(message)s")
+    ap = argparse.ArgumentParser(prog="operator_amd", description=__doc__,
+                                 formatter_class=argparse.RawDescriptionHelpFormatter)
+    sub = ap.add_subparsers(dest="cmd", required=True)
+
+    def common(p):
+        p.add_argument("--config", default=None)
+        p.add_argument("--set", action="append", help="override, e.g. --set engine.model=tiny")
+
+    p = sub.add_parser("run")
+    common(p)
+    p.add_argument("--fake", action="store_true", help="in-memory FakeKube instead of a cluster")
+    p.add_argument("--gpus", type=int, default=1)
+    p = sub.add_parser("manifests")
+    p.add_argument("--namespace", default="podmortem-system")
+    p.add_argument("--image", default="ghcr.io/podmortem/operator-amd:latest")
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--out", default=None)
+    p = sub.add_parser("scan")
+    common(p)
+    p.add_argument("logs", nargs="+")
+    p.add_argument("--patterns", action="append", help="pattern YAML file or directory")
+    p.add_argument("--device", default=None)
+    p = sub.add_parser("explain")
+    common(p)
+    p.add_argument("logs", nargs="+")
+    p.add_argument("--patterns", action="append")
+    p.add_argument("--max-tokens", type=int, default=500)
+    p.add_argument("--temperature", type=float, default=0.3)
+    p = sub.add_parser("serve-compat")
+    common(p)
+    p.add_argument("--patterns", action="append")
+    p.add_argument("--port", type=int, default=None)
+    sub.add_parser("bench", add_help=False)
+    args, rest = ap.parse_known_args(argv)
+    if args.cmd == "bench":
+        return cmd_bench(args, rest)
+    if rest:
+        ap.error(f"unrecognized arguments: {rest}")
+    return {"run": cmd_run, "manifests": cmd_manifests, "scan": cmd_scan, "explain": cmd_explain,
+            "serve-compat": cmd_serve_compat}[args.cmd](args)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -88,9 +88,10 @@ class Group:
         """Gather equal-shaped tensors along a new leading dim: [world, *t.shape]."""
         if self.world == 1:
             return t.unsqueeze(0)
-        out = torch.empty((self.world, *t.shape), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(out, t.contiguous(), group=self.pg)
-        return out
+        t = t.contiguous()
+        out = torch.empty((self.world * t.shape[0], *t.shape[1:]), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t, group=self.pg)
+        return out.view(self.world, *t.shape)
 
     def broadcast_(self, t: torch.Tensor, src_local: int = 0) -> torch.Tensor:
         if self.world > 1:

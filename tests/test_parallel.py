@@ -1,0 +1,107 @@
+"""Tensor / data parallel logic on the CPU tier: gloo, world_size 2 (SURVEY.md §4.2
+"Distributed"). TP=2 must reproduce the TP=1 model (logits and greedy/sampled
+tokens), and the collective wrappers must behave like their definitions."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _tp_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from operator_amd.engine.llm import GenRequest, LLMEngine
+    from operator_amd.models.config import get_config
+    from operator_amd.models.kv_cache import PagedKVCache
+    from operator_amd.models.llama import ForwardBatch, LlamaModel
+    from operator_amd.parallel.comm import Group, init_from_env, split_groups
+
+    init_from_env(backend="gloo")
+    tp, dp = split_groups(world)
+    g = Group()
+    # collectives sanity
+    t = torch.tensor([float(rank + 1)])
+    g.all_reduce_(t)
+    assert t.item() == sum(range(1, world + 1))
+    ag = g.all_gather(torch.tensor([rank]), dim=0)
+    assert ag.tolist() == list(range(world))
+
+    cfg = get_config("tiny-gqa4")
+    m = LlamaModel(cfg, device="cpu", tp=tp, dtype=torch.float32).init_random(seed=9)
+    kv = PagedKVCache(cfg.layers, 64, m.hkv, cfg.head_dim, 16, device="cpu", dtype=torch.float32)
+    ids = torch.arange(3, 40) % cfg.vocab_size
+    T = ids.numel()
+    fb = ForwardBatch(ids, torch.arange(T), torch.full((T,), -1, dtype=torch.long), True, None, seq_lens=[T])
+    logits_local = m.forward(fb, kv)
+    logits = tp.all_gather(logits_local, dim=1)
+    eng = LLMEngine(m, kv, max_batch=4, max_context=256, use_graphs=False)
+    reqs = [GenRequest([5, 6, 7, 8], max_tokens=10, temperature=0.0, ignore_eos=True),
+            GenRequest(list(range(20, 45)), max_tokens=10, temperature=0.9, seed=4, ignore_eos=True)]
+    eng.generate(reqs)
+    if rank == 0:
+        torch.save({"logits": logits, "out": [r.output for r in reqs]}, os.path.join(out_dir, "tp.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_tp2_matches_tp1(tmp_path):
+    from operator_amd.engine.llm import GenRequest, LLMEngine
+    from operator_amd.models.config import get_config
+    from operator_amd.models.kv_cache import PagedKVCache
+    from operator_amd.models.llama import ForwardBatch, LlamaModel
+
+    port = _free_port()
+    mp.start_processes(_tp_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True, start_method="spawn")
+    got = torch.load(tmp_path / "tp.pt", weights_only=True)
+    cfg = get_config("tiny-gqa4")
+    m = LlamaModel(cfg, device="cpu", dtype=torch.float32).init_random(seed=9)
+    kv = PagedKVCache(cfg.layers, 64, cfg.kv_heads, cfg.head_dim, 16, device="cpu", dtype=torch.float32)
+    ids = torch.arange(3, 40) % cfg.vocab_size
+    T = ids.numel()
+    fb = ForwardBatch(ids, torch.arange(T), torch.full((T,), -1, dtype=torch.long), True, None, seq_lens=[T])
+    ref = m.forward(fb, kv)
+    torch.testing.assert_close(got["logits"], ref, atol=1e-4, rtol=1e-4)
+    eng = LLMEngine(m, kv, max_batch=4, max_context=256, use_graphs=False)
+    reqs = [GenRequest([5, 6, 7, 8], max_tokens=10, temperature=0.0, ignore_eos=True),
+            GenRequest(list(range(20, 45)), max_tokens=10, temperature=0.9, seed=4, ignore_eos=True)]
+    eng.generate(reqs)
+    assert got["out"] == [r.output for r in reqs]
+
+
+def _dp_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from operator_amd.parallel.dp import DPRouter
+    from operator_amd.parallel.comm import init_from_env
+
+    init_from_env(backend="gloo")
+    router = DPRouter()
+    items = [f"pod-{i}" for i in range(11)]
+    mine = router.shard(items)
+    results = [f"{x}@{rank}" for x in mine]
+    merged = router.gather(results)
+    if rank == 0:
+        torch.save(merged, os.path.join(out_dir, "dp.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_shard_and_gather(tmp_path):
+    port = _free_port()
+    mp.start_processes(_dp_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True, start_method="spawn")
+    merged = torch.load(tmp_path / "dp.pt", weights_only=True)
+    assert sorted(x.split("@")[0] for x in merged) == sorted(f"pod-{i}" for i in range(11))
+    assert {x.split("@")[1] for x in merged} == {"0", "1"}

@@ -1,0 +1,49 @@
+"""Decode-attention microbenchmark: time per call and effective HBM GB/s."""
+import argparse
+import json
+import math
+
+import torch
+
+from operator_amd import ops
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--batch", type=int, default=256)
+ap.add_argument("--ctx", type=str, default="545,1024,2048")
+ap.add_argument("--hq", type=int, default=32)
+ap.add_argument("--hkv", type=int, default=8)
+ap.add_argument("--page", type=int, default=64)
+ap.add_argument("--splits", type=str, default="need,8,16")
+ap.add_argument("--pages-total", type=int, default=0)
+a = ap.parse_args()
+D = 128
+for ctx in [int(c) for c in a.ctx.split(",")]:
+    B = a.batch
+    per = (ctx + a.page - 1) // a.page
+    total = a.pages_total or B * per + 8
+    kc = torch.randn(total, a.hkv, a.page, D, device="cuda", dtype=torch.bfloat16)
+    vc = torch.randn_like(kc)
+    bt = torch.arange(B * per, device="cuda", dtype=torch.int32).reshape(B, per)
+    sl = torch.full((B,), ctx, dtype=torch.int32, device="cuda")
+    q = torch.randn(B, a.hq, D, device="cuda", dtype=torch.bfloat16)
+    for sp in a.splits.split(","):
+        ns = ops.decode_splits(ctx) if sp == "need" else int(sp)
+        if ns * 256 < ctx:
+            continue
+        ws = (torch.empty(B * a.hq * ns * D, device="cuda"), torch.empty(B * a.hq * ns * 2, device="cuda"))
+        out = torch.empty_like(q)
+        for _ in range(3):
+            ops.attn_decode(q, kc, vc, bt, sl, 1 / math.sqrt(D), ns, out=out, workspace=ws)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
+        n = 20
+        e0.record()
+        for _ in range(n):
+            ops.attn_decode(q, kc, vc, bt, sl, 1 / math.sqrt(D), ns, out=out, workspace=ws)
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) / n * 1e3
+        byts = B * ctx * a.hkv * D * 2 * 2
+        print(json.dumps({"ctx": ctx, "B": B, "splits": ns, "us": round(us, 1), "GBps": round(byts / us / 1e3, 1)}),
+              flush=True)
+    del kc, vc
