@@ -33,12 +33,45 @@ __device__ __forceinline__ u16x8 ld16(const bf16_t* p) {
   return __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(p));
 }
 
+// Work list: one item per (sequence, 256-token split) that actually holds tokens,
+// built on the device from seq_lens so a captured graph needs no host data.
+// Empty workgroups are expensive (measured ~22 ns each: at B = 256 a grid sized
+// for the model's max context spent more time dispatching empty splits than
+// attending), so live items are packed first and the grid is sized by the
+// caller's per-call bound.
+// work[0] = total items, work[1 + i] = (b << 8) | split, i < total.
+__global__ void attn_decode_plan_kernel(const int* __restrict__ seq_lens, int B, int max_tokens, int num_splits,
+                                        int* __restrict__ work) {
+  __shared__ int pre[1025];
+  const int tid = threadIdx.x;
+  int total = 0;
+  for (int base = 0; base < B; base += 1024) {
+    const int b = base + tid;
+    int ns = 0;
+    if (b < B) {
+      const int len = min(seq_lens[b], max_tokens);
+      ns = min((len + kSplit - 1) / kSplit, num_splits);
+    }
+    pre[tid + 1] = ns;
+    if (tid == 0) pre[0] = 0;
+    __syncthreads();
+    if (tid == 0)
+      for (int i = 1; i <= 1024; ++i) pre[i] += pre[i - 1];
+    __syncthreads();
+    if (b < B)
+      for (int s = 0; s < ns; ++s) work[1 + total + pre[tid] + s] = (b << 8) | s;
+    total += pre[1024];
+    __syncthreads();
+  }
+  if (tid == 0) work[0] = total;
+}
+
 template <int G>
-__global__ void __launch_bounds__(256) attn_decode_kernel(
+__device__ __forceinline__ void attn_decode_item(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
     const int* __restrict__ block_tables, const int* __restrict__ seq_lens,
     bf16_t* __restrict__ out, float* __restrict__ o_part, float* __restrict__ ml_part, int Hkv,
-    int page_size, int log2_page, int max_pages, int num_splits, float scale_log2) {
+    int page_size, int log2_page, int max_pages, int num_splits, float scale_log2, int b, int s, int kvh) {
   constexpr int D = 128;
   constexpr int GP = (G < 4) ? 4 : G;  // score row stride (float4-aligned)
   __shared__ __attribute__((aligned(16))) float sc[kSplit * GP];   // [token][head]
@@ -47,18 +80,13 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(
 
   __shared__ int pg_lds[kSplit / 16 + 2];
 
-  const int s = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
   const int Hq = Hkv * G;
   const int len = min(seq_lens[b], max_pages * page_size);  // never index past the block table
   const int start = s * kSplit;
-  if (start >= len && !(num_splits == 1 && len == 0)) return;  // empty split: combine skips it
-  const int n = min(len - start, kSplit);
+  const int n = min(len - start, kSplit);  // >= 1: the plan only lists non-empty splits
+  const int ns_b = (len + kSplit - 1) / kSplit;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int l15 = lane & 15, lg = lane >> 4;
-  if (n <= 0) {  // empty sequence (single split): zero output
-    for (int e = tid; e < G * D; e += 256) out[((int64_t)b * Hq + kvh * G) * D + e] = 0;
-    return;
-  }
   // Stage this split's page ids in LDS. The data loads below then depend only on
   // LDS (lgkmcnt), so hipcc can issue all of them back to back; a per-token
   // global block-table load would share vmcnt with the data loads and force a
@@ -191,7 +219,7 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(
     const float o = red[(0 * G + h) * D + d] + red[(1 * G + h) * D + d] + red[(2 * G + h) * D + d] +
                     red[(3 * G + h) * D + d];
     const int hq = kvh * G + h;
-    if (num_splits == 1) {
+    if (ns_b == 1) {  // whole context in this split: final output, combine skips it
       const float l = lh[h];
       out[((int64_t)b * Hq + hq) * D + d] = f2bf(l > 0.f ? o / l : 0.f);
     } else {
@@ -205,6 +233,20 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(
   }
 }
 
+template <int G>
+__global__ void __launch_bounds__(256, (G <= 4 ? 3 : 2)) attn_decode_kernel(
+    const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+    const int* __restrict__ block_tables, const int* __restrict__ seq_lens,
+    bf16_t* __restrict__ out, float* __restrict__ o_part, float* __restrict__ ml_part, int Hkv,
+    int page_size, int log2_page, int max_pages, int num_splits, float scale_log2,
+    const int* __restrict__ work) {
+  const int wi = blockIdx.x;
+  if (wi >= work[0]) return;  // grid is sized for the host's bound; the plan may hold fewer items
+  const int item = work[1 + wi];
+  attn_decode_item<G>(q, kc, vc, block_tables, seq_lens, out, o_part, ml_part, Hkv, page_size, log2_page,
+                      max_pages, num_splits, scale_log2, item >> 8, item & 255, blockIdx.y);
+}
+
 // Combine the per-split partials: grid (B*Hq), block D threads.
 __global__ void attn_decode_combine_kernel(const float* __restrict__ o_part, const float* __restrict__ ml_part,
                                            const int* __restrict__ seq_lens, bf16_t* __restrict__ out, int Hq,
@@ -213,6 +255,11 @@ __global__ void attn_decode_combine_kernel(const float* __restrict__ o_part, con
   const int bh = blockIdx.x, b = bh / Hq, d = threadIdx.x;
   const int len = min(seq_lens[b], max_tokens);
   const int ns = min(num_splits, (len + kSplit - 1) / kSplit);
+  if (ns == 1) return;  // written directly by the attention kernel
+  if (ns == 0) {
+    out[(int64_t)bh * D + d] = 0;
+    return;
+  }
   const float* ml = ml_part + (int64_t)bh * num_splits * 2;
   float M = -INFINITY;
   for (int s = 0; s < ns; ++s) M = fmaxf(M, ml[2 * s]);
@@ -226,8 +273,8 @@ __global__ void attn_decode_combine_kernel(const float* __restrict__ o_part, con
 }
 
 int attn_decode(const bf16_t* q, const bf16_t* k_cache, const bf16_t* v_cache, const int* block_tables,
-                const int* seq_lens, bf16_t* out, float* o_part, float* ml_part, int B, int Hq, int Hkv,
-                int head_dim, int page_size, int max_pages, int num_splits, float scale,
+                const int* seq_lens, bf16_t* out, float* o_part, float* ml_part, int* work, int B, int Hq,
+                int Hkv, int head_dim, int page_size, int max_pages, int num_splits, float scale,
                 hipStream_t stream) {
   if (B == 0) return 0;
   if (head_dim != 128) return -1;
@@ -235,12 +282,19 @@ int attn_decode(const bf16_t* q, const bf16_t* k_cache, const bf16_t* v_cache, c
   int log2p = 0;
   while ((1 << log2p) < page_size) ++log2p;
   const int G = Hq / Hkv;
+  if (num_splits > 255) return -4;  // split index is packed in 8 bits
   const float scale_log2 = scale * 1.4426950408889634f;
-  dim3 grid(num_splits, Hkv, B);
+  attn_decode_plan_kernel<<<1, 1024, 0, stream>>>(seq_lens, B, max_pages * page_size, num_splits, work);
+  OAMD_LAUNCH_CHECK();
+  // One workgroup per (work item, kv head). num_splits is the caller's bound on the
+  // splits of the longest sequence in THIS call (not the model's max context): the
+  // engine captures one graph per bound, so the grid has no empty splits when the
+  // batch is length-uniform, and the packed work list keeps the live items first.
+  dim3 grid(B * num_splits, Hkv, 1);
 #define OAMD_DEC(GG)                                                                                 \
   attn_decode_kernel<GG><<<grid, 256, 0, stream>>>(q, k_cache, v_cache, block_tables, seq_lens, out, \
                                                    o_part, ml_part, Hkv, page_size, log2p, max_pages,  \
-                                                   num_splits, scale_log2)
+                                                   num_splits, scale_log2, work)
   switch (G) {
     case 1: OAMD_DEC(1); break;
     case 2: OAMD_DEC(2); break;
@@ -250,11 +304,9 @@ int attn_decode(const bf16_t* q, const bf16_t* k_cache, const bf16_t* v_cache, c
   }
 #undef OAMD_DEC
   OAMD_LAUNCH_CHECK();
-  if (num_splits > 1) {
-    attn_decode_combine_kernel<<<B * Hq, 128, 0, stream>>>(o_part, ml_part, seq_lens, out, Hq, num_splits,
-                                                           max_pages * page_size);
-    OAMD_LAUNCH_CHECK();
-  }
+  attn_decode_combine_kernel<<<B * Hq, 128, 0, stream>>>(o_part, ml_part, seq_lens, out, Hq, num_splits,
+                                                         max_pages * page_size);
+  OAMD_LAUNCH_CHECK();
   return 0;
 }
 

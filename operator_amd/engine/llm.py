@@ -75,10 +75,10 @@ def _buckets(max_batch: int) -> list[int]:
     return out
 
 
-class _DecodeGraph:
-    """Device-resident decode state for one batch bucket + its captured step.
+class _BucketState:
+    """Device-resident decode state of one batch bucket (shared by its graphs).
 
-    One replay = forward + sample + state advance (ids <- sampled token,
+    One step = forward + sample + state advance (ids <- sampled token,
     pos/ctx += 1 on active rows, token appended to ``hist[:, step]``), so the
     host can replay several steps back-to-back and read ``hist`` once.
     Rows with ctx == 0 are padding: slot -1 (no KV write), zero attention.
@@ -95,42 +95,6 @@ class _DecodeGraph:
         self.seeds = torch.zeros(bp, dtype=torch.long, device=dev)
         self.hist = torch.zeros(bp, eng.multi_step, dtype=torch.long, device=dev)
         self.step = torch.zeros(1, dtype=torch.long, device=dev)
-        self.graph: torch.cuda.CUDAGraph | None = None
-        self.eng = eng
-
-    def _run(self) -> None:
-        e = self.eng
-        P = e.kv.page_size
-        act = self.ctx > 0
-        pg = torch.gather(self.bt, 1, torch.clamp(self.pos // P, max=e.max_pages - 1).unsqueeze(1)).squeeze(1)
-        slots = torch.where(act, pg.to(torch.long) * P + self.pos % P, torch.full_like(self.pos, -1))
-        fb = ForwardBatch(self.ids, self.pos, slots, False, None, block_tables=self.bt, context_lens=self.ctx,
-                          num_splits=e.num_splits)
-        logits = e.model.forward(fb, e.kv)
-        tok = e.model.sample(logits, self.temp, self.seeds, self.pos + 1)
-        self.ids.copy_(tok)
-        self.hist.index_copy_(1, self.step, tok.unsqueeze(1))
-        self.pos.add_(act.to(torch.long))
-        self.ctx.add_(act.to(torch.int32))
-        self.step.add_(1)
-
-    def capture(self, pool) -> None:
-        # warm up on a side stream (allocator + hipBLASLt heuristics), then capture
-        snap = [t.clone() for t in (self.ids, self.pos, self.ctx)]
-        s = torch.cuda.Stream(device=self.eng.device)
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            for _ in range(2):
-                self.step.zero_()
-                self._run()
-        torch.cuda.current_stream().wait_stream(s)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, pool=pool):
-            self._run()
-        self.graph = g
-        for t, v in zip((self.ids, self.pos, self.ctx), snap):
-            t.copy_(v)
-        self.step.zero_()
 
     def load(self, reqs: list[GenRequest], max_pages: int) -> None:
         """Write the per-row state of ``reqs`` (rows beyond are padding)."""
@@ -153,6 +117,53 @@ class _DecodeGraph:
                          (self.seeds, seeds)):
             dst.copy_(src.pin_memory() if nb else src, non_blocking=nb)
 
+
+class _DecodeGraph:
+    """One decode step over a bucket's state, with the attention grid sized for
+    ``splits`` (the bound on 256-token splits of the longest sequence)."""
+
+    def __init__(self, eng: "LLMEngine", st: _BucketState, splits: int):
+        self.eng, self.st, self.splits = eng, st, splits
+        self.graph: torch.cuda.CUDAGraph | None = None
+
+    def _run(self) -> None:
+        e, st = self.eng, self.st
+        P = e.kv.page_size
+        act = st.ctx > 0
+        pg = torch.gather(st.bt, 1, torch.clamp(st.pos // P, max=e.max_pages - 1).unsqueeze(1)).squeeze(1)
+        slots = torch.where(act, pg.to(torch.long) * P + st.pos % P, torch.full_like(st.pos, -1))
+        fb = ForwardBatch(st.ids, st.pos, slots, False, None, block_tables=st.bt, context_lens=st.ctx,
+                          num_splits=self.splits)
+        logits = e.model.forward(fb, e.kv)
+        tok = e.model.sample(logits, st.temp, st.seeds, st.pos + 1)
+        st.ids.copy_(tok)
+        st.hist.index_copy_(1, st.step, tok.unsqueeze(1))
+        st.pos.add_(act.to(torch.long))
+        st.ctx.add_(act.to(torch.int32))
+        st.step.add_(1)
+
+    def capture(self, pool) -> None:
+        # warm up on a side stream (allocator + hipBLASLt heuristics), then capture; the
+        # state is snapshotted and restored so capture never perturbs live rows
+        st = self.st
+        snap = [t.clone() for t in (st.ids, st.pos, st.ctx, st.step)]
+        s = torch.cuda.Stream(device=self.eng.device)
+        s.wait_stream(torch.cuda.current_stream())
+        saved_ctx = st.ctx.clone()
+        st.ctx.zero_()  # all rows padding while warming up: no KV writes
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                st.step.zero_()
+                self._run()
+        torch.cuda.current_stream().wait_stream(s)
+        st.ctx.copy_(torch.zeros_like(saved_ctx))
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, pool=pool):
+            self._run()
+        self.graph = g
+        for t, v in zip((st.ids, st.pos, st.ctx, st.step), snap):
+            t.copy_(v)
+
     def run(self, use_graph: bool) -> None:
         if use_graph and self.graph is not None:
             self.graph.replay()
@@ -172,12 +183,13 @@ class LLMEngine:
         self.num_splits = ops.decode_splits(self.max_context)
         self.use_graphs = use_graphs and self.device.type == "cuda"
         self.multi_step = max(1, multi_step)
-        self._active: _DecodeGraph | None = None   # bucket whose device state matches self.running
+        self._active: _BucketState | None = None   # bucket whose device state matches self.running
         self.waiting: deque[GenRequest] = deque()
         self.running: list[GenRequest] = []
         self.stats = EngineStats()
         self._rid = itertools.count()
-        self._graphs: dict[int, _DecodeGraph] = {}
+        self._graphs: dict[tuple[int, int], _DecodeGraph] = {}
+        self._states: dict[int, _BucketState] = {}
         self._pool = None
         self.buckets = _buckets(max_batch)
         self.eos = set(model.cfg.eos_ids)
@@ -217,12 +229,17 @@ class LLMEngine:
             self.step()
         return reqs
 
-    def warmup(self, buckets: list[int] | None = None) -> None:
-        """Capture decode graphs ahead of time (largest first so they share one pool)."""
+    def warmup(self, buckets: list[int] | None = None, splits: list[int] | None = None) -> None:
+        """Capture decode graphs ahead of time (largest first so they share one pool).
+        ``splits`` defaults to every split bound up to max_context for the largest
+        bucket and to the single-split bound for the others."""
         if not self.use_graphs:
             return
-        for bp in sorted(buckets or self.buckets, reverse=True):
-            self._graph(bp)
+        bs = sorted(buckets or self.buckets, reverse=True)
+        for i, bp in enumerate(bs):
+            for ns in (splits or (range(1, self.num_splits + 1) if i == 0 else [1, 2])):
+                if 1 <= ns <= self.num_splits:
+                    self._graph(bp, ns)
         torch.cuda.synchronize(self.device)
 
     # ------------------------------------------------------------------ scheduling
@@ -291,33 +308,41 @@ class LLMEngine:
         self.stats.prefill_tokens += len(ids)
         self.stats.prefill_s += now - t0
 
-    def _graph(self, bp: int) -> _DecodeGraph:
-        g = self._graphs.get(bp)
+    def _state(self, bp: int) -> _BucketState:
+        st = self._states.get(bp)
+        if st is None:
+            st = self._states[bp] = _BucketState(self, bp)
+        return st
+
+    def _graph(self, bp: int, splits: int) -> _DecodeGraph:
+        g = self._graphs.get((bp, splits))
         if g is None:
-            g = _DecodeGraph(self, bp)
+            g = _DecodeGraph(self, self._state(bp), splits)
             if self.use_graphs:
                 if self._pool is None:
                     self._pool = torch.cuda.graph_pool_handle()
                 g.capture(self._pool)
-            self._graphs[bp] = g
+            self._graphs[(bp, splits)] = g
         return g
 
     def _decode(self) -> None:
         """Up to ``multi_step`` decode steps with no host round trip in between."""
         t0 = time.perf_counter()
         B = len(self.running)
-        g = self._active
-        if g is None:
-            bp = next(b for b in self.buckets if b >= B)
-            g = self._graph(bp)
-            g.load(self.running, self.max_pages)
-            self._active = g
+        bp = next(b for b in self.buckets if b >= B)
         k = min(self.multi_step, min(r.max_tokens - len(r.output) for r in self.running))
         k = max(1, k)
-        g.step.zero_()
+        # attention grid bound: splits of the longest context reached in this window
+        splits = min(self.num_splits, ops.decode_splits(max(r.length for r in self.running) + k - 1))
+        g = self._graph(bp, splits)
+        st = g.st
+        if self._active is not st:
+            st.load(self.running, self.max_pages)
+            self._active = st
+        st.step.zero_()
         for _ in range(k):
             g.run(self.use_graphs)
-        toks = g.hist[:B, :k].tolist()
+        toks = st.hist[:B, :k].tolist()
         for r, row in zip(self.running, toks):
             for tk in row:
                 if r.done_pending:

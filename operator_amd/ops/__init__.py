@@ -14,6 +14,7 @@ from ._native import kernels, native_available, patterns
 __all__ = [
     "rmsnorm", "silu_mul", "embedding", "rope_kv", "attn_prefill", "attn_decode", "sample",
     "kernels", "patterns", "native_available", "reference", "prefill_work_list", "decode_splits",
+    "decode_workspace",
 ]
 
 DECODE_SPLIT_TOKENS = 256  # must match kSplit in csrc/kernels/attn_decode.hip
@@ -119,6 +120,14 @@ def decode_splits(max_context: int) -> int:
     return max(1, (int(max_context) + DECODE_SPLIT_TOKENS - 1) // DECODE_SPLIT_TOKENS)
 
 
+def decode_workspace(B: int, Hq: int, num_splits: int, device, D: int = 128):
+    """(o_part fp32, ml_part fp32, work list int32) buffers for attn_decode."""
+    n = max(1, B * Hq * num_splits)
+    return (torch.empty(n * D, dtype=torch.float32, device=device),
+            torch.empty(n * 2, dtype=torch.float32, device=device),
+            torch.empty(B * num_splits + 1, dtype=torch.int32, device=device))
+
+
 def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
                 seq_lens: torch.Tensor, scale: float, num_splits: int, out: torch.Tensor | None = None,
                 workspace: tuple[torch.Tensor, torch.Tensor] | None = None) -> torch.Tensor:
@@ -132,11 +141,9 @@ def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, b
     B, Hq, D = q.shape
     o = out if out is not None else torch.empty_like(q)
     if workspace is None:
-        n = max(1, B * Hq * num_splits)
-        workspace = (torch.empty(n * D, dtype=torch.float32, device=q.device),
-                     torch.empty(n * 2, dtype=torch.float32, device=q.device))
+        workspace = decode_workspace(B, Hq, num_splits, q.device)
     kernels().attn_decode(q, k_cache, v_cache, block_tables, seq_lens, o, workspace[0], workspace[1],
-                          num_splits, scale)
+                          workspace[2], num_splits, scale)
     return o
 
 

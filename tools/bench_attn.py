@@ -30,7 +30,7 @@ for ctx in [int(c) for c in a.ctx.split(",")]:
         ns = ops.decode_splits(ctx) if sp == "need" else int(sp)
         if ns * 256 < ctx:
             continue
-        ws = (torch.empty(B * a.hq * ns * D, device="cuda"), torch.empty(B * a.hq * ns * 2, device="cuda"))
+        ws = ops.decode_workspace(B, a.hq, ns, "cuda")
         out = torch.empty_like(q)
         for _ in range(3):
             ops.attn_decode(q, kc, vc, bt, sl, 1 / math.sqrt(D), ns, out=out, workspace=ws)
