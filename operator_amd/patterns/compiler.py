@@ -159,7 +159,49 @@ def compile_patterns(ps: PatternSet, build_dfa: bool = True) -> CompiledPatterns
 
     cp = CompiledPatterns(ps, matchers, prim, secs, factors, fmat, verify, unfiltered, regexes)
     if build_dfa and factors:
-        from operator_amd.ops._native import patterns as native
-
-        cp.dfa = native().compile_dfa(factors)
+        cp.dfa = compile_dfa_cached(factors)
     return cp
+
+
+def _cache_dir():
+    import os
+    from pathlib import Path
+
+    return Path(os.environ.get("OAMD_CACHE_DIR", Path(__file__).resolve().parent.parent / ".cache")) / "dfa"
+
+
+def compile_dfa_cached(factors: list[bytes]) -> dict:
+    """Native DFA compile with an on-disk cache keyed by the factor set (restarts and
+    PatternLibrary re-syncs with unchanged patterns skip the compile)."""
+    import hashlib
+    import json
+    import os
+
+    from operator_amd.ops._native import patterns as native
+
+    h = hashlib.sha256(b"dfa-v1\0" + b"\0".join(factors)).hexdigest()[:24]
+    f = _cache_dir() / f"{h}.npz"
+    if f.exists():
+        try:
+            import numpy as np
+
+            z = np.load(f, allow_pickle=False)
+            d = json.loads(bytes(z["meta"]).decode())
+            for k in ("cls_map", "table", "out_off", "out_ids"):
+                d[k] = z[k].tobytes()
+            return d
+        except Exception:  # noqa: BLE001 - corrupt cache entry: recompile
+            pass
+    d = native().compile_dfa(factors)
+    try:
+        import numpy as np
+
+        f.parent.mkdir(parents=True, exist_ok=True)
+        meta = {k: v for k, v in d.items() if k not in ("cls_map", "table", "out_off", "out_ids")}
+        tmp = f.with_suffix(f".{os.getpid()}.tmp.npz")
+        np.savez(tmp, meta=np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8),
+                 **{k: np.frombuffer(d[k], dtype=np.uint8) for k in ("cls_map", "table", "out_off", "out_ids")})
+        os.replace(tmp, f)
+    except OSError:
+        pass
+    return d

@@ -31,15 +31,18 @@ def bench_llm(model_name, batches, ctx, prompt_len, max_context):
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         n = 0
+        gen0 = sum(len(r.output) for r in reqs)
         while eng.running:
             eng.step()
             n += 1
         torch.cuda.synchronize()
         t2 = time.perf_counter()
+        toks = sum(len(r.output) for r in reqs) - gen0
         print(json.dumps({"bench": "llm", "model": model_name, "batch": B, "prompt": prompt_len,
                           "prefill_s": round(t1 - t0, 4), "prefill_tok_s": round(B * prompt_len / (t1 - t0), 1),
-                          "decode_steps": n, "decode_ms_per_step": round((t2 - t1) / max(n, 1) * 1e3, 3),
-                          "decode_tok_s": round(B * n / (t2 - t1), 1)}), flush=True)
+                          "engine_steps": n, "decode_tokens": toks,
+                          "ms_per_token_step": round((t2 - t1) / max(toks / B, 1) * 1e3, 3),
+                          "decode_tok_s": round(toks / (t2 - t1), 1)}), flush=True)
 
 
 def bench_scan(n_docs, doc_kb, n_patterns):
