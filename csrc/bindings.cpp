@@ -107,7 +107,7 @@ void rope_kv(const at::Tensor& qkv, const at::Tensor& pos, const at::Tensor& cos
 
 void attn_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                  const at::Tensor& block_tables, const at::Tensor& seq_lens, at::Tensor& out,
-                 at::Tensor& o_part, at::Tensor& ml_part, at::Tensor& work, int64_t num_splits, double scale) {
+                 at::Tensor& o_part, at::Tensor& ml_part, int64_t num_splits, double scale, int64_t variant) {
   CHECK_DEV(q); CHECK_BF16(q); CHECK_CONTIG(q); CHECK_BF16(out); CHECK_CONTIG(out);
   CHECK_BF16(k_cache); CHECK_BF16(v_cache); CHECK_CONTIG(k_cache); CHECK_CONTIG(v_cache);
   CHECK_DT(block_tables, at::kInt); CHECK_CONTIG(block_tables); CHECK_DT(seq_lens, at::kInt); CHECK_CONTIG(seq_lens);
@@ -120,18 +120,16 @@ void attn_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tenso
   TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) == B && seq_lens.numel() == B, "tables shape");
   TORCH_CHECK(out.numel() == B * Hq * D, "out shape");
   TORCH_CHECK(num_splits >= 1, "num_splits >= 1");
-  TORCH_CHECK(num_splits <= 255, "num_splits must be <= 255");
-  TORCH_CHECK(o_part.numel() >= B * Hq * num_splits * D && ml_part.numel() >= B * Hq * num_splits * 2,
+  TORCH_CHECK(block_tables.size(1) <= 1024, "at most 1024 pages per sequence");
+  TORCH_CHECK(num_splits == 1 ||
+                  (o_part.numel() >= B * Hq * num_splits * D && ml_part.numel() >= B * Hq * num_splits * 2),
               "partial buffers too small");
-  CHECK_DT(work, at::kInt); CHECK_CONTIG(work);
-  TORCH_CHECK(work.numel() >= B * num_splits + 1, "work list buffer too small");
-  TORCH_CHECK(B <= (1 << 23), "batch too large for the packed work list");
+  TORCH_CHECK(B * num_splits < (1LL << 31), "grid too large");
   const c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
   RC(oamd::attn_decode(ptr<bf16_t>(q), ptr<bf16_t>(k_cache), ptr<bf16_t>(v_cache), ptr<int>(block_tables),
-                       ptr<int>(seq_lens), ptr<bf16_t>(out), ptr<float>(o_part), ptr<float>(ml_part),
-                       ptr<int>(work), (int)B,
+                       ptr<int>(seq_lens), ptr<bf16_t>(out), ptr<float>(o_part), ptr<float>(ml_part), (int)B,
                        (int)Hq, (int)Hkv, (int)D, (int)page, (int)block_tables.size(1), (int)num_splits,
-                       (float)scale, cur_stream()));
+                       (float)scale, (int)variant, cur_stream()));
 }
 
 void attn_prefill(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor& o,

@@ -1,20 +1,24 @@
-// Paged decode attention, split-KV ("flash-decoding"), GQA.
+// Paged decode attention, GQA, streaming split-KV.
 //
-// One query token per sequence. Workgroup = (split of 256 cached tokens,
-// kv-head, sequence); the G = Hq/Hkv query heads sharing the kv-head are
-// processed together so every K/V row is read from HBM exactly once.
-// This op is HBM-bound (B x ctx x Hkv x 512 B per layer), so the structure is
-// built around bytes in flight, not arithmetic:
-//   * every lane issues ALL of its K loads (16 x 16 B) and V loads (16 x 16 B)
-//     at kernel entry — 64 KiB of K+V per workgroup in flight — and the
-//     QK^T, softmax and PV work then runs under that traffic;
-//   * S = K Q^T runs on MFMA (v_mfma_f32_16x16x32_bf16, K tile = A operand,
-//     the G query heads zero-padded to 16 columns = B operand), so no
-//     cross-lane reduction is needed for the dot products;
-//   * softmax is two-pass over the split (max, then exp2/sum) in LDS — no
-//     online rescaling; PV runs on the VALU (16 B V rows per lane, P read as
-//     one ds_read_b128 per token for G = 4) and reduces over the 4 token
-//     sub-slots with 2 xor-shuffles.
+// One query token per sequence. Workgroup = (sequence, split, kv-head); the
+// G = Hq/Hkv query heads sharing the kv-head are processed together so every
+// K/V row is read from HBM exactly once. The op is HBM-bound
+// (B x ctx x Hkv x 512 B per layer), so the structure is built around keeping
+// bytes in flight for the WHOLE life of a workgroup:
+//   * a workgroup walks its token range in chunks of 4 x TW tokens (TW per
+//     wave), with the K/V registers double-buffered: the loads of chunk c+1
+//     are issued before chunk c is consumed (counted vmcnt, no drain), so
+//     there is no per-chunk load/compute bubble;
+//   * the per-call split count is chosen by the host so that only small
+//     batches are split (B x Hkv workgroups already fill 256 CUs at B >= 128):
+//     at serving batch sizes there is no partial output, no combine kernel and
+//     no per-call planning kernel at all;
+//   * each wave runs its own online softmax (running max / sum per head kept
+//     per lane, rescale factors broadcast with v_readlane) — no block barrier
+//     inside the loop; the 4 waves are merged once at the end through LDS;
+//   * S = K Q^T on MFMA (v_mfma_f32_16x16x32_bf16, K tile = A operand, the G
+//     heads zero-padded to 16 columns = B operand); P V on the VALU from the V
+//     rows already in registers (16 B per lane, P read back as float4).
 // Fragment maps (cdna_hip_programming.md §3): A lane l -> A[l&15][8(l>>4)+j];
 // B lane l -> B[8(l>>4)+j][l&15]; C col = l&15, row = 4(l>>4)+r. The dims of a
 // k-step are permuted so lane group g covers dims 32g..32g+31 over the 4
@@ -25,7 +29,7 @@
 
 namespace oamd {
 
-constexpr int kSplit = 256;  // tokens per split == threads per block
+constexpr int kMaxPagesLds = 1024;  // page ids of one split staged in LDS
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 
@@ -33,169 +37,184 @@ __device__ __forceinline__ u16x8 ld16(const bf16_t* p) {
   return __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(p));
 }
 
-// Work list: one item per (sequence, 256-token split) that actually holds tokens,
-// built on the device from seq_lens so a captured graph needs no host data.
-// Empty workgroups are expensive (measured ~22 ns each: at B = 256 a grid sized
-// for the model's max context spent more time dispatching empty splits than
-// attending), so live items are packed first and the grid is sized by the
-// caller's per-call bound.
-// work[0] = total items, work[1 + i] = (b << 8) | split, i < total.
-__global__ void attn_decode_plan_kernel(const int* __restrict__ seq_lens, int B, int max_tokens, int num_splits,
-                                        int* __restrict__ work) {
-  __shared__ int pre[1025];
-  const int tid = threadIdx.x;
-  int total = 0;
-  for (int base = 0; base < B; base += 1024) {
-    const int b = base + tid;
-    int ns = 0;
-    if (b < B) {
-      const int len = min(seq_lens[b], max_tokens);
-      ns = min((len + kSplit - 1) / kSplit, num_splits);
-    }
-    pre[tid + 1] = ns;
-    if (tid == 0) pre[0] = 0;
-    __syncthreads();
-    if (tid == 0)
-      for (int i = 1; i <= 1024; ++i) pre[i] += pre[i - 1];
-    __syncthreads();
-    if (b < B)
-      for (int s = 0; s < ns; ++s) work[1 + total + pre[tid] + s] = (b << 8) | s;
-    total += pre[1024];
-    __syncthreads();
-  }
-  if (tid == 0) work[0] = total;
+// Token range of split s of a sequence of `len` tokens cut into at most
+// `num_splits` pieces of a multiple of `chunk` tokens. Shared with the combine
+// kernel so both agree on how many splits a sequence really has.
+__device__ __forceinline__ int split_len(int len, int num_splits, int chunk) {
+  const int per = (len + num_splits - 1) / num_splits;
+  return (per + chunk - 1) / chunk * chunk;
 }
 
-template <int G>
-__device__ __forceinline__ void attn_decode_item(
+template <int NT>
+struct KVRegs {
+  u16x8 k[NT][4];   // K tile i: token 16i + l15, dims 32*lg + 8*ks
+  u16x8 v[4 * NT];  // token 4*it + lg, dims 8*l15
+};
+
+template <int G, int NT>
+__global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2) attn_decode_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
-    const int* __restrict__ block_tables, const int* __restrict__ seq_lens,
-    bf16_t* __restrict__ out, float* __restrict__ o_part, float* __restrict__ ml_part, int Hkv,
-    int page_size, int log2_page, int max_pages, int num_splits, float scale_log2, int b, int s, int kvh) {
+    const int* __restrict__ block_tables, const int* __restrict__ seq_lens, bf16_t* __restrict__ out,
+    float* __restrict__ o_part, float* __restrict__ ml_part, int Hkv, int page_size, int log2_page,
+    int max_pages, int num_splits, float scale_log2) {
   constexpr int D = 128;
-  constexpr int GP = (G < 4) ? 4 : G;  // score row stride (float4-aligned)
-  __shared__ __attribute__((aligned(16))) float sc[kSplit * GP];   // [token][head]
-  __shared__ __attribute__((aligned(16))) float red[4 * G * D];
-  __shared__ float wred[4][G];
+  constexpr int TW = 16 * NT;  // tokens per wave per chunk
+  constexpr int CH = 4 * TW;   // tokens per workgroup per chunk
+  constexpr int GP = (G < 4) ? 4 : G;
+  __shared__ int pg_lds[kMaxPagesLds];
+  __shared__ __attribute__((aligned(16))) float pw[4][TW * GP];  // per-wave P tile [token][head]
+  __shared__ __attribute__((aligned(16))) float red[4][G][D];
+  __shared__ float mls[4][G][2];
 
-  __shared__ int pg_lds[kSplit / 16 + 2];
-
+  const int b = blockIdx.x / num_splits, s = blockIdx.x - b * num_splits, kvh = blockIdx.y;
   const int Hq = Hkv * G;
   const int len = min(seq_lens[b], max_pages * page_size);  // never index past the block table
-  const int start = s * kSplit;
-  const int n = min(len - start, kSplit);  // >= 1: the plan only lists non-empty splits
-  const int ns_b = (len + kSplit - 1) / kSplit;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int l15 = lane & 15, lg = lane >> 4;
-  // Stage this split's page ids in LDS. The data loads below then depend only on
-  // LDS (lgkmcnt), so hipcc can issue all of them back to back; a per-token
-  // global block-table load would share vmcnt with the data loads and force a
-  // vmcnt(0) before every one of them.
-  const int page0 = start >> log2_page;
-  const int npg = min(((start + n - 1) >> log2_page) - page0 + 1, kSplit / 16 + 2);
-  if (tid < npg) pg_lds[tid] = block_tables[(int64_t)b * max_pages + page0 + tid];
-  __syncthreads();
-  auto row_off = [&](int t) -> int64_t {  // t already clamped to [0, n)
-    const int tok = start + t;
-    const int64_t page = pg_lds[(tok >> log2_page) - page0];
-    return ((page * Hkv + kvh) * page_size + (tok & (page_size - 1))) * (int64_t)D;
-  };
+  if (len <= 0) {  // padding row: zero output (written once, by split 0)
+    if (s == 0)
+      for (int e = tid; e < G * D; e += 256) out[((int64_t)b * Hq + kvh * G) * D + e] = 0;
+    return;
+  }
+  const int per = split_len(len, num_splits, CH);
+  const int start = s * per;
+  if (start >= len) return;  // this sequence has fewer splits than the grid
+  const int end = min(len, start + per);
+  const int ns_b = (len + per - 1) / per;
+  const int nch = (end - start + CH - 1) / CH;
 
-  // ---- q first (the first MFMA needs it), as the B operand: column = head ----
+  // Page ids of the split -> LDS: the data loads then depend only on LDS
+  // (lgkmcnt), never on a global load that would share vmcnt with them.
+  const int page0 = start >> log2_page;
+  const int npg = ((end - 1) >> log2_page) - page0 + 1;
+  for (int i = tid; i < npg; i += 256) pg_lds[i] = block_tables[(int64_t)b * max_pages + page0 + i];
+
+  // q as the MFMA B operand: column = head (zero past G)
   u16x8 qb[4];
   {
     const int hq = kvh * G + (l15 < G ? l15 : 0);
     const bf16_t* qp = q + ((int64_t)b * Hq + hq) * D + 32 * lg;
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) qb[ks] = *reinterpret_cast<const u16x8*>(qp + 8 * ks);
-  }
-  // ---- then every K and V load of this lane, branch-free (rows past n are clamped
-  // duplicates; their scores are masked to -inf and their P to 0) ----
-  u16x8 kf[4][4];  // [tile][kstep]: token w*64 + 16*i + l15, dims 32*lg + 8*ks
-  u16x8 vf[16];    // token w*64 + 4*it + lg, dims 8*l15
+    if (l15 >= G) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const bf16_t* p = kc + row_off(min(w * 64 + 16 * i + l15, n - 1)) + 32 * lg;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) kf[i][ks] = ld16(p + 8 * ks);
-  }
-#pragma unroll
-  for (int it = 0; it < 16; ++it) vf[it] = ld16(vc + row_off(min(w * 64 + 4 * it + lg, n - 1)) + 8 * l15);
-  if (l15 >= G) {
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) qb[ks] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-  }
-
-  // ---- S = K Q^T on MFMA, scaled scores -> LDS [token][head] ----
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, kf[i][ks]),
-                                                    __builtin_bit_cast(bf16x8_t, qb[ks]), acc, 0, 0, 0);
-    if (l15 < G) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int t = w * 64 + 16 * i + 4 * lg + r;
-        sc[t * GP + l15] = (t < n) ? acc[r] * scale_log2 : -INFINITY;
-      }
+      for (int ks = 0; ks < 4; ++ks) qb[ks] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
     }
   }
   __syncthreads();
 
-  // ---- two-pass softmax over the split: thread tid <-> token tid ----
-  float mh[G], lh[G];
+  const int64_t head_off = (int64_t)kvh * page_size * D;
+  const int64_t page_stride = (int64_t)Hkv * page_size * D;
+  auto row_off = [&](int tok) -> int64_t {  // tok in [start, end)
+    const int64_t page = pg_lds[(tok >> log2_page) - page0];
+    return page * page_stride + head_off + (int64_t)(tok & (page_size - 1)) * D;
+  };
+  // Branch-free chunk load: rows past `end` are clamped duplicates (masked later).
+  auto load = [&](KVRegs<NT>& r, int c) {
+    const int base = start + c * CH + w * TW;
 #pragma unroll
-  for (int h = 0; h < G; ++h) {
-    const float m = wave_max(sc[tid * GP + h]);
-    if (lane == 0) wred[w][h] = m;
-  }
-  __syncthreads();
+    for (int i = 0; i < NT; ++i) {
+      const bf16_t* p = kc + row_off(min(base + 16 * i + l15, end - 1)) + 32 * lg;
 #pragma unroll
-  for (int h = 0; h < G; ++h) mh[h] = fmaxf(fmaxf(wred[0][h], wred[1][h]), fmaxf(wred[2][h], wred[3][h]));
-  __syncthreads();
+      for (int ks = 0; ks < 4; ++ks) r.k[i][ks] = ld16(p + 8 * ks);
+    }
 #pragma unroll
-  for (int h = 0; h < G; ++h) {
-    const float sv = sc[tid * GP + h];
-    const float p = (tid < n) ? exp2f(sv - mh[h]) : 0.f;
-    sc[tid * GP + h] = p;
-    const float ls = wave_sum(p);
-    if (lane == 0) wred[w][h] = ls;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int h = 0; h < G; ++h) lh[h] = wred[0][h] + wred[1][h] + wred[2][h] + wred[3][h];
+    for (int it = 0; it < 4 * NT; ++it) r.v[it] = ld16(vc + row_off(min(base + 4 * it + lg, end - 1)) + 8 * l15);
+  };
 
-  // ---- O = P V on the VALU (V already in registers) ----
+  float m_run = -1e30f, l_run = 0.f;  // per lane: head l15 (finite start: no inf - inf)
   float acc[G][8];
 #pragma unroll
   for (int h = 0; h < G; ++h)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[h][j] = 0.f;
+  float* pwv = pw[w];
+
+  auto consume = [&](const KVRegs<NT>& r, int c) {
+    const int base = start + c * CH + w * TW;
+    float sc[NT][4];
+    float cmax = -INFINITY;
 #pragma unroll
-  for (int it = 0; it < 16; ++it) {
-    const int t = w * 64 + 4 * it + lg;
-    float p[G];
-    if constexpr (G % 4 == 0) {
+    for (int i = 0; i < NT; ++i) {
+      f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int h4 = 0; h4 < G; h4 += 4) {
-        const f32x4 pv = *reinterpret_cast<const f32x4*>(&sc[t * GP + h4]);
-        p[h4] = pv[0]; p[h4 + 1] = pv[1]; p[h4 + 2] = pv[2]; p[h4 + 3] = pv[3];
+      for (int ks = 0; ks < 4; ++ks)
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, r.k[i][ks]),
+                                                  __builtin_bit_cast(bf16x8_t, qb[ks]), a, 0, 0, 0);
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int tok = base + 16 * i + 4 * lg + rr;
+        sc[i][rr] = (tok < end) ? a[rr] * scale_log2 : -INFINITY;
+        cmax = fmaxf(cmax, sc[i][rr]);
       }
-    } else {
-#pragma unroll
-      for (int h = 0; h < G; ++h) p[h] = sc[t * GP + h];
     }
-    float vv[8];
+    cmax = fmaxf(cmax, __shfl_xor(cmax, 16, kWave));
+    cmax = fmaxf(cmax, __shfl_xor(cmax, 32, kWave));
+    const float m_new = fmaxf(m_run, cmax);
+    const float alpha = exp2f(m_run - m_new);
+    float psum = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) vv[j] = bf2f(vf[it][j]);
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const float p = exp2f(sc[i][rr] - m_new);
+        psum += p;
+        if (l15 < G) pwv[(16 * i + 4 * lg + rr) * GP + l15] = p;
+      }
+    psum += __shfl_xor(psum, 16, kWave);
+    psum += __shfl_xor(psum, 32, kWave);
+    l_run = l_run * alpha + psum;
+    m_run = m_new;
+    float al[G];
+#pragma unroll
+    for (int h = 0; h < G; ++h) al[h] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(alpha), h));
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
     for (int h = 0; h < G; ++h)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[h][j] += p[h] * vv[j];
+      for (int j = 0; j < 8; ++j) acc[h][j] *= al[h];
+#pragma unroll
+    for (int it = 0; it < 4 * NT; ++it) {
+      const int t = 4 * it + lg;
+      float p[G];
+      if constexpr (G % 4 == 0) {
+#pragma unroll
+        for (int h4 = 0; h4 < G; h4 += 4) {
+          const f32x4 pv = *reinterpret_cast<const f32x4*>(&pwv[t * GP + h4]);
+          p[h4] = pv[0]; p[h4 + 1] = pv[1]; p[h4 + 2] = pv[2]; p[h4 + 3] = pv[3];
+        }
+      } else {
+#pragma unroll
+        for (int h = 0; h < G; ++h) p[h] = pwv[t * GP + h];
+      }
+      float vv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) vv[j] = bf2f(r.v[it][j]);
+#pragma unroll
+      for (int h = 0; h < G; ++h)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[h][j] += p[h] * vv[j];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+
+  // Double-buffered stream over the chunks: the next chunk's loads are always in
+  // flight while the current one is consumed. Loads past the last chunk re-read
+  // the last chunk (branch-free, L2 hits) so hipcc's wait counts stay exact.
+  KVRegs<NT> ra, rb;
+  load(ra, 0);
+  for (int c = 0; c < nch; c += 2) {
+    load(rb, min(c + 1, nch - 1));
+    consume(ra, c);
+    load(ra, min(c + 2, nch - 1));
+    if (c + 1 < nch) consume(rb, c + 1);
   }
-  // reduce over the 4 token sub-slots of the wave (lanes l, l^16, l^32, l^48)
+
+  // ---- merge the 4 waves: reduce the 4 token sub-slots, then across waves ----
 #pragma unroll
   for (int h = 0; h < G; ++h)
 #pragma unroll
@@ -208,58 +227,53 @@ __device__ __forceinline__ void attn_decode_item(
   if (lg == 0) {
 #pragma unroll
     for (int h = 0; h < G; ++h) {
-      float* r = red + (w * G + h) * D + 8 * l15;
-      *reinterpret_cast<f32x4*>(r) = f32x4{acc[h][0], acc[h][1], acc[h][2], acc[h][3]};
-      *reinterpret_cast<f32x4*>(r + 4) = f32x4{acc[h][4], acc[h][5], acc[h][6], acc[h][7]};
+      float* rp = &red[w][h][8 * l15];
+      *reinterpret_cast<f32x4*>(rp) = f32x4{acc[h][0], acc[h][1], acc[h][2], acc[h][3]};
+      *reinterpret_cast<f32x4*>(rp + 4) = f32x4{acc[h][4], acc[h][5], acc[h][6], acc[h][7]};
+    }
+    if (l15 < G) {
+      mls[w][l15][0] = m_run;
+      mls[w][l15][1] = l_run;
     }
   }
   __syncthreads();
   for (int e = tid; e < G * D; e += 256) {
     const int h = e / D, d = e % D;
-    const float o = red[(0 * G + h) * D + d] + red[(1 * G + h) * D + d] + red[(2 * G + h) * D + d] +
-                    red[(3 * G + h) * D + d];
+    float M = mls[0][h][0];
+#pragma unroll
+    for (int ww = 1; ww < 4; ++ww) M = fmaxf(M, mls[ww][h][0]);
+    float o = 0.f, L = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) {
+      const float f = exp2f(mls[ww][h][0] - M);
+      o += f * red[ww][h][d];
+      L += f * mls[ww][h][1];
+    }
     const int hq = kvh * G + h;
-    if (ns_b == 1) {  // whole context in this split: final output, combine skips it
-      const float l = lh[h];
-      out[((int64_t)b * Hq + hq) * D + d] = f2bf(l > 0.f ? o / l : 0.f);
+    if (ns_b == 1) {  // whole context in this workgroup: final output, no combine
+      out[((int64_t)b * Hq + hq) * D + d] = f2bf(L > 0.f ? o / L : 0.f);
     } else {
       o_part[(((int64_t)b * Hq + hq) * num_splits + s) * D + d] = o;
       if (d == 0) {
         float* ml = ml_part + (((int64_t)b * Hq + hq) * num_splits + s) * 2;
-        ml[0] = mh[h];
-        ml[1] = lh[h];
+        ml[0] = M;
+        ml[1] = L;
       }
     }
   }
 }
 
-template <int G>
-__global__ void __launch_bounds__(256, (G <= 4 ? 3 : 2)) attn_decode_kernel(
-    const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
-    const int* __restrict__ block_tables, const int* __restrict__ seq_lens,
-    bf16_t* __restrict__ out, float* __restrict__ o_part, float* __restrict__ ml_part, int Hkv,
-    int page_size, int log2_page, int max_pages, int num_splits, float scale_log2,
-    const int* __restrict__ work) {
-  const int wi = blockIdx.x;
-  if (wi >= work[0]) return;  // grid is sized for the host's bound; the plan may hold fewer items
-  const int item = work[1 + wi];
-  attn_decode_item<G>(q, kc, vc, block_tables, seq_lens, out, o_part, ml_part, Hkv, page_size, log2_page,
-                      max_pages, num_splits, scale_log2, item >> 8, item & 255, blockIdx.y);
-}
-
-// Combine the per-split partials: grid (B*Hq), block D threads.
+// Combine the per-split partials of split sequences: grid (B*Hq), D threads.
 __global__ void attn_decode_combine_kernel(const float* __restrict__ o_part, const float* __restrict__ ml_part,
                                            const int* __restrict__ seq_lens, bf16_t* __restrict__ out, int Hq,
-                                           int num_splits, int max_tokens) {
+                                           int num_splits, int max_tokens, int chunk) {
   constexpr int D = 128;
   const int bh = blockIdx.x, b = bh / Hq, d = threadIdx.x;
   const int len = min(seq_lens[b], max_tokens);
-  const int ns = min(num_splits, (len + kSplit - 1) / kSplit);
+  if (len <= 0) return;  // zeroed by the attention kernel
+  const int per = split_len(len, num_splits, chunk);
+  const int ns = (len + per - 1) / per;
   if (ns == 1) return;  // written directly by the attention kernel
-  if (ns == 0) {
-    out[(int64_t)bh * D + d] = 0;
-    return;
-  }
   const float* ml = ml_part + (int64_t)bh * num_splits * 2;
   float M = -INFINITY;
   for (int s = 0; s < ns; ++s) M = fmaxf(M, ml[2 * s]);
@@ -273,40 +287,45 @@ __global__ void attn_decode_combine_kernel(const float* __restrict__ o_part, con
 }
 
 int attn_decode(const bf16_t* q, const bf16_t* k_cache, const bf16_t* v_cache, const int* block_tables,
-                const int* seq_lens, bf16_t* out, float* o_part, float* ml_part, int* work, int B, int Hq,
-                int Hkv, int head_dim, int page_size, int max_pages, int num_splits, float scale,
+                const int* seq_lens, bf16_t* out, float* o_part, float* ml_part, int B, int Hq, int Hkv,
+                int head_dim, int page_size, int max_pages, int num_splits, float scale, int variant,
                 hipStream_t stream) {
   if (B == 0) return 0;
   if (head_dim != 128) return -1;
-  if (page_size < 16 || (page_size & (page_size - 1)) != 0) return -2;  // pg_lds holds <= 18 pages
+  if (page_size < 16 || (page_size & (page_size - 1)) != 0) return -2;
+  if (max_pages > kMaxPagesLds) return -4;
+  if (num_splits < 1) return -5;
   int log2p = 0;
   while ((1 << log2p) < page_size) ++log2p;
   const int G = Hq / Hkv;
-  if (num_splits > 255) return -4;  // split index is packed in 8 bits
   const float scale_log2 = scale * 1.4426950408889634f;
-  attn_decode_plan_kernel<<<1, 1024, 0, stream>>>(seq_lens, B, max_pages * page_size, num_splits, work);
-  OAMD_LAUNCH_CHECK();
-  // One workgroup per (work item, kv head). num_splits is the caller's bound on the
-  // splits of the longest sequence in THIS call (not the model's max context): the
-  // engine captures one graph per bound, so the grid has no empty splits when the
-  // batch is length-uniform, and the packed work list keeps the live items first.
+  // variant: 0 = default (NT = 1: 16 tokens per wave per chunk, 164 VGPRs at
+  // G = 4 -> 3 workgroups/CU); 2 = NT = 2 (32 tokens per wave, 238 VGPRs,
+  // measured 4-10 % slower at B = 256; G = 8 spills, so it stays NT = 1).
+  int chunk = 0;
   dim3 grid(B * num_splits, Hkv, 1);
-#define OAMD_DEC(GG)                                                                                 \
-  attn_decode_kernel<GG><<<grid, 256, 0, stream>>>(q, k_cache, v_cache, block_tables, seq_lens, out, \
-                                                   o_part, ml_part, Hkv, page_size, log2p, max_pages,  \
-                                                   num_splits, scale_log2, work)
+#define OAMD_DEC(GG, NTT)                                                                               \
+  do {                                                                                                  \
+    attn_decode_kernel<GG, NTT><<<grid, 256, 0, stream>>>(q, k_cache, v_cache, block_tables, seq_lens, \
+                                                          out, o_part, ml_part, Hkv, page_size, log2p,  \
+                                                          max_pages, num_splits, scale_log2);           \
+    chunk = 64 * NTT;                                                                                   \
+  } while (0)
+  const bool nt2 = variant == 2;
   switch (G) {
-    case 1: OAMD_DEC(1); break;
-    case 2: OAMD_DEC(2); break;
-    case 4: OAMD_DEC(4); break;
-    case 8: OAMD_DEC(8); break;
+    case 1: if (nt2) OAMD_DEC(1, 2); else OAMD_DEC(1, 1); break;
+    case 2: if (nt2) OAMD_DEC(2, 2); else OAMD_DEC(2, 1); break;
+    case 4: if (nt2) OAMD_DEC(4, 2); else OAMD_DEC(4, 1); break;
+    case 8: OAMD_DEC(8, 1); break;
     default: return -3;
   }
 #undef OAMD_DEC
   OAMD_LAUNCH_CHECK();
-  attn_decode_combine_kernel<<<B * Hq, 128, 0, stream>>>(o_part, ml_part, seq_lens, out, Hq, num_splits,
-                                                         max_pages * page_size);
-  OAMD_LAUNCH_CHECK();
+  if (num_splits > 1) {
+    attn_decode_combine_kernel<<<B * Hq, 128, 0, stream>>>(o_part, ml_part, seq_lens, out, Hq, num_splits,
+                                                           max_pages * page_size, chunk);
+    OAMD_LAUNCH_CHECK();
+  }
   return 0;
 }
 

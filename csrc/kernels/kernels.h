@@ -21,8 +21,8 @@ int rope_kv(const bf16_t* qkv, int64_t qkv_stride, const int64_t* pos, const flo
             bf16_t* k_out, bf16_t* v_out, bf16_t* k_cache, bf16_t* v_cache, const int64_t* slots,
             int page_size, int64_t max_pos, hipStream_t stream);
 int attn_decode(const bf16_t* q, const bf16_t* k_cache, const bf16_t* v_cache, const int* block_tables,
-                const int* seq_lens, bf16_t* out, float* o_part, float* ml_part, int* work, int B, int Hq,
-                int Hkv, int head_dim, int page_size, int max_pages, int num_splits, float scale,
+                const int* seq_lens, bf16_t* out, float* o_part, float* ml_part, int B, int Hq, int Hkv,
+                int head_dim, int page_size, int max_pages, int num_splits, float scale, int variant,
                 hipStream_t stream);
 int attn_prefill(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, const int* cu_seqlens,
                  const int* work_seq, const int* work_q0, int num_work, int Hq, int Hkv, int head_dim,

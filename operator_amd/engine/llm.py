@@ -119,8 +119,8 @@ class _BucketState:
 
 
 class _DecodeGraph:
-    """One decode step over a bucket's state, with the attention grid sized for
-    ``splits`` (the bound on 256-token splits of the longest sequence)."""
+    """One decode step over a bucket's state, with ``splits`` decode-attention
+    workgroups per (sequence, kv-head) (``ops.decode_splits``)."""
 
     def __init__(self, eng: "LLMEngine", st: _BucketState, splits: int):
         self.eng, self.st, self.splits = eng, st, splits
@@ -180,7 +180,7 @@ class LLMEngine:
         self.max_prefill_tokens = max_prefill_tokens
         self.max_context = min(max_context or model.cfg.max_position, model.cfg.max_position)
         self.max_pages = kv.pages_needed(self.max_context)
-        self.num_splits = ops.decode_splits(self.max_context)
+        self.hkv = model.hkv
         self.use_graphs = use_graphs and self.device.type == "cuda"
         self.multi_step = max(1, multi_step)
         self._active: _BucketState | None = None   # bucket whose device state matches self.running
@@ -231,15 +231,13 @@ class LLMEngine:
 
     def warmup(self, buckets: list[int] | None = None, splits: list[int] | None = None) -> None:
         """Capture decode graphs ahead of time (largest first so they share one pool).
-        ``splits`` defaults to every split bound up to max_context for the largest
-        bucket and to the single-split bound for the others."""
+        ``splits`` defaults to every split count a bucket can use up to max_context."""
         if not self.use_graphs:
             return
         bs = sorted(buckets or self.buckets, reverse=True)
-        for i, bp in enumerate(bs):
-            for ns in (splits or (range(1, self.num_splits + 1) if i == 0 else [1, 2])):
-                if 1 <= ns <= self.num_splits:
-                    self._graph(bp, ns)
+        for bp in bs:
+            for ns in (splits or self.split_options(bp)):
+                self._graph(bp, ns)
         torch.cuda.synchronize(self.device)
 
     # ------------------------------------------------------------------ scheduling
@@ -314,6 +312,10 @@ class LLMEngine:
             st = self._states[bp] = _BucketState(self, bp)
         return st
 
+    def split_options(self, bp: int) -> list[int]:
+        top = ops.decode_splits(self.max_context, bp, self.hkv)
+        return [1 << i for i in range(top.bit_length())]
+
     def _graph(self, bp: int, splits: int) -> _DecodeGraph:
         g = self._graphs.get((bp, splits))
         if g is None:
@@ -332,8 +334,8 @@ class LLMEngine:
         bp = next(b for b in self.buckets if b >= B)
         k = min(self.multi_step, min(r.max_tokens - len(r.output) for r in self.running))
         k = max(1, k)
-        # attention grid bound: splits of the longest context reached in this window
-        splits = min(self.num_splits, ops.decode_splits(max(r.length for r in self.running) + k - 1))
+        # decode-attention split count for the longest context reached in this window
+        splits = ops.decode_splits(max(r.length for r in self.running) + k - 1, bp, self.hkv)
         g = self._graph(bp, splits)
         st = g.st
         if self._active is not st:

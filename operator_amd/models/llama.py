@@ -187,6 +187,9 @@ class LlamaModel:
         h = ops.embedding(fb.input_ids, self.embed)          # residual stream [T, H]
         x = ops.rmsnorm(h, self.layers[0].attn_norm, c.rms_eps)
         T = h.shape[0]
+        ws = None
+        if not fb.is_prefill and h.is_cuda:  # split-KV partials, shared by every layer
+            ws = ops.decode_workspace(T, self.hq, fb.num_splits, h.device)
         for i, lw in enumerate(self.layers):
             kc, vc = kv.layer(i)
             qkv = F.linear(x, lw.wqkv)
@@ -195,7 +198,8 @@ class LlamaModel:
             if fb.is_prefill:
                 o = ops.attn_prefill(q, k, v, fb.seq_lens, self.scale, work=fb.prefill_work)
             else:
-                o = ops.attn_decode(q, kc, vc, fb.block_tables, fb.context_lens, self.scale, fb.num_splits)
+                o = ops.attn_decode(q, kc, vc, fb.block_tables, fb.context_lens, self.scale, fb.num_splits,
+                                    workspace=ws)
             a = F.linear(o.view(T, self.hq * c.head_dim), lw.wo)
             self.tp.all_reduce_(a)
             x = ops.rmsnorm(a, lw.mlp_norm, c.rms_eps, residual=h)

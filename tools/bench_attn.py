@@ -13,7 +13,8 @@ ap.add_argument("--ctx", type=str, default="545,1024,2048")
 ap.add_argument("--hq", type=int, default=32)
 ap.add_argument("--hkv", type=int, default=8)
 ap.add_argument("--page", type=int, default=64)
-ap.add_argument("--splits", type=str, default="need,8,16")
+ap.add_argument("--splits", type=str, default="need")
+ap.add_argument("--variants", type=str, default="0,2")
 ap.add_argument("--pages-total", type=int, default=0)
 a = ap.parse_args()
 D = 128
@@ -27,23 +28,22 @@ for ctx in [int(c) for c in a.ctx.split(",")]:
     sl = torch.full((B,), ctx, dtype=torch.int32, device="cuda")
     q = torch.randn(B, a.hq, D, device="cuda", dtype=torch.bfloat16)
     for sp in a.splits.split(","):
-        ns = ops.decode_splits(ctx) if sp == "need" else int(sp)
-        if ns * 256 < ctx:
-            continue
+      for var in [int(x) for x in a.variants.split(",")]:
+        ns = ops.decode_splits(ctx, B, a.hkv) if sp == "need" else int(sp)
         ws = ops.decode_workspace(B, a.hq, ns, "cuda")
         out = torch.empty_like(q)
         for _ in range(3):
-            ops.attn_decode(q, kc, vc, bt, sl, 1 / math.sqrt(D), ns, out=out, workspace=ws)
+            ops.attn_decode(q, kc, vc, bt, sl, 1 / math.sqrt(D), ns, out=out, workspace=ws, variant=var)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
         n = 20
         e0.record()
         for _ in range(n):
-            ops.attn_decode(q, kc, vc, bt, sl, 1 / math.sqrt(D), ns, out=out, workspace=ws)
+            ops.attn_decode(q, kc, vc, bt, sl, 1 / math.sqrt(D), ns, out=out, workspace=ws, variant=var)
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) / n * 1e3
         byts = B * ctx * a.hkv * D * 2 * 2
-        print(json.dumps({"ctx": ctx, "B": B, "splits": ns, "us": round(us, 1), "GBps": round(byts / us / 1e3, 1)}),
-              flush=True)
+        print(json.dumps({"ctx": ctx, "B": B, "splits": ns, "variant": var, "us": round(us, 1),
+                          "GBps": round(byts / us / 1e3, 1)}), flush=True)
     del kc, vc
