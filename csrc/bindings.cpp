@@ -105,6 +105,29 @@ void rope_kv(const at::Tensor& qkv, const at::Tensor& pos, const at::Tensor& cos
                    cur_stream()));
 }
 
+void gemm_decode(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const c10::optional<at::Tensor>& p,
+                 int64_t splits, int64_t bn, int64_t bm) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(y); CHECK_CONTIG(x); CHECK_CONTIG(w); CHECK_CONTIG(y);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 2, "x [M,K], w [N,K], y [M,N]");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && y.size(0) == M && y.size(1) == N, "gemm shapes");
+  if (bm == 0) bm = std::min<int64_t>(M, 256);
+  TORCH_CHECK((bm == 64 || bm == 128 || bm == 256) && M % bm == 0, "gemm_decode: M % bm, bm in {64,128,256}");
+  TORCH_CHECK((bn == 64 || bn == 128) && N % bn == 0, "gemm_decode: N % bn, bn in {64, 128}");
+  TORCH_CHECK(splits >= 1 && 8 % splits == 0 && K % (64 * splits) == 0, "gemm_decode: bad split count");
+  float* pp = nullptr;
+  if (splits > 1) {
+    TORCH_CHECK(p.has_value(), "split-K needs a partial buffer");
+    CHECK_DT(*p, at::kFloat); CHECK_CONTIG(*p);
+    TORCH_CHECK(p->numel() >= splits * M * N, "partial buffer too small");
+    pp = p->data_ptr<float>();
+  }
+  TORCH_CHECK(K < (1LL << 31) / 64 && M * K < (1LL << 31) && N * K < (1LL << 40), "gemm too large");
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  RC(oamd::gemm_decode(ptr<bf16_t>(x), ptr<bf16_t>(w), ptr<bf16_t>(y), pp, (int)M, (int)N, (int)K, (int)splits,
+                       (int)bn, (int)bm, cur_stream()));
+}
+
 void attn_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                  const at::Tensor& block_tables, const at::Tensor& seq_lens, at::Tensor& out,
                  at::Tensor& o_part, at::Tensor& ml_part, int64_t num_splits, double scale, int64_t variant) {
@@ -179,6 +202,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("embedding", &embedding);
   m.def("rope_kv", &rope_kv);
   m.def("attn_decode", &attn_decode);
+  m.def("gemm_decode", &gemm_decode, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"),
+        pybind11::arg("p") = pybind11::none(), pybind11::arg("splits") = 1, pybind11::arg("bn") = 64,
+        pybind11::arg("bm") = 0);
   m.def("attn_prefill", &attn_prefill);
   m.def("sample", &sample, pybind11::arg("logits"), pybind11::arg("temperature"), pybind11::arg("seeds"),
         pybind11::arg("positions"), pybind11::arg("out"), pybind11::arg("col_offset") = 0,

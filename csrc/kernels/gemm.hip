@@ -1,0 +1,196 @@
+// Decode-shape GEMM: Y[M, N] = X[M, K] . W[N, K]^T, bf16 in, fp32 accumulate
+// (SURVEY.md §2.4 N7 — the explanation model's projections at decode batch).
+//
+// At decode the activations are small (M = bucket size, 64..256 rows) and the
+// weights are streamed once per step, so the kernel is designed around the
+// two streams rather than around a square tile:
+//   * W (HBM, read once) and X (L2-resident, re-read by every column tile) are
+//     both staged through LDS by LDS-DMA (global_load_lds_dwordx4) in full
+//     128-B lines — no VGPR round trip, no fragment-shaped global loads
+//     (cdna_hip_programming.md §5 "Projection GEMM at M = 256", item 3);
+//   * a 3-deep LDS ring with a counted vmcnt + raw s_barrier keeps two stages
+//     of both operands in flight across every barrier (never a vmcnt(0) drain
+//     inside the k-loop);
+//   * the LDS image is XOR-swizzled on the SOURCE address (the DMA writes LDS
+//     lane-linearly), slot = chunk ^ ((row >> 1) & 7), which makes every
+//     ds_read_b128 fragment read conflict-free;
+//   * 8 waves (4 x 2), two per SIMD; the tile is BM = M rows x 64 columns; K is split S ways when N / 64
+//     column tiles alone cannot fill 256 CUs. Split-K partials are fp32 slabs
+//     [S][M][N] summed by gemm_splitk_reduce (or by a consumer kernel). With
+//     S | 8 the blocks of one K-slice share an XCD (block id % 8), so each
+//     XCD's L2 holds only its slice of X.
+// MFMA v_mfma_f32_16x16x32_bf16; fragment maps as in attn_decode.hip.
+#include "common.h"
+#include "kernels.h"
+
+namespace oamd {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+
+constexpr int kBK = 64;     // K per stage: one 128-B line per row
+constexpr int kStages = 3;  // LDS ring depth
+
+// 8 waves (2 per SIMD: one wave's LDS-read latency hides under the other's
+// MFMAs) laid out 4 (M) x 2 (N).
+constexpr int kWaves = 8;
+
+// BN = 128 halves the LDS fragment traffic per MFMA (64 x 64 wave tiles at
+// M = 256: 0.5 KB of ds_read per MFMA vs 0.75 KB at BN = 64, where the LDS
+// port, not the MFMA, sets the pace); BN = 64 gives twice the column tiles for
+// the narrow projections.
+template <int BM, int BN>
+struct GemmCfg {
+  static constexpr int WM = 4;                           // waves along M
+  static constexpr int WN = kWaves / WM;                 // waves along N
+  static constexpr int FM = BM / WM / 16;                // 16-row fragments per wave
+  static constexpr int FN = BN / WN / 16;                // 16-col fragments per wave
+  static constexpr int ROWS = BM + BN;                   // rows of one stage (A then B)
+  static constexpr int STAGE_BYTES = ROWS * kBK * 2;     // bf16
+  static constexpr int GL = ROWS / 8 / kWaves;           // LDS-DMA instructions per wave per stage
+  static constexpr int LDS_BYTES = kStages * STAGE_BYTES;
+  static_assert(ROWS % (8 * kWaves) == 0, "stage rows must split evenly over the waves");
+};
+
+__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int BM, int BN, bool PARTIAL>
+__global__ void __launch_bounds__(kWaves * 64, 1) gemm_tn_kernel(const bf16_t* __restrict__ X,
+                                                                 const bf16_t* __restrict__ W, bf16_t* __restrict__ Y,
+                                                                 float* __restrict__ P, int M, int N, int K, int S) {
+  using C = GemmCfg<BM, BN>;
+  __shared__ __attribute__((aligned(1024))) char lds[C::LDS_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kz = blockIdx.x % S, nt = blockIdx.x / S;
+  const int n0 = nt * BN;
+  const int m0 = blockIdx.y * BM;  // row tile (M may be split into BM-row tiles)
+  X += (int64_t)m0 * K;
+  const int Kc = K / S;
+  const int kbase = kz * Kc;
+  const int T = Kc / kBK;
+
+  // ---- LDS-DMA issue of one stage: instruction q covers rows 8q..8q+7 of the
+  // stage (A rows [0, BM), then B rows [BM, BM + BN)); lane l -> row 8q + l/8,
+  // LDS slot l%8, global chunk swz(row, slot).
+  const int lrow = lane >> 3, lslot = lane & 7;
+  auto issue = [&](int t, int buf) {
+    const int k0 = kbase + t * kBK;
+    char* sbase = lds + buf * C::STAGE_BYTES;
+#pragma unroll
+    for (int i = 0; i < C::GL; ++i) {
+      const int q = w + kWaves * i;
+      const int row = 8 * q + lrow;
+      const int chunk = swz(row, lslot);
+      const bf16_t* src = (row < BM) ? X + (int64_t)row * K + k0 + chunk * 8
+                                     : W + (int64_t)(n0 + row - BM) * K + k0 + chunk * 8;
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(sbase + q * 1024), 16, 0, 0);
+    }
+  };
+
+  const int wm = w / C::WN, wn = w % C::WN;
+  const int l15 = lane & 15, lg = lane >> 4;
+  f32x4 acc[C::FM][C::FN];
+#pragma unroll
+  for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int buf) {
+    const char* sbase = lds + buf * C::STAGE_BYTES;
+#pragma unroll
+    for (int s = 0; s < kBK / 32; ++s) {
+      const int chunk = 4 * s + lg;
+      u16x8 a[C::FM], b[C::FN];
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i) {
+        const int row = wm * (BM / C::WM) + 16 * i + l15;
+        a[i] = *reinterpret_cast<const u16x8*>(sbase + row * 128 + (swz(row, chunk) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < C::FN; ++j) {
+        const int row = BM + wn * (BN / C::WN) + 16 * j + l15;
+        b[j] = *reinterpret_cast<const u16x8*>(sbase + row * 128 + (swz(row, chunk) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a[i]),
+                                                              __builtin_bit_cast(bf16x8_t, b[j]), acc[i][j], 0, 0, 0);
+    }
+  };
+
+  issue(0, 0);
+  if (T > 1) issue(1, 1);
+  for (int t = 0; t < T; ++t) {
+    if (t + 1 < T) wait_vmcnt<C::GL>();
+    else wait_vmcnt<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + 2 < T) issue(t + 2, (t + 2) % kStages);
+    compute(t % kStages);
+  }
+
+  // ---- epilogue: C lane l -> row 4*lg + r, col l15 of each fragment ----
+#pragma unroll
+  for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j) {
+      const int col = n0 + wn * (BN / C::WN) + 16 * j + l15;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * (BM / C::WM) + 16 * i + 4 * lg + r;
+        if constexpr (PARTIAL) P[((int64_t)kz * M + m0 + row) * N + col] = acc[i][j][r];
+        else Y[(int64_t)(m0 + row) * N + col] = f2bf(acc[i][j][r]);
+      }
+    }
+}
+
+// Y[m, n] = bf16(sum_s P[s, m, n]); 4 columns per thread.
+__global__ void gemm_splitk_reduce_kernel(const float* __restrict__ P, bf16_t* __restrict__ Y, int64_t MN, int S) {
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i >= MN) return;
+  f32x4 a = *reinterpret_cast<const f32x4*>(P + i);
+  for (int s = 1; s < S; ++s) a += *reinterpret_cast<const f32x4*>(P + s * MN + i);
+  uint2 o;
+  o.x = pack_bf2(a[0], a[1]);
+  o.y = pack_bf2(a[2], a[3]);
+  *reinterpret_cast<uint2*>(Y + i) = o;
+}
+
+int gemm_decode(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, int N, int K, int S, int BN,
+                int BM, hipStream_t stream) {
+  if ((BM != 64 && BM != 128 && BM != 256) || M % BM != 0) return -1;
+  if ((BN != 64 && BN != 128) || N % BN != 0) return -2;
+  if (S < 1 || 8 % S != 0 || K % (kBK * S) != 0) return -3;
+  if (S > 1 && P == nullptr) return -4;
+  const dim3 grid((N / BN) * S, M / BM);
+#define OAMD_GEMM2(BM, BNN)                                                                                   \
+  if (S > 1) gemm_tn_kernel<BM, BNN, true><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, S);       \
+  else gemm_tn_kernel<BM, BNN, false><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, S)
+#define OAMD_GEMM(BM) \
+  if (BN == 64) { OAMD_GEMM2(BM, 64); } else { OAMD_GEMM2(BM, 128); }
+  switch (BM) {
+    case 64: OAMD_GEMM(64); break;
+    case 128: OAMD_GEMM(128); break;
+    default: OAMD_GEMM(256); break;
+  }
+#undef OAMD_GEMM
+#undef OAMD_GEMM2
+  OAMD_LAUNCH_CHECK();
+  if (S > 1) {
+    const int64_t MN = (int64_t)M * N;
+    const int64_t threads = MN / 4;
+    gemm_splitk_reduce_kernel<<<(threads + 255) / 256, 256, 0, stream>>>(P, Y, MN, S);
+    OAMD_LAUNCH_CHECK();
+  }
+  return 0;
+}
+
+}  // namespace oamd

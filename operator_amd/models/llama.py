@@ -20,7 +20,8 @@ Tensor parallelism is Megatron-style: QKV and gate|up column-parallel (whole
 heads / whole FFN columns per rank), O and down row-parallel followed by one
 all-reduce each (2 per layer), embeddings replicated (2.1 GB at 70B, fits the
 288 GB HBM trivially), lm_head vocab-parallel.
-Plain GEMMs go to hipBLASLt through torch (F.linear); everything else is a
+Decode-bucket GEMMs go to the gfx950 gemm_decode kernel where it wins (ops.linear),
+prefill GEMMs to hipBLASLt through torch; everything else is a
 hand-written HIP kernel (operator_amd.ops).
 """
 from __future__ import annotations
@@ -192,7 +193,7 @@ class LlamaModel:
             ws = ops.decode_workspace(T, self.hq, fb.num_splits, h.device)
         for i, lw in enumerate(self.layers):
             kc, vc = kv.layer(i)
-            qkv = F.linear(x, lw.wqkv)
+            qkv = ops.linear(x, lw.wqkv)
             q, k, v = ops.rope_kv(qkv, fb.positions, self.cos, self.sin, self.hq, self.hkv, kc, vc, fb.slots,
                                   want_kv=fb.is_prefill)
             if fb.is_prefill:
@@ -200,18 +201,18 @@ class LlamaModel:
             else:
                 o = ops.attn_decode(q, kc, vc, fb.block_tables, fb.context_lens, self.scale, fb.num_splits,
                                     workspace=ws)
-            a = F.linear(o.view(T, self.hq * c.head_dim), lw.wo)
+            a = ops.linear(o.view(T, self.hq * c.head_dim), lw.wo)
             self.tp.all_reduce_(a)
             x = ops.rmsnorm(a, lw.mlp_norm, c.rms_eps, residual=h)
-            gu = F.linear(x, lw.wgu)
+            gu = ops.linear(x, lw.wgu)
             m = ops.silu_mul(gu)
-            d = F.linear(m, lw.wd)
+            d = ops.linear(m, lw.wd)
             self.tp.all_reduce_(d)
             nw = self.layers[i + 1].attn_norm if i + 1 < len(self.layers) else self.final_norm
             x = ops.rmsnorm(d, nw, c.rms_eps, residual=h)
         if fb.logits_index is not None:
             x = x.index_select(0, fb.logits_index)
-        return F.linear(x, self.lm_head)
+        return ops.linear(x, self.lm_head)
 
     def sample(self, logits: torch.Tensor, temperature: torch.Tensor, seeds: torch.Tensor,
                positions: torch.Tensor) -> torch.Tensor:

@@ -6,7 +6,11 @@ reference implementations in :mod:`operator_amd.ops.reference`.
 """
 from __future__ import annotations
 
+import json
+import os
+
 import torch
+import torch.nn.functional as F
 
 from . import reference
 from ._native import kernels, native_available, patterns
@@ -14,7 +18,7 @@ from ._native import kernels, native_available, patterns
 __all__ = [
     "rmsnorm", "silu_mul", "embedding", "rope_kv", "attn_prefill", "attn_decode", "sample",
     "kernels", "patterns", "native_available", "reference", "prefill_work_list", "decode_splits",
-    "decode_workspace",
+    "decode_workspace", "linear", "gemm_splits", "gemm_plan",
 ]
 
 DECODE_MIN_SPLIT_TOKENS = 256  # never split a sequence into pieces shorter than this
@@ -115,6 +119,72 @@ def attn_prefill(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, seq_lens: li
                 torch.tensor(wq, dtype=torch.int32, device=dev))
     kernels().attn_prefill(q, k, v, o, work[0], work[1], work[2], scale)
     return o
+
+
+GEMM_DECODE_M = (64, 128, 256)  # decode buckets the gfx950 gemm_decode kernel is tuned for
+_GEMM_TABLE_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_tuned.json")
+_gemm_table: dict | None = None
+
+
+def _gemm_table_get() -> dict:
+    """Measured best (bm, bn, splits) per decode GEMM shape on MI355X, written by
+    ``tools/bench_gemm.py --write-table`` ("blas" = hipBLASLt wins that shape)."""
+    global _gemm_table
+    if _gemm_table is None:
+        try:
+            with open(_GEMM_TABLE_PATH) as f:
+                _gemm_table = {tuple(int(x) for x in k.split(",")): v for k, v in json.load(f).items()}
+        except (OSError, ValueError):
+            _gemm_table = {}
+    return _gemm_table
+
+
+def gemm_splits(M: int, N: int, K: int) -> int:
+    """Heuristic split-K ways for gemm_decode (shapes not in the tuned table): the
+    smallest S | 8 whose (N/64) x S blocks reach one block per CU (256)."""
+    tiles = N // 64
+    best = 1
+    for S in (1, 2, 4, 8):
+        if K % (64 * S):
+            break
+        best = S
+        if tiles * S >= 256:
+            return S
+    return best
+
+
+def gemm_plan(M: int, N: int, K: int):
+    """(bm, bn, splits) for the gfx950 gemm_decode kernel, or None for hipBLASLt."""
+    if M % 64 or N % 64 or K % 64 or M > 256:
+        return None
+    t = _gemm_table_get().get((M, N, K))
+    if t == "blas":
+        return None
+    if t is not None:
+        return tuple(t)
+    return (min(M, 256), 64, gemm_splits(M, N, K))
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None, splits: int | None = None,
+           partial: torch.Tensor | None = None, bn: int | None = None, bm: int | None = None) -> torch.Tensor:
+    """y = x @ w^T (bf16). Decode-bucket shapes (M a multiple of 64, <= 256) run on the
+    gfx950 gemm_decode kernel when it beats hipBLASLt for the shape (tuned table);
+    everything else (prefill, odd shapes, CPU) on hipBLASLt / torch."""
+    M, K = x.shape
+    N = w.shape[0]
+    plan = None
+    if x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous():
+        plan = gemm_plan(M, N, K)
+        if plan is None and (splits or bn or bm) and M % 64 == 0 and N % 64 == 0 and K % 64 == 0:
+            plan = (min(M, 256), 64, 1)  # explicit request (tests / tuning)
+    if plan is None:
+        return F.linear(x, w, out=out) if out is not None else F.linear(x, w)
+    bm, bn, S = bm or plan[0], bn or plan[1], splits or plan[2]
+    y = out if out is not None else torch.empty(M, N, dtype=x.dtype, device=x.device)
+    if S > 1 and (partial is None or partial.numel() < S * M * N):
+        partial = torch.empty(S * M * N, dtype=torch.float32, device=x.device)
+    kernels().gemm_decode(x, w, y, partial if S > 1 else None, S, bn, bm)
+    return y
 
 
 def decode_splits(max_context: int, batch: int = 1, kv_heads: int = 8) -> int:

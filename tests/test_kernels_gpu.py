@@ -140,3 +140,22 @@ def test_sample(dtype):
     assert tok[0] == int(torch.argmax(logits[0].float()))
     # deterministic replay
     assert torch.equal(ops.sample(logits, temp, seeds, pos).cpu(), tok)
+
+
+@pytest.mark.parametrize("M", [64, 128, 256])
+@pytest.mark.parametrize("N,K", [(256, 512), (640, 2048), (128, 4096)])
+def test_gemm_decode(M, N, K):
+    torch.manual_seed(7)
+    x = _rand(M, K)
+    w = _rand(N, K) * 0.05
+    ref_ = (x.float() @ w.float().t())
+    for bm in (64, 128, 256):
+        for bn in (64, 128):
+            for S in (1, 2, 4, 8):
+                if bm > M or K % (64 * S) or N % bn:
+                    continue
+                y = ops.linear(x, w, splits=S, bn=bn, bm=bm)
+                torch.testing.assert_close(y.float(), ref_, atol=2e-2, rtol=2e-2)
+    # default split choice and the hipBLASLt fallback shape agree too
+    torch.testing.assert_close(ops.linear(x, w).float(), ref_, atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(ops.linear(x[:M - 3].contiguous(), w).float(), ref_[:M - 3], atol=2e-2, rtol=2e-2)

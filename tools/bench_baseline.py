@@ -43,10 +43,9 @@ def main() -> int:
     from transformers import LlamaConfig as HFConfig
     from transformers import LlamaForCausalLM
 
-    from operator_amd.api.models import AIProviderConfig
     from operator_amd.engine.match import MatchEngine
     from operator_amd.engine.prompt import render_bounded
-    from operator_amd.engine.tokenizer import get_tokenizer
+    from operator_amd.engine.tokenizer import Tokenizer
     from operator_amd.models.config import get_config
     from operator_amd.patterns import oracle
     from operator_amd.patterns.compiler import compile_patterns
@@ -57,21 +56,20 @@ def main() -> int:
     fac = LogFactory(n_patterns=a.patterns, seed=0)
     docs, _ = fac.batch(a.failures, a.log_kb * 1024, n_failures=3, seed=1000)
     cp = compile_patterns(ps, build_dfa=False)
-    tok = get_tokenizer()
+    cfg = get_config(a.model)
+    tok = Tokenizer(cfg.vocab_size, cfg.bos_id, cfg.eos_ids[0])
     meng = MatchEngine(ps, device="cpu")
     results = meng.analyze(docs, [(f"app-{i}", "default") for i in range(len(docs))])
     prompts = [render_bounded(r, tok, a.prompt_tokens) for r in results]
 
-    cfg = get_config(a.model)
-    hfc = HFConfig(vocab_size=cfg.vocab_size, hidden_size=cfg.hidden, intermediate_size=cfg.ffn,
+    hfc = HFConfig(vocab_size=cfg.vocab_size, hidden_size=cfg.hidden, intermediate_size=cfg.intermediate,
                    num_hidden_layers=cfg.layers, num_attention_heads=cfg.heads, num_key_value_heads=cfg.kv_heads,
-                   max_position_embeddings=8192, rope_theta=cfg.rope_theta, rms_norm_eps=cfg.norm_eps,
+                   max_position_embeddings=8192, rope_theta=cfg.rope_theta, rms_norm_eps=cfg.rms_eps,
                    tie_word_embeddings=False, attn_implementation="sdpa", pad_token_id=0)
     torch.set_default_dtype(torch.bfloat16)
     with torch.device(dev):
         model = LlamaForCausalLM(hfc)
     model.eval()
-    _ = AIProviderConfig()
 
     # ---- timed: per-failure regex analysis + batched HF generate ----
     lat = []

@@ -1,19 +1,35 @@
-"""Decode-shape GEMM microbenchmark: hipBLASLt default heuristic vs TunableOp-tuned
-(hipBLASLt + rocBLAS solution search). y[M,N] = x[M,K] @ W[N,K]^T, bf16."""
+"""Decode-shape GEMM microbenchmark: y[M,N] = x[M,K] @ W[N,K]^T, bf16.
+
+Compares hipBLASLt (F.linear, default heuristic or --tune TunableOp) with the
+gfx950 gemm_decode kernel at every split-K count. Weights rotate through enough
+copies (>= 1 GB) that nothing is served from the 256 MB MALL, as in a real
+32-layer decode step."""
 import argparse
 import json
 import os
+import sys
 
 import torch
 import torch.nn.functional as F
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from operator_amd import ops  # noqa: E402
+
 ap = argparse.ArgumentParser()
-ap.add_argument("--m", default="1,16,64,128,256")
+ap.add_argument("--m", default="64,128,256")
 ap.add_argument("--tune", action="store_true")
+ap.add_argument("--no-custom", action="store_true")
 ap.add_argument("--file", default="gpurun_out/tunableop_results.csv")
+ap.add_argument("--write-table", default=None, help="write the best (bm, bn, splits) per shape as JSON")
+ap.add_argument("--tp", type=int, default=1, help="also cover the TP-sharded shapes of this degree")
 a = ap.parse_args()
 shapes = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336),
           "lm_head": (128256, 4096)}
+if a.tp > 1:
+    t = a.tp
+    shapes = {f"{k}_tp{t}": ((n // t, kk) if k in ("qkv", "gate_up", "lm_head") else (n, kk // t))
+              for k, (n, kk) in shapes.items()}
+table = {}
 if a.tune:
     import torch.cuda.tunable as tun
     tun.enable(True)
@@ -21,31 +37,76 @@ if a.tune:
     tun.set_filename(a.file)
     tun.set_max_tuning_duration(200)
     tun.set_max_tuning_iterations(30)
-# rotate through enough weight copies (>=1 GB) that nothing is served from the 256 MB MALL,
-# as in a real 32-layer decode step
+    tun.set_rotating_buffer_size(1024)
 ws = {k: [torch.randn(n, kk, device="cuda", dtype=torch.bfloat16) * 0.02
           for _ in range(max(1, min(16, -(-(1 << 30) // (n * kk * 2)))))] for k, (n, kk) in shapes.items()}
+
+
+def timeit(fn, wl, it=32):
+    for w in wl:
+        fn(w)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
+    e0.record()
+    for i in range(it):
+        fn(wl[i % len(wl)])
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / it * 1e3
+
+
 for M in [int(x) for x in a.m.split(",")]:
-    tot = 0.0
+    tot = {"hipblaslt": 0.0, "best": 0.0}
     for name, (N, K) in shapes.items():
         x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
-        wl = ws[name]
-        for w in wl:
-            F.linear(x, w)
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
-        it = 32
-        e0.record()
-        for i in range(it):
-            F.linear(x, wl[i % len(wl)])
-        e1.record()
-        torch.cuda.synchronize()
-        us = e0.elapsed_time(e1) / it * 1e3
-        tot += us * (1 if name == "lm_head" else 32)
-        print(json.dumps({"M": M, "gemm": name, "N": N, "K": K, "us": round(us, 1),
-                          "TFLOPs": round(2 * M * N * K / us / 1e6, 1), "TBps_w": round(N * K * 2 / us / 1e6, 2),
-                          "tuned": a.tune}), flush=True)
-    print(json.dumps({"M": M, "per_step_gemm_ms": round(tot / 1e3, 3), "tuned": a.tune}), flush=True)
+        mult = 1 if name == "lm_head" else 32
+        res = {"hipblaslt": timeit(lambda w: F.linear(x, w), ws[name])}
+        if not a.no_custom and M in ops.GEMM_DECODE_M:
+            y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+            part = torch.empty(8 * M * N, device="cuda", dtype=torch.float32)
+            ref = F.linear(x, ws[name][0]).float()
+            for bm in (64, 128, 256):
+                for bn in (64, 128):
+                    for S in (1, 2, 4, 8):
+                        if bm > M or K % (64 * S) or N % bn:
+                            continue
+                        got = ops.linear(x, ws[name][0], out=y, splits=S, partial=part, bn=bn, bm=bm).float()
+                        err = (got - ref).abs().max().item()
+                        if err > 0.1:
+                            print("BAD", name, M, bm, bn, S, err, flush=True)
+                            continue
+                        key = f"m{bm}n{bn}s{S}"
+                        res[key] = timeit(lambda w: ops.linear(x, w, out=y, splits=S, partial=part, bn=bn, bm=bm),
+                                          ws[name])
+        times = dict(res)
+        best = min(times, key=times.get)
+        if M in ops.GEMM_DECODE_M:
+            # the custom kernel must win by >= 3 % to displace hipBLASLt (noise margin)
+            if best != "hipblaslt" and times[best] < 0.97 * times["hipblaslt"]:
+                bm_, rest = best[1:].split("n")
+                bn_, s_ = rest.split("s")
+                table[f"{M},{N},{K}"] = [int(bm_), int(bn_), int(s_)]
+            else:
+                table[f"{M},{N},{K}"] = "blas"
+                best = "hipblaslt"
+        tot["hipblaslt"] += res["hipblaslt"] * mult
+        tot["best"] += times[best] * mult
+        out = {"M": M, "gemm": name, "N": N, "K": K, "best": best,
+               "best_TBps_w": round(N * K * 2 / times[best] / 1e6, 2)}
+        top = sorted(times.items(), key=lambda kv: kv[1])[:4]
+        out.update({"hipblaslt": round(res["hipblaslt"], 1), "top": [(k, round(v, 1)) for k, v in top]})
+        print(json.dumps(out), flush=True)
+    print(json.dumps({"M": M, "per_step_gemm_ms_hipblaslt": round(tot["hipblaslt"] / 1e3, 3),
+                      "per_step_gemm_ms_best": round(tot["best"] / 1e3, 3)}), flush=True)
+if a.write_table:
+    old = {}
+    if os.path.exists(a.write_table):
+        with open(a.write_table) as f:
+            old = json.load(f)
+    old.update(table)
+    with open(a.write_table, "w") as f:
+        json.dump(old, f, indent=1, sort_keys=True)
 if a.tune:
     import torch.cuda.tunable as tun
-    tun.write_file()
+    for r in tun.get_results():
+        print("tuned:", r, flush=True)
