@@ -181,10 +181,12 @@ def main() -> int:
 
     sync()
     t0 = time.perf_counter()
+    mono0 = time.monotonic_ns()  # same clock as rocprofv3 timestamps: lets a trace be cut to the timed region
     for w in range(a.warmup, waves):
         run_wave(w)
     sync()
     elapsed = time.perf_counter() - t0
+    mono1 = time.monotonic_ns()
 
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev if info.backend == "nccl" else "cpu")
     p50_local = statistics.median(lat) if lat else float("nan")
@@ -209,7 +211,7 @@ def main() -> int:
                    "mode": a.mode, "hipgraph": not a.no_graphs},
         "detail": {"init_s": round(init_s, 1), "prefill_tokens_per_gpu": ptoks, "decode_tokens_per_gpu": dtoks,
                    "decode_tok_s_per_gpu": round(dtoks / elapsed, 1), "outcomes": counter["outcomes"],
-                   "dfa_states": getattr(meng, "dfa_states", None)},
+                   "dfa_states": getattr(meng, "dfa_states", None), "timed_monotonic_ns": [mono0, mono1]},
     }
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -31,7 +31,7 @@ from operator_amd.models.kv_cache import PagedKVCache
 from operator_amd.models.llama import ForwardBatch, LlamaModel
 
 
-@dataclass
+@dataclass(eq=False)  # identity semantics: two requests are never "equal"
 class GenRequest:
     prompt: list[int]
     max_tokens: int = 500
@@ -64,6 +64,17 @@ class EngineStats:
     decode_s: float = 0.0
     steps: int = 0
     graph_replays: int = 0
+
+
+@dataclass
+class _Window:
+    """A launched multi-step decode window whose tokens are still on the device."""
+    st: "_BucketState"
+    reqs: list[GenRequest]
+    B: int
+    k: int
+    host: torch.Tensor
+    event: object
 
 
 def _buckets(max_batch: int) -> list[int]:
@@ -194,6 +205,16 @@ class LLMEngine:
         self.buckets = _buckets(max_batch)
         self.eos = set(model.cfg.eos_ids)
         self._lock = threading.Lock()
+        # Decode windows are pipelined on the GPU: window w+1 is launched before the
+        # host reads window w's tokens, so the device never idles on the host's
+        # per-window bookkeeping (EOS rows of window w+1 are discarded).
+        self.pipeline = self.use_graphs
+        self._inflight: _Window | None = None
+        self._hb = 0
+        self._host_bufs = None
+        if self.device.type == "cuda":
+            self._host_bufs = [torch.empty(max_batch, self.multi_step, dtype=torch.long, pin_memory=True)
+                               for _ in range(2)]
 
     # ------------------------------------------------------------------ API
     def submit(self, req: GenRequest) -> GenRequest:
@@ -243,12 +264,19 @@ class LLMEngine:
     # ------------------------------------------------------------------ scheduling
     def step(self) -> list[GenRequest]:
         self.stats.steps += 1
-        batch = self._admit()
+        if self._inflight is not None and (self._admittable() or not self.running):
+            self._consume(self._inflight)   # composition is about to change: drain first
+            self._inflight = None
+            return self._reap()
+        batch = self._admit() if self._inflight is None else []
         if batch:
             self._prefill(batch)
         elif self.running:
             self._decode()
         return self._reap()
+
+    def _admittable(self) -> bool:
+        return bool(self.waiting) and len(self.running) < self.max_batch
 
     def _admit(self) -> list[GenRequest]:
         out, toks = [], 0
@@ -327,33 +355,65 @@ class LLMEngine:
             self._graphs[(bp, splits)] = g
         return g
 
-    def _decode(self) -> None:
-        """Up to ``multi_step`` decode steps with no host round trip in between."""
-        t0 = time.perf_counter()
-        B = len(self.running)
+    def _launch(self, ahead: int = 0) -> _Window:
+        """Launch one window of up to ``multi_step`` decode steps for ``self.running``;
+        ``ahead`` tokens per request are already in flight in an earlier window."""
+        reqs = list(self.running)
+        B = len(reqs)
         bp = next(b for b in self.buckets if b >= B)
-        k = min(self.multi_step, min(r.max_tokens - len(r.output) for r in self.running))
-        k = max(1, k)
+        k = max(1, min(self.multi_step, min(r.max_tokens - len(r.output) - ahead for r in reqs)))
         # decode-attention split count for the longest context reached in this window
-        splits = ops.decode_splits(max(r.length for r in self.running) + k - 1, bp, self.hkv)
+        splits = ops.decode_splits(max(r.length for r in reqs) + ahead + k - 1, bp, self.hkv)
         g = self._graph(bp, splits)
         st = g.st
         if self._active is not st:
-            st.load(self.running, self.max_pages)
+            assert ahead == 0, "device state must be current before it is reloaded"
+            st.load(reqs, self.max_pages)
             self._active = st
         st.step.zero_()
         for _ in range(k):
             g.run(self.use_graphs)
-        toks = st.hist[:B, :k].tolist()
-        for r, row in zip(self.running, toks):
+        if self._host_bufs is not None:
+            self._hb ^= 1
+            host = self._host_bufs[self._hb]
+            host[:B, :k].copy_(st.hist[:B, :k], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        else:
+            host, ev = st.hist, None
+        self.stats.graph_replays += k if self.use_graphs else 0
+        return _Window(st, reqs, B, k, host, ev)
+
+    def _consume(self, win: _Window) -> None:
+        if win.event is not None:
+            win.event.synchronize()
+        toks = win.host[:win.B, :win.k].tolist()
+        for r, row in zip(win.reqs, toks):
+            if r.done:   # finished (EOS / cancel) in an earlier window: discard
+                continue
             for tk in row:
                 if r.done_pending:
                     break
                 r.output.append(int(tk))
                 if (not r.ignore_eos) and int(tk) in self.eos:
                     r.done_pending = True
-        self.stats.graph_replays += k if self.use_graphs else 0
-        self.stats.decode_tokens += B * k
+        self.stats.decode_tokens += win.B * win.k
+
+    def _decode(self) -> None:
+        """Up to ``multi_step`` decode steps per window with no host round trip in
+        between; the next window is queued behind the current one when the batch
+        composition cannot change at the boundary."""
+        t0 = time.perf_counter()
+        prev = self._inflight or self._launch()
+        self._inflight = None
+        nxt = None
+        same = len(prev.reqs) == len(self.running) and all(a is b for a, b in zip(prev.reqs, self.running))
+        if (self.pipeline and same and self._active is prev.st
+                and not self._admittable()
+                and all(r.max_tokens - len(r.output) - prev.k >= 1 for r in prev.reqs)):
+            nxt = self._launch(ahead=prev.k)
+        self._consume(prev)
+        self._inflight = nxt
         self.stats.decode_s += time.perf_counter() - t0
 
     def _reap(self) -> list[GenRequest]:

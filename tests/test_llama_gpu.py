@@ -67,3 +67,38 @@ def test_llama3_8b_architecture_smoke():
     eng.generate(reqs)
     for r in reqs:
         assert len(r.output) == 6 and all(0 <= t < cfg.vocab_size for t in r.output)
+
+
+def test_pipelined_windows_eos_and_arrivals():
+    """Pipelined multi-step decode windows (graphs) must produce exactly the eager
+    engine's tokens with staggered lengths, EOS inside a window and requests that
+    arrive while others decode."""
+    cfg = get_config("tiny-gqa4")
+    m = LlamaModel(cfg, device="cuda").init_random(seed=6)
+
+    def run(graphs, eos):
+        kv = PagedKVCache(cfg.layers, 256, cfg.kv_heads, 128, 16, device="cuda")
+        eng = LLMEngine(m, kv, max_batch=8, max_context=1024, use_graphs=graphs, multi_step=4)
+        if eos is not None:
+            eng.eos = {eos}
+        first = [GenRequest(list(range(3, 3 + n)), max_tokens=mt, temperature=0.8, seed=s)
+                 for n, mt, s in [(9, 30, 0), (40, 7, 1), (120, 19, 2)]]
+        late = [GenRequest(list(range(50, 50 + n)), max_tokens=mt, temperature=0.8, seed=s)
+                for n, mt, s in [(33, 11, 3), (5, 26, 4)]]
+        for r in first:
+            eng.submit(r)
+        for _ in range(3):
+            eng.step()
+        for r in late:
+            eng.submit(r)
+        while any(not r.done for r in first + late):
+            eng.step()
+        assert kv.allocator.free == kv.num_pages
+        return [r.output for r in first + late]
+
+    base = run(False, None)
+    assert run(True, None) == base
+    eos = base[0][12]  # a token request 0 samples mid-stream: EOS inside a window
+    ref = run(False, eos)
+    assert len(ref[0]) == 13
+    assert run(True, eos) == ref
