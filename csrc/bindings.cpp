@@ -53,12 +53,14 @@ void rmsnorm(const at::Tensor& x, const c10::optional<at::Tensor>& residual, con
                    (int)hidden, x.stride(0), rstride, y.stride(0), (float)eps, cur_stream()));
 }
 
-void silu_mul(const at::Tensor& gu, at::Tensor& out) {
+void silu_mul(const at::Tensor& gu, at::Tensor& out, int64_t block) {
   CHECK_DEV(gu); CHECK_BF16(gu); CHECK_BF16(out); ROWMAJOR_VEC(gu); ROWMAJOR_VEC(out);
   const int64_t rows = gu.size(0), inter = out.size(1);
   TORCH_CHECK(gu.size(1) == 2 * inter && out.size(0) == rows && inter % 8 == 0, "silu_mul shape mismatch");
+  if (block == 0) block = inter;
+  TORCH_CHECK(block % 8 == 0 && inter % block == 0, "silu_mul: interleave block must divide inter, % 8");
   const c10::hip::HIPGuardMasqueradingAsCUDA g(gu.device());
-  RC(oamd::silu_mul(ptr<bf16_t>(gu), ptr<bf16_t>(out), rows, (int)inter, gu.stride(0), out.stride(0),
+  RC(oamd::silu_mul(ptr<bf16_t>(gu), ptr<bf16_t>(out), rows, (int)inter, (int)block, gu.stride(0), out.stride(0),
                     cur_stream()));
 }
 
@@ -106,11 +108,12 @@ void rope_kv(const at::Tensor& qkv, const at::Tensor& pos, const at::Tensor& cos
 }
 
 void gemm_decode(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const c10::optional<at::Tensor>& p,
-                 int64_t splits, int64_t bn, int64_t bm) {
+                 int64_t splits, int64_t bn, int64_t bm, bool silu_gu) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(y); CHECK_CONTIG(x); CHECK_CONTIG(w); CHECK_CONTIG(y);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 2, "x [M,K], w [N,K], y [M,N]");
   const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
-  TORCH_CHECK(w.size(1) == K && y.size(0) == M && y.size(1) == N, "gemm shapes");
+  TORCH_CHECK(w.size(1) == K && y.size(0) == M && y.size(1) == (silu_gu ? N / 2 : N), "gemm shapes");
+  TORCH_CHECK(!silu_gu || (bn == 128 && splits == 1), "fused SwiGLU needs bn = 128, splits = 1");
   if (bm == 0) bm = std::min<int64_t>(M, 256);
   TORCH_CHECK((bm == 64 || bm == 128 || bm == 256) && M % bm == 0, "gemm_decode: M % bm, bm in {64,128,256}");
   TORCH_CHECK((bn == 64 || bn == 128) && N % bn == 0, "gemm_decode: N % bn, bn in {64, 128}");
@@ -125,7 +128,7 @@ void gemm_decode(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const 
   TORCH_CHECK(K < (1LL << 31) / 64 && M * K < (1LL << 31) && N * K < (1LL << 40), "gemm too large");
   const c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   RC(oamd::gemm_decode(ptr<bf16_t>(x), ptr<bf16_t>(w), ptr<bf16_t>(y), pp, (int)M, (int)N, (int)K, (int)splits,
-                       (int)bn, (int)bm, cur_stream()));
+                       (int)bn, (int)bm, silu_gu, cur_stream()));
 }
 
 void attn_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
@@ -198,13 +201,13 @@ void register_scan_bindings(pybind11::module_& m);
 PYBIND11_MODULE(_C, m) {
   m.doc() = "operator_amd gfx950 kernels";
   m.def("rmsnorm", &rmsnorm, "RMSNorm with optional fused residual add");
-  m.def("silu_mul", &silu_mul);
+  m.def("silu_mul", &silu_mul, pybind11::arg("gu"), pybind11::arg("out"), pybind11::arg("block") = 0);
   m.def("embedding", &embedding);
   m.def("rope_kv", &rope_kv);
   m.def("attn_decode", &attn_decode);
   m.def("gemm_decode", &gemm_decode, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"),
         pybind11::arg("p") = pybind11::none(), pybind11::arg("splits") = 1, pybind11::arg("bn") = 64,
-        pybind11::arg("bm") = 0);
+        pybind11::arg("bm") = 0, pybind11::arg("silu_gu") = false);
   m.def("attn_prefill", &attn_prefill);
   m.def("sample", &sample, pybind11::arg("logits"), pybind11::arg("temperature"), pybind11::arg("seeds"),
         pybind11::arg("positions"), pybind11::arg("out"), pybind11::arg("col_offset") = 0,

@@ -58,7 +58,12 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int BM, int BN, bool PARTIAL>
+// Epilogues: plain bf16 store, fp32 split-K slab, or the fused SwiGLU of the
+// gate|up projection (weights interleaved in 64-row blocks: tile columns
+// [0,64) = gate, [64,128) = up of the same 64 features; output [M, N/2]).
+enum { kEpiStore = 0, kEpiPartial = 1, kEpiSiluGU = 2 };
+
+template <int BM, int BN, int EPI>
 __global__ void __launch_bounds__(kWaves * 64, 1) gemm_tn_kernel(const bf16_t* __restrict__ X,
                                                                  const bf16_t* __restrict__ W, bf16_t* __restrict__ Y,
                                                                  float* __restrict__ P, int M, int N, int K, int S) {
@@ -137,19 +142,54 @@ __global__ void __launch_bounds__(kWaves * 64, 1) gemm_tn_kernel(const bf16_t* _
     compute(t % kStages);
   }
 
-  // ---- epilogue: C lane l -> row 4*lg + r, col l15 of each fragment ----
+  if constexpr (EPI == kEpiSiluGU) {
+    // Stage the tile through LDS (the ring is idle now) so each thread sees a
+    // feature's gate and up values: HF numerics, act(bf16(g)) rounded to bf16,
+    // times bf16(u), rounded.
+    static_assert(BN == 128, "fused SwiGLU needs gate and up halves in one tile");
+    constexpr int LD = BN + 4;  // fp32 row stride (+4: spreads the column writes over banks)
+    static_assert(BM * LD * 4 <= C::LDS_BYTES, "C tile must fit the LDS ring");
+    float* ct = reinterpret_cast<float*>(lds);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
 #pragma unroll
-  for (int i = 0; i < C::FM; ++i)
+    for (int i = 0; i < C::FM; ++i)
 #pragma unroll
-    for (int j = 0; j < C::FN; ++j) {
-      const int col = n0 + wn * (BN / C::WN) + 16 * j + l15;
+      for (int j = 0; j < C::FN; ++j) {
+        const int col = wn * (BN / C::WN) + 16 * j + l15;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = wm * (BM / C::WM) + 16 * i + 4 * lg + r;
-        if constexpr (PARTIAL) P[((int64_t)kz * M + m0 + row) * N + col] = acc[i][j][r];
-        else Y[(int64_t)(m0 + row) * N + col] = f2bf(acc[i][j][r]);
+        for (int r = 0; r < 4; ++r) ct[(wm * (BM / C::WM) + 16 * i + 4 * lg + r) * LD + col] = acc[i][j][r];
       }
+    __syncthreads();
+    const int NO = N / 2;  // output features
+    for (int v = tid; v < BM * 8; v += kWaves * 64) {
+      const int row = v >> 3, f0 = (v & 7) * 8;
+      const float* cr = ct + row * LD;
+      u16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float g = bf2f(f2bf(cr[f0 + e]));
+        const float u = bf2f(f2bf(cr[64 + f0 + e]));
+        const float sg = bf2f(f2bf(g / (1.f + __expf(-g))));
+        o[e] = f2bf(sg * u);
+      }
+      *reinterpret_cast<u16x8*>(Y + (int64_t)(m0 + row) * NO + nt * 64 + f0) = o;
     }
+  } else {
+    // ---- C lane l -> row 4*lg + r, col l15 of each fragment ----
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+      for (int j = 0; j < C::FN; ++j) {
+        const int col = n0 + wn * (BN / C::WN) + 16 * j + l15;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = wm * (BM / C::WM) + 16 * i + 4 * lg + r;
+          if constexpr (EPI == kEpiPartial) P[((int64_t)kz * M + m0 + row) * N + col] = acc[i][j][r];
+          else Y[(int64_t)(m0 + row) * N + col] = f2bf(acc[i][j][r]);
+        }
+      }
+  }
 }
 
 // Y[m, n] = bf16(sum_s P[s, m, n]); 4 columns per thread.
@@ -165,15 +205,26 @@ __global__ void gemm_splitk_reduce_kernel(const float* __restrict__ P, bf16_t* _
 }
 
 int gemm_decode(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, int N, int K, int S, int BN,
-                int BM, hipStream_t stream) {
+                int BM, bool silu_gu, hipStream_t stream) {
   if ((BM != 64 && BM != 128 && BM != 256) || M % BM != 0) return -1;
+  if (silu_gu) {  // fused SwiGLU: one K slice, 128-column tiles of 64 gate + 64 up rows
+    if (BN != 128 || S != 1 || N % 128 != 0 || K % kBK != 0) return -5;
+    const dim3 grid(N / 128, M / BM);
+    switch (BM) {
+      case 64: gemm_tn_kernel<64, 128, kEpiSiluGU><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, 1); break;
+      case 128: gemm_tn_kernel<128, 128, kEpiSiluGU><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, 1); break;
+      default: gemm_tn_kernel<256, 128, kEpiSiluGU><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, 1); break;
+    }
+    OAMD_LAUNCH_CHECK();
+    return 0;
+  }
   if ((BN != 64 && BN != 128) || N % BN != 0) return -2;
   if (S < 1 || 8 % S != 0 || K % (kBK * S) != 0) return -3;
   if (S > 1 && P == nullptr) return -4;
   const dim3 grid((N / BN) * S, M / BM);
 #define OAMD_GEMM2(BM, BNN)                                                                                   \
-  if (S > 1) gemm_tn_kernel<BM, BNN, true><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, S);       \
-  else gemm_tn_kernel<BM, BNN, false><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, S)
+  if (S > 1) gemm_tn_kernel<BM, BNN, kEpiPartial><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, S); \
+  else gemm_tn_kernel<BM, BNN, kEpiStore><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, S)
 #define OAMD_GEMM(BM) \
   if (BN == 64) { OAMD_GEMM2(BM, 64); } else { OAMD_GEMM2(BM, 128); }
   switch (BM) {

@@ -12,7 +12,7 @@ typedef uint16_t bf16_t;
 // ---- explanation-model ops ----
 int rmsnorm(const bf16_t* x, bf16_t* residual, const bf16_t* w, bf16_t* y, int rows, int hidden,
             int64_t x_stride, int64_t r_stride, int64_t y_stride, float eps, hipStream_t stream);
-int silu_mul(const bf16_t* gu, bf16_t* out, int64_t rows, int inter, int64_t in_stride,
+int silu_mul(const bf16_t* gu, bf16_t* out, int64_t rows, int inter, int block, int64_t in_stride,
              int64_t out_stride, hipStream_t stream);
 int embedding(const int64_t* ids, const bf16_t* table, bf16_t* out, int tokens, int hidden,
               int64_t vocab, hipStream_t stream);
@@ -23,7 +23,7 @@ int rope_kv(const bf16_t* qkv, int64_t qkv_stride, const int64_t* pos, const flo
 // Y[M,N] = X[M,K] W[N,K]^T for decode buckets (M a multiple of the BM-row tile, BM in {64,128,256}); S-way split-K
 // (S | 8) with fp32 slabs P[S][M][N] reduced into Y; BN in {64, 128} columns per tile.
 int gemm_decode(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, int N, int K, int S, int BN,
-                int BM, hipStream_t stream);
+                int BM, bool silu_gu, hipStream_t stream);
 
 int attn_decode(const bf16_t* q, const bf16_t* k_cache, const bf16_t* v_cache, const int* block_tables,
                 const int* seq_lens, bf16_t* out, float* o_part, float* ml_part, int B, int Hq, int Hkv,

@@ -82,17 +82,21 @@ int rmsnorm(const bf16_t* x, bf16_t* residual, const bf16_t* w, bf16_t* y,
   return 0;
 }
 
-// out[m, i] = silu(gu[m, i]) * gu[m, I + i]; grid-stride over 8-element vectors.
+// out[m, i] = silu(gate) * up; grid-stride over 8-element vectors. gate|up
+// columns are interleaved in blocks of `block` features (block == inter: the
+// plain [gate | up] concatenation): gate of feature i at (i / block) * 2 * block
+// + i % block, up `block` columns later.
 __global__ void silu_mul_kernel(const bf16_t* __restrict__ gu, bf16_t* __restrict__ out,
-                                int64_t rows, int inter, int64_t in_stride, int64_t out_stride) {
+                                int64_t rows, int inter, int block, int64_t in_stride, int64_t out_stride) {
   const int vpr = inter >> 3;
   const int64_t total = rows * vpr;
   for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
     const int64_t m = idx / vpr;
     const int c = static_cast<int>(idx - m * vpr) << 3;
-    const u16x8 g = *reinterpret_cast<const u16x8*>(gu + m * in_stride + c);
-    const u16x8 u = *reinterpret_cast<const u16x8*>(gu + m * in_stride + inter + c);
+    const int gc = (c / block) * 2 * block + c % block;
+    const u16x8 g = *reinterpret_cast<const u16x8*>(gu + m * in_stride + gc);
+    const u16x8 u = *reinterpret_cast<const u16x8*>(gu + m * in_stride + gc + block);
     u16x8 o;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -105,14 +109,16 @@ __global__ void silu_mul_kernel(const bf16_t* __restrict__ gu, bf16_t* __restric
   }
 }
 
-int silu_mul(const bf16_t* gu, bf16_t* out, int64_t rows, int inter,
+int silu_mul(const bf16_t* gu, bf16_t* out, int64_t rows, int inter, int block,
              int64_t in_stride, int64_t out_stride, hipStream_t stream) {
   if (rows == 0) return 0;
+  if (block <= 0 || block % 8 != 0 || inter % block != 0) return -1;
   const int64_t total = rows * (inter / 8);
   const int nt = 256;
   int64_t blocks = (total + nt - 1) / nt;
   if (blocks > 256 * 16) blocks = 256 * 16;
-  silu_mul_kernel<<<static_cast<int>(blocks), nt, 0, stream>>>(gu, out, rows, inter, in_stride, out_stride);
+  silu_mul_kernel<<<static_cast<int>(blocks), nt, 0, stream>>>(gu, out, rows, inter, block, in_stride,
+                                                               out_stride);
   OAMD_LAUNCH_CHECK();
   return 0;
 }

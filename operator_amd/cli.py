@@ -84,6 +84,23 @@ def cmd_explain(args) -> int:
     return 0
 
 
+def _build_pool(s, patterns):
+    """One engine process per GPU: the controller stays a CPU process."""
+    from operator_amd.engine.pool import EnginePool, PoolExplainService, PoolMatchService
+
+    if s.engine.device == "cpu":
+        devices = ["cpu"] * max(1, s.engine.gpus)
+    else:
+        import torch
+
+        n = torch.cuda.device_count()  # counts devices without initialising the GPU
+        devices = [f"cuda:{i}" for i in range(min(max(1, s.engine.gpus), max(1, n)))]
+    roles = tuple(r for r, on in (("match", s.services.match in ("local", "cpu")),
+                                  ("explain", s.services.explain == "local")) if on)
+    pool = EnginePool(s, patterns, devices, roles=roles)
+    return pool, PoolMatchService(pool), PoolExplainService(pool)
+
+
 def _build_services(s, metrics):
     from operator_amd.engine.factory import build_explain_service, build_match_engine
     from operator_amd.engine.service import LocalMatchService, RemoteLogParser
@@ -106,12 +123,26 @@ def cmd_run(args) -> int:
     from operator_amd.utils.metrics import Metrics
 
     s = _settings(args)
+    if args.gpus and args.gpus > 1:
+        s.engine.gpus = args.gpus
+    pool = None
+    metrics = Metrics()
     if s.kube.mode == "fake" or args.fake:
         kube = FakeKube()
     else:
         kube = KubeClient.auto(s.kube.mode, s.kube.kubeconfig, s.kube.request_timeout_s)
-    metrics = Metrics()
-    matcher, factory, explainer = _build_services(s, metrics)
+    if s.engine.gpus > 1 or s.engine.pool:
+        # engines first, before anything in this process could initialise a GPU
+        from operator_amd.controller.operator import load_patterns
+
+        pool, matcher, pool_explainer = _build_pool(s, load_patterns(s, kube))
+        explainer = pool_explainer if "explain" in pool.roles else None
+        if "match" not in pool.roles:
+            matcher, factory, _ = _build_services(s, metrics)
+        else:
+            factory = lambda ps: ps  # noqa: E731 - the pool rebuilds the DFA in every worker
+    else:
+        matcher, factory, explainer = _build_services(s, metrics)
     op = Operator(kube, s, match_service=matcher, explain_service=explainer, metrics=metrics,
                   match_engine_factory=factory)
     op.start()
@@ -121,6 +152,8 @@ def cmd_run(args) -> int:
     logging.getLogger(__name__).info("running; health on :%d", s.health.port)
     stop.wait()
     op.stop()
+    if pool is not None:
+        pool.close()
     return 0
 
 
@@ -164,7 +197,7 @@ def main(argv: list[str] | None = None) -> int:
     p = sub.add_parser("run")
     common(p)
     p.add_argument("--fake", action="store_true", help="in-memory FakeKube instead of a cluster")
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=0, help="engine processes, one per GPU (engine.gpus)")
     p = sub.add_parser("manifests")
     p.add_argument("--namespace", default="podmortem-system")
     p.add_argument("--image", default="ghcr.io/podmortem/operator-amd:latest")

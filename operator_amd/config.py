@@ -81,6 +81,8 @@ class ServicesCfg(BaseModel):
 
 
 class EngineCfg(BaseModel):
+    gpus: int = 1                     # engine processes (one per GPU) behind the controller
+    pool: bool = False                # run the engines out of process even with one GPU
     model: str = "llama3-8b"
     model_path: Optional[str] = None  # HF safetensors dir; random init when absent
     seed: int = 0

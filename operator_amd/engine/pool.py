@@ -1,0 +1,336 @@
+"""Multi-GPU engine pool: one engine process per GPU behind the CPU controller.
+
+SURVEY.md §5.8 "Process model": the controller (kube watches, reconcilers,
+sinks) is a CPU process; each GPU gets its own engine process holding the
+log-scan DFA and a TP=1 explanation model (P1 / P2: data parallel over
+failures and over explanation requests). The reference's two single-replica
+REST services (``K/log-parser-deployment.yaml:8``,
+``K/ai-interface-deployment.yaml:8``) become these workers, reached over
+local pipes instead of HTTP.
+
+* Routing: least outstanding requests among live, ready workers — every
+  worker holds the full pattern set and model, so any worker can serve any
+  failure; batching happens inside the worker (LocalMatchService micro-batches
+  scans, the LLM engine continuously batches explanations).
+* Health loop (SURVEY.md §5.3 "GPU-worker health loop"): a worker that exits
+  (GPU fault, OOM kill) or stops heart-beating is drained — its in-flight
+  requests are re-queued to the surviving workers — and respawned up to
+  ``max_restarts`` times.
+* Fault injection: ``inject_crash(i)`` makes worker i exit abruptly, for the
+  recovery tests (the engine-side half of the §5.3 fault matrix).
+* Pattern updates (PatternLibrary sync) are broadcast to every worker.
+
+Workers are started with the ``spawn`` method before the controller touches
+any GPU, so no process ever forks a GPU-initialised parent.
+"""
+from __future__ import annotations
+
+import itertools
+import logging
+import multiprocessing as mp
+import os
+import queue
+import threading
+import time
+from concurrent.futures import Future
+
+from operator_amd.api.models import AIProviderConfig, AIResponse, AnalysisResult, PodFailureData
+
+log = logging.getLogger(__name__)
+
+
+class WorkerDied(RuntimeError):
+    pass
+
+
+# ---------------------------------------------------------------- worker process
+def _worker_main(idx: int, device: str, settings_obj: dict, patterns, roles: tuple[str, ...], inq, outq,
+                 heartbeat_s: float) -> None:
+    logging.basicConfig(level=os.environ.get("PODMORTEM_LOG_LEVEL", "WARNING"))
+    from concurrent.futures import ThreadPoolExecutor
+
+    from operator_amd.config import Settings
+    from operator_amd.engine import factory, service
+
+    s = Settings.model_validate(settings_obj)
+    s.engine.device = device
+    if device == "cpu":
+        s.services.match = "cpu"
+    matcher = explainer = None
+    try:
+        if "match" in roles:
+            matcher = service.LocalMatchService(factory.build_match_engine(s, patterns, device=device),
+                                                s.services.match_max_batch, s.services.match_batch_wait_ms)
+        if "explain" in roles:
+            explainer = factory.build_explain_service(s)
+    except Exception as e:  # noqa: BLE001 - reported to the controller, which marks the worker dead
+        outq.put(("fatal", idx, f"{type(e).__name__}: {e}"))
+        return
+    stop = threading.Event()
+
+    def beat():
+        while not stop.wait(heartbeat_s):
+            outq.put(("hb", idx, time.time()))
+
+    threading.Thread(target=beat, daemon=True).start()
+    outq.put(("ready", idx, {"device": device, "pid": os.getpid(), "roles": list(roles)}))
+    pool = ThreadPoolExecutor(max_workers=max(4, s.operator.workers))
+
+    def run(rid, kind, payload):
+        try:
+            if kind == "match":
+                res = matcher.analyze(PodFailureData.model_validate(payload))
+                outq.put(("ok", idx, rid, res.to_obj()))
+            else:
+                res = explainer.explain(AnalysisResult.model_validate(payload[0]),
+                                        AIProviderConfig.model_validate(payload[1]))
+                outq.put(("ok", idx, rid, res.to_obj()))
+        except Exception as e:  # noqa: BLE001 - per-request failure, worker stays up
+            outq.put(("err", idx, rid, f"{type(e).__name__}: {e}"))
+
+    while True:
+        msg = inq.get()
+        kind = msg[0]
+        if kind == "stop":
+            break
+        if kind == "crash":           # fault injection: die like a GPU fault would
+            os._exit(int(msg[1]))
+        if kind == "hang":            # fault injection: stop heart-beating and serving
+            stop.set()
+            time.sleep(3600)
+        if kind == "patterns":
+            if matcher is not None:
+                matcher.swap_engine(factory.build_match_engine(s, msg[1], device=device))
+            continue
+        if kind in ("match", "explain"):
+            pool.submit(run, msg[1], kind, msg[2])
+    stop.set()
+    pool.shutdown(wait=True)
+    if matcher is not None:
+        matcher.close()
+
+
+# ---------------------------------------------------------------- controller side
+class _Worker:
+    def __init__(self, idx: int, device: str):
+        self.idx, self.device = idx, device
+        self.proc = None
+        self.inq = None
+        self.ready = False
+        self.alive = False
+        self.last_beat = 0.0
+        self.restarts = 0
+        self.inflight: dict[int, tuple] = {}
+        self.info: dict = {}
+
+
+class EnginePool:
+    def __init__(self, settings, patterns, devices: list[str], roles: tuple[str, ...] = ("match", "explain"),
+                 heartbeat_s: float = 2.0, heartbeat_timeout_s: float = 30.0, max_restarts: int = 3):
+        self.settings, self.patterns, self.roles = settings, patterns, roles
+        self.heartbeat_s, self.heartbeat_timeout_s = heartbeat_s, heartbeat_timeout_s
+        self.max_restarts = max_restarts
+        self._ctx = mp.get_context("spawn")
+        self._outq = self._ctx.Queue()
+        self._lock = threading.Lock()
+        self._ready_cv = threading.Condition(self._lock)
+        self._ids = itertools.count()
+        self._closing = False
+        self.workers = [_Worker(i, d) for i, d in enumerate(devices)]
+        self.stats = {"requeued": 0, "restarts": 0, "deaths": 0}
+        for w in self.workers:
+            self._spawn(w)
+        self._reader = threading.Thread(target=self._read_loop, name="pool-reader", daemon=True)
+        self._reader.start()
+        self._monitor = threading.Thread(target=self._monitor_loop, name="pool-monitor", daemon=True)
+        self._monitor.start()
+
+    # ---------------------------------------------------------------- lifecycle
+    def _spawn(self, w: _Worker) -> None:
+        w.inq = self._ctx.Queue()
+        w.ready, w.alive, w.last_beat = False, True, time.time()
+        w.proc = self._ctx.Process(
+            target=_worker_main, name=f"engine-{w.idx}",
+            args=(w.idx, w.device, self.settings.model_dump(), self.patterns, self.roles, w.inq, self._outq,
+                  self.heartbeat_s), daemon=True)
+        w.proc.start()
+
+    def wait_ready(self, timeout: float = 600.0, n: int | None = None) -> int:
+        """Block until ``n`` (default: all) workers are ready; returns the ready count."""
+        need = len(self.workers) if n is None else n
+        deadline = time.time() + timeout
+        with self._ready_cv:
+            while sum(w.ready for w in self.workers) < need:
+                left = deadline - time.time()
+                if left <= 0 or not any(w.alive for w in self.workers):
+                    break
+                self._ready_cv.wait(min(left, 1.0))
+            return sum(w.ready for w in self.workers)
+
+    def close(self, timeout: float = 30.0) -> None:
+        self._closing = True
+        for w in self.workers:
+            if w.alive:
+                try:
+                    w.inq.put(("stop",))
+                except (OSError, ValueError):
+                    pass
+        for w in self.workers:
+            if w.proc is not None:
+                w.proc.join(timeout)
+                if w.proc.is_alive():
+                    w.proc.kill()
+                    w.proc.join(5)
+        with self._lock:
+            for w in self.workers:
+                for rid, (kind, payload, fut) in list(w.inflight.items()):
+                    if not fut.done():
+                        fut.set_exception(WorkerDied("engine pool closed"))
+                w.inflight.clear()
+
+    # ---------------------------------------------------------------- requests
+    def _pick(self) -> _Worker | None:
+        live = [w for w in self.workers if w.alive and w.ready]
+        if not live:
+            return None
+        return min(live, key=lambda w: (len(w.inflight), w.idx))
+
+    def _dispatch(self, kind: str, payload, fut: Future, rid: int | None = None) -> None:
+        with self._lock:
+            w = self._pick()
+            if w is None:
+                if any(x.alive for x in self.workers):   # still starting: wait for one
+                    self._ready_cv.wait_for(lambda: self._pick() is not None or self._closing, timeout=600)
+                    w = self._pick()
+                if w is None:
+                    fut.set_exception(WorkerDied("no live engine worker"))
+                    return
+            rid = next(self._ids) if rid is None else rid
+            w.inflight[rid] = (kind, payload, fut)
+            w.inq.put((kind, rid, payload))
+
+    def submit_match(self, data: PodFailureData) -> Future:
+        fut: Future = Future()
+        self._dispatch("match", data.model_dump(by_alias=True, exclude_none=True), fut)
+        return fut
+
+    def submit_explain(self, result: AnalysisResult, cfg: AIProviderConfig) -> Future:
+        fut: Future = Future()
+        self._dispatch("explain", (result.to_obj(), cfg.model_dump(by_alias=True, exclude_none=True)), fut)
+        return fut
+
+    def set_patterns(self, patterns) -> None:
+        self.patterns = patterns
+        with self._lock:
+            for w in self.workers:
+                if w.alive:
+                    w.inq.put(("patterns", patterns))
+
+    def inject_crash(self, idx: int, code: int = 139) -> None:
+        self.workers[idx].inq.put(("crash", code))
+
+    def inject_hang(self, idx: int) -> None:
+        self.workers[idx].inq.put(("hang",))
+
+    # ---------------------------------------------------------------- background loops
+    def _read_loop(self) -> None:
+        while True:
+            try:
+                msg = self._outq.get(timeout=0.5)
+            except queue.Empty:
+                if self._closing:
+                    return
+                continue
+            except (EOFError, OSError):
+                return
+            kind, idx = msg[0], msg[1]
+            w = self.workers[idx]
+            with self._lock:
+                if kind == "hb":
+                    w.last_beat = time.time()
+                elif kind == "ready":
+                    w.ready, w.info, w.last_beat = True, msg[2], time.time()
+                    self._ready_cv.notify_all()
+                elif kind == "fatal":
+                    log.error("engine worker %d failed to start: %s", idx, msg[2])
+                    w.info["fatal"] = msg[2]
+                    w.restarts = self.max_restarts  # a start-up failure is not transient
+                elif kind in ("ok", "err"):
+                    item = w.inflight.pop(msg[2], None)
+                    if item is not None and not item[2].done():
+                        if kind == "ok":
+                            cls = AnalysisResult if item[0] == "match" else AIResponse
+                            item[2].set_result(cls.model_validate(msg[3]))
+                        else:
+                            item[2].set_exception(RuntimeError(msg[3]))
+
+    def _monitor_loop(self) -> None:
+        while not self._closing:
+            time.sleep(min(0.5, self.heartbeat_s))
+            now = time.time()
+            for w in self.workers:
+                if not w.alive or self._closing:
+                    continue
+                dead = not w.proc.is_alive()
+                hung = w.ready and now - w.last_beat > self.heartbeat_timeout_s
+                if dead or hung:
+                    if hung and w.proc.is_alive():
+                        w.proc.kill()
+                    self._on_death(w, "exited with %s" % w.proc.exitcode if dead else "stopped heart-beating")
+
+    def _on_death(self, w: _Worker, why: str) -> None:
+        with self._lock:
+            w.alive, w.ready = False, False
+            orphans = list(w.inflight.items())
+            w.inflight.clear()
+            self.stats["deaths"] += 1
+        log.error("engine worker %d (%s) %s; re-queueing %d in-flight requests", w.idx, w.device, why,
+                  len(orphans))
+        if w.restarts < self.max_restarts and not self._closing:
+            w.restarts += 1
+            self.stats["restarts"] += 1
+            self._spawn(w)
+        live = [(rid, item) for rid, item in orphans if not item[2].done()]
+        self.stats["requeued"] += len(live)
+        if live:  # re-dispatch off the monitor thread (it may wait for a worker to become ready)
+            threading.Thread(target=lambda: [self._dispatch(k, p, f, rid) for rid, (k, p, f) in live],
+                             name="pool-requeue", daemon=True).start()
+
+    def health(self) -> dict:
+        with self._lock:
+            return {"workers": [{"idx": w.idx, "device": w.device, "alive": w.alive, "ready": w.ready,
+                                 "inflight": len(w.inflight), "restarts": w.restarts} for w in self.workers],
+                    **self.stats}
+
+
+class PoolMatchService:
+    """LocalMatchService-compatible front for an EnginePool."""
+
+    def __init__(self, pool: EnginePool, timeout_s: float = 600.0):
+        self.pool, self.timeout_s = pool, timeout_s
+
+    def analyze(self, data: PodFailureData) -> AnalysisResult:
+        return self.pool.submit_match(data).result(self.timeout_s)
+
+    def swap_engine(self, patterns) -> None:  # the pool rebuilds the DFA inside each worker
+        self.pool.set_patterns(patterns)
+
+    def close(self) -> None:
+        pass
+
+
+class PoolExplainService:
+    """LocalExplainService-compatible front for an EnginePool."""
+
+    def __init__(self, pool: EnginePool, timeout_s: float = 3600.0):
+        self.pool, self.timeout_s = pool, timeout_s
+
+    def explain(self, result: AnalysisResult, cfg: AIProviderConfig) -> AIResponse:
+        return self.pool.submit_explain(result, cfg).result(self.timeout_s)
+
+    def explain_many(self, items):
+        futs = [self.pool.submit_explain(r, c) for r, c in items]
+        return [f.result(self.timeout_s) for f in futs]
+
+    def ready(self) -> bool:
+        return any(w.ready for w in self.pool.workers)

@@ -11,7 +11,7 @@ AIInterfaceRestClient.java:37-39). Per layer:
     a   = o @ Wo^T        [TP: all-reduce]    GEMM
     x   = rmsnorm(a + h)                      HIP
     gu  = x @ Wgu^T                           GEMM (fused gate|up)
-    m   = silu(g) * u                         HIP
+    m   = silu(g) * u                         HIP (fused into the gate|up GEMM at decode)
     d   = m @ Wd^T        [TP: all-reduce]    GEMM
 logits = rmsnorm(h) @ Wlm^T (vocab-parallel under TP); tokens = Gumbel-max
 sampler on each vocab shard + a max over shards.
@@ -86,6 +86,8 @@ class LlamaModel:
             raise ValueError(f"{cfg.name}: heads/kv_heads/intermediate/vocab must divide by tp={W}")
         self.hq = cfg.heads // W
         self.hkv = cfg.kv_heads // W
+        # gate|up rows interleaved in 64-feature blocks (fused SwiGLU GEMM epilogue)
+        self.gu_block = ops.GU_BLOCK if (cfg.intermediate // W) % ops.GU_BLOCK == 0 else None
         self.inter = cfg.intermediate // W
         self.vocab_local = cfg.vocab_size // W
         self.vocab_offset = self.tp.rank * self.vocab_local
@@ -139,9 +141,17 @@ class LlamaModel:
         return LayerWeights(
             wqkv=torch.cat([q, k, v], 0).contiguous(),
             wo=wo[:, r * self.hq * D:(r + 1) * self.hq * D].contiguous(),
-            wgu=torch.cat([g, u], 0).contiguous(),
+            wgu=(ops.interleave_gate_up(g, u, self.gu_block) if self.gu_block else torch.cat([g, u], 0).contiguous()),
             wd=wd[:, r * self.inter:(r + 1) * self.inter].contiguous(),
             attn_norm=an.contiguous(), mlp_norm=mn.contiguous())
+
+    def split_gate_up(self, wgu: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+        """(gate, up) rows of a layer's fused gate|up weight (undoes the interleave)."""
+        inter = wgu.shape[0] // 2
+        if not self.gu_block:
+            return wgu[:inter], wgu[inter:]
+        v = wgu.reshape(inter // self.gu_block, 2, self.gu_block, wgu.shape[1])
+        return v[:, 0].reshape(inter, -1), v[:, 1].reshape(inter, -1)
 
     def load_hf(self, path: str) -> "LlamaModel":
         """Load a HuggingFace Llama checkpoint directory (safetensors) and shard it."""
@@ -204,8 +214,7 @@ class LlamaModel:
             a = ops.linear(o.view(T, self.hq * c.head_dim), lw.wo)
             self.tp.all_reduce_(a)
             x = ops.rmsnorm(a, lw.mlp_norm, c.rms_eps, residual=h)
-            gu = ops.linear(x, lw.wgu)
-            m = ops.silu_mul(gu)
+            m = ops.gate_up_silu(x, lw.wgu, self.gu_block)
             d = ops.linear(m, lw.wd)
             self.tp.all_reduce_(d)
             nw = self.layers[i + 1].attn_norm if i + 1 < len(self.layers) else self.final_norm

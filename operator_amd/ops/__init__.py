@@ -18,7 +18,7 @@ from ._native import kernels, native_available, patterns
 __all__ = [
     "rmsnorm", "silu_mul", "embedding", "rope_kv", "attn_prefill", "attn_decode", "sample",
     "kernels", "patterns", "native_available", "reference", "prefill_work_list", "decode_splits",
-    "decode_workspace", "linear", "gemm_splits", "gemm_plan",
+    "decode_workspace", "linear", "gemm_splits", "gemm_plan", "gate_up_silu", "interleave_gate_up",
 ]
 
 DECODE_MIN_SPLIT_TOKENS = 256  # never split a sequence into pieces shorter than this
@@ -41,17 +41,45 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: torch.Tensor
     return y
 
 
-def silu_mul(gu: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+def silu_mul(gu: torch.Tensor, out: torch.Tensor | None = None, block: int | None = None) -> torch.Tensor:
+    """silu(gate) * up for gate|up interleaved in ``block``-feature blocks (None: [gate | up])."""
     if not gu.is_cuda:
-        r = reference.silu_mul(gu)
+        r = reference.silu_mul(gu, block)
         if out is not None:
             out.copy_(r)
             return out
         return r
     inter = gu.shape[1] // 2
     o = out if out is not None else torch.empty(gu.shape[0], inter, dtype=gu.dtype, device=gu.device)
-    kernels().silu_mul(gu, o)
+    kernels().silu_mul(gu, o, block or 0)
     return o
+
+
+GU_BLOCK = 64  # gate|up weight rows interleaved in 64-feature blocks (fused SwiGLU epilogue)
+
+
+def interleave_gate_up(g: torch.Tensor, u: torch.Tensor, block: int = GU_BLOCK) -> torch.Tensor:
+    """[g; u] rows -> blocks of ``block`` gate rows followed by the same features' up rows."""
+    inter, H = g.shape
+    return torch.stack([g.reshape(inter // block, block, H), u.reshape(inter // block, block, H)], 1).reshape(
+        2 * inter, H).contiguous()
+
+
+def gate_up_silu(x: torch.Tensor, wgu: torch.Tensor, block: int | None) -> torch.Tensor:
+    """silu(x Wg^T) * (x Wu^T) from the interleaved gate|up weight. Decode buckets run
+    one fused gfx950 kernel (GEMM + SwiGLU epilogue, no [M, 2I] intermediate);
+    other shapes run the GEMM then the silu_mul kernel."""
+    M, K = x.shape
+    N = wgu.shape[0]
+    if (x.is_cuda and block == 64 and x.dtype == torch.bfloat16 and M % 64 == 0 and M <= 256 and N % 128 == 0
+            and K % 64 == 0 and x.is_contiguous() and wgu.is_contiguous()):
+        t = _gemm_table_get().get(("silu", M, N, K))
+        if t != "blas":
+            bm = t[0] if t else min(M, 256)
+            y = torch.empty(M, N // 2, dtype=x.dtype, device=x.device)
+            kernels().gemm_decode(x, wgu, y, None, 1, 128, bm, True)
+            return y
+    return silu_mul(linear(x, wgu), block=block)
 
 
 def embedding(ids: torch.Tensor, table: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
@@ -133,7 +161,8 @@ def _gemm_table_get() -> dict:
     if _gemm_table is None:
         try:
             with open(_GEMM_TABLE_PATH) as f:
-                _gemm_table = {tuple(int(x) for x in k.split(",")): v for k, v in json.load(f).items()}
+                _gemm_table = {tuple(x if x == "silu" else int(x) for x in k.split(",")): v
+                               for k, v in json.load(f).items()}
         except (OSError, ValueError):
             _gemm_table = {}
     return _gemm_table
@@ -183,7 +212,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None, sp
     y = out if out is not None else torch.empty(M, N, dtype=x.dtype, device=x.device)
     if S > 1 and (partial is None or partial.numel() < S * M * N):
         partial = torch.empty(S * M * N, dtype=torch.float32, device=x.device)
-    kernels().gemm_decode(x, w, y, partial if S > 1 else None, S, bn, bm)
+    kernels().gemm_decode(x, w, y, partial if S > 1 else None, S, bn, bm, False)
     return y
 
 

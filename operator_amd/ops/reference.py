@@ -24,9 +24,15 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: torch.Tensor
     return (y.float() * w.float()).to(x.dtype), new_res
 
 
-def silu_mul(gu: torch.Tensor) -> torch.Tensor:
+def silu_mul(gu: torch.Tensor, block: int | None = None) -> torch.Tensor:
+    """silu(gate) * up; gate|up columns interleaved in blocks of ``block`` features
+    (None: the plain [gate | up] concatenation)."""
     inter = gu.shape[-1] // 2
-    g, u = gu[..., :inter], gu[..., inter:]
+    if block and block != inter:
+        v = gu.reshape(*gu.shape[:-1], inter // block, 2, block)
+        g, u = v[..., 0, :].reshape(*gu.shape[:-1], inter), v[..., 1, :].reshape(*gu.shape[:-1], inter)
+    else:
+        g, u = gu[..., :inter], gu[..., inter:]
     s = torch.nn.functional.silu(g.float()).to(gu.dtype)
     return (s.float() * u.float()).to(gu.dtype)
 

@@ -36,7 +36,7 @@ def test_matches_transformers_llama():
     sd = {"model.embed_tokens.weight": m.embed, "model.norm.weight": m.final_norm, "lm_head.weight": m.lm_head}
     for i, lw in enumerate(m.layers):
         q, k, v = torch.split(lw.wqkv, [cfg.heads * D, cfg.kv_heads * D, cfg.kv_heads * D])
-        g, u = torch.split(lw.wgu, [cfg.intermediate, cfg.intermediate])
+        g, u = m.split_gate_up(lw.wgu)
         p = f"model.layers.{i}."
         sd.update({p + "self_attn.q_proj.weight": q, p + "self_attn.k_proj.weight": k,
                    p + "self_attn.v_proj.weight": v, p + "self_attn.o_proj.weight": lw.wo,

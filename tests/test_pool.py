@@ -1,0 +1,126 @@
+"""Engine pool (one engine process per device) on the CPU tier: routing, parity
+with the in-process engines, pattern broadcast, and the §5.3 health loop —
+a worker that crashes or hangs is drained, its in-flight requests finish on the
+survivors, and it is respawned."""
+import time
+
+import pytest
+
+from operator_amd.api.models import AIProviderConfig, PodFailureData
+from operator_amd.config import load_settings
+from operator_amd.engine.match import MatchEngine
+from operator_amd.engine.pool import EnginePool, PoolExplainService, PoolMatchService, WorkerDied
+from operator_amd.kube.fake import failed_pod
+from operator_amd.patterns.schema import PatternSet
+from operator_amd.patterns.synth import LogFactory, catalog_library
+
+LOG_OOM = "\n".join(["starting app", "loading config"] * 20 + [
+    "java.lang.OutOfMemoryError: Java heap space", "\tat com.example.Cache.grow(Cache.java:42)"] + ["tick"] * 10)
+
+
+def _settings(**extra):
+    ov = {"engine.model": "tiny", "engine.device": "cpu", "engine.kv_cache_gb": 0.02, "engine.use_graphs": False,
+          "engine.max_context": 512, "engine.max_prompt_tokens": 256, "engine.max_batch": 8,
+          "services.explain": "local", "services.match": "cpu", "operator.workers": 4,
+          "services.match_batch_wait_ms": 1.0}
+    ov.update(extra)
+    return load_settings(env={}, overrides=ov)
+
+
+@pytest.fixture(scope="module")
+def pool():
+    p = EnginePool(_settings(), catalog_library(), ["cpu", "cpu"], heartbeat_s=0.2, heartbeat_timeout_s=8.0,
+                   max_restarts=2)
+    try:
+        assert p.wait_ready(600) == 2, p.health()
+        yield p
+    finally:
+        p.close()
+
+
+def _data(name, log=LOG_OOM):
+    return PodFailureData(pod=failed_pod(name), logs=log, events=[])
+
+
+def test_pool_match_matches_in_process_engine(pool):
+    ms = PoolMatchService(pool)
+    eng = MatchEngine(catalog_library(), device="cpu")
+    fac = LogFactory(n_patterns=30, seed=3)
+    docs, _ = fac.batch(6, 8 * 1024, n_failures=2, seed=5)
+    for i, d in enumerate(docs):
+        got = ms.analyze(_data(f"p{i}", d.decode()))
+        want = eng.analyze([d], [(f"p{i}", "default")])[0]
+        assert got.to_obj()["summary"] == want.to_obj()["summary"]
+        assert [e["matchedPattern"]["id"] for e in got.to_obj()["events"]] == \
+               [e["matchedPattern"]["id"] for e in want.to_obj()["events"]]
+
+
+def test_pool_explain_and_routing(pool):
+    ms, es = PoolMatchService(pool), PoolExplainService(pool)
+    res = ms.analyze(_data("exp"))
+    assert res.summary.highest_severity in ("CRITICAL", "HIGH")
+    outs = es.explain_many([(res, AIProviderConfig(max_tokens=6, temperature=0.0))] * 4)
+    assert all(o.explanation for o in outs)
+    # greedy decoding is deterministic across workers
+    assert len({o.explanation for o in outs}) == 1
+    # both workers served traffic (least-outstanding routing under concurrency)
+    futs = [pool.submit_match(_data(f"r{i}")) for i in range(16)]
+    assert all(f.result(120).summary.highest_severity == res.summary.highest_severity for f in futs)
+
+
+def test_pool_pattern_broadcast(pool):
+    ms = PoolMatchService(pool)
+    custom = PatternSet.from_yaml_text("""
+metadata: {library_id: custom}
+patterns:
+  - id: zz-custom
+    name: Custom marker
+    severity: CRITICAL
+    primary_pattern: {regex: "ZZ_CUSTOM_FAILURE_[0-9]+"}
+""")
+    ms.swap_engine(custom)
+    time.sleep(0.5)
+    r = ms.analyze(_data("c", "ok\nZZ_CUSTOM_FAILURE_42\nbye"))
+    assert [e.matched_pattern.id for e in r.events] == ["zz-custom"]
+    ms.swap_engine(catalog_library())
+    time.sleep(0.5)
+
+
+def test_pool_crash_requeues_and_respawns(pool):
+    before = pool.stats["deaths"]
+    futs = [pool.submit_match(_data(f"c{i}")) for i in range(24)]
+    pool.inject_crash(0)
+    results = [f.result(300) for f in futs]
+    assert all(r.summary.highest_severity for r in results)
+    deadline = time.time() + 120
+    while pool.stats["deaths"] == before and time.time() < deadline:
+        time.sleep(0.1)
+    assert pool.stats["deaths"] == before + 1
+    assert pool.wait_ready(600) == 2, pool.health()
+    assert pool.workers[0].restarts >= 1
+
+
+def test_pool_hang_detected(pool):
+    before = pool.stats["deaths"]
+    pool.inject_hang(1)
+    deadline = time.time() + 120
+    while pool.stats["deaths"] == before and time.time() < deadline:
+        time.sleep(0.2)
+    assert pool.stats["deaths"] == before + 1
+    assert pool.wait_ready(600) == 2, pool.health()
+    assert PoolMatchService(pool).analyze(_data("after-hang")).summary.highest_severity
+
+
+def test_pool_start_failure_is_fatal():
+    p = EnginePool(_settings(**{"engine.model": "no-such-model"}), catalog_library(), ["cpu"], heartbeat_s=0.2,
+                   max_restarts=3)
+    try:
+        assert p.wait_ready(300) == 0
+        deadline = time.time() + 60
+        while p.workers[0].alive and time.time() < deadline:
+            time.sleep(0.1)
+        assert not p.workers[0].alive and "fatal" in p.workers[0].info
+        with pytest.raises(WorkerDied):
+            p.submit_match(_data("x")).result(10)
+    finally:
+        p.close()

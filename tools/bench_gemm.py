@@ -96,6 +96,21 @@ for M in [int(x) for x in a.m.split(",")]:
         top = sorted(times.items(), key=lambda kv: kv[1])[:4]
         out.update({"hipblaslt": round(res["hipblaslt"], 1), "top": [(k, round(v, 1)) for k, v in top]})
         print(json.dumps(out), flush=True)
+    # fused gate|up + SwiGLU vs hipBLASLt + silu_mul (interleaved layout)
+    if not a.no_custom and M in ops.GEMM_DECODE_M and "gate_up" in shapes:
+        N, K = shapes["gate_up"]
+        x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+        res = {"blas+silu": timeit(lambda w: ops.silu_mul(F.linear(x, w), block=64), ws["gate_up"])}
+        yo = torch.empty(M, N // 2, device="cuda", dtype=torch.bfloat16)
+        for bm in (64, 128, 256):
+            if bm <= M:
+                res[f"fused_m{bm}"] = timeit(lambda w: ops.kernels().gemm_decode(x, w, yo, None, 1, 128, bm, True),
+                                             ws["gate_up"])
+        best = min(res, key=res.get)
+        table[f"silu,{M},{N},{K}"] = ([int(best.split("_m")[1])] if best != "blas+silu" and
+                                      res[best] < 0.97 * res["blas+silu"] else "blas")
+        print(json.dumps({"M": M, "gemm": "gate_up+silu", "best": best,
+                          **{k: round(v, 1) for k, v in res.items()}}), flush=True)
     print(json.dumps({"M": M, "per_step_gemm_ms_hipblaslt": round(tot["hipblaslt"] / 1e3, 3),
                       "per_step_gemm_ms_best": round(tot["best"] / 1e3, 3)}), flush=True)
 if a.write_table:
