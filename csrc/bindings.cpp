@@ -131,6 +131,42 @@ void gemm_decode(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const 
                        (int)bn, (int)bm, silu_gu, cur_stream()));
 }
 
+void quantize_fp8(const at::Tensor& x, at::Tensor& q, at::Tensor& sx) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(q); CHECK_CONTIG(sx); CHECK_DT(sx, at::kFloat);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be [M, K] row-major");
+  TORCH_CHECK(q.scalar_type() == at::kByte || q.scalar_type() == at::kFloat8_e4m3fn, "q must be uint8 / e4m3fn");
+  const int64_t M = x.size(0), K = x.size(1);
+  TORCH_CHECK(q.numel() == M * K && sx.numel() == M && K % 8 == 0, "quantize_fp8 shapes");
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  RC(oamd::quantize_fp8_rows(ptr<bf16_t>(x), static_cast<uint8_t*>(q.data_ptr()), ptr<float>(sx), (int)M, (int)K,
+                             x.stride(0), cur_stream()));
+}
+
+void gemm_fp8(const at::Tensor& x8, const at::Tensor& w8, const at::Tensor& sx, const at::Tensor& sw, at::Tensor& y,
+              const c10::optional<at::Tensor>& p, int64_t splits, int64_t bn, int64_t bm) {
+  CHECK_DEV(x8); CHECK_CONTIG(x8); CHECK_CONTIG(w8); CHECK_CONTIG(sx); CHECK_CONTIG(sw); CHECK_BF16(y);
+  CHECK_CONTIG(y); CHECK_DT(sx, at::kFloat); CHECK_DT(sw, at::kFloat);
+  for (auto* t : {&x8, &w8})
+    TORCH_CHECK(t->scalar_type() == at::kByte || t->scalar_type() == at::kFloat8_e4m3fn, "fp8 operands");
+  TORCH_CHECK(x8.dim() == 2 && w8.dim() == 2, "x8 [M,K], w8 [N,K]");
+  const int64_t M = x8.size(0), K = x8.size(1), N = w8.size(0);
+  TORCH_CHECK(w8.size(1) == K && y.size(0) == M && y.size(1) == N && sx.numel() == M && sw.numel() == N,
+              "gemm_fp8 shapes");
+  TORCH_CHECK((bn == 64 || bn == 128) && N % bn == 0, "gemm_fp8: N % bn");
+  TORCH_CHECK(bm == 64 || bm == 128 || bm == 256, "gemm_fp8: bm in {64,128,256}");
+  TORCH_CHECK(splits >= 1 && 8 % splits == 0 && K % (128 * splits) == 0, "gemm_fp8: K % (128 * splits)");
+  float* pp = nullptr;
+  if (splits > 1) {
+    TORCH_CHECK(p.has_value() && p->scalar_type() == at::kFloat && p->numel() >= splits * M * N,
+                "split-K needs an fp32 partial buffer");
+    pp = p->data_ptr<float>();
+  }
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(x8.device());
+  RC(oamd::gemm_fp8(static_cast<const uint8_t*>(x8.data_ptr()), static_cast<const uint8_t*>(w8.data_ptr()),
+                    ptr<float>(sx), ptr<float>(sw), ptr<bf16_t>(y), pp, (int)M, (int)N, (int)K, (int)splits, (int)bn,
+                    (int)bm, cur_stream()));
+}
+
 void attn_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                  const at::Tensor& block_tables, const at::Tensor& seq_lens, at::Tensor& out,
                  at::Tensor& o_part, at::Tensor& ml_part, int64_t num_splits, double scale, int64_t variant) {
@@ -205,6 +241,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("embedding", &embedding);
   m.def("rope_kv", &rope_kv);
   m.def("attn_decode", &attn_decode);
+  m.def("quantize_fp8", &quantize_fp8);
+  m.def("gemm_fp8", &gemm_fp8, pybind11::arg("x8"), pybind11::arg("w8"), pybind11::arg("sx"), pybind11::arg("sw"),
+        pybind11::arg("y"), pybind11::arg("p") = pybind11::none(), pybind11::arg("splits") = 1,
+        pybind11::arg("bn") = 64, pybind11::arg("bm") = 64);
   m.def("gemm_decode", &gemm_decode, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"),
         pybind11::arg("p") = pybind11::none(), pybind11::arg("splits") = 1, pybind11::arg("bn") = 64,
         pybind11::arg("bm") = 0, pybind11::arg("silu_gu") = false);

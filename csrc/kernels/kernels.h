@@ -25,6 +25,12 @@ int rope_kv(const bf16_t* qkv, int64_t qkv_stride, const int64_t* pos, const flo
 int gemm_decode(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, int N, int K, int S, int BN,
                 int BM, bool silu_gu, hipStream_t stream);
 
+// FP8 e4m3fn W8A8: Y = (X8 . W8^T) * sx[m] * sw[n]; any M (BM-row tiles), S | 8 split-K.
+int gemm_fp8(const uint8_t* X, const uint8_t* W, const float* sx, const float* sw, bf16_t* Y, float* P, int M,
+             int N, int K, int S, int BN, int BM, hipStream_t stream);
+// Per-row dynamic quantization to e4m3fn: sx[m] = max|x[m]| / 448.
+int quantize_fp8_rows(const bf16_t* x, uint8_t* q, float* sx, int M, int K, int64_t ld, hipStream_t stream);
+
 int attn_decode(const bf16_t* q, const bf16_t* k_cache, const bf16_t* v_cache, const int* block_tables,
                 const int* seq_lens, bf16_t* out, float* o_part, float* ml_part, int B, int Hq, int Hkv,
                 int head_dim, int page_size, int max_pages, int num_splits, float scale, int variant,

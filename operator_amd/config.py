@@ -87,6 +87,7 @@ class EngineCfg(BaseModel):
     model_path: Optional[str] = None  # HF safetensors dir; random init when absent
     seed: int = 0
     dtype: str = "bfloat16"
+    weight_dtype: str = "bfloat16"   # bfloat16 | fp8 (W8A8 e4m3fn projections, e.g. Llama-3-70B)
     device: str = "cuda"
     tp: int = 1
     max_batch: int = 256

@@ -23,7 +23,7 @@ def build_llm(s: Settings, device: str | torch.device | None = None, tp=None):
     dev = torch.device(device or e.device)
     cfg = get_config(e.model)
     dtype = getattr(torch, e.dtype)
-    model = LlamaModel(cfg, device=dev, tp=tp, dtype=dtype)
+    model = LlamaModel(cfg, device=dev, tp=tp, dtype=dtype, weight_dtype=e.weight_dtype)
     if e.model_path:
         model.load_hf(e.model_path)
     else:

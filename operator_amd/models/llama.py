@@ -68,6 +68,11 @@ class LayerWeights:
     wd: torch.Tensor
     attn_norm: torch.Tensor
     mlp_norm: torch.Tensor
+    # fp8 (e4m3fn) weights: per-output-row scales; None = bf16 weights
+    sqkv: torch.Tensor | None = None
+    so: torch.Tensor | None = None
+    sgu: torch.Tensor | None = None
+    sd: torch.Tensor | None = None
 
 
 def _seed_for(seed: int, name: str) -> int:
@@ -76,8 +81,13 @@ def _seed_for(seed: int, name: str) -> int:
 
 class LlamaModel:
     def __init__(self, cfg: LlamaConfig, device: str | torch.device = "cuda", tp: Group | None = None,
-                 dtype: torch.dtype = torch.bfloat16):
+                 dtype: torch.dtype = torch.bfloat16, weight_dtype: str = "bfloat16"):
         self.cfg = cfg
+        if weight_dtype not in ("bfloat16", "fp8"):
+            raise ValueError(f"weight_dtype must be bfloat16 or fp8, not {weight_dtype}")
+        # fp8: the four projection GEMMs run W8A8 e4m3fn (per-channel weight scales,
+        # per-token activation scales); embeddings, norms and lm_head stay bf16
+        self.fp8 = weight_dtype == "fp8"
         self.device = torch.device(device)
         self.tp = tp or Group.single()
         self.dtype = dtype
@@ -131,6 +141,18 @@ class LlamaModel:
             torch.cuda.synchronize(self.device)
         return self
 
+    def _quantize_layer(self, lw: LayerWeights) -> LayerWeights:
+        if not self.fp8:
+            return lw
+        for name in ("wqkv", "wo", "wgu", "wd"):
+            q, sc = ops.quantize_fp8(getattr(lw, name))
+            setattr(lw, name, q)
+            setattr(lw, {"wqkv": "sqkv", "wo": "so", "wgu": "sgu", "wd": "sd"}[name], sc)
+        return lw
+
+    def _lin(self, x: torch.Tensor, w: torch.Tensor, sc: torch.Tensor | None) -> torch.Tensor:
+        return ops.linear(x, w) if sc is None else ops.linear_fp8(x, w, sc)
+
     def _shard_layer(self, wq, wk, wv, wo, wg, wu, wd, an, mn) -> LayerWeights:
         r, D = self.tp.rank, self.cfg.head_dim
         q = wq[r * self.hq * D:(r + 1) * self.hq * D]
@@ -138,12 +160,12 @@ class LlamaModel:
         v = wv[r * self.hkv * D:(r + 1) * self.hkv * D]
         g = wg[r * self.inter:(r + 1) * self.inter]
         u = wu[r * self.inter:(r + 1) * self.inter]
-        return LayerWeights(
+        return self._quantize_layer(LayerWeights(
             wqkv=torch.cat([q, k, v], 0).contiguous(),
             wo=wo[:, r * self.hq * D:(r + 1) * self.hq * D].contiguous(),
             wgu=(ops.interleave_gate_up(g, u, self.gu_block) if self.gu_block else torch.cat([g, u], 0).contiguous()),
             wd=wd[:, r * self.inter:(r + 1) * self.inter].contiguous(),
-            attn_norm=an.contiguous(), mlp_norm=mn.contiguous())
+            attn_norm=an.contiguous(), mlp_norm=mn.contiguous()))
 
     def split_gate_up(self, wgu: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
         """(gate, up) rows of a layer's fused gate|up weight (undoes the interleave)."""
@@ -186,10 +208,11 @@ class LlamaModel:
         return self
 
     def weight_bytes(self) -> int:
-        n = self.embed.numel() + self.final_norm.numel() + self.lm_head.numel()
+        n = sum(t.numel() * t.element_size() for t in (self.embed, self.final_norm, self.lm_head))
         for lw in self.layers:
-            n += sum(t.numel() for t in (lw.wqkv, lw.wo, lw.wgu, lw.wd, lw.attn_norm, lw.mlp_norm))
-        return n * self.embed.element_size()
+            n += sum(t.numel() * t.element_size() for t in (lw.wqkv, lw.wo, lw.wgu, lw.wd, lw.attn_norm, lw.mlp_norm,
+                                                            lw.sqkv, lw.so, lw.sgu, lw.sd) if t is not None)
+        return n
 
     # ------------------------------------------------------------------ forward
     def forward(self, fb: ForwardBatch, kv: PagedKVCache) -> torch.Tensor:
@@ -203,7 +226,7 @@ class LlamaModel:
             ws = ops.decode_workspace(T, self.hq, fb.num_splits, h.device)
         for i, lw in enumerate(self.layers):
             kc, vc = kv.layer(i)
-            qkv = ops.linear(x, lw.wqkv)
+            qkv = self._lin(x, lw.wqkv, lw.sqkv)
             q, k, v = ops.rope_kv(qkv, fb.positions, self.cos, self.sin, self.hq, self.hkv, kc, vc, fb.slots,
                                   want_kv=fb.is_prefill)
             if fb.is_prefill:
@@ -211,11 +234,14 @@ class LlamaModel:
             else:
                 o = ops.attn_decode(q, kc, vc, fb.block_tables, fb.context_lens, self.scale, fb.num_splits,
                                     workspace=ws)
-            a = ops.linear(o.view(T, self.hq * c.head_dim), lw.wo)
+            a = self._lin(o.view(T, self.hq * c.head_dim), lw.wo, lw.so)
             self.tp.all_reduce_(a)
             x = ops.rmsnorm(a, lw.mlp_norm, c.rms_eps, residual=h)
-            m = ops.gate_up_silu(x, lw.wgu, self.gu_block)
-            d = ops.linear(m, lw.wd)
+            if lw.sgu is None:
+                m = ops.gate_up_silu(x, lw.wgu, self.gu_block)
+            else:
+                m = ops.silu_mul(ops.linear_fp8(x, lw.wgu, lw.sgu), block=self.gu_block)
+            d = self._lin(m, lw.wd, lw.sd)
             self.tp.all_reduce_(d)
             nw = self.layers[i + 1].attn_norm if i + 1 < len(self.layers) else self.final_norm
             x = ops.rmsnorm(d, nw, c.rms_eps, residual=h)

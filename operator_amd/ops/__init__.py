@@ -19,6 +19,7 @@ __all__ = [
     "rmsnorm", "silu_mul", "embedding", "rope_kv", "attn_prefill", "attn_decode", "sample",
     "kernels", "patterns", "native_available", "reference", "prefill_work_list", "decode_splits",
     "decode_workspace", "linear", "gemm_splits", "gemm_plan", "gate_up_silu", "interleave_gate_up",
+    "quantize_fp8", "linear_fp8", "fp8_plan",
 ]
 
 DECODE_MIN_SPLIT_TOKENS = 256  # never split a sequence into pieces shorter than this
@@ -213,6 +214,55 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None, sp
     if S > 1 and (partial is None or partial.numel() < S * M * N):
         partial = torch.empty(S * M * N, dtype=torch.float32, device=x.device)
     kernels().gemm_decode(x, w, y, partial if S > 1 else None, S, bn, bm, False)
+    return y
+
+
+FP8_MAX = 448.0  # OCP e4m3fn
+
+
+def quantize_fp8(x: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """Per-row e4m3fn quantization: (q [M, K] float8_e4m3fn, s [M] fp32), x ~= q * s."""
+    M, K = x.shape
+    if x.is_cuda:
+        q = torch.empty(M, K, dtype=torch.float8_e4m3fn, device=x.device)
+        sx = torch.empty(M, dtype=torch.float32, device=x.device)
+        kernels().quantize_fp8(x.contiguous(), q, sx)
+        return q, sx
+    xf = x.float()
+    amax = xf.abs().amax(1)
+    sx = torch.where(amax > 0, amax / FP8_MAX, torch.ones_like(amax))
+    return (xf / sx[:, None]).to(torch.float8_e4m3fn), sx
+
+
+def fp8_plan(M: int, N: int, K: int) -> tuple[int, int, int]:
+    """(bm, bn, splits) for gemm_fp8: row tile by M, 128-column tiles for wide N, and
+    split-K until the blocks reach one per CU (K permitting)."""
+    bm = 64 if M <= 64 else 128 if M <= 128 else 256
+    bn = 128 if N % 128 == 0 and N // 128 >= 192 else 64
+    mt = -(-M // bm)
+    S = 1
+    for s in (1, 2, 4, 8):
+        if K % (128 * s):
+            break
+        S = s
+        if (N // bn) * s * mt >= 256:
+            break
+    return bm, bn, S
+
+
+def linear_fp8(x: torch.Tensor, w8: torch.Tensor, sw: torch.Tensor, out: torch.Tensor | None = None,
+               plan: tuple[int, int, int] | None = None) -> torch.Tensor:
+    """y = x @ (w8 * sw)^T with x quantized per token to e4m3fn (W8A8, fp32 accumulate)."""
+    M, K = x.shape
+    N = w8.shape[0]
+    q, sx = quantize_fp8(x)
+    if not x.is_cuda:
+        y = (q.float() * sx[:, None]) @ (w8.float() * sw[:, None]).t()
+        return out.copy_(y) if out is not None else y.to(x.dtype)
+    bm, bn, S = plan or fp8_plan(M, N, K)
+    y = out if out is not None else torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
+    part = torch.empty(S * M * N, dtype=torch.float32, device=x.device) if S > 1 else None
+    kernels().gemm_fp8(q, w8, sx, sw, y, part, S, bn, bm)
     return y
 
 

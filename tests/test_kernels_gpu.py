@@ -176,3 +176,41 @@ def test_gate_up_silu_fused(M):
     # the unfused path over the same interleaved layout agrees
     un = ops.silu_mul(torch.nn.functional.linear(x, wgu), block=ops.GU_BLOCK)
     torch.testing.assert_close(un.float(), ref_.float(), atol=2e-2, rtol=2e-2)
+
+
+def test_quantize_fp8_matches_torch():
+    torch.manual_seed(9)
+    x = _rand(37, 1024) * 3
+    x[5] = 0  # all-zero row: scale 1, zeros
+    q, sx = ops.quantize_fp8(x)
+    amax = x.float().abs().amax(1)
+    want_s = torch.where(amax > 0, amax / 448.0, torch.ones_like(amax))
+    torch.testing.assert_close(sx, want_s)
+    want_q = (x.float() / want_s[:, None]).to(torch.float8_e4m3fn).float()
+    got = q.float()
+    # round-to-nearest-even both ways; allow one e4m3 ulp where 1/s products differ in the last bit
+    ulp = torch.clamp(want_q.abs(), min=2 ** -6) * 2 ** -3
+    assert ((got - want_q).abs() <= ulp + 1e-12).all()
+    assert (q[5].float() == 0).all()
+
+
+@pytest.mark.parametrize("M", [1, 37, 64, 200, 256])
+@pytest.mark.parametrize("N,K", [(256, 512), (640, 2048), (128, 4096)])
+def test_gemm_fp8(M, N, K):
+    torch.manual_seed(10)
+    x = _rand(M, K)
+    w = _rand(N, K) * 0.05
+    w8, sw = ops.quantize_fp8(w)
+    q, sx = ops.quantize_fp8(x)
+    ref_ = (q.float() * sx[:, None]) @ (w8.float() * sw[:, None]).t()
+    for bm in (64, 128, 256):
+        for bn in (64, 128):
+            for S in (1, 2, 4, 8):
+                if K % (128 * S) or N % bn:
+                    continue
+                y = ops.linear_fp8(x, w8, sw, plan=(bm, bn, S))
+                torch.testing.assert_close(y.float(), ref_, atol=2e-2, rtol=2e-2)
+    # and W8A8 stays close to the bf16 product (e4m3: ~3 mantissa bits per operand)
+    exact = x.float() @ w.float().t()
+    rel = (ops.linear_fp8(x, w8, sw).float() - exact).norm() / exact.norm()
+    assert rel < 0.06, float(rel)

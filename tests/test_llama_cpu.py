@@ -76,3 +76,19 @@ def test_sampling_is_seeded_and_batch_invariant():
     c = eng.generate([GenRequest([1, 2, 3], max_tokens=8, temperature=0.8, seed=12, ignore_eos=True)])[0].output
     assert a == b
     assert a != c
+
+
+def test_fp8_weight_model_tracks_bf16():
+    cfg = get_config("tiny-gqa4")
+    logits = {}
+    for wd in ("bfloat16", "fp8"):
+        m = LlamaModel(cfg, device="cpu", dtype=torch.float32, weight_dtype=wd).init_random(seed=7)
+        kv = PagedKVCache(cfg.layers, 64, cfg.kv_heads, cfg.head_dim, page_size=16, device="cpu", dtype=torch.float32)
+        logits[wd] = _full_logits(m, kv, list(range(3, 40)))
+        if wd == "fp8":
+            assert m.layers[0].wqkv.dtype == torch.float8_e4m3fn and m.layers[0].sqkv is not None
+            eng = LLMEngine(m, kv, max_batch=2, max_context=256, use_graphs=False)
+            r = eng.generate([GenRequest([5, 6, 7], max_tokens=5, temperature=0.0, ignore_eos=True)])[0]
+            assert len(r.output) == 5
+    cos = torch.nn.functional.cosine_similarity(logits["fp8"].flatten(), logits["bfloat16"].flatten(), dim=0)
+    assert cos > 0.98, float(cos)

@@ -102,3 +102,22 @@ def test_pipelined_windows_eos_and_arrivals():
     ref = run(False, eos)
     assert len(ref[0]) == 13
     assert run(True, eos) == ref
+
+
+def test_fp8_weights_model_runs_and_tracks_bf16():
+    cfg = get_config("tiny-gqa4")
+    outs = {}
+    for wd in ("bfloat16", "fp8"):
+        m = LlamaModel(cfg, device="cuda", weight_dtype=wd).init_random(seed=11)
+        kv = PagedKVCache(cfg.layers, 64, cfg.kv_heads, 128, 16, device="cuda")
+        T = 48
+        fb = ForwardBatch(torch.arange(T, device="cuda"), torch.arange(T, device="cuda"),
+                          torch.full((T,), -1, dtype=torch.long, device="cuda"), True, None, seq_lens=[T],
+                          prefill_work=None)
+        outs[wd] = m.forward(fb, kv).float()
+        eng = LLMEngine(m, kv, max_batch=4, max_context=512, use_graphs=True)
+        reqs = [GenRequest(list(range(2, 40)), max_tokens=9, temperature=0.5, seed=1, ignore_eos=True)]
+        eng.generate(reqs)
+        assert len(reqs[0].output) == 9
+    cos = torch.nn.functional.cosine_similarity(outs["fp8"].flatten(), outs["bfloat16"].flatten(), dim=0)
+    assert cos > 0.98, float(cos)

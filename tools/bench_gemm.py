@@ -22,9 +22,14 @@ ap.add_argument("--no-custom", action="store_true")
 ap.add_argument("--file", default="gpurun_out/tunableop_results.csv")
 ap.add_argument("--write-table", default=None, help="write the best (bm, bn, splits) per shape as JSON")
 ap.add_argument("--tp", type=int, default=1, help="also cover the TP-sharded shapes of this degree")
+ap.add_argument("--fp8", action="store_true", help="also time the W8A8 e4m3fn gemm_fp8 path")
+ap.add_argument("--model", default="8b", choices=["8b", "70b"])
 a = ap.parse_args()
 shapes = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336),
           "lm_head": (128256, 4096)}
+if a.model == "70b":
+    shapes = {"qkv": (10240, 8192), "o": (8192, 8192), "gate_up": (57344, 8192), "down": (8192, 28672),
+              "lm_head": (128256, 8192)}
 if a.tp > 1:
     t = a.tp
     shapes = {f"{k}_tp{t}": ((n // t, kk) if k in ("qkv", "gate_up", "lm_head") else (n, kk // t))
@@ -78,6 +83,19 @@ for M in [int(x) for x in a.m.split(",")]:
                         key = f"m{bm}n{bn}s{S}"
                         res[key] = timeit(lambda w: ops.linear(x, w, out=y, splits=S, partial=part, bn=bn, bm=bm),
                                           ws[name])
+        if a.fp8:
+            # enough quantized copies (>= 1 GB) that nothing is served from the MALL
+            n8 = max(1, min(16, -(-(1 << 30) // (N * K))))
+            w8s = [ops.quantize_fp8(ws[name][i % len(ws[name])]) for i in range(n8)]
+            q, sx = ops.quantize_fp8(x)
+            y8 = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+            bm, bn, S = ops.fp8_plan(M, N, K)
+            part = torch.empty(S * M * N, device="cuda", dtype=torch.float32) if S > 1 else None
+            fp8_us = timeit(lambda wp: ops.kernels().gemm_fp8(q, wp[0], sx, wp[1], y8, part, S, bn, bm), w8s)
+            quant_us = timeit(lambda _: ops.quantize_fp8(x), [None])
+            print(json.dumps({"M": M, "gemm": name, "fp8_us": round(fp8_us, 1), "fp8_quant_us": round(quant_us, 1),
+                              "fp8_plan": [bm, bn, S], "fp8_TBps_w": round(N * K / fp8_us / 1e6, 2)}), flush=True)
+            del w8s
         times = dict(res)
         best = min(times, key=times.get)
         if M in ops.GEMM_DECODE_M:
