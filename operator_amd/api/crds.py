@@ -178,8 +178,15 @@ def rbac(namespace: str = "podmortem-system", name: str = "podmortem-operator") 
 
 
 def deployment(namespace: str = "podmortem-system", image: str = "ghcr.io/podmortem/operator-amd:latest",
-               gpus: int = 1, name: str = "podmortem-operator") -> list[dict]:
+               gpus: int = 1, name: str = "podmortem-operator", replicas: int = 1) -> list[dict]:
+    """PVC + operator Deployment + Service. ``replicas`` > 1 turns on Lease leader
+    election (one active replica, the others warm standbys)."""
     labels = {"app.kubernetes.io/name": name}
+    env = [{"name": "PODMORTEM_PATTERNS__CACHE_DIR", "value": "/shared/patterns"},
+           {"name": "HSA_ENABLE_IPC_MODE_LEGACY", "value": "0"}]
+    if replicas > 1:
+        env += [{"name": "PODMORTEM_OPERATOR__LEADER_ELECTION", "value": "true"},
+                {"name": "PODMORTEM_OPERATOR__LEASE_NAMESPACE", "value": namespace}]
     probe = lambda path, d: {"httpGet": {"path": path, "port": 8080}, "initialDelaySeconds": d,  # noqa: E731
                              "periodSeconds": 10}
     return [
@@ -188,15 +195,14 @@ def deployment(namespace: str = "podmortem-system", image: str = "ghcr.io/podmor
          "spec": {"accessModes": ["ReadWriteOnce"], "resources": {"requests": {"storage": "5Gi"}}}},
         {"apiVersion": "apps/v1", "kind": "Deployment", "metadata": {"name": name, "namespace": namespace,
                                                                      "labels": labels},
-         "spec": {"replicas": 1, "selector": {"matchLabels": labels},
+         "spec": {"replicas": replicas, "selector": {"matchLabels": labels},
                   "template": {"metadata": {"labels": labels}, "spec": {
                       "serviceAccountName": name,
                       "securityContext": {"runAsNonRoot": True, "runAsUser": 1001},
                       "containers": [{
                           "name": "operator", "image": image,
                           "command": ["python", "-m", "operator_amd", "run", "--gpus", str(gpus)],
-                          "env": [{"name": "PODMORTEM_PATTERNS__CACHE_DIR", "value": "/shared/patterns"},
-                                  {"name": "HSA_ENABLE_IPC_MODE_LEGACY", "value": "0"}],
+                          "env": env,
                           "ports": [{"containerPort": 8080, "name": "http"}],
                           "resources": {"limits": {"amd.com/gpu": gpus, "memory": "64Gi"},
                                         "requests": {"cpu": "4", "memory": "32Gi"}},
@@ -211,6 +217,41 @@ def deployment(namespace: str = "podmortem-system", image: str = "ghcr.io/podmor
     ]
 
 
+def compat_services(namespace: str = "podmortem-system", image: str = "ghcr.io/podmortem/operator-amd:latest",
+                    gpus: int = 1) -> list[dict]:
+    """The on-node engines behind the reference's two service names
+    (K/log-parser-deployment.yaml + K/log-parser-service.yaml,
+    K/ai-interface-deployment.yaml + K/ai-interface-service.yaml): an unmodified
+    reference operator pointed at these Services gets GPU pattern analysis and
+    local-LLM explanations (``operator_amd serve-compat``)."""
+    out = []
+    for svc, role in (("podmortem-log-parser", "match"), ("podmortem-ai-interface", "explain")):
+        labels = {"app.kubernetes.io/name": svc}
+        env = [{"name": "HSA_ENABLE_IPC_MODE_LEGACY", "value": "0"},
+               {"name": "PODMORTEM_SERVICES__EXPLAIN", "value": "local" if role == "explain" else "none"}]
+        res = {"limits": {"amd.com/gpu": gpus, "memory": "64Gi"}, "requests": {"cpu": "4", "memory": "16Gi"}}
+        out += [
+            {"apiVersion": "apps/v1", "kind": "Deployment", "metadata": {"name": svc, "namespace": namespace,
+                                                                         "labels": labels},
+             "spec": {"replicas": 1, "selector": {"matchLabels": labels},
+                      "template": {"metadata": {"labels": labels}, "spec": {
+                          "securityContext": {"runAsNonRoot": True, "runAsUser": 1001},
+                          "containers": [{"name": svc, "image": image,
+                                          "command": ["python", "-m", "operator_amd", "serve-compat", "--port", "8080"],
+                                          "env": env, "ports": [{"containerPort": 8080, "name": "http"}],
+                                          "resources": res,
+                                          "readinessProbe": {"httpGet": {"path": "/q/health/ready", "port": 8080},
+                                                             "initialDelaySeconds": 30, "periodSeconds": 10}}]}}}},
+            {"apiVersion": "v1", "kind": "Service", "metadata": {"name": f"{svc}-service", "namespace": namespace},
+             "spec": {"selector": labels, "ports": [{"name": "http", "port": 8080, "targetPort": 8080}]}},
+        ]
+    return out
+
+
 def render_all(**kw) -> str:
+    compat = kw.pop("compat", False)
     docs = crds() + rbac(kw.get("namespace", "podmortem-system")) + deployment(**kw)
+    if compat:
+        docs += compat_services(kw.get("namespace", "podmortem-system"), kw.get("image", "ghcr.io/podmortem/operator-amd:latest"),
+                                kw.get("gpus", 1))
     return yaml.safe_dump_all(docs, sort_keys=False)

@@ -43,7 +43,8 @@ def _patterns(s, paths: list[str] | None):
 def cmd_manifests(args) -> int:
     from operator_amd.api.crds import render_all
 
-    text = render_all(namespace=args.namespace, image=args.image, gpus=args.gpus)
+    text = render_all(namespace=args.namespace, image=args.image, gpus=args.gpus, replicas=args.replicas,
+                      compat=args.compat_services)
     if args.out:
         with open(args.out, "w") as f:
             f.write(text)
@@ -202,6 +203,9 @@ def main(argv: list[str] | None = None) -> int:
     p.add_argument("--namespace", default="podmortem-system")
     p.add_argument("--image", default="ghcr.io/podmortem/operator-amd:latest")
     p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--replicas", type=int, default=1, help=">1 enables Lease leader election")
+    p.add_argument("--compat-services", action="store_true",
+                   help="also emit log-parser / ai-interface Deployments+Services backed by serve-compat")
     p.add_argument("--out", default=None)
     p = sub.add_parser("scan")
     common(p)

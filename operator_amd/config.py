@@ -34,6 +34,12 @@ class OperatorCfg(BaseModel):
     name: str = "podmortem-operator"
     workers: int = 16                 # analysis pipeline thread pool
     io_workers: int = 8               # kube write pool (annotations, status, events)
+    leader_election: bool = False     # reference: 1 replica, no lease; true = HA replicas behind a Lease
+    lease_name: str = "podmortem-operator-leader"
+    lease_namespace: str = "podmortem-system"
+    lease_duration_s: float = 15.0
+    lease_renew_deadline_s: float = 10.0
+    lease_retry_period_s: float = 2.0
 
 
 class KubeCfg(BaseModel):

@@ -76,11 +76,23 @@ class Operator:
         self.pipeline = AnalysisPipeline(kube, self.matcher, self.explainer, self.events, self.storage, self.status,
                                          self.pool, self.metrics)
         self.deduper = FailureDeduper(s.watch.dedupe_max_entries, s.watch.dedupe_ttl_s)
+        self.sync = PatternSync(s.patterns.cache_dir)
+        self._make_workers()
+        self.elector = None
+        self._workers_running = False
+        self._workers_lock = threading.Lock()
+        self.readiness = PatternLibraryReadiness(kube, s.patterns.cache_dir, s.health.grace_s)
+        self.health: HealthServer | None = None
+        self._reload_lock = threading.Lock()
+        self.pattern_count = 0
+
+    def _make_workers(self) -> None:
+        """Watcher, informer and reconcilers: what only the leader runs."""
+        s, kube = self.settings, self.kube
         self.monitors = MonitorCache(kube)
         self.watcher = PodFailureWatcher(kube, self.pipeline, self.deduper, s.watch.namespaces, self.monitors,
                                          s.watch.restart_delay_s, s.watch.include_last_state,
                                          s.watch.include_init_containers)
-        self.sync = PatternSync(s.patterns.cache_dir)
         self.pm_reconciler = PodmortemReconciler(kube, self.pipeline, self.deduper, s.watch.include_last_state)
         self.pl_reconciler = PatternLibraryReconciler(kube, self.sync, on_synced=lambda lib: self.reload_patterns())
         self.aip_reconciler = AIProviderReconciler(kube, self.explainer, s.engine.model)
@@ -89,10 +101,33 @@ class Operator:
             Controller(kube, PATTERNLIBRARIES, self.pl_reconciler.reconcile, name="patternlibrary"),
             Controller(kube, AIPROVIDERS, self.aip_reconciler.reconcile, name="aiprovider"),
         ]
-        self.readiness = PatternLibraryReadiness(kube, s.patterns.cache_dir, s.health.grace_s)
-        self.health: HealthServer | None = None
-        self._reload_lock = threading.Lock()
-        self.pattern_count = 0
+
+    def _start_workers(self) -> None:
+        with self._workers_lock:
+            if self._workers_running:
+                return
+            if getattr(self, "_workers_used", False):  # re-elected after a loss: fresh watch state
+                self._make_workers()
+            self._workers_used = True
+            self.monitors.start()
+            for c in self.controllers:
+                c.start()
+            self.watcher.start()
+            self._workers_running = True
+
+    def _stop_workers(self) -> None:
+        with self._workers_lock:
+            if not self._workers_running:
+                return
+            self.watcher.stop()
+            for c in self.controllers:
+                c.stop()
+            self.monitors.stop()
+            self._workers_running = False
+
+    @property
+    def is_leader(self) -> bool:
+        return self.elector.leading if self.elector is not None else self._workers_running
 
     # ------------------------------------------------------------------ patterns
     def reload_patterns(self) -> int:
@@ -117,10 +152,18 @@ class Operator:
                                              self.settings.services.match_max_batch,
                                              self.settings.services.match_batch_wait_ms, self.metrics)
             self.pipeline.matcher = self.matcher
-        self.monitors.start()
-        for c in self.controllers:
-            c.start()
-        self.watcher.start()
+        o = self.settings.operator
+        if o.leader_election:
+            from operator_amd.controller.leader import LeaderElector
+
+            self.elector = LeaderElector(self.kube, o.lease_name, o.lease_namespace,
+                                         lease_duration_s=o.lease_duration_s,
+                                         renew_deadline_s=o.lease_renew_deadline_s,
+                                         retry_period_s=o.lease_retry_period_s,
+                                         on_started_leading=self._start_workers,
+                                         on_stopped_leading=self._stop_workers).start()
+        else:
+            self._start_workers()
         if http if http is not None else self.settings.health.enabled:
             self.health = HealthServer(self.settings.health.host, self.settings.health.port,
                                        readiness=[self.readiness, self._engine_ready],
@@ -130,10 +173,9 @@ class Operator:
         return self
 
     def stop(self) -> None:
-        self.watcher.stop()
-        for c in self.controllers:
-            c.stop()
-        self.monitors.stop()
+        if self.elector is not None:
+            self.elector.stop()
+        self._stop_workers()
         if self.health is not None:
             self.health.stop()
         self.pool.shutdown(wait=False, cancel_futures=True)
