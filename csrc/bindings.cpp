@@ -36,10 +36,16 @@ template <typename T>
 T* optr(const c10::optional<at::Tensor>& t) { return t.has_value() ? reinterpret_cast<T*>(t->data_ptr()) : nullptr; }
 
 void rmsnorm(const at::Tensor& x, const c10::optional<at::Tensor>& residual, const at::Tensor& w,
-             at::Tensor& y, double eps) {
+             at::Tensor& y, double eps, const c10::optional<at::Tensor>& partial, int64_t splits) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(y); ROWMAJOR_VEC(x); ROWMAJOR_VEC(y);
   CHECK_CONTIG(w);
   const int64_t rows = x.size(0), hidden = x.size(1);
+  const float* xp = nullptr;
+  if (partial.has_value()) {  // x = bf16(sum of `splits` fp32 [rows, hidden] slabs); x only gives the shape
+    CHECK_DT(*partial, at::kFloat); CHECK_CONTIG(*partial);
+    TORCH_CHECK(splits >= 1 && partial->numel() >= splits * rows * hidden, "rmsnorm: partial slabs too small");
+    xp = partial->data_ptr<float>();
+  }
   TORCH_CHECK(hidden % 8 == 0 && hidden <= 256 * 8 * 8, "hidden must be a multiple of 8 and <= 16384");
   TORCH_CHECK(w.numel() == hidden && y.size(0) == rows && y.size(1) == hidden, "rmsnorm shape mismatch");
   int64_t rstride = 0;
@@ -50,7 +56,7 @@ void rmsnorm(const at::Tensor& x, const c10::optional<at::Tensor>& residual, con
   }
   const c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   RC(oamd::rmsnorm(ptr<bf16_t>(x), optr<bf16_t>(residual), ptr<bf16_t>(w), ptr<bf16_t>(y), (int)rows,
-                   (int)hidden, x.stride(0), rstride, y.stride(0), (float)eps, cur_stream()));
+                   (int)hidden, x.stride(0), rstride, y.stride(0), (float)eps, xp, (int)splits, cur_stream()));
 }
 
 void silu_mul(const at::Tensor& gu, at::Tensor& out, int64_t block) {
@@ -107,12 +113,22 @@ void rope_kv(const at::Tensor& qkv, const at::Tensor& pos, const at::Tensor& cos
                    cur_stream()));
 }
 
-void gemm_decode(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const c10::optional<at::Tensor>& p,
+void gemm_decode(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& y_opt,
+                 const c10::optional<at::Tensor>& p,
                  int64_t splits, int64_t bn, int64_t bm, bool silu_gu) {
-  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(y); CHECK_CONTIG(x); CHECK_CONTIG(w); CHECK_CONTIG(y);
-  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 2, "x [M,K], w [N,K], y [M,N]");
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2, "x [M,K], w [N,K]");
   const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
-  TORCH_CHECK(w.size(1) == K && y.size(0) == M && y.size(1) == (silu_gu ? N / 2 : N), "gemm shapes");
+  bf16_t* yp = nullptr;
+  if (y_opt.has_value()) {
+    const at::Tensor& y = *y_opt;
+    CHECK_BF16(y); CHECK_CONTIG(y);
+    TORCH_CHECK(y.dim() == 2 && y.size(0) == M && y.size(1) == (silu_gu ? N / 2 : N), "gemm shapes");
+    yp = ptr<bf16_t>(y);
+  } else {
+    TORCH_CHECK(splits > 1 && !silu_gu, "y may be omitted only for split-K slabs summed by the consumer");
+  }
+  TORCH_CHECK(w.size(1) == K, "gemm shapes");
   TORCH_CHECK(!silu_gu || (bn == 128 && splits == 1), "fused SwiGLU needs bn = 128, splits = 1");
   if (bm == 0) bm = std::min<int64_t>(M, 256);
   TORCH_CHECK((bm == 64 || bm == 128 || bm == 256) && M % bm == 0, "gemm_decode: M % bm, bm in {64,128,256}");
@@ -127,7 +143,7 @@ void gemm_decode(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const 
   }
   TORCH_CHECK(K < (1LL << 31) / 64 && M * K < (1LL << 31) && N * K < (1LL << 40), "gemm too large");
   const c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
-  RC(oamd::gemm_decode(ptr<bf16_t>(x), ptr<bf16_t>(w), ptr<bf16_t>(y), pp, (int)M, (int)N, (int)K, (int)splits,
+  RC(oamd::gemm_decode(ptr<bf16_t>(x), ptr<bf16_t>(w), yp, pp, (int)M, (int)N, (int)K, (int)splits,
                        (int)bn, (int)bm, silu_gu, cur_stream()));
 }
 
@@ -236,7 +252,9 @@ void register_scan_bindings(pybind11::module_& m);
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "operator_amd gfx950 kernels";
-  m.def("rmsnorm", &rmsnorm, "RMSNorm with optional fused residual add");
+  m.def("rmsnorm", &rmsnorm, "RMSNorm with optional fused residual add (and split-K slab sum)", pybind11::arg("x"),
+        pybind11::arg("residual"), pybind11::arg("w"), pybind11::arg("y"), pybind11::arg("eps"),
+        pybind11::arg("partial") = pybind11::none(), pybind11::arg("splits") = 1);
   m.def("silu_mul", &silu_mul, pybind11::arg("gu"), pybind11::arg("out"), pybind11::arg("block") = 0);
   m.def("embedding", &embedding);
   m.def("rope_kv", &rope_kv);

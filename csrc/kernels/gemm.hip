@@ -235,7 +235,7 @@ int gemm_decode(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, in
 #undef OAMD_GEMM
 #undef OAMD_GEMM2
   OAMD_LAUNCH_CHECK();
-  if (S > 1) {
+  if (S > 1 && Y != nullptr) {  // Y == nullptr: the consumer sums the slabs (rmsnorm)
     const int64_t MN = (int64_t)M * N;
     const int64_t threads = MN / 4;
     gemm_splitk_reduce_kernel<<<(threads + 255) / 256, 256, 0, stream>>>(P, Y, MN, S);

@@ -11,7 +11,8 @@ typedef uint16_t bf16_t;
 
 // ---- explanation-model ops ----
 int rmsnorm(const bf16_t* x, bf16_t* residual, const bf16_t* w, bf16_t* y, int rows, int hidden,
-            int64_t x_stride, int64_t r_stride, int64_t y_stride, float eps, hipStream_t stream);
+            int64_t x_stride, int64_t r_stride, int64_t y_stride, float eps, const float* xp, int S,
+            hipStream_t stream);
 int silu_mul(const bf16_t* gu, bf16_t* out, int64_t rows, int inter, int block, int64_t in_stride,
              int64_t out_stride, hipStream_t stream);
 int embedding(const int64_t* ids, const bf16_t* table, bf16_t* out, int tokens, int hidden,

@@ -10,11 +10,16 @@ namespace oamd {
 // One 256-thread block per row. Each thread owns up to MAXV vectors of 8 bf16
 // kept in registers between the reduction and the scaling pass, so the row is
 // read from HBM exactly once (x, and residual when fused).
+// With `xp` set, x is not read: the row is the bf16 rounding of the sum of S
+// fp32 split-K slabs xp[s * slab + row * hidden + c] written by gemm_decode —
+// the GEMM's reduction pass is folded into this kernel (same numerics: the
+// projection output is rounded to bf16 once, then added to the residual).
 template <int NT, int MAXV>
 __global__ void __launch_bounds__(NT) rmsnorm_kernel(
     const bf16_t* __restrict__ x, bf16_t* __restrict__ residual,
     const bf16_t* __restrict__ w, bf16_t* __restrict__ y, int hidden,
-    int64_t x_stride, int64_t r_stride, int64_t y_stride, float eps) {
+    int64_t x_stride, int64_t r_stride, int64_t y_stride, float eps,
+    const float* __restrict__ xp, int S, int64_t slab) {
   __shared__ float scratch[NT / 64];
   const int row = blockIdx.x;
   const int nvec = hidden >> 3;
@@ -26,7 +31,22 @@ __global__ void __launch_bounds__(NT) rmsnorm_kernel(
   for (int i = 0; i < MAXV; ++i) {
     const int vi = threadIdx.x + i * NT;
     if (vi < nvec) {
-      u16x8 a = xr[vi];
+      u16x8 a;
+      if (xp) {
+        const float* pr = xp + (int64_t)row * hidden + vi * 8;
+        f32x4 lo = *reinterpret_cast<const f32x4*>(pr), hi = *reinterpret_cast<const f32x4*>(pr + 4);
+        for (int sp = 1; sp < S; ++sp) {
+          lo += *reinterpret_cast<const f32x4*>(pr + sp * slab);
+          hi += *reinterpret_cast<const f32x4*>(pr + sp * slab + 4);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          a[j] = f2bf(lo[j]);
+          a[4 + j] = f2bf(hi[j]);
+        }
+      } else {
+        a = xr[vi];
+      }
       if (rr) {
         u16x8 b = rr[vi];
         u16x8 s;
@@ -67,16 +87,20 @@ __global__ void __launch_bounds__(NT) rmsnorm_kernel(
 
 int rmsnorm(const bf16_t* x, bf16_t* residual, const bf16_t* w, bf16_t* y,
             int rows, int hidden, int64_t x_stride, int64_t r_stride,
-            int64_t y_stride, float eps, hipStream_t stream) {
+            int64_t y_stride, float eps, const float* xp, int S, hipStream_t stream) {
   if (rows == 0) return 0;
   constexpr int NT = 256;
   const int nvec = hidden / 8;
+  const int64_t slab = (int64_t)rows * hidden;
   if (nvec <= NT * 2) {
-    rmsnorm_kernel<NT, 2><<<rows, NT, 0, stream>>>(x, residual, w, y, hidden, x_stride, r_stride, y_stride, eps);
+    rmsnorm_kernel<NT, 2><<<rows, NT, 0, stream>>>(x, residual, w, y, hidden, x_stride, r_stride, y_stride, eps,
+                                                   xp, S, slab);
   } else if (nvec <= NT * 4) {
-    rmsnorm_kernel<NT, 4><<<rows, NT, 0, stream>>>(x, residual, w, y, hidden, x_stride, r_stride, y_stride, eps);
+    rmsnorm_kernel<NT, 4><<<rows, NT, 0, stream>>>(x, residual, w, y, hidden, x_stride, r_stride, y_stride, eps,
+                                                   xp, S, slab);
   } else {
-    rmsnorm_kernel<NT, 8><<<rows, NT, 0, stream>>>(x, residual, w, y, hidden, x_stride, r_stride, y_stride, eps);
+    rmsnorm_kernel<NT, 8><<<rows, NT, 0, stream>>>(x, residual, w, y, hidden, x_stride, r_stride, y_stride, eps,
+                                                   xp, S, slab);
   }
   OAMD_LAUNCH_CHECK();
   return 0;

@@ -150,8 +150,12 @@ class LlamaModel:
             setattr(lw, {"wqkv": "sqkv", "wo": "so", "wgu": "sgu", "wd": "sd"}[name], sc)
         return lw
 
-    def _lin(self, x: torch.Tensor, w: torch.Tensor, sc: torch.Tensor | None) -> torch.Tensor:
-        return ops.linear(x, w) if sc is None else ops.linear_fp8(x, w, sc)
+    def _lin(self, x: torch.Tensor, w: torch.Tensor, sc: torch.Tensor | None, defer: bool = False):
+        """Projection; ``defer`` lets a split-K decode GEMM hand its fp32 slabs to the
+        following rmsnorm (only when no TP all-reduce sits in between)."""
+        if sc is not None:
+            return ops.linear_fp8(x, w, sc)
+        return ops.linear(x, w, defer_reduce=defer and self.tp.world == 1)
 
     def _shard_layer(self, wq, wk, wv, wo, wg, wu, wd, an, mn) -> LayerWeights:
         r, D = self.tp.rank, self.cfg.head_dim
@@ -234,14 +238,14 @@ class LlamaModel:
             else:
                 o = ops.attn_decode(q, kc, vc, fb.block_tables, fb.context_lens, self.scale, fb.num_splits,
                                     workspace=ws)
-            a = self._lin(o.view(T, self.hq * c.head_dim), lw.wo, lw.so)
+            a = self._lin(o.view(T, self.hq * c.head_dim), lw.wo, lw.so, defer=True)
             self.tp.all_reduce_(a)
             x = ops.rmsnorm(a, lw.mlp_norm, c.rms_eps, residual=h)
             if lw.sgu is None:
                 m = ops.gate_up_silu(x, lw.wgu, self.gu_block)
             else:
                 m = ops.silu_mul(ops.linear_fp8(x, lw.wgu, lw.sgu), block=self.gu_block)
-            d = self._lin(m, lw.wd, lw.sd)
+            d = self._lin(m, lw.wd, lw.sd, defer=True)
             self.tp.all_reduce_(d)
             nw = self.layers[i + 1].attn_norm if i + 1 < len(self.layers) else self.final_norm
             x = ops.rmsnorm(d, nw, c.rms_eps, residual=h)

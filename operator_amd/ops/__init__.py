@@ -19,16 +19,37 @@ __all__ = [
     "rmsnorm", "silu_mul", "embedding", "rope_kv", "attn_prefill", "attn_decode", "sample",
     "kernels", "patterns", "native_available", "reference", "prefill_work_list", "decode_splits",
     "decode_workspace", "linear", "gemm_splits", "gemm_plan", "gate_up_silu", "interleave_gate_up",
-    "quantize_fp8", "linear_fp8", "fp8_plan",
+    "quantize_fp8", "linear_fp8", "fp8_plan", "SplitK",
 ]
 
 DECODE_MIN_SPLIT_TOKENS = 256  # never split a sequence into pieces shorter than this
 DECODE_TARGET_BLOCKS = 512     # split only while B x Hkv decode-attention workgroups < this
 
 
-def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: torch.Tensor | None = None,
+class SplitK:
+    """A decode GEMM's output left as S fp32 split-K slabs [S, M, N]; the consumer
+    (rmsnorm) sums them, so the GEMM's separate reduction pass disappears."""
+
+    __slots__ = ("p", "S", "shape", "device", "dtype", "is_cuda")
+
+    def __init__(self, p: torch.Tensor, S: int, M: int, N: int):
+        self.p, self.S, self.shape = p, S, (M, N)
+        self.device, self.dtype, self.is_cuda = p.device, torch.bfloat16, True
+
+    def materialize(self) -> torch.Tensor:
+        M, N = self.shape
+        return self.p[: self.S * M * N].view(self.S, M, N).sum(0).to(torch.bfloat16)
+
+
+def rmsnorm(x, w: torch.Tensor, eps: float, residual: torch.Tensor | None = None,
             out: torch.Tensor | None = None) -> torch.Tensor:
-    """RMSNorm; if ``residual`` is given it is updated in place to x + residual first."""
+    """RMSNorm; if ``residual`` is given it is updated in place to x + residual first.
+    ``x`` may be a :class:`SplitK` (slabs summed inside the kernel)."""
+    if isinstance(x, SplitK):
+        M, N = x.shape
+        y = out if out is not None else torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
+        kernels().rmsnorm(y, residual, w, y, eps, x.p, x.S)  # y doubles as the shape carrier
+        return y
     if not x.is_cuda:
         y, r = reference.rmsnorm(x, w, eps, residual)
         if residual is not None:
@@ -196,7 +217,8 @@ def gemm_plan(M: int, N: int, K: int):
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None, splits: int | None = None,
-           partial: torch.Tensor | None = None, bn: int | None = None, bm: int | None = None) -> torch.Tensor:
+           partial: torch.Tensor | None = None, bn: int | None = None, bm: int | None = None,
+           defer_reduce: bool = False):
     """y = x @ w^T (bf16). Decode-bucket shapes (M a multiple of 64, <= 256) run on the
     gfx950 gemm_decode kernel when it beats hipBLASLt for the shape (tuned table);
     everything else (prefill, odd shapes, CPU) on hipBLASLt / torch."""
@@ -210,9 +232,12 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None, sp
     if plan is None:
         return F.linear(x, w, out=out) if out is not None else F.linear(x, w)
     bm, bn, S = bm or plan[0], bn or plan[1], splits or plan[2]
-    y = out if out is not None else torch.empty(M, N, dtype=x.dtype, device=x.device)
     if S > 1 and (partial is None or partial.numel() < S * M * N):
         partial = torch.empty(S * M * N, dtype=torch.float32, device=x.device)
+    if defer_reduce and S > 1 and out is None:
+        kernels().gemm_decode(x, w, None, partial, S, bn, bm, False)
+        return SplitK(partial, S, M, N)
+    y = out if out is not None else torch.empty(M, N, dtype=x.dtype, device=x.device)
     kernels().gemm_decode(x, w, y, partial if S > 1 else None, S, bn, bm, False)
     return y
 
