@@ -83,14 +83,26 @@ void embedding(const at::Tensor& ids, const at::Tensor& table, at::Tensor& out) 
 void rope_kv(const at::Tensor& qkv, const at::Tensor& pos, const at::Tensor& cos_t, const at::Tensor& sin_t,
              int64_t Hq, int64_t Hkv, at::Tensor& q_out, const c10::optional<at::Tensor>& k_out,
              const c10::optional<at::Tensor>& v_out, const c10::optional<at::Tensor>& k_cache,
-             const c10::optional<at::Tensor>& v_cache, const c10::optional<at::Tensor>& slots) {
-  CHECK_DEV(qkv); CHECK_BF16(qkv); ROWMAJOR_VEC(qkv);
-  CHECK_DT(pos, at::kLong); CHECK_CONTIG(pos);
+             const c10::optional<at::Tensor>& v_cache, const c10::optional<at::Tensor>& slots,
+             const c10::optional<at::Tensor>& partial, int64_t splits) {
+  CHECK_DT(pos, at::kLong); CHECK_CONTIG(pos); CHECK_DEV(pos);
   CHECK_DT(cos_t, at::kFloat); CHECK_DT(sin_t, at::kFloat); CHECK_CONTIG(cos_t); CHECK_CONTIG(sin_t);
-  const int64_t T = qkv.size(0);
+  const int64_t T = pos.numel();
   const int64_t D = cos_t.size(1) * 2;
   TORCH_CHECK(D == 128, "only head_dim 128 is supported");
-  TORCH_CHECK(qkv.size(1) == (Hq + 2 * Hkv) * D, "qkv width != (Hq+2Hkv)*D");
+  const float* xp = nullptr;
+  const bf16_t* qp = nullptr;
+  int64_t qstride = 0;
+  if (partial.has_value()) {  // qkv = bf16(sum of `splits` fp32 [T, (Hq+2Hkv)D] slabs); qkv unused
+    CHECK_DT(*partial, at::kFloat); CHECK_CONTIG(*partial);
+    TORCH_CHECK(splits >= 1 && partial->numel() >= splits * T * (Hq + 2 * Hkv) * D, "rope_kv: slabs too small");
+    xp = partial->data_ptr<float>();
+  } else {
+    CHECK_DEV(qkv); CHECK_BF16(qkv); ROWMAJOR_VEC(qkv);
+    TORCH_CHECK(qkv.size(0) == T && qkv.size(1) == (Hq + 2 * Hkv) * D, "qkv must be [T, (Hq+2Hkv)*D]");
+    qp = ptr<bf16_t>(qkv);
+    qstride = qkv.stride(0);
+  }
   TORCH_CHECK(pos.numel() == T && sin_t.sizes() == cos_t.sizes(), "pos/cos/sin shape");
   CHECK_BF16(q_out); CHECK_CONTIG(q_out);
   TORCH_CHECK(q_out.numel() == T * Hq * D, "q_out shape");
@@ -106,11 +118,11 @@ void rope_kv(const at::Tensor& qkv, const at::Tensor& pos, const at::Tensor& cos
     TORCH_CHECK(slots->numel() == T, "slots shape");
     page = (int)k_cache->size(2);
   }
-  const c10::hip::HIPGuardMasqueradingAsCUDA g(qkv.device());
-  RC(oamd::rope_kv(ptr<bf16_t>(qkv), qkv.stride(0), ptr<int64_t>(pos), ptr<float>(cos_t), ptr<float>(sin_t),
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(pos.device());
+  RC(oamd::rope_kv(qp, qstride, ptr<int64_t>(pos), ptr<float>(cos_t), ptr<float>(sin_t),
                    (int)T, (int)Hq, (int)Hkv, (int)D, ptr<bf16_t>(q_out), optr<bf16_t>(k_out), optr<bf16_t>(v_out),
                    optr<bf16_t>(k_cache), optr<bf16_t>(v_cache), optr<int64_t>(slots), page, cos_t.size(0),
-                   cur_stream()));
+                   xp, (int)splits, cur_stream()));
 }
 
 void gemm_decode(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& y_opt,
@@ -257,7 +269,10 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("partial") = pybind11::none(), pybind11::arg("splits") = 1);
   m.def("silu_mul", &silu_mul, pybind11::arg("gu"), pybind11::arg("out"), pybind11::arg("block") = 0);
   m.def("embedding", &embedding);
-  m.def("rope_kv", &rope_kv);
+  m.def("rope_kv", &rope_kv, pybind11::arg("qkv"), pybind11::arg("pos"), pybind11::arg("cos"),
+        pybind11::arg("sin"), pybind11::arg("Hq"), pybind11::arg("Hkv"), pybind11::arg("q_out"),
+        pybind11::arg("k_out"), pybind11::arg("v_out"), pybind11::arg("k_cache"), pybind11::arg("v_cache"),
+        pybind11::arg("slots"), pybind11::arg("partial") = pybind11::none(), pybind11::arg("splits") = 1);
   m.def("attn_decode", &attn_decode);
   m.def("quantize_fp8", &quantize_fp8);
   m.def("gemm_fp8", &gemm_fp8, pybind11::arg("x8"), pybind11::arg("w8"), pybind11::arg("sx"), pybind11::arg("sw"),

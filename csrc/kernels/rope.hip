@@ -19,11 +19,31 @@ __global__ void __launch_bounds__(256) rope_kv_kernel(
     const float* __restrict__ cos_t, const float* __restrict__ sin_t, int Hq, int Hkv,
     bf16_t* __restrict__ q_out, bf16_t* __restrict__ k_out, bf16_t* __restrict__ v_out,
     bf16_t* __restrict__ k_cache, bf16_t* __restrict__ v_cache,
-    const int64_t* __restrict__ slots, int page_size, int64_t max_pos) {
+    const int64_t* __restrict__ slots, int page_size, int64_t max_pos,
+    const float* __restrict__ xp, int S, int64_t slab) {
   constexpr int HALF = D / 2;
   constexpr int GPH = HALF / 8;  // 8-element groups per half-head
   const int t = blockIdx.x;
   const bf16_t* row = qkv + t * qkv_stride;
+  const int ncol = (Hq + 2 * Hkv) * D;
+  // 8 consecutive qkv values of this row: from the bf16 row, or (xp set) the bf16
+  // rounding of the sum of S fp32 split-K slabs of the QKV projection
+  auto ld8 = [&](int col) -> u16x8 {
+    if (!xp) return *reinterpret_cast<const u16x8*>(row + col);
+    const float* pr = xp + (int64_t)t * ncol + col;
+    f32x4 lo = *reinterpret_cast<const f32x4*>(pr), hi = *reinterpret_cast<const f32x4*>(pr + 4);
+    for (int sp = 1; sp < S; ++sp) {
+      lo += *reinterpret_cast<const f32x4*>(pr + sp * slab);
+      hi += *reinterpret_cast<const f32x4*>(pr + sp * slab + 4);
+    }
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      o[j] = f2bf(lo[j]);
+      o[4 + j] = f2bf(hi[j]);
+    }
+    return o;
+  };
   int64_t p = pos[t];
   if (p < 0) p = 0;
   if (p >= max_pos) p = max_pos - 1;
@@ -40,9 +60,8 @@ __global__ void __launch_bounds__(256) rope_kv_kernel(
   for (int it = threadIdx.x; it < rot_items + copy_items; it += blockDim.x) {
     if (it < rot_items) {
       const int h = it / GPH, g = (it % GPH) * 8;
-      const bf16_t* src = row + h * D;
-      const u16x8 x1 = *reinterpret_cast<const u16x8*>(src + g);
-      const u16x8 x2 = *reinterpret_cast<const u16x8*>(src + HALF + g);
+      const u16x8 x1 = ld8(h * D + g);
+      const u16x8 x2 = ld8(h * D + HALF + g);
       const f32x4 c0 = *reinterpret_cast<const f32x4*>(cr + g);
       const f32x4 c1 = *reinterpret_cast<const f32x4*>(cr + g + 4);
       const f32x4 s0 = *reinterpret_cast<const f32x4*>(sr + g);
@@ -76,7 +95,7 @@ __global__ void __launch_bounds__(256) rope_kv_kernel(
     } else {
       const int ci = it - rot_items;
       const int kh = ci / (D / 8), g = (ci % (D / 8)) * 8;
-      const u16x8 v = *reinterpret_cast<const u16x8*>(row + (Hq + Hkv + kh) * D + g);
+      const u16x8 v = ld8((Hq + Hkv + kh) * D + g);
       if (v_out) *reinterpret_cast<u16x8*>(v_out + ((int64_t)t * Hkv + kh) * D + g) = v;
       if (cache_base_k >= 0)
         *reinterpret_cast<u16x8*>(v_cache + cache_base_k + (int64_t)kh * page_size * D + g) = v;
@@ -87,11 +106,13 @@ __global__ void __launch_bounds__(256) rope_kv_kernel(
 int rope_kv(const bf16_t* qkv, int64_t qkv_stride, const int64_t* pos, const float* cos_t,
             const float* sin_t, int tokens, int Hq, int Hkv, int head_dim, bf16_t* q_out,
             bf16_t* k_out, bf16_t* v_out, bf16_t* k_cache, bf16_t* v_cache,
-            const int64_t* slots, int page_size, int64_t max_pos, hipStream_t stream) {
+            const int64_t* slots, int page_size, int64_t max_pos, const float* xp, int S,
+            hipStream_t stream) {
   if (tokens == 0) return 0;
   if (head_dim != 128) return -1;
+  const int64_t slab = (int64_t)tokens * (Hq + 2 * Hkv) * head_dim;
   rope_kv_kernel<128><<<tokens, 256, 0, stream>>>(qkv, qkv_stride, pos, cos_t, sin_t, Hq, Hkv, q_out, k_out,
-                                                 v_out, k_cache, v_cache, slots, page_size, max_pos);
+                                                 v_out, k_cache, v_cache, slots, page_size, max_pos, xp, S, slab);
   OAMD_LAUNCH_CHECK();
   return 0;
 }

@@ -124,6 +124,15 @@ def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, cos: torch.Tensor, sin: torch.
 
     Returns (q [T,Hq,D], k [T,Hkv,D] | None, v [T,Hkv,D] | None).
     """
+    if isinstance(qkv, SplitK):
+        T = qkv.shape[0]
+        D = cos.shape[1] * 2
+        dev = qkv.device
+        q = q_out if q_out is not None else torch.empty(T, Hq, D, dtype=torch.bfloat16, device=dev)
+        k = torch.empty(T, Hkv, D, dtype=torch.bfloat16, device=dev) if want_kv else None
+        v = torch.empty(T, Hkv, D, dtype=torch.bfloat16, device=dev) if want_kv else None
+        kernels().rope_kv(q, pos, cos, sin, Hq, Hkv, q, k, v, k_cache, v_cache, slots, qkv.p, qkv.S)
+        return q, k, v
     if not qkv.is_cuda:
         q, k, v = reference.rope_kv(qkv, pos, cos, sin, Hq, Hkv, k_cache, v_cache, slots)
         if q_out is not None:

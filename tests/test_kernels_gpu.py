@@ -254,3 +254,21 @@ def test_deferred_splitk_decode_matches_plain():
     b = m.forward(fb, kv)
     m._lin = lin
     torch.testing.assert_close(a.float(), b.float(), atol=3e-2, rtol=3e-2)
+
+
+def test_rope_kv_from_splitk_slabs():
+    torch.manual_seed(12)
+    T, Hq, Hkv, D, S = 64, 8, 2, 128, 4
+    W = (Hq + 2 * Hkv) * D
+    P = torch.randn(S * T * W, device=DEV, dtype=torch.float32)
+    sk = ops.SplitK(P, S, T, W)
+    cos, sin = ref.rope_tables(4096, D, 500000.0)
+    cos, sin = cos.to(DEV), sin.to(DEV)
+    pos = torch.randint(0, 4000, (T,), device=DEV)
+    kc1 = torch.zeros(8, Hkv, 16, D, device=DEV, dtype=torch.bfloat16)
+    vc1, kc2, vc2 = kc1.clone(), kc1.clone(), kc1.clone()
+    slots = torch.randperm(128, device=DEV)[:T]
+    q1, k1, v1 = ops.rope_kv(sk, pos, cos, sin, Hq, Hkv, kc1, vc1, slots)
+    q2, k2, v2 = ops.rope_kv(sk.materialize(), pos, cos, sin, Hq, Hkv, kc2, vc2, slots)
+    for a, b in ((q1, q2), (k1, k2), (v1, v2), (kc1, kc2), (vc1, vc2)):
+        torch.testing.assert_close(a.float(), b.float(), atol=3e-2, rtol=2e-2)
