@@ -23,7 +23,10 @@
 // B lane l -> B[8(l>>4)+j][l&15]; C col = l&15, row = 4(l>>4)+r. The dims of a
 // k-step are permuted so lane group g covers dims 32g..32g+31 over the 4
 // k-steps (Q uses the same permutation, so the contraction is unchanged).
-// KV cache layout: [pages, Hkv, page_size, D] bf16.
+// KV cache layout: [pages, Hkv, page_size, D] bf16. V rows are token-major; K is
+// stored in 16-token tiles laid out [ks 4][lg 4][token 16][8 dims] (d = 32*lg +
+// 8*ks + j), so each K fragment load (fixed ks) is ONE contiguous 1 KB wave
+// access instead of 16 token rows x 64 B (written that way by rope_kv).
 #include "common.h"
 #include "kernels.h"
 
@@ -114,9 +117,12 @@ __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2) attn_decode_
     const int base = start + c * CH + w * TW;
 #pragma unroll
     for (int i = 0; i < NT; ++i) {
-      const bf16_t* p = kc + row_off(min(base + 16 * i + l15, end - 1)) + 32 * lg;
+      const int tok = min(base + 16 * i + l15, end - 1);
+      const int t16 = tok & 15;
+      // tile of `tok`: its 16-token-aligned row, then (lg*16 + t16)*8 inside each ks block
+      const bf16_t* p = kc + row_off(tok) - (int64_t)t16 * D + (lg * 16 + t16) * 8;
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) r.k[i][ks] = ld16(p + 8 * ks);
+      for (int ks = 0; ks < 4; ++ks) r.k[i][ks] = ld16(p + ks * 512);
     }
 #pragma unroll
     for (int it = 0; it < 4 * NT; ++it) r.v[it] = ld16(vc + row_off(min(base + 4 * it + lg, end - 1)) + 8 * l15);

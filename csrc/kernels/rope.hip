@@ -7,7 +7,8 @@
 // trig: cdna_hip_programming.md App. B "Element-wise"). Outputs:
 //   q_out  [T, Hq, D]            rotated q (always)
 //   k_out/v_out [T, Hkv, D]      rotated k / copied v (optional, prefill path)
-//   k_cache/v_cache [pages, Hkv, P, D] at slot_mapping[t] (optional; slot<0 skips)
+//   k_cache/v_cache [pages, Hkv, P, D] at slot_mapping[t] (optional; slot<0 skips);
+//   K is stored in 16-token MFMA tiles (see attn_decode.hip), V row-major
 #include "common.h"
 #include "kernels.h"
 
@@ -50,10 +51,13 @@ __global__ void __launch_bounds__(256) rope_kv_kernel(
   const float* cr = cos_t + p * HALF;
   const float* sr = sin_t + p * HALF;
   int64_t slot = slots ? slots[t] : -1;
-  int64_t cache_base_k = -1;
+  int64_t cache_base_k = -1, tile_base_k = -1;  // V row / K tile of this token (+ h*page_size*D)
+  int t16 = 0;
   if (slot >= 0) {
     const int64_t page = slot / page_size, off = slot % page_size;
-    cache_base_k = (page * Hkv * page_size + off) * D;  // + h*page_size*D
+    cache_base_k = (page * Hkv * page_size + off) * D;
+    tile_base_k = (page * Hkv * page_size + (off & ~15)) * D;
+    t16 = static_cast<int>(off & 15);
   }
   const int rot_items = (Hq + Hkv) * GPH;
   const int copy_items = Hkv * (D / 8);
@@ -87,9 +91,12 @@ __global__ void __launch_bounds__(256) rope_kv_kernel(
           *reinterpret_cast<u16x8*>(dst + HALF + g) = o2;
         }
         if (cache_base_k >= 0) {
-          bf16_t* dst = k_cache + cache_base_k + (int64_t)kh * page_size * D;
-          *reinterpret_cast<u16x8*>(dst + g) = o1;
-          *reinterpret_cast<u16x8*>(dst + HALF + g) = o2;
+          // tiled K layout (attn_decode.hip): [16-token tile][ks][lg][token][8 dims],
+          // dim d = 32*lg + 8*ks + j
+          bf16_t* tile = k_cache + tile_base_k + (int64_t)kh * page_size * D;
+          const int d1 = g, d2 = HALF + g;
+          *reinterpret_cast<u16x8*>(tile + ((((d1 & 31) >> 3) * 4 + (d1 >> 5)) * 16 + t16) * 8) = o1;
+          *reinterpret_cast<u16x8*>(tile + ((((d2 & 31) >> 3) * 4 + (d2 >> 5)) * 16 + t16) * 8) = o2;
         }
       }
     } else {

@@ -70,12 +70,43 @@ def apply_rope(x: torch.Tensor, pos: torch.Tensor, cos: torch.Tensor, sin: torch
     return torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], dim=-1).to(x.dtype)
 
 
+K_TILE = 16  # tokens per K-cache tile
+
+
+def k_tile_index(D: int = 128) -> torch.Tensor:
+    """Physical offset inside a [16 tokens x D] K-cache tile of logical element (t, d).
+
+    K is stored so that each MFMA fragment load of the decode-attention kernel is
+    one contiguous 1 KB wave access: a tile is [ks 4][lg 4][token 16][8 dims]
+    with d = 32*lg + 8*ks + j (lg = lane >> 4 group, ks = k-step) — instead of
+    16 token rows x 64 B per instruction. V keeps the row layout."""
+    t = torch.arange(K_TILE)[:, None]
+    d = torch.arange(D)[None, :]
+    lg, ks, j = d // 32, (d % 32) // 8, d % 8
+    return ((ks * 4 + lg) * K_TILE + t) * 8 + j
+
+
+def k_cache_logical(k_cache: torch.Tensor) -> torch.Tensor:
+    """[pages, Hkv, P, D] tiled K cache -> logical (token-row) copy."""
+    pages, Hkv, P, D = k_cache.shape
+    idx = k_tile_index(D).flatten().to(k_cache.device)
+    return k_cache.reshape(pages, Hkv, P // K_TILE, K_TILE * D)[..., idx].reshape(pages, Hkv, P, D)
+
+
+def k_cache_write(k_cache: torch.Tensor, page: int, off: int, k: torch.Tensor) -> None:
+    """k_cache[page, :, off] = k ([Hkv, D]) in the tiled K layout."""
+    pages, Hkv, P, D = k_cache.shape
+    idx = k_tile_index(D)[off % K_TILE].to(k_cache.device)
+    k_cache.view(pages, Hkv, P // K_TILE, K_TILE * D)[page, :, off // K_TILE, idx] = k
+
+
 def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, Hq: int, Hkv: int,
             k_cache: torch.Tensor | None = None, v_cache: torch.Tensor | None = None,
             slots: torch.Tensor | None = None):
     """Split packed qkv, rotate q/k, optionally scatter k/v into the paged cache.
 
-    Cache layout [pages, Hkv, page, D]; slot = page*page_size + offset; slot < 0 skips.
+    Cache layout [pages, Hkv, page, D] (K tiled, see k_tile_index; V row-major);
+    slot = page*page_size + offset; slot < 0 skips.
     Returns (q [T,Hq,D], k [T,Hkv,D], v [T,Hkv,D]).
     """
     T = qkv.shape[0]
@@ -91,7 +122,7 @@ def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, cos: torch.Tensor, sin: torch.
             s = int(slots[t])
             if s < 0:
                 continue
-            k_cache[s // P, :, s % P] = k[t]
+            k_cache_write(k_cache, s // P, s % P, k[t])
             v_cache[s // P, :, s % P] = v[t]
     return q, k.contiguous(), v.contiguous()
 
@@ -121,9 +152,10 @@ def attn_prefill(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cu_seqlens: 
 
 def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
                 seq_lens: torch.Tensor, scale: float) -> torch.Tensor:
-    """One query token per sequence over a paged cache [pages, Hkv, page, D]."""
+    """One query token per sequence over a paged cache [pages, Hkv, page, D] (K tiled)."""
     B, Hq, D = q.shape
     Hkv, P = k_cache.shape[1], k_cache.shape[2]
+    k_cache = k_cache_logical(k_cache)
     G = Hq // Hkv
     out = torch.zeros_like(q)
     for b in range(B):
