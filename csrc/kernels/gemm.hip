@@ -66,7 +66,8 @@ enum { kEpiStore = 0, kEpiPartial = 1, kEpiSiluGU = 2 };
 template <int BM, int BN, int EPI>
 __global__ void __launch_bounds__(kWaves * 64, 1) gemm_tn_kernel(const bf16_t* __restrict__ X,
                                                                  const bf16_t* __restrict__ W, bf16_t* __restrict__ Y,
-                                                                 float* __restrict__ P, int M, int N, int K, int S) {
+                                                                 float* __restrict__ P, int M, int N, int K, int S,
+                                                                 int w_tiled) {
   using C = GemmCfg<BM, BN>;
   __shared__ __attribute__((aligned(1024))) char lds[C::LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -83,18 +84,25 @@ __global__ void __launch_bounds__(kWaves * 64, 1) gemm_tn_kernel(const bf16_t* _
   // stage (A rows [0, BM), then B rows [BM, BM + BN)); lane l -> row 8q + l/8,
   // LDS slot l%8, global chunk swz(row, slot).
   const int lrow = lane >> 3, lslot = lane & 7;
-  auto issue = [&](int t, int buf) {
+  auto issue_one = [&](int t, int buf, int i) {
     const int k0 = kbase + t * kBK;
     char* sbase = lds + buf * C::STAGE_BYTES;
-#pragma unroll
-    for (int i = 0; i < C::GL; ++i) {
+    {
       const int q = w + kWaves * i;
       const int row = 8 * q + lrow;
       const int chunk = swz(row, lslot);
-      const bf16_t* src = (row < BM) ? X + (int64_t)row * K + k0 + chunk * 8
-                                     : W + (int64_t)(n0 + row - BM) * K + k0 + chunk * 8;
+      const int wn_ = n0 + row - BM;
+      // tiled W ([N/64][K/64][64][64]): each 8-row x 128-B piece of a stage is one
+      // contiguous 1 KB of HBM instead of 8 separate 128-B row segments
+      const bf16_t* wsrc = w_tiled ? W + ((int64_t)(wn_ >> 6) * (K >> 6) + (k0 >> 6)) * 4096 + (wn_ & 63) * 64 + chunk * 8
+                                   : W + (int64_t)wn_ * K + k0 + chunk * 8;
+      const bf16_t* src = (row < BM) ? X + (int64_t)row * K + k0 + chunk * 8 : wsrc;
       __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(sbase + q * 1024), 16, 0, 0);
     }
+  };
+  auto issue = [&](int t, int buf) {
+#pragma unroll
+    for (int i = 0; i < C::GL; ++i) issue_one(t, buf, i);
   };
 
   const int wm = w / C::WN, wn = w % C::WN;
@@ -105,7 +113,12 @@ __global__ void __launch_bounds__(kWaves * 64, 1) gemm_tn_kernel(const bf16_t* _
 #pragma unroll
     for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto compute = [&](int buf) {
+  // One stage of MFMAs; the LDS-DMA pieces of stage `tn` are spread between them
+  // (piece g after MFMA ((g+1) * TOT) / (GL+1)) so the issue cost of the DMA
+  // overlaps MFMA execution instead of stalling both waves of a SIMD after the
+  // barrier.
+  constexpr int TOT = (kBK / 32) * C::FM * C::FN;
+  auto compute = [&](int buf, int tn, bool do_issue) {
     const char* sbase = lds + buf * C::STAGE_BYTES;
 #pragma unroll
     for (int s = 0; s < kBK / 32; ++s) {
@@ -124,9 +137,14 @@ __global__ void __launch_bounds__(kWaves * 64, 1) gemm_tn_kernel(const bf16_t* _
 #pragma unroll
       for (int i = 0; i < C::FM; ++i)
 #pragma unroll
-        for (int j = 0; j < C::FN; ++j)
+        for (int j = 0; j < C::FN; ++j) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a[i]),
                                                               __builtin_bit_cast(bf16x8_t, b[j]), acc[i][j], 0, 0, 0);
+          const int idx = (s * C::FM + i) * C::FN + j + 1;
+#pragma unroll
+          for (int g = 0; g < C::GL; ++g)
+            if (idx == ((g + 1) * TOT) / (C::GL + 1) && do_issue) issue_one(tn, tn % kStages, g);
+        }
     }
   };
 
@@ -138,8 +156,7 @@ __global__ void __launch_bounds__(kWaves * 64, 1) gemm_tn_kernel(const bf16_t* _
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (t + 2 < T) issue(t + 2, (t + 2) % kStages);
-    compute(t % kStages);
+    compute(t % kStages, t + 2, t + 2 < T);
   }
 
   if constexpr (EPI == kEpiSiluGU) {
@@ -205,15 +222,17 @@ __global__ void gemm_splitk_reduce_kernel(const float* __restrict__ P, bf16_t* _
 }
 
 int gemm_decode(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, int N, int K, int S, int BN,
-                int BM, bool silu_gu, hipStream_t stream) {
+                int BM, bool silu_gu, bool w_tiled_b, hipStream_t stream) {
+  const int w_tiled = w_tiled_b ? 1 : 0;
+  if (w_tiled && (N % 64 != 0 || K % 64 != 0)) return -6;
   if ((BM != 64 && BM != 128 && BM != 256) || M % BM != 0) return -1;
   if (silu_gu) {  // fused SwiGLU: one K slice, 128-column tiles of 64 gate + 64 up rows
     if (BN != 128 || S != 1 || N % 128 != 0 || K % kBK != 0) return -5;
     const dim3 grid(N / 128, M / BM);
     switch (BM) {
-      case 64: gemm_tn_kernel<64, 128, kEpiSiluGU><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, 1); break;
-      case 128: gemm_tn_kernel<128, 128, kEpiSiluGU><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, 1); break;
-      default: gemm_tn_kernel<256, 128, kEpiSiluGU><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, 1); break;
+      case 64: gemm_tn_kernel<64, 128, kEpiSiluGU><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, 1, w_tiled); break;
+      case 128: gemm_tn_kernel<128, 128, kEpiSiluGU><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, 1, w_tiled); break;
+      default: gemm_tn_kernel<256, 128, kEpiSiluGU><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, 1, w_tiled); break;
     }
     OAMD_LAUNCH_CHECK();
     return 0;
@@ -223,8 +242,8 @@ int gemm_decode(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, in
   if (S > 1 && P == nullptr) return -4;
   const dim3 grid((N / BN) * S, M / BM);
 #define OAMD_GEMM2(BM, BNN)                                                                                   \
-  if (S > 1) gemm_tn_kernel<BM, BNN, kEpiPartial><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, S); \
-  else gemm_tn_kernel<BM, BNN, kEpiStore><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, S)
+  if (S > 1) gemm_tn_kernel<BM, BNN, kEpiPartial><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, S, w_tiled); \
+  else gemm_tn_kernel<BM, BNN, kEpiStore><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, S, w_tiled)
 #define OAMD_GEMM(BM) \
   if (BN == 64) { OAMD_GEMM2(BM, 64); } else { OAMD_GEMM2(BM, 128); }
   switch (BM) {

@@ -240,3 +240,7 @@ class AIResponse(KModel):
     tokens_generated: Optional[int] = None
     latency_ms: Optional[float] = None
     cached: Optional[bool] = None
+    # on-node engine stage timings (absent from remote providers)
+    prompt_tokens: Optional[int] = None
+    queue_ms: Optional[float] = None      # request -> first token (admission wait + prefill)
+    decode_ms: Optional[float] = None     # first token -> last token

@@ -174,7 +174,9 @@ class ExplainEngine:
         r = p.req
         text = self.tok.decode(r.output)
         resp = AIResponse(explanation=text, provider_id=cfg.provider_id or "local", model_id=cfg.model_id or self.model_id,
-                          tokens_generated=len(r.output), latency_ms=round((r.t_done - p.t0) * 1e3, 3), cached=False)
+                          tokens_generated=len(r.output), latency_ms=round((r.t_done - p.t0) * 1e3, 3), cached=False,
+                          prompt_tokens=len(r.prompt), queue_ms=round((r.t_first - p.t0) * 1e3, 3),
+                          decode_ms=round((r.t_done - r.t_first) * 1e3, 3))
         if p.key is not None:
             with self._lock:
                 self._cache[p.key] = resp

@@ -29,6 +29,7 @@ import torch
 from operator_amd import ops
 from operator_amd.models.kv_cache import PagedKVCache
 from operator_amd.models.llama import ForwardBatch, LlamaModel
+from operator_amd.utils.tracing import trace_range
 
 
 @dataclass(eq=False)  # identity semantics: two requests are never "equal"
@@ -304,6 +305,10 @@ class LLMEngine:
         return out
 
     def _prefill(self, batch: list[GenRequest]) -> None:
+        with trace_range(f"prefill[{len(batch)}]"):
+            self._prefill_impl(batch)
+
+    def _prefill_impl(self, batch: list[GenRequest]) -> None:
         t0 = time.perf_counter()
         dev = self.device
         ids, pos, slots, lens, last = [], [], [], [], []
@@ -371,8 +376,9 @@ class LLMEngine:
             st.load(reqs, self.max_pages)
             self._active = st
         st.step.zero_()
-        for _ in range(k):
-            g.run(self.use_graphs)
+        with trace_range(f"decode[{bp}x{k}]"):
+            for _ in range(k):
+                g.run(self.use_graphs)
         if self._host_bufs is not None:
             self._hb ^= 1
             host = self._host_bufs[self._hb]

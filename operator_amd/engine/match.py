@@ -142,6 +142,12 @@ class MatchEngine:
 
     def scan_gpu(self, docs: list[bytes]) -> np.ndarray:
         """Raw factor hits as int64 array [n, 4] = (doc, factor, line, end_offset_in_doc)."""
+        from operator_amd.utils.tracing import trace_range
+
+        with trace_range(f"scan[{len(docs)}]"):
+            return self._scan_gpu(docs)
+
+    def _scan_gpu(self, docs: list[bytes]) -> np.ndarray:
         from operator_amd.ops import kernels, patterns
 
         P = patterns()

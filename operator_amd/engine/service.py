@@ -119,6 +119,9 @@ class LocalExplainService:
         if self.metrics:
             self.metrics.explain_seconds.observe(time.perf_counter() - t0)
             self.metrics.tokens_generated.inc(r.tokens_generated or 0)
+            if r.queue_ms is not None and not r.cached:
+                self.metrics.stage_seconds.labels(stage="explain_queue_prefill").observe(r.queue_ms / 1e3)
+                self.metrics.stage_seconds.labels(stage="explain_decode").observe((r.decode_ms or 0) / 1e3)
         return r
 
     def explain_many(self, items):
