@@ -195,6 +195,37 @@ void gemm_fp8(const at::Tensor& x8, const at::Tensor& w8, const at::Tensor& sx, 
                     (int)bm, cur_stream()));
 }
 
+void score_events(const at::Tensor& keys, const at::Tensor& hit_doc, const at::Tensor& doc_ptr,
+                  const at::Tensor& prim_ptr, const at::Tensor& prim_pat, const at::Tensor& ev_ptr,
+                  const at::Tensor& ev_doc_ptr, const at::Tensor& sec_ptr, const at::Tensor& sec_matcher,
+                  const at::Tensor& sec_w, const at::Tensor& sec_win, const at::Tensor& conf,
+                  const at::Tensor& severity, double significance, at::Tensor& ev_score, at::Tensor& ev_pat,
+                  at::Tensor& ev_line, at::Tensor& order, at::Tensor& summary) {
+  CHECK_DEV(keys); CHECK_DT(keys, at::kLong); CHECK_CONTIG(keys);
+  for (auto* t : {&hit_doc, &doc_ptr, &prim_ptr, &prim_pat, &ev_ptr, &ev_doc_ptr, &sec_ptr, &sec_matcher, &sec_win,
+                  &severity}) {
+    CHECK_DT(*t, at::kInt); CHECK_CONTIG(*t); CHECK_DEV(*t);
+  }
+  for (auto* t : {&sec_w, &conf}) { CHECK_DT(*t, at::kDouble); CHECK_CONTIG(*t); }
+  CHECK_DT(ev_score, at::kDouble); CHECK_DT(ev_pat, at::kInt); CHECK_DT(ev_line, at::kInt); CHECK_DT(order, at::kInt);
+  CHECK_DT(summary, at::kInt);
+  const int64_t n_hits = keys.numel(), n_docs = doc_ptr.numel() - 1;
+  const int64_t n_pat = conf.numel(), n_m = prim_ptr.numel() - 1;
+  TORCH_CHECK(hit_doc.numel() == n_hits && ev_ptr.numel() == n_hits + 1 && ev_doc_ptr.numel() == n_docs + 1,
+              "score_events: hit index shapes");
+  TORCH_CHECK(sec_ptr.numel() == n_pat + 1 && severity.numel() == n_pat && sec_matcher.numel() == sec_w.numel() &&
+                  sec_w.numel() == sec_win.numel(), "score_events: pattern table shapes");
+  TORCH_CHECK(summary.numel() >= 3 * n_docs, "summary [docs, 3]");
+  const int64_t n_ev = ev_score.numel();
+  TORCH_CHECK(ev_pat.numel() == n_ev && ev_line.numel() == n_ev && order.numel() == n_ev, "event buffer shapes");
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(keys.device());
+  RC(oamd::score_events(ptr<int64_t>(keys), ptr<int>(hit_doc), ptr<int>(doc_ptr), (int)n_hits, (int)n_docs,
+                        ptr<int>(prim_ptr), ptr<int>(prim_pat), ptr<int>(ev_ptr), ptr<int>(ev_doc_ptr),
+                        ptr<int>(sec_ptr), ptr<int>(sec_matcher), ptr<double>(sec_w), ptr<int>(sec_win),
+                        ptr<double>(conf), ptr<int>(severity), (int)n_m, significance, ptr<double>(ev_score),
+                        ptr<int>(ev_pat), ptr<int>(ev_line), ptr<int>(order), ptr<int>(summary), cur_stream()));
+}
+
 void attn_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                  const at::Tensor& block_tables, const at::Tensor& seq_lens, at::Tensor& out,
                  at::Tensor& o_part, at::Tensor& ml_part, int64_t num_splits, double scale, int64_t variant) {
@@ -275,6 +306,7 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("slots"), pybind11::arg("partial") = pybind11::none(), pybind11::arg("splits") = 1);
   m.def("attn_decode", &attn_decode);
   m.def("quantize_fp8", &quantize_fp8);
+  m.def("score_events", &score_events);
   m.def("gemm_fp8", &gemm_fp8, pybind11::arg("x8"), pybind11::arg("w8"), pybind11::arg("sx"), pybind11::arg("sw"),
         pybind11::arg("y"), pybind11::arg("p") = pybind11::none(), pybind11::arg("splits") = 1,
         pybind11::arg("bn") = 64, pybind11::arg("bm") = 64);

@@ -32,6 +32,13 @@ int gemm_fp8(const uint8_t* X, const uint8_t* W, const float* sx, const float* s
 // Per-row dynamic quantization to e4m3fn: sx[m] = max|x[m]| / 448.
 int quantize_fp8_rows(const bf16_t* x, uint8_t* q, float* sx, int M, int K, int64_t ld, hipStream_t stream);
 
+// Pattern-event scoring + per-doc ranking / summary (N5), see score.hip.
+int score_events(const int64_t* keys, const int* hit_doc, const int* doc_ptr, int n_hits, int n_docs,
+                 const int* prim_ptr, const int* prim_pat, const int* ev_ptr, const int* ev_doc_ptr,
+                 const int* sec_ptr, const int* sec_matcher, const double* sec_w, const int* sec_win,
+                 const double* conf, const int* severity, int num_matchers, double significance, double* ev_score,
+                 int* ev_pat, int* ev_line, int* order, int* summary, hipStream_t stream);
+
 int attn_decode(const bf16_t* q, const bf16_t* k_cache, const bf16_t* v_cache, const int* block_tables,
                 const int* seq_lens, bf16_t* out, float* o_part, float* ml_part, int B, int Hq, int Hkv,
                 int head_dim, int page_size, int max_pages, int num_splits, float scale, int variant,

@@ -85,7 +85,8 @@ class MatchEngine:
 
     def __init__(self, patterns: PatternSet | CompiledPatterns, device: str | torch.device = "cuda",
                  seg_bytes: int = 1024, max_events: int = 50, significance: float = 0.5,
-                 match_cap: int = 1 << 20, grid_blocks: int = 0, use_native_scorer: bool = True):
+                 match_cap: int = 1 << 20, grid_blocks: int = 0, use_native_scorer: bool = True,
+                 gpu_scorer: bool | None = None):
         self.cp = patterns if isinstance(patterns, CompiledPatterns) else compile_patterns(patterns)
         self.device = torch.device(device)
         self.seg_bytes = int(seg_bytes)
@@ -94,6 +95,9 @@ class MatchEngine:
         self.match_cap = int(match_cap)
         self.grid_blocks = grid_blocks
         self.use_native_scorer = use_native_scorer
+        # score + rank events on the GPU (score.hip) when scanning there
+        self.gpu_scorer = (self.device.type == "cuda") if gpu_scorer is None else gpu_scorer
+        self._score_tables = None
         self.stats = ScanStats()
         self._lock = threading.Lock()
         self._pinned: torch.Tensor | None = None
@@ -254,9 +258,72 @@ class MatchEngine:
         self.stats.host_ms += (time.perf_counter() - t1) * 1e3
         return arr, offs
 
+    def _gpu_tables(self):
+        """Static pattern tables for score.hip (CSR), uploaded once per pattern set."""
+        if self._score_tables is None:
+            cp, dev = self.cp, self.device
+            pats = cp.patset.patterns
+            nm = cp.num_matchers
+            prim_of: list[list[int]] = [[] for _ in range(nm)]
+            for p_, m_ in enumerate(cp.pattern_primary):
+                prim_of[m_].append(p_)
+            prim_ptr = np.zeros(nm + 1, np.int64)
+            prim_ptr[1:] = np.cumsum([len(x) for x in prim_of])
+            sec_ptr = np.zeros(len(pats) + 1, np.int64)
+            sec_ptr[1:] = np.cumsum([len(p.secondary) for p in pats])
+            t = lambda a, dt=torch.int32: torch.as_tensor(np.asarray(a), dtype=dt).to(dev)  # noqa: E731
+            self._score_tables = dict(
+                npat=np.asarray([len(x) for x in prim_of], np.int64),
+                prim_ptr=t(prim_ptr), prim_pat=t([p_ for x in prim_of for p_ in x] or [0]),
+                sec_ptr=t(sec_ptr), sec_matcher=t([m_ for x in cp.pattern_secondary for m_ in x] or [0]),
+                sec_w=t([s_.weight for p in pats for s_ in p.secondary] or [0.0], torch.float64),
+                sec_win=t([s_.window for p in pats for s_ in p.secondary] or [0]),
+                conf=t([p.primary.confidence for p in pats], torch.float64),
+                severity=t([p.severity_rank for p in pats]))
+        return self._score_tables
+
+    def _events_gpu(self, hits: np.ndarray, n_docs: int) -> list[list[oracle.Event]]:
+        from operator_amd.ops import kernels
+
+        T = self._gpu_tables()
+        dev = self.device
+        n = hits.shape[0]
+        doc, mat, line = hits[:, 0], hits[:, 1], hits[:, 2]
+        doc_ptr = np.zeros(n_docs + 1, np.int64)
+        doc_ptr[1:] = np.cumsum(np.bincount(doc, minlength=n_docs))
+        nm = T["npat"].shape[0]
+        per_hit = np.where(mat < nm, T["npat"][np.minimum(mat, nm - 1)], 0)
+        ev_ptr = np.zeros(n + 1, np.int64)
+        ev_ptr[1:] = np.cumsum(per_hit)
+        ev_doc_ptr = ev_ptr[doc_ptr]
+        E = int(ev_ptr[-1])
+        i32 = lambda a: torch.as_tensor(a, dtype=torch.int32).to(dev, non_blocking=True)  # noqa: E731
+        keys = torch.as_tensor((mat << 32) | line, dtype=torch.long).to(dev, non_blocking=True)
+        ev_score = torch.empty(max(E, 1), dtype=torch.float64, device=dev)[:E]
+        ev_pat = torch.empty(E, dtype=torch.int32, device=dev)
+        ev_line = torch.empty(E, dtype=torch.int32, device=dev)
+        order = torch.empty(E, dtype=torch.int32, device=dev)
+        summary = torch.empty(3 * max(n_docs, 1), dtype=torch.int32, device=dev)
+        kernels().score_events(keys, i32(doc), i32(doc_ptr), T["prim_ptr"], T["prim_pat"], i32(ev_ptr),
+                               i32(ev_doc_ptr), T["sec_ptr"], T["sec_matcher"], T["sec_w"], T["sec_win"], T["conf"],
+                               T["severity"], float(self.significance), ev_score, ev_pat, ev_line, order, summary)
+        sc, pt, ln, od = (x.cpu().numpy() for x in (ev_score, ev_pat, ev_line, order))
+        sev = T["severity"].cpu().numpy()
+        out = []
+        for d in range(n_docs):
+            a, b = int(ev_doc_ptr[d]), int(ev_doc_ptr[d + 1])
+            if b - a > 2048:  # beyond the LDS sort cap: rank on the host (same key)
+                idx = sorted(range(a, b), key=lambda i: (-sc[i], -sev[pt[i]], ln[i], pt[i]))
+            else:
+                idx = od[a:b]
+            out.append([oracle.Event(int(pt[i]), int(ln[i]), float(sc[i])) for i in idx])
+        return out
+
     def events(self, docs: list[bytes]) -> tuple[list[list[oracle.Event]], dict]:
         hits, offs = self.hits(docs)
         cp = self.cp
+        if self.gpu_scorer and self.device.type == "cuda":
+            return self._events_gpu(hits, len(docs)), offs
         if self.use_native_scorer:
             from operator_amd.ops import patterns
 

@@ -85,3 +85,25 @@ def test_large_batch_throughput_smoke():
     want = sum(d.lower().count(b"oomkilled") for d in docs)
     assert int((raw[:, 1] == fid).sum()) == want
     torch.cuda.synchronize()
+
+
+def test_gpu_scorer_matches_host_scorer():
+    """score.hip (score + rank + summary on the GPU) == the C++ host scorer."""
+    from operator_amd.engine.match import MatchEngine
+    from operator_amd.patterns.synth import LogFactory, synthetic_library
+
+    ps = synthetic_library(300, seed=2)
+    fac = LogFactory(n_patterns=300, seed=4)
+    docs, _ = fac.batch(24, 32 * 1024, n_failures=4, seed=9)
+    docs.append(b"")  # empty doc
+    g = MatchEngine(ps, device="cuda", gpu_scorer=True)
+    h = MatchEngine(ps, device="cuda", gpu_scorer=False)
+    eg, _ = g.events(docs)
+    eh, _ = h.events(docs)
+    assert len(eg) == len(eh)
+    for a, b in zip(eg, eh):
+        assert [(e.pattern, e.line) for e in a] == [(e.pattern, e.line) for e in b]
+        assert all(abs(x.score - y.score) < 1e-9 for x, y in zip(a, b))
+    ra = [r.to_obj()["summary"] for r in g.analyze(docs)]
+    rb = [r.to_obj()["summary"] for r in h.analyze(docs)]
+    assert ra == rb
