@@ -208,7 +208,7 @@ def main() -> int:
         "config": {"model": a.model, "global_batch": a.batch * world, "seq_len": a.prompt_tokens + a.max_tokens,
                    "parallelism": f"dp{world}", "tp": 1, "max_tokens": a.max_tokens,
                    "prompt_tokens_cap": a.prompt_tokens, "log_kib": a.log_kb, "patterns": a.patterns,
-                   "mode": a.mode, "hipgraph": not a.no_graphs},
+                   "mode": a.mode, "hipgraph": bool(llm.use_graphs)},
         "detail": {"init_s": round(init_s, 1), "prefill_tokens_per_gpu": ptoks, "decode_tokens_per_gpu": dtoks,
                    "decode_tok_s_per_gpu": round(dtoks / elapsed, 1), "outcomes": counter["outcomes"],
                    "dfa_states": getattr(meng, "dfa_states", None), "timed_monotonic_ns": [mono0, mono1]},
