@@ -51,6 +51,7 @@ def parse_args():
     ap.add_argument("--log-kb", type=int, default=64)
     ap.add_argument("--patterns", type=int, default=1000)
     ap.add_argument("--max-batch", type=int, default=256, help="LLM continuous-batching width")
+    ap.add_argument("--prefill-tokens", type=int, default=16384, help="max tokens per prefill batch")
     ap.add_argument("--mode", choices=["pipeline", "engine"], default="pipeline")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--kv-gb", type=float, default=None, help="KV-cache budget (default 96 GB on GPU, 1 GB on CPU)")
@@ -83,6 +84,7 @@ def main() -> int:
 
     s = load_settings(env={}, overrides={
         "engine.model": a.model, "engine.device": dev, "engine.max_batch": a.max_batch,
+        "engine.max_prefill_tokens": a.prefill_tokens,
         "engine.max_context": a.prompt_tokens + a.max_tokens + 64, "engine.max_prompt_tokens": a.prompt_tokens,
         "engine.kv_cache_gb": a.kv_gb or (96.0 if dev != "cpu" else 1.0), "engine.use_graphs": not a.no_graphs, "engine.ignore_eos": True,
         "engine.seed": 0, "health.enabled": False, "operator.workers": a.batch + 16, "operator.io_workers": 16,

@@ -127,7 +127,7 @@ void rope_kv(const at::Tensor& qkv, const at::Tensor& pos, const at::Tensor& cos
 
 void gemm_decode(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& y_opt,
                  const c10::optional<at::Tensor>& p,
-                 int64_t splits, int64_t bn, int64_t bm, bool silu_gu, bool w_tiled) {
+                 int64_t splits, int64_t bn, int64_t bm, bool silu_gu, bool w_tiled, int64_t stages) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2, "x [M,K], w [N,K]");
   const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
@@ -156,7 +156,7 @@ void gemm_decode(const at::Tensor& x, const at::Tensor& w, const c10::optional<a
   TORCH_CHECK(K < (1LL << 31) / 64 && M * K < (1LL << 31) && N * K < (1LL << 40), "gemm too large");
   const c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   RC(oamd::gemm_decode(ptr<bf16_t>(x), ptr<bf16_t>(w), yp, pp, (int)M, (int)N, (int)K, (int)splits,
-                       (int)bn, (int)bm, silu_gu, w_tiled, cur_stream()));
+                       (int)bn, (int)bm, silu_gu, w_tiled, (int)stages, cur_stream()));
 }
 
 void quantize_fp8(const at::Tensor& x, at::Tensor& q, at::Tensor& sx) {
@@ -312,7 +312,8 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("bn") = 64, pybind11::arg("bm") = 64);
   m.def("gemm_decode", &gemm_decode, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"),
         pybind11::arg("p") = pybind11::none(), pybind11::arg("splits") = 1, pybind11::arg("bn") = 64,
-        pybind11::arg("bm") = 0, pybind11::arg("silu_gu") = false, pybind11::arg("w_tiled") = false);
+        pybind11::arg("bm") = 0, pybind11::arg("silu_gu") = false, pybind11::arg("w_tiled") = false,
+        pybind11::arg("stages") = 3);
   m.def("attn_prefill", &attn_prefill);
   m.def("sample", &sample, pybind11::arg("logits"), pybind11::arg("temperature"), pybind11::arg("seeds"),
         pybind11::arg("positions"), pybind11::arg("out"), pybind11::arg("col_offset") = 0,

@@ -28,7 +28,7 @@ namespace oamd {
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 
 constexpr int kBK = 64;     // K per stage: one 128-B line per row
-constexpr int kStages = 3;  // LDS ring depth
+constexpr int kStages = 3;  // default LDS ring depth (2: two blocks per CU for the smaller tiles)
 
 // 8 waves (2 per SIMD: one wave's LDS-read latency hides under the other's
 // MFMAs) laid out 4 (M) x 2 (N).
@@ -38,7 +38,7 @@ constexpr int kWaves = 8;
 // M = 256: 0.5 KB of ds_read per MFMA vs 0.75 KB at BN = 64, where the LDS
 // port, not the MFMA, sets the pace); BN = 64 gives twice the column tiles for
 // the narrow projections.
-template <int BM, int BN>
+template <int BM, int BN, int NS = kStages>
 struct GemmCfg {
   static constexpr int WM = 4;                           // waves along M
   static constexpr int WN = kWaves / WM;                 // waves along N
@@ -47,7 +47,7 @@ struct GemmCfg {
   static constexpr int ROWS = BM + BN;                   // rows of one stage (A then B)
   static constexpr int STAGE_BYTES = ROWS * kBK * 2;     // bf16
   static constexpr int GL = ROWS / 8 / kWaves;           // LDS-DMA instructions per wave per stage
-  static constexpr int LDS_BYTES = kStages * STAGE_BYTES;
+  static constexpr int LDS_BYTES = NS * STAGE_BYTES;
   static_assert(ROWS % (8 * kWaves) == 0, "stage rows must split evenly over the waves");
 };
 
@@ -63,12 +63,12 @@ __device__ __forceinline__ void wait_vmcnt() {
 // [0,64) = gate, [64,128) = up of the same 64 features; output [M, N/2]).
 enum { kEpiStore = 0, kEpiPartial = 1, kEpiSiluGU = 2 };
 
-template <int BM, int BN, int EPI>
-__global__ void __launch_bounds__(kWaves * 64, 1) gemm_tn_kernel(const bf16_t* __restrict__ X,
+template <int BM, int BN, int EPI, int NS = kStages>
+__global__ void __launch_bounds__(kWaves * 64, NS == 2 ? 2 : 1) gemm_tn_kernel(const bf16_t* __restrict__ X,
                                                                  const bf16_t* __restrict__ W, bf16_t* __restrict__ Y,
                                                                  float* __restrict__ P, int M, int N, int K, int S,
                                                                  int w_tiled) {
-  using C = GemmCfg<BM, BN>;
+  using C = GemmCfg<BM, BN, NS>;
   __shared__ __attribute__((aligned(1024))) char lds[C::LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -143,20 +143,22 @@ __global__ void __launch_bounds__(kWaves * 64, 1) gemm_tn_kernel(const bf16_t* _
           const int idx = (s * C::FM + i) * C::FN + j + 1;
 #pragma unroll
           for (int g = 0; g < C::GL; ++g)
-            if (idx == ((g + 1) * TOT) / (C::GL + 1) && do_issue) issue_one(tn, tn % kStages, g);
+            if (idx == ((g + 1) * TOT) / (C::GL + 1) && do_issue) issue_one(tn, tn % NS, g);
         }
     }
   };
 
+  // prologue: stages 0 .. NS-2 in flight; iteration t issues stage t + NS - 1
+  // into the buffer compute(t - 1) just released (fenced by the barrier)
   issue(0, 0);
-  if (T > 1) issue(1, 1);
+  if (NS == 3 && T > 1) issue(1, 1);
   for (int t = 0; t < T; ++t) {
-    if (t + 1 < T) wait_vmcnt<C::GL>();
+    if (NS == 3 && t + 1 < T) wait_vmcnt<C::GL>();  // leave stage t+1 in flight
     else wait_vmcnt<0>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    compute(t % kStages, t + 2, t + 2 < T);
+    compute(t % NS, t + NS - 1, t + NS - 1 < T);
   }
 
   if constexpr (EPI == kEpiSiluGU) {
@@ -222,7 +224,7 @@ __global__ void gemm_splitk_reduce_kernel(const float* __restrict__ P, bf16_t* _
 }
 
 int gemm_decode(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, int N, int K, int S, int BN,
-                int BM, bool silu_gu, bool w_tiled_b, hipStream_t stream) {
+                int BM, bool silu_gu, bool w_tiled_b, int stages, hipStream_t stream) {
   const int w_tiled = w_tiled_b ? 1 : 0;
   if (w_tiled && (N % 64 != 0 || K % 64 != 0)) return -6;
   if ((BM != 64 && BM != 128 && BM != 256) || M % BM != 0) return -1;
@@ -230,7 +232,10 @@ int gemm_decode(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, in
     if (BN != 128 || S != 1 || N % 128 != 0 || K % kBK != 0) return -5;
     const dim3 grid(N / 128, M / BM);
     switch (BM) {
-      case 64: gemm_tn_kernel<64, 128, kEpiSiluGU><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, 1, w_tiled); break;
+      case 64:
+        if (stages == 2) gemm_tn_kernel<64, 128, kEpiSiluGU, 2><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, 1, w_tiled);
+        else gemm_tn_kernel<64, 128, kEpiSiluGU><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, 1, w_tiled);
+        break;
       case 128: gemm_tn_kernel<128, 128, kEpiSiluGU><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, 1, w_tiled); break;
       default: gemm_tn_kernel<256, 128, kEpiSiluGU><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, 1, w_tiled); break;
     }
@@ -241,9 +246,12 @@ int gemm_decode(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, in
   if (S < 1 || 8 % S != 0 || K % (kBK * S) != 0) return -3;
   if (S > 1 && P == nullptr) return -4;
   const dim3 grid((N / BN) * S, M / BM);
-#define OAMD_GEMM2(BM, BNN)                                                                                   \
-  if (S > 1) gemm_tn_kernel<BM, BNN, kEpiPartial><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, S, w_tiled); \
-  else gemm_tn_kernel<BM, BNN, kEpiStore><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, S, w_tiled)
+#define OAMD_GEMM3(BM, BNN, NSS)                                                                               \
+  if (S > 1) gemm_tn_kernel<BM, BNN, kEpiPartial, NSS><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, S,   \
+                                                                                       w_tiled);              \
+  else gemm_tn_kernel<BM, BNN, kEpiStore, NSS><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, S, w_tiled)
+#define OAMD_GEMM2(BM, BNN) \
+  if (stages == 2 && BM <= 128) { OAMD_GEMM3(BM, BNN, 2); } else { OAMD_GEMM3(BM, BNN, 3); }
 #define OAMD_GEMM(BM) \
   if (BN == 64) { OAMD_GEMM2(BM, 64); } else { OAMD_GEMM2(BM, 128); }
   switch (BM) {
@@ -253,6 +261,7 @@ int gemm_decode(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, in
   }
 #undef OAMD_GEMM
 #undef OAMD_GEMM2
+#undef OAMD_GEMM3
   OAMD_LAUNCH_CHECK();
   if (S > 1 && Y != nullptr) {  // Y == nullptr: the consumer sums the slabs (rmsnorm)
     const int64_t MN = (int64_t)M * N;

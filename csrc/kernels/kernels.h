@@ -24,7 +24,7 @@ int rope_kv(const bf16_t* qkv, int64_t qkv_stride, const int64_t* pos, const flo
 // Y[M,N] = X[M,K] W[N,K]^T for decode buckets (M a multiple of the BM-row tile, BM in {64,128,256}); S-way split-K
 // (S | 8) with fp32 slabs P[S][M][N] reduced into Y; BN in {64, 128} columns per tile.
 int gemm_decode(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, int N, int K, int S, int BN,
-                int BM, bool silu_gu, bool w_tiled, hipStream_t stream);
+                int BM, bool silu_gu, bool w_tiled, int stages, hipStream_t stream);
 
 // FP8 e4m3fn W8A8: Y = (X8 . W8^T) * sx[m] * sw[n]; any M (BM-row tiles), S | 8 split-K.
 int gemm_fp8(const uint8_t* X, const uint8_t* W, const float* sx, const float* sw, bf16_t* Y, float* P, int M,

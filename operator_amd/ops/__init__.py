@@ -98,8 +98,9 @@ def gate_up_silu(x: torch.Tensor, wgu: torch.Tensor, block: int | None) -> torch
         t = _gemm_table_get().get(("silu", M, N, K))
         if t != "blas":
             bm = t[0] if t else min(M, 256)
+            ns = t[1] if t and len(t) > 1 else 3
             y = torch.empty(M, N // 2, dtype=x.dtype, device=x.device)
-            kernels().gemm_decode(x, wgu, y, None, 1, 128, bm, True)
+            kernels().gemm_decode(x, wgu, y, None, 1, 128, bm, True, False, ns)
             return y
     return silu_mul(linear(x, wgu), block=block)
 
@@ -227,7 +228,7 @@ def gemm_plan(M: int, N: int, K: int):
 
 def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None, splits: int | None = None,
            partial: torch.Tensor | None = None, bn: int | None = None, bm: int | None = None,
-           defer_reduce: bool = False):
+           defer_reduce: bool = False, stages: int | None = None):
     """y = x @ w^T (bf16). Decode-bucket shapes (M a multiple of 64, <= 256) run on the
     gfx950 gemm_decode kernel when it beats hipBLASLt for the shape (tuned table);
     everything else (prefill, odd shapes, CPU) on hipBLASLt / torch."""
@@ -241,13 +242,14 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None, sp
     if plan is None:
         return F.linear(x, w, out=out) if out is not None else F.linear(x, w)
     bm, bn, S = bm or plan[0], bn or plan[1], splits or plan[2]
+    ns = stages or (plan[3] if len(plan) > 3 else 3)
     if S > 1 and (partial is None or partial.numel() < S * M * N):
         partial = torch.empty(S * M * N, dtype=torch.float32, device=x.device)
     if defer_reduce and S > 1 and out is None:
-        kernels().gemm_decode(x, w, None, partial, S, bn, bm, False)
+        kernels().gemm_decode(x, w, None, partial, S, bn, bm, False, False, ns)
         return SplitK(partial, S, M, N)
     y = out if out is not None else torch.empty(M, N, dtype=x.dtype, device=x.device)
-    kernels().gemm_decode(x, w, y, partial if S > 1 else None, S, bn, bm, False)
+    kernels().gemm_decode(x, w, y, partial if S > 1 else None, S, bn, bm, False, False, ns)
     return y
 
 

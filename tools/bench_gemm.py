@@ -73,16 +73,18 @@ for M in [int(x) for x in a.m.split(",")]:
             for bm in (64, 128, 256):
                 for bn in (64, 128):
                     for S in (1, 2, 4, 8):
-                        if bm > M or K % (64 * S) or N % bn:
-                            continue
-                        got = ops.linear(x, ws[name][0], out=y, splits=S, partial=part, bn=bn, bm=bm).float()
-                        err = (got - ref).abs().max().item()
-                        if err > 0.1:
-                            print("BAD", name, M, bm, bn, S, err, flush=True)
-                            continue
-                        key = f"m{bm}n{bn}s{S}"
-                        res[key] = timeit(lambda w: ops.linear(x, w, out=y, splits=S, partial=part, bn=bn, bm=bm),
-                                          ws[name])
+                        for ns in ((2, 3) if bm <= 128 else (3,)):
+                            if bm > M or K % (64 * S) or N % bn:
+                                continue
+                            got = ops.linear(x, ws[name][0], out=y, splits=S, partial=part, bn=bn, bm=bm,
+                                             stages=ns).float()
+                            err = (got - ref).abs().max().item()
+                            if err > 0.1:
+                                print("BAD", name, M, bm, bn, S, ns, err, flush=True)
+                                continue
+                            key = f"m{bm}n{bn}s{S}x{ns}"
+                            res[key] = timeit(lambda w: ops.linear(x, w, out=y, splits=S, partial=part, bn=bn, bm=bm,
+                                                                   stages=ns), ws[name])
         if a.fp8:
             # enough quantized copies (>= 1 GB) that nothing is served from the MALL
             n8 = max(1, min(16, -(-(1 << 30) // (N * K))))
@@ -102,8 +104,9 @@ for M in [int(x) for x in a.m.split(",")]:
             # the custom kernel must win by >= 3 % to displace hipBLASLt (noise margin)
             if best != "hipblaslt" and times[best] < 0.97 * times["hipblaslt"]:
                 bm_, rest = best[1:].split("n")
-                bn_, s_ = rest.split("s")
-                table[f"{M},{N},{K}"] = [int(bm_), int(bn_), int(s_)]
+                bn_, rest = rest.split("s")
+                s_, ns_ = rest.split("x")
+                table[f"{M},{N},{K}"] = [int(bm_), int(bn_), int(s_), int(ns_)]
             else:
                 table[f"{M},{N},{K}"] = "blas"
                 best = "hipblaslt"
@@ -121,11 +124,12 @@ for M in [int(x) for x in a.m.split(",")]:
         res = {"blas+silu": timeit(lambda w: ops.silu_mul(F.linear(x, w), block=64), ws["gate_up"])}
         yo = torch.empty(M, N // 2, device="cuda", dtype=torch.bfloat16)
         for bm in (64, 128, 256):
-            if bm <= M:
-                res[f"fused_m{bm}"] = timeit(lambda w: ops.kernels().gemm_decode(x, w, yo, None, 1, 128, bm, True),
-                                             ws["gate_up"])
+            for ns in ((2, 3) if bm == 64 else (3,)):
+                if bm <= M:
+                    res[f"fused_m{bm}x{ns}"] = timeit(
+                        lambda w: ops.kernels().gemm_decode(x, w, yo, None, 1, 128, bm, True, False, ns), ws["gate_up"])
         best = min(res, key=res.get)
-        table[f"silu,{M},{N},{K}"] = ([int(best.split("_m")[1])] if best != "blas+silu" and
+        table[f"silu,{M},{N},{K}"] = ([int(v) for v in best.split("_m")[1].split("x")] if best != "blas+silu" and
                                       res[best] < 0.97 * res["blas+silu"] else "blas")
         print(json.dumps({"M": M, "gemm": "gate_up+silu", "best": best,
                           **{k: round(v, 1) for k, v in res.items()}}), flush=True)
