@@ -6,8 +6,8 @@ PY ?= python
 build:            ## compile csrc/kernels/*.hip for gfx950 + the host C++ modules, in-tree
 	$(PY) -m operator_amd._build -v
 
-build-asan:       ## host C++ (pattern compiler / packer / scorer) with ASan + UBSan
-	OAMD_SANITIZE=1 $(PY) -m operator_amd._build -v -f
+build-asan:       ## host C++ (pattern compiler / packer / scorer) with ASan + UBSan, fuzzed in a child process
+	$(PY) -m pytest tests/test_sanitizers.py -q
 
 test:             ## CPU tier (no GPU): controllers, patterns, reference ops, TP/DP over gloo, engine pool
 	$(PY) -m pytest tests/ -x -q -m "not gpu"

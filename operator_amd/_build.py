@@ -67,10 +67,14 @@ def _torch_flags():
     return inc, libdirs, abi, torch_lib
 
 
-def build_patterns(verbose: bool = False, force: bool = False) -> Path:
+def build_patterns(verbose: bool = False, force: bool = False, out_dir: Path | None = None,
+                   sanitize: bool | None = None) -> Path:
+    """Host C++ module. ``sanitize`` (default: $OAMD_SANITIZE) adds ASan + UBSan —
+    build it into ``out_dir`` and load it with libasan preloaded (tests/test_sanitizers.py)."""
     import pybind11
 
-    out = PKG / f"_patterns{_ext_suffix()}"
+    out = (Path(out_dir) if out_dir else PKG) / f"_patterns{_ext_suffix()}"
+    sanitize = bool(os.environ.get("OAMD_SANITIZE")) if sanitize is None else sanitize
     srcs = sorted((CSRC / "patterns").glob("*.cpp"))
     hdr = _newest_header_mtime()
     if not force and out.exists() and all(out.stat().st_mtime >= s.stat().st_mtime for s in srcs) \
@@ -79,8 +83,8 @@ def build_patterns(verbose: bool = False, force: bool = False) -> Path:
     cmd = [CXX, "-O3", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", "-pthread",
            f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}", f"-I{CSRC}",
            *map(str, srcs), "-o", str(out)]
-    if os.environ.get("OAMD_SANITIZE"):
-        cmd[1:1] = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-g"]
+    if sanitize:
+        cmd[1:1] = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-g", "-O1"]
     _run(cmd, verbose)
     return out
 
