@@ -54,6 +54,10 @@ class WatchCfg(BaseModel):
     restart_delay_s: float = 5.0
     include_last_state: bool = False  # treat lastState.terminated (CrashLoopBackOff) as a failure
     include_init_containers: bool = False
+    # Q11: the reference fetches the default container's whole current log
+    log_container: Optional[str] = None     # a fixed container name instead of the default one
+    log_previous: bool = False              # the previous (crashed) instance's log
+    log_limit_bytes: Optional[int] = None   # tail bytes cap (None = whole log, as the reference)
     dedupe_max_entries: int = 100_000
     dedupe_ttl_s: float = 7 * 24 * 3600
 

@@ -74,7 +74,8 @@ class Operator:
         self.matcher = match_service
         self.explainer = explain_service
         self.pipeline = AnalysisPipeline(kube, self.matcher, self.explainer, self.events, self.storage, self.status,
-                                         self.pool, self.metrics)
+                                         self.pool, self.metrics, log_container=s.watch.log_container,
+                                         log_previous=s.watch.log_previous, log_limit_bytes=s.watch.log_limit_bytes)
         self.deduper = FailureDeduper(s.watch.dedupe_max_entries, s.watch.dedupe_ttl_s)
         self.sync = PatternSync(s.patterns.cache_dir)
         self._make_workers()
