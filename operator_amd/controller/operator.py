@@ -110,10 +110,11 @@ class Operator:
             if getattr(self, "_workers_used", False):  # re-elected after a loss: fresh watch state
                 self._make_workers()
             self._workers_used = True
+            # watch before the controllers' first reconcile pass, so a failure is seen by one or the other
             self.monitors.start()
+            self.watcher.start()
             for c in self.controllers:
                 c.start()
-            self.watcher.start()
             self._workers_running = True
 
     def _stop_workers(self) -> None:
@@ -128,7 +129,7 @@ class Operator:
 
     @property
     def is_leader(self) -> bool:
-        return self.elector.leading if self.elector is not None else self._workers_running
+        return self._workers_running and (self.elector is None or self.elector.leading)
 
     # ------------------------------------------------------------------ patterns
     def reload_patterns(self) -> int:

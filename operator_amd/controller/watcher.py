@@ -121,7 +121,17 @@ class PodFailureWatcher:
         self._stop.clear()
         targets: list[str | None] = list(self.allowed) if self.allowed else [None]
         for ns in targets:
-            t = threading.Thread(target=self._run_watch, args=(ns,), name=f"pod-watch-{ns or 'all'}", daemon=True)
+            # open the first watch here, not in the thread: once start() returns, no pod update is missed
+            # (a new leader's reconcile pass covers failures that happened before it)
+            first = None
+            try:
+                first = self.kube.watch(PODS, ns, resource_version=self._rv.get(ns))
+                with self._lock:
+                    self._watches.append(first)
+            except (ApiError, OSError) as e:
+                log.error("Pod watcher could not start: %s", e)
+            t = threading.Thread(target=self._run_watch, args=(ns, first), name=f"pod-watch-{ns or 'all'}",
+                                 daemon=True)
             t.start()
             self._threads.append(t)
 
@@ -135,14 +145,15 @@ class PodFailureWatcher:
             except Exception:  # noqa: BLE001
                 pass
 
-    def _run_watch(self, ns: str | None) -> None:
+    def _run_watch(self, ns: str | None, first=None) -> None:
         delay = self.restart_delay_s
         while not self._stop.is_set():
-            w = None
+            w, first = first, None
             try:
-                w = self.kube.watch(PODS, ns, resource_version=self._rv.get(ns))
-                with self._lock:
-                    self._watches.append(w)
+                if w is None:
+                    w = self.kube.watch(PODS, ns, resource_version=self._rv.get(ns))
+                    with self._lock:
+                        self._watches.append(w)
                 delay = self.restart_delay_s
                 for typ, pod in w:
                     self._rv[ns] = (pod.get("metadata") or {}).get("resourceVersion", self._rv.get(ns))

@@ -87,10 +87,18 @@ def selector_is_empty(sel: Mapping[str, Any] | None) -> bool:
     return not sel or (not sel.get("matchLabels") and not sel.get("matchExpressions"))
 
 
+def as_selector(sel: Mapping[str, Any] | None) -> Mapping[str, Any] | None:
+    """A LabelSelector as is; a plain {label: value} map as its matchLabels."""
+    if sel and "matchLabels" not in sel and "matchExpressions" not in sel:
+        return {"matchLabels": dict(sel)}
+    return sel
+
+
 def match_selector(sel: Mapping[str, Any] | None, labels: Mapping[str, str] | None) -> bool:
     """Full metav1.LabelSelector semantics (matchLabels AND matchExpressions).
     An empty/absent selector matches everything here; callers decide policy."""
     labels = labels or {}
+    sel = as_selector(sel)
     if not sel:
         return True
     if not match_labels(sel.get("matchLabels"), labels):
@@ -102,6 +110,7 @@ _SET_RE = re.compile(r"^\s*([A-Za-z0-9_./-]+)\s+(in|notin)\s+\(([^)]*)\)\s*$")
 
 
 def selector_to_string(sel: Mapping[str, Any] | None) -> str:
+    sel = as_selector(sel)
     if not sel:
         return ""
     parts = [f"{k}={v}" for k, v in sorted((sel.get("matchLabels") or {}).items())]

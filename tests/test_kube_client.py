@@ -1,0 +1,156 @@
+"""The HTTPS kube client against the FakeKube REST server (wire level), the
+operator running over it end to end, the compat REST server, and the CLI."""
+import json
+import subprocess
+import sys
+import threading
+import time
+
+import httpx
+import pytest
+
+from operator_amd.config import load_settings
+from operator_amd.controller.operator import Operator
+from operator_amd.engine.match import MatchEngine
+from operator_amd.engine.server import CompatServer
+from operator_amd.engine.service import EchoExplainService, LocalMatchService
+from operator_amd.kube.client import KubeClient, KubeConfig
+from operator_amd.kube.fake import FakeKube, failed_pod, running_pod
+from operator_amd.kube.fake_server import FakeKubeServer
+from operator_amd.kube.resources import EVENTS, PODMORTEMS, PODS, ApiError, WatchClosed
+from operator_amd.patterns.synth import catalog_library
+
+
+def wait_for(fn, timeout=20.0):
+    end = time.time() + timeout
+    while time.time() < end:
+        v = fn()
+        if v:
+            return v
+        time.sleep(0.02)
+    raise AssertionError("timed out")
+
+
+@pytest.fixture
+def server():
+    fk = FakeKube()
+    srv = FakeKubeServer(fk).start()
+    kc = KubeClient(KubeConfig(srv.url, token="test-token"), timeout_s=10)
+    yield fk, srv, kc
+    srv.stop()
+
+
+def test_verbs_over_http(server):
+    fk, srv, kc = server
+    p = kc.create(PODS, running_pod("web-1", labels={"app": "x", "tier": "a"}))
+    assert p["metadata"]["name"] == "web-1" and p["metadata"]["resourceVersion"]
+    kc.create(PODS, running_pod("web-2", labels={"app": "y"}))
+    assert kc.get(PODS, "web-1", "default")["kind"] == "Pod"
+    assert kc.get(PODS, "nope", "default") is None
+    assert [o["metadata"]["name"] for o in kc.list(PODS, "default", label_selector={"app": "x"})] == ["web-1"]
+    assert [o["metadata"]["name"] for o in kc.list(PODS, "default", label_selector="app in (x,y)")] == \
+        ["web-1", "web-2"]
+    # optimistic concurrency: a stale resourceVersion gets 409
+    stale = kc.get(PODS, "web-1", "default")
+    fresh = kc.get(PODS, "web-1", "default")
+    fresh["metadata"].setdefault("annotations", {})["a"] = "1"
+    kc.replace(PODS, fresh)
+    stale["metadata"].setdefault("annotations", {})["a"] = "2"
+    with pytest.raises(ApiError) as e:
+        kc.replace(PODS, stale)
+    assert e.value.code == 409
+    kc.patch(PODS, "web-1", "default", {"metadata": {"annotations": {"b": "2"}}})
+    ann = kc.get(PODS, "web-1", "default")["metadata"]["annotations"]
+    assert ann == {"a": "1", "b": "2"}
+    pm = kc.create(PODMORTEMS, {"metadata": {"name": "m", "namespace": "default"},
+                                "spec": {"podSelector": {"matchLabels": {"app": "x"}}}})
+    kc.patch_status(PODMORTEMS, "m", "default", {"phase": "Ready"})
+    assert kc.get(PODMORTEMS, "m", "default")["status"]["phase"] == "Ready"
+    assert pm["kind"] == "Podmortem"
+    fk.set_log("default", "web-1", b"line1\nline2\n")
+    assert kc.pod_log("web-1", "default") == "line1\nline2\n"
+    assert kc.delete(PODS, "web-2", "default")
+    assert kc.get(PODS, "web-2", "default") is None
+
+
+def test_watch_stream_and_close(server):
+    fk, srv, kc = server
+    w = kc.watch(PODS, "default")
+    got = []
+
+    def reader():
+        try:
+            for typ, obj in w:
+                got.append((typ, obj["metadata"]["name"]))
+        except WatchClosed:
+            got.append(("CLOSED", ""))
+
+    t = threading.Thread(target=reader, daemon=True)
+    t.start()
+    time.sleep(0.2)
+    fk.create(PODS, running_pod("a"))
+    cur = fk.get(PODS, "a", "default")
+    cur["status"] = failed_pod("a")["status"]
+    fk.replace(PODS, cur)
+    fk.delete(PODS, "a", "default")
+    wait_for(lambda: len(got) >= 3)
+    assert [g[0] for g in got[:3]] == ["ADDED", "MODIFIED", "DELETED"]
+    fk.fail_watches("boom")
+    wait_for(lambda: got and got[-1][0] == "CLOSED")
+
+
+def test_operator_end_to_end_over_http(server, tmp_path):
+    fk, srv, kc = server
+    s = load_settings(env={}, overrides={"patterns.cache_dir": str(tmp_path / "p"), "health.enabled": False,
+                                         "watch.restart_delay_s": 0.05})
+    op = Operator(kc, s, match_service=LocalMatchService(MatchEngine(catalog_library(), device="cpu"), max_wait_ms=1),
+                  explain_service=EchoExplainService()).start(http=False)
+    try:
+        kc.create(PODMORTEMS, {"metadata": {"name": "mon", "namespace": "default"},
+                               "spec": {"podSelector": {"matchLabels": {"app": "demo"}}, "aiAnalysisEnabled": False}})
+        wait_for(lambda: op.monitors.list())
+        kc.create(PODS, running_pod("api-1", labels={"app": "demo"}))
+        fk.set_log("default", "api-1", b"boot\njava.lang.OutOfMemoryError: Java heap space\n")
+        cur = kc.get(PODS, "api-1", "default")
+        cur["status"] = failed_pod("api-1", finished_at="2025-08-29T10:00:00Z")["status"]
+        kc.replace(PODS, cur)
+        pod = wait_for(lambda: (lambda p: p if "podmortem.io/analysis" in (p["metadata"].get("annotations") or {})
+                                else None)(kc.get(PODS, "api-1", "default")))
+        assert pod["metadata"]["annotations"]["podmortem.io/severity"] in ("CRITICAL", "HIGH")
+        wait_for(lambda: any(e["reason"] == "PodmortemAnalysisComplete" for e in kc.list(EVENTS, "default")))
+    finally:
+        op.stop()
+
+
+def test_compat_server_contracts():
+    matcher = LocalMatchService(MatchEngine(catalog_library(), device="cpu"), max_wait_ms=1)
+    srv = CompatServer(matcher, EchoExplainService(), "127.0.0.1", 0).start()
+    try:
+        base = f"http://127.0.0.1:{srv.port}"
+        body = {"pod": failed_pod("p"), "logs": "start\nOOMKilled: container exceeded memory limit\n", "events": []}
+        r = httpx.post(base + "/parse", json=body, timeout=30)
+        assert r.status_code == 200
+        res = r.json()
+        assert res["summary"]["highestSeverity"] in ("CRITICAL", "HIGH") and res["events"]
+        r2 = httpx.post(base + "/api/v1/analysis/analyze",
+                        json={"analysisResult": res, "providerConfig": {"providerId": "echo", "maxTokens": 50}},
+                        timeout=30)
+        assert r2.status_code == 200 and r2.json()["explanation"]
+        assert httpx.get(base + "/q/health/ready").json()["status"] == "UP"
+        assert httpx.post(base + "/nope", json={}).status_code == 404
+    finally:
+        srv.stop()
+
+
+def test_cli_manifests_and_scan(tmp_path):
+    r = subprocess.run([sys.executable, "-m", "operator_amd", "manifests", "--replicas", "2"], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0 and "kind: CustomResourceDefinition" in r.stdout
+    assert "PODMORTEM_OPERATOR__LEADER_ELECTION" in r.stdout
+    log = tmp_path / "pod.log"
+    log.write_text("hello\njava.lang.OutOfMemoryError: Java heap space\nbye\n")
+    r = subprocess.run([sys.executable, "-m", "operator_amd", "scan", str(log), "--device", "cpu"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads(r.stdout)
+    assert out[0]["summary"]["highestSeverity"] in ("CRITICAL", "HIGH")
