@@ -292,6 +292,7 @@ void sample(const at::Tensor& logits, const at::Tensor& temperature, const at::T
 }  // namespace
 
 void register_scan_bindings(pybind11::module_& m);
+void register_comm_bindings(pybind11::module_& m);
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "operator_amd gfx950 kernels";
@@ -319,5 +320,6 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("positions"), pybind11::arg("out"), pybind11::arg("col_offset") = 0,
         pybind11::arg("out_val") = pybind11::none());
   register_scan_bindings(m);
+  register_comm_bindings(m);
   m.attr("ARCH") = "gfx950";
 }

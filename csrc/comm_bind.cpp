@@ -1,0 +1,105 @@
+// Binding for the one-shot IPC all-reduce (csrc/kernels/allreduce.hip):
+// operator_amd._C.CustomAllReduce. The handle exchange itself happens in
+// Python over the process group (operator_amd/parallel/custom_ar.py); this
+// object owns the local fine-grained buffer and the opened peer mappings.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+
+#include <string>
+#include <vector>
+
+#include "kernels/kernels.h"
+
+namespace {
+
+class CustomAllReduce {
+ public:
+  CustomAllReduce(int64_t cap_bytes, int64_t rank, int64_t world, int64_t blocks, int64_t device)
+      : cap_(cap_bytes), rank_(rank), world_(world), blocks_(blocks), device_(device) {
+    TORCH_CHECK(world >= 1 && world <= 8, "CustomAllReduce: world must be 1..8");
+    TORCH_CHECK(rank >= 0 && rank < world, "CustomAllReduce: bad rank");
+    TORCH_CHECK(cap_bytes > 0 && cap_bytes % 16 == 0, "CustomAllReduce: capacity must be a positive multiple of 16 B");
+    TORCH_CHECK(blocks >= 1 && blocks <= 64, "CustomAllReduce: blocks must be 1..64");
+    const c10::hip::HIPGuardMasqueradingAsCUDA g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device));
+    char h[64];
+    const int rc = oamd::car_alloc((size_t)cap_bytes, (int)world, &base_, h);
+    TORCH_CHECK(rc == 0, "CustomAllReduce: buffer allocation / IPC export failed rc=", rc);
+    handle_.assign(h, 64);
+    bases_.assign(world, nullptr);
+    bases_[rank] = base_;
+  }
+  ~CustomAllReduce() { close(); }
+
+  pybind11::bytes handle() const { return pybind11::bytes(handle_); }
+
+  void open(const std::vector<std::string>& handles) {
+    TORCH_CHECK((int64_t)handles.size() == world_, "CustomAllReduce.open: need one handle per rank");
+    const c10::hip::HIPGuardMasqueradingAsCUDA g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device_));
+    for (int64_t p = 0; p < world_; ++p) {
+      if (p == rank_) continue;
+      TORCH_CHECK(handles[p].size() == 64, "CustomAllReduce.open: handle of rank ", p, " is not 64 bytes");
+      void* ptr = nullptr;
+      const int rc = oamd::car_open(handles[p].data(), &ptr);
+      TORCH_CHECK(rc == 0, "CustomAllReduce.open: hipIpcOpenMemHandle of rank ", p, " failed rc=", rc);
+      bases_[p] = ptr;
+    }
+    opened_ = true;
+  }
+
+  void all_reduce(const at::Tensor& in, at::Tensor& out) {
+    TORCH_CHECK(opened_ || world_ == 1, "CustomAllReduce: open() the peer handles first");
+    TORCH_CHECK(in.is_cuda() && out.is_cuda() && in.device().index() == device_, "tensors must be on this device");
+    TORCH_CHECK(in.is_contiguous() && out.is_contiguous(), "tensors must be contiguous");
+    TORCH_CHECK(in.scalar_type() == out.scalar_type() && in.numel() == out.numel(), "in/out mismatch");
+    TORCH_CHECK(in.scalar_type() == at::kBFloat16 || in.scalar_type() == at::kFloat, "dtype must be bf16 or fp32");
+    const int64_t bytes = in.numel() * in.element_size();
+    TORCH_CHECK(bytes % 16 == 0 && bytes <= cap_, "size must be a multiple of 16 B and <= capacity");
+    const c10::hip::HIPGuardMasqueradingAsCUDA g(in.device());
+    const int rc = oamd::car_all_reduce(in.data_ptr(), out.data_ptr(), bytes, in.scalar_type() == at::kBFloat16,
+                                        (int)rank_, (int)world_, bases_.data(), (size_t)cap_, (int)blocks_,
+                                        c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream());
+    TORCH_CHECK(rc == 0, "one-shot all-reduce launch failed rc=", rc);
+  }
+
+  int64_t error(bool clear) {
+    const c10::hip::HIPGuardMasqueradingAsCUDA g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device_));
+    return oamd::car_error(base_, clear ? 1 : 0);
+  }
+
+  void close() {
+    if (base_ == nullptr) return;
+    const c10::hip::HIPGuardMasqueradingAsCUDA g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device_));
+    (void)hipDeviceSynchronize();
+    for (int64_t p = 0; p < world_; ++p)
+      if (p != rank_ && bases_[p] != nullptr) (void)oamd::car_close(bases_[p]);
+    (void)oamd::car_free(base_);
+    base_ = nullptr;
+    bases_.assign(world_, nullptr);
+    opened_ = false;
+  }
+
+  int64_t capacity() const { return cap_; }
+
+ private:
+  int64_t cap_, rank_, world_, blocks_, device_;
+  void* base_ = nullptr;
+  std::string handle_;
+  std::vector<void*> bases_;
+  bool opened_ = false;
+};
+
+}  // namespace
+
+void register_comm_bindings(pybind11::module_& m) {
+  pybind11::class_<CustomAllReduce>(m, "CustomAllReduce")
+      .def(pybind11::init<int64_t, int64_t, int64_t, int64_t, int64_t>(), pybind11::arg("cap_bytes"),
+           pybind11::arg("rank"), pybind11::arg("world"), pybind11::arg("blocks"), pybind11::arg("device"))
+      .def("handle", &CustomAllReduce::handle)
+      .def("open", &CustomAllReduce::open)
+      .def("all_reduce", &CustomAllReduce::all_reduce)
+      .def("error", &CustomAllReduce::error, pybind11::arg("clear") = false)
+      .def("close", &CustomAllReduce::close)
+      .def_property_readonly("capacity", &CustomAllReduce::capacity);
+}

@@ -1,0 +1,218 @@
+// One-shot all-reduce over peer-mapped HBM.
+//
+// Tensor-parallel decode all-reduces are small (M x hidden x 2 B: 16 KB per
+// token at 70B) and latency-bound. A ring all-reduce over xGMI takes
+// 2 (n - 1) dependent link hops; here every rank PUSHES its whole input into
+// a per-source slot of every peer's receive buffer (one hop over the direct
+// point-to-point link to each peer; the 7 links of an MI355X run in
+// parallel), raises a per-block flag in each peer, waits for the flags of all
+// peers and reduces the n slots from its OWN HBM. One kernel, one fabric hop.
+//
+// Memory: each rank owns one fine-grained (uncached) allocation, exported
+// with hipIpcGetMemHandle and opened by every peer:
+//   [0, 2 KB)        flags[kMaxBlocks][kMaxRanks]  u32, written by peers
+//   [8 KB, 8 KB+256) rounds[kMaxBlocks]            u32, this rank's per-block call counter
+//   [12 KB]          err                           u32, set when a wait times out
+//   [64 KB, ...)     recv[2][world][cap]           parity-double-buffered slots
+// Ordering (cdna_hip_programming.md Guideline 16, at SYSTEM scope because the
+// producer is another device): data stores -> __threadfence_system ->
+// barrier -> release store of the flag into the peer; the consumer's acquire
+// load of its flag invalidates its caches before it reads the slots.
+// Round numbers are per block and kept on the device, so a call is a pure
+// kernel launch (capturable into a hipGraph) and ranks never exchange host
+// state per call. Parity buffers make slot reuse safe: a peer can be at most
+// one round ahead (it needs this rank's flag of round r+1 to finish r+1, and
+// that flag is raised only after this rank finished reading round r).
+// Every wait is bounded (wall clock, ~2 s): a missing peer sets `err` and the
+// kernel drains instead of spinning forever.
+#include <cstring>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace oamd {
+
+namespace car {
+constexpr int kMaxRanks = 8;
+constexpr int kMaxBlocks = 64;
+constexpr int kThreads = 512;
+constexpr size_t kFlagsOff = 0;
+constexpr size_t kRoundsOff = 8 << 10;
+constexpr size_t kErrOff = 12 << 10;
+constexpr size_t kDataOff = 64 << 10;
+constexpr uint64_t kTimeoutTicks = 200000000ull;  // wall_clock64 runs at 100 MHz: 2 s
+}  // namespace car
+
+struct CarPeers {
+  char* base[car::kMaxRanks];
+};
+
+__device__ __forceinline__ void acc8(float* a, uint4 v, bool is_bf16) {
+  if (is_bf16) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      a[2 * i] += __uint_as_float(w[i] << 16);
+      a[2 * i + 1] += __uint_as_float(w[i] & 0xffff0000u);
+    }
+  } else {
+    a[0] += __uint_as_float(v.x);
+    a[1] += __uint_as_float(v.y);
+    a[2] += __uint_as_float(v.z);
+    a[3] += __uint_as_float(v.w);
+  }
+}
+
+// One 16-B vector = 8 bf16 or 4 fp32 elements.
+template <int W, bool BF16>
+__global__ void __launch_bounds__(car::kThreads) oneshot_allreduce_kernel(const uint4* __restrict__ in,
+                                                                          uint4* __restrict__ out, int64_t nvec,
+                                                                          int64_t capvec, int rank, CarPeers peers) {
+  __shared__ uint32_t s_round;
+  __shared__ uint32_t s_err;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  char* mine = peers.base[rank];
+  uint32_t* rounds = reinterpret_cast<uint32_t*>(mine + car::kRoundsOff);
+  if (tid == 0) {
+    s_round = rounds[b] + 1;
+    s_err = 0;
+  }
+  __syncthreads();
+  const uint32_t round = s_round;
+  const int par = round & 1;
+  const int64_t per = (nvec + gridDim.x - 1) / gridDim.x;
+  const int64_t v0 = min(nvec, per * b), v1 = min(nvec, v0 + per);
+
+  // ---- push: my slice of `in` into slot [par][rank] of every rank (me included)
+  for (int64_t v = v0 + tid; v < v1; v += car::kThreads) {
+    const uint4 x = in[v];
+#pragma unroll
+    for (int p = 0; p < W; ++p) {
+      uint4* dst = reinterpret_cast<uint4*>(peers.base[p] + car::kDataOff) + ((int64_t)par * W + rank) * capvec;
+      dst[v] = x;
+    }
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (tid < W) {
+    uint32_t* f = reinterpret_cast<uint32_t*>(peers.base[tid] + car::kFlagsOff) + b * car::kMaxRanks + rank;
+    __hip_atomic_store(f, round, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  // ---- wait for every peer's slice of this block (bounded)
+  if (tid < W) {
+    uint32_t* f = reinterpret_cast<uint32_t*>(mine + car::kFlagsOff) + b * car::kMaxRanks + tid;
+    const uint64_t t0 = (uint64_t)wall_clock64();
+    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < round) {
+      __builtin_amdgcn_s_sleep(2);
+      if ((uint64_t)wall_clock64() - t0 > car::kTimeoutTicks) {
+        s_err = 1;
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  if (s_err) {
+    if (tid == 0) {
+      __hip_atomic_store(reinterpret_cast<uint32_t*>(mine + car::kErrOff), 1u, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+      rounds[b] = round;
+    }
+    return;
+  }
+  // ---- reduce the W slots from local HBM, fp32 accumulation in rank order
+  const uint4* slots = reinterpret_cast<const uint4*>(mine + car::kDataOff) + (int64_t)par * W * capvec;
+  for (int64_t v = v0 + tid; v < v1; v += car::kThreads) {
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    uint4 x[W];
+#pragma unroll
+    for (int p = 0; p < W; ++p) x[p] = slots[(int64_t)p * capvec + v];
+#pragma unroll
+    for (int p = 0; p < W; ++p) acc8(a, x[p], BF16);
+    uint4 o;
+    if (BF16) {
+      o.x = pack_bf2(a[0], a[1]);
+      o.y = pack_bf2(a[2], a[3]);
+      o.z = pack_bf2(a[4], a[5]);
+      o.w = pack_bf2(a[6], a[7]);
+    } else {
+      o.x = __float_as_uint(a[0]);
+      o.y = __float_as_uint(a[1]);
+      o.z = __float_as_uint(a[2]);
+      o.w = __float_as_uint(a[3]);
+    }
+    out[v] = o;
+  }
+  if (tid == 0) rounds[b] = round;
+}
+
+// ------------------------------------------------------------------ host side
+
+size_t car_buffer_bytes(size_t cap_bytes, int world) { return car::kDataOff + 2 * (size_t)world * cap_bytes; }
+
+int car_alloc(size_t cap_bytes, int world, void** base, void* handle_out) {
+  if (world < 1 || world > car::kMaxRanks || cap_bytes % 16 != 0) return -1;
+  const size_t bytes = car_buffer_bytes(cap_bytes, world);
+  hipError_t e = hipExtMallocWithFlags(base, bytes, hipDeviceMallocUncached);
+  if (e != hipSuccess) return (int)e;
+  e = hipMemset(*base, 0, car::kDataOff);
+  if (e != hipSuccess) return (int)e;
+  e = hipDeviceSynchronize();
+  if (e != hipSuccess) return (int)e;
+  hipIpcMemHandle_t h;
+  e = hipIpcGetMemHandle(&h, *base);
+  if (e != hipSuccess) return (int)e;
+  std::memcpy(handle_out, &h, sizeof(h));
+  return 0;
+}
+
+int car_open(const void* handle, void** ptr) {
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle, sizeof(h));
+  return (int)hipIpcOpenMemHandle(ptr, h, hipIpcMemLazyEnablePeerAccess);
+}
+
+int car_close(void* ptr) { return (int)hipIpcCloseMemHandle(ptr); }
+
+int car_free(void* base) { return (int)hipFree(base); }
+
+int car_error(void* base, int clear) {
+  uint32_t v = 0;
+  char* p = static_cast<char*>(base) + car::kErrOff;
+  if (hipMemcpy(&v, p, 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  if (clear && v && hipMemset(p, 0, 4) != hipSuccess) return -1;
+  return (int)v;
+}
+
+int car_all_reduce(const void* in, void* out, int64_t bytes, bool bf16, int rank, int world, void* const* bases,
+                   size_t cap_bytes, int blocks, hipStream_t stream) {
+  if (world < 1 || world > car::kMaxRanks || rank < 0 || rank >= world) return -1;
+  if (bytes % 16 != 0 || (size_t)bytes > cap_bytes || cap_bytes % 16 != 0) return -2;
+  if (blocks < 1 || blocks > car::kMaxBlocks) return -3;
+  if ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15) return -4;
+  CarPeers peers{};
+  for (int p = 0; p < world; ++p) peers.base[p] = static_cast<char*>(bases[p]);
+  const int64_t nvec = bytes / 16, capvec = cap_bytes / 16;
+  const uint4* i4 = static_cast<const uint4*>(in);
+  uint4* o4 = static_cast<uint4*>(out);
+#define OAMD_CAR(W)                                                                                               \
+  case W:                                                                                                         \
+    if (bf16) oneshot_allreduce_kernel<W, true><<<blocks, car::kThreads, 0, stream>>>(i4, o4, nvec, capvec, rank, peers); \
+    else oneshot_allreduce_kernel<W, false><<<blocks, car::kThreads, 0, stream>>>(i4, o4, nvec, capvec, rank, peers);     \
+    break;
+  switch (world) {
+    OAMD_CAR(1)
+    OAMD_CAR(2)
+    OAMD_CAR(3)
+    OAMD_CAR(4)
+    OAMD_CAR(5)
+    OAMD_CAR(6)
+    OAMD_CAR(7)
+    OAMD_CAR(8)
+    default: return -1;
+  }
+#undef OAMD_CAR
+  OAMD_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace oamd

@@ -50,4 +50,14 @@ int sample_tokens(const void* logits, bool logits_bf16, int64_t stride, int rows
                   const float* temperature, const int64_t* seeds, const int64_t* positions,
                   int64_t* out_tokens, int64_t col_offset, float* out_val, hipStream_t stream);
 
+// One-shot all-reduce over peer-mapped fine-grained buffers (allreduce.hip).
+size_t car_buffer_bytes(size_t cap_bytes, int world);
+int car_alloc(size_t cap_bytes, int world, void** base, void* handle_out /* 64 B hipIpcMemHandle_t */);
+int car_open(const void* handle, void** ptr);
+int car_close(void* ptr);
+int car_free(void* base);
+int car_error(void* base, int clear);
+int car_all_reduce(const void* in, void* out, int64_t bytes, bool bf16, int rank, int world, void* const* bases,
+                   size_t cap_bytes, int blocks, hipStream_t stream);
+
 }  // namespace oamd

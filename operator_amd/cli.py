@@ -126,13 +126,16 @@ def cmd_run(args) -> int:
     s = _settings(args)
     if args.gpus and args.gpus > 1:
         s.engine.gpus = args.gpus
+    if args.tp and args.tp > 1:
+        s.engine.tp = args.tp
+        s.engine.gpus = max(s.engine.gpus, args.tp)
     pool = None
     metrics = Metrics()
     if s.kube.mode == "fake" or args.fake:
         kube = FakeKube()
     else:
         kube = KubeClient.auto(s.kube.mode, s.kube.kubeconfig, s.kube.request_timeout_s)
-    if s.engine.gpus > 1 or s.engine.pool:
+    if s.engine.gpus > 1 or s.engine.pool or s.engine.tp > 1:
         # engines first, before anything in this process could initialise a GPU
         from operator_amd.controller.operator import load_patterns
 
@@ -199,6 +202,8 @@ def main(argv: list[str] | None = None) -> int:
     common(p)
     p.add_argument("--fake", action="store_true", help="in-memory FakeKube instead of a cluster")
     p.add_argument("--gpus", type=int, default=0, help="engine processes, one per GPU (engine.gpus)")
+    p.add_argument("--tp", type=int, default=0,
+                   help="GPUs per explanation-model replica (engine.tp); --gpus 8 --tp 8 = one 70B replica")
     p = sub.add_parser("manifests")
     p.add_argument("--namespace", default="podmortem-system")
     p.add_argument("--image", default="ghcr.io/podmortem/operator-amd:latest")

@@ -100,6 +100,7 @@ class EngineCfg(BaseModel):
     weight_dtype: str = "bfloat16"   # bfloat16 | fp8 (W8A8 e4m3fn projections, e.g. Llama-3-70B)
     device: str = "cuda"
     tp: int = 1
+    oneshot_allreduce_mb: float = 8.0  # TP all-reduces up to this size use the one-shot IPC kernel; 0 = RCCL only
     max_batch: int = 256
     max_prefill_tokens: int = 16384
     max_context: int = 4096

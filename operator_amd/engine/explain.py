@@ -43,7 +43,7 @@ class EngineLoop(threading.Thread):
         super().__init__(name="llm-engine-loop", daemon=True)
         self.llm = llm
         self._cv = threading.Condition()
-        self._stop = False
+        self._stopping = False
         self.error: BaseException | None = None
 
     def notify(self) -> None:
@@ -52,7 +52,7 @@ class EngineLoop(threading.Thread):
 
     def stop(self) -> None:
         with self._cv:
-            self._stop = True
+            self._stopping = True
             self._cv.notify()
 
     def run(self) -> None:
@@ -60,9 +60,12 @@ class EngineLoop(threading.Thread):
             torch.cuda.set_device(self.llm.device)
         while True:
             with self._cv:
-                while not self._stop and not self.llm.has_work():
+                while not self._stopping and not self.llm.has_work():
                     self._cv.wait(timeout=0.5)
-                if self._stop:
+                if self._stopping:
+                    close = getattr(self.llm, "close", None)
+                    if close is not None:   # TP leader: release the followers
+                        close()
                     return
             try:
                 self.llm.step()
@@ -99,8 +102,10 @@ class ExplainEngine:
         if start_loop:
             self.loop.start()
 
-    def close(self) -> None:
+    def close(self, join_s: float = 0.0) -> None:
         self.loop.stop()
+        if join_s and self.loop.is_alive():
+            self.loop.join(join_s)
 
     # ------------------------------------------------------------------ helpers
     def build_prompt(self, result: AnalysisResult, cfg: AIProviderConfig) -> list[int]:

@@ -23,6 +23,9 @@ def build_llm(s: Settings, device: str | torch.device | None = None, tp=None):
     dev = torch.device(device or e.device)
     cfg = get_config(e.model)
     dtype = getattr(torch, e.dtype)
+    if tp is not None and tp.world > 1 and dev.type == "cuda" and e.oneshot_allreduce_mb > 0 \
+            and getattr(tp, "oneshot", None) is None:
+        tp.enable_oneshot(dev, int(e.oneshot_allreduce_mb * (1 << 20)))
     model = LlamaModel(cfg, device=dev, tp=tp, dtype=dtype, weight_dtype=e.weight_dtype)
     if e.model_path:
         model.load_hf(e.model_path)
@@ -31,8 +34,14 @@ def build_llm(s: Settings, device: str | torch.device | None = None, tp=None):
     pages = PagedKVCache.pages_for_budget(int(e.kv_cache_gb * 1e9), cfg.layers, model.hkv, cfg.head_dim,
                                           e.page_size, torch.finfo(dtype).bits // 8)
     kv = PagedKVCache(cfg.layers, pages, model.hkv, cfg.head_dim, e.page_size, device=dev, dtype=dtype)
-    llm = LLMEngine(model, kv, max_batch=e.max_batch, max_prefill_tokens=e.max_prefill_tokens,
-                    max_context=e.max_context, use_graphs=e.use_graphs, multi_step=e.multi_step)
+    kw = dict(max_batch=e.max_batch, max_prefill_tokens=e.max_prefill_tokens, max_context=e.max_context,
+              use_graphs=e.use_graphs, multi_step=e.multi_step)
+    if tp is not None and tp.world > 1:   # one replica over the TP group: lock-stepped engines
+        from operator_amd.engine.tp import TPLLMEngine, control_group
+
+        llm = TPLLMEngine(model, kv, tp_group=tp, ctrl_group=control_group(tp), **kw)
+    else:
+        llm = LLMEngine(model, kv, **kw)
     tok = Tokenizer(cfg.vocab_size, cfg.bos_id, cfg.eos_ids[0],
                     path=(f"{e.model_path}/tokenizer.json" if e.model_path else None))
     log.info("explanation model %s: %.1f GB weights, %d KV pages (%d tokens)", cfg.name,

@@ -43,9 +43,53 @@ class WorkerDied(RuntimeError):
     pass
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
 # ---------------------------------------------------------------- worker process
+def _tp_init(tp_rank: int, tp_world: int, tp_port: int, device: str):
+    """Process group of one TP replica (its own rendezvous port; RCCL on GPUs, gloo on CPU)."""
+    import torch
+    import torch.distributed as dist
+
+    from operator_amd.parallel.comm import Group
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(tp_port)
+    backend = "nccl" if device.startswith("cuda") else "gloo"
+    kw = {}
+    if backend == "nccl":
+        torch.cuda.set_device(torch.device(device))
+        kw["device_id"] = torch.device(device)
+    dist.init_process_group(backend, rank=tp_rank, world_size=tp_world, **kw)
+    return Group()
+
+
+def _follower_main(idx: int, device: str, settings_obj: dict, tp_rank: int, tp_world: int, tp_port: int,
+                   outq) -> None:
+    """Non-leader rank of a TP replica: holds its model shard and mirrors the leader's steps."""
+    logging.basicConfig(level=os.environ.get("PODMORTEM_LOG_LEVEL", "WARNING"))
+    from operator_amd.config import Settings
+    from operator_amd.engine import factory
+
+    s = Settings.model_validate(settings_obj)
+    s.engine.device = device
+    try:
+        tp = _tp_init(tp_rank, tp_world, tp_port, device)
+        _, _, llm, _ = factory.build_llm(s, device=device, tp=tp)
+    except Exception as e:  # noqa: BLE001
+        outq.put(("fatal", idx, f"TP rank {tp_rank}: {type(e).__name__}: {e}"))
+        return
+    llm.follow()
+
+
 def _worker_main(idx: int, device: str, settings_obj: dict, patterns, roles: tuple[str, ...], inq, outq,
-                 heartbeat_s: float) -> None:
+                 heartbeat_s: float, tp_world: int = 1, tp_port: int = 0) -> None:
     logging.basicConfig(level=os.environ.get("PODMORTEM_LOG_LEVEL", "WARNING"))
     from concurrent.futures import ThreadPoolExecutor
 
@@ -58,11 +102,12 @@ def _worker_main(idx: int, device: str, settings_obj: dict, patterns, roles: tup
         s.services.match = "cpu"
     matcher = explainer = None
     try:
+        tp = _tp_init(0, tp_world, tp_port, device) if tp_world > 1 else None
         if "match" in roles:
             matcher = service.LocalMatchService(factory.build_match_engine(s, patterns, device=device),
                                                 s.services.match_max_batch, s.services.match_batch_wait_ms)
         if "explain" in roles:
-            explainer = factory.build_explain_service(s)
+            explainer = factory.build_explain_service(s, tp=tp)
     except Exception as e:  # noqa: BLE001 - reported to the controller, which marks the worker dead
         outq.put(("fatal", idx, f"{type(e).__name__}: {e}"))
         return
@@ -108,13 +153,20 @@ def _worker_main(idx: int, device: str, settings_obj: dict, patterns, roles: tup
     pool.shutdown(wait=True)
     if matcher is not None:
         matcher.close()
+    ee = getattr(explainer, "ee", None)
+    if ee is not None:   # stops the engine loop (a TP leader releases its followers)
+        ee.close(join_s=30.0)
 
 
 # ---------------------------------------------------------------- controller side
 class _Worker:
-    def __init__(self, idx: int, device: str):
+    """One engine replica: a single process, or a TP group (leader = ``proc``, + ``followers``)."""
+
+    def __init__(self, idx: int, device: str, follower_devices: list[str] | None = None):
         self.idx, self.device = idx, device
+        self.follower_devices = list(follower_devices or [])
         self.proc = None
+        self.followers: list = []
         self.inq = None
         self.ready = False
         self.alive = False
@@ -136,7 +188,11 @@ class EnginePool:
         self._ready_cv = threading.Condition(self._lock)
         self._ids = itertools.count()
         self._closing = False
-        self.workers = [_Worker(i, d) for i, d in enumerate(devices)]
+        self.tp = max(1, int(getattr(settings.engine, "tp", 1)))
+        if len(devices) % self.tp:
+            raise ValueError(f"{len(devices)} devices cannot be split into TP groups of {self.tp}")
+        groups = [devices[i:i + self.tp] for i in range(0, len(devices), self.tp)]
+        self.workers = [_Worker(i, g[0], g[1:]) for i, g in enumerate(groups)]
         self.stats = {"requeued": 0, "restarts": 0, "deaths": 0}
         for w in self.workers:
             self._spawn(w)
@@ -149,11 +205,23 @@ class EnginePool:
     def _spawn(self, w: _Worker) -> None:
         w.inq = self._ctx.Queue()
         w.ready, w.alive, w.last_beat = False, True, time.time()
+        world = 1 + len(w.follower_devices)
+        port = _free_port() if world > 1 else 0
+        settings = self.settings.model_dump()
         w.proc = self._ctx.Process(
             target=_worker_main, name=f"engine-{w.idx}",
-            args=(w.idx, w.device, self.settings.model_dump(), self.patterns, self.roles, w.inq, self._outq,
-                  self.heartbeat_s), daemon=True)
+            args=(w.idx, w.device, settings, self.patterns, self.roles, w.inq, self._outq,
+                  self.heartbeat_s, world, port), daemon=True)
+        w.followers = [self._ctx.Process(target=_follower_main, name=f"engine-{w.idx}-tp{r}",
+                                         args=(w.idx, d, settings, r, world, port, self._outq), daemon=True)
+                       for r, d in enumerate(w.follower_devices, start=1)]
         w.proc.start()
+        for f in w.followers:
+            f.start()
+
+    @staticmethod
+    def _procs(w: _Worker) -> list:
+        return [p for p in [w.proc, *w.followers] if p is not None]
 
     def wait_ready(self, timeout: float = 600.0, n: int | None = None) -> int:
         """Block until ``n`` (default: all) workers are ready; returns the ready count."""
@@ -176,11 +244,11 @@ class EnginePool:
                 except (OSError, ValueError):
                     pass
         for w in self.workers:
-            if w.proc is not None:
-                w.proc.join(timeout)
-                if w.proc.is_alive():
-                    w.proc.kill()
-                    w.proc.join(5)
+            for p in self._procs(w):
+                p.join(timeout)
+                if p.is_alive():
+                    p.kill()
+                    p.join(5)
         with self._lock:
             for w in self.workers:
                 for rid, (kind, payload, fut) in list(w.inflight.items()):
@@ -271,12 +339,14 @@ class EnginePool:
             for w in self.workers:
                 if not w.alive or self._closing:
                     continue
-                dead = not w.proc.is_alive()
+                gone = [p for p in self._procs(w) if not p.is_alive()]
                 hung = w.ready and now - w.last_beat > self.heartbeat_timeout_s
-                if dead or hung:
-                    if hung and w.proc.is_alive():
-                        w.proc.kill()
-                    self._on_death(w, "exited with %s" % w.proc.exitcode if dead else "stopped heart-beating")
+                if gone or hung:
+                    for p in self._procs(w):   # a TP replica lives and dies as a whole
+                        if p.is_alive():
+                            p.kill()
+                    self._on_death(w, f"{gone[0].name} exited with {gone[0].exitcode}" if gone
+                                   else "stopped heart-beating")
 
     def _on_death(self, w: _Worker, why: str) -> None:
         with self._lock:
@@ -298,7 +368,8 @@ class EnginePool:
 
     def health(self) -> dict:
         with self._lock:
-            return {"workers": [{"idx": w.idx, "device": w.device, "alive": w.alive, "ready": w.ready,
+            return {"workers": [{"idx": w.idx, "device": w.device, "tp_devices": [w.device, *w.follower_devices],
+                                 "alive": w.alive, "ready": w.ready,
                                  "inflight": len(w.inflight), "restarts": w.restarts} for w in self.workers],
                     **self.stats}
 

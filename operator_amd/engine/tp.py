@@ -1,0 +1,137 @@
+"""Tensor-parallel serving: one LLM engine replica spread over the ranks of a
+TP group (BASELINE config 5 "Llama-3-70B, TP=8 over xGMI").
+
+Every rank holds a column/row shard of the model (models/llama.py) and must
+run the SAME engine steps on the SAME requests: each step's forward has 2
+all-reduces per layer plus the vocab-parallel sampler's all-gather, so a rank
+that admitted a different batch would deadlock or corrupt the collectives.
+
+Scheduling in ``LLMEngine`` is deterministic given the order of submissions
+and cancellations relative to steps, so only those need to be replicated:
+
+* the **leader** (TP rank 0) owns request intake. ``submit``/``cancel`` from
+  any thread only queue; at the top of each ``step`` the leader broadcasts the
+  queued submissions (prompt + sampling params) and cancellations over a small
+  gloo control group, applies them to its own engine, and steps;
+* each **follower** blocks in ``follow()``: receive the step's control message,
+  apply it identically (same request ids by construction), step; a ``None``
+  message ends the loop.
+
+Tokens need no broadcast: the sampler already agrees across ranks (global
+max over vocab shards), so every rank appends the same tokens and retires the
+same requests. The leader steps only when it has work, so idle followers just
+wait in the broadcast. Device-side collectives (RCCL, or the one-shot IPC
+all-reduce of parallel/custom_ar.py for decode-size messages) run inside the
+captured decode graphs exactly as at TP=1.
+"""
+from __future__ import annotations
+
+import threading
+
+import torch.distributed as dist
+
+from .llm import GenRequest, LLMEngine
+
+
+def control_group(tp_group):
+    """A gloo group over the TP ranks for host-side control messages."""
+    ranks = getattr(tp_group, "ranks", None)
+    return dist.new_group(ranks=ranks, backend="gloo")
+
+
+class TPLLMEngine(LLMEngine):
+    def __init__(self, *args, tp_group=None, ctrl_group=None, **kw):
+        super().__init__(*args, **kw)
+        self.tp_group = tp_group
+        self.ctrl = ctrl_group
+        self.leader = tp_group is None or tp_group.rank == 0
+        self._src = tp_group.ranks[0] if tp_group is not None else 0
+        self._pending: list[GenRequest] = []
+        self._cancels: list[GenRequest] = []
+        self._by_rid: dict[int, GenRequest] = {}
+        self._qlock = threading.Lock()
+        self.closed = False
+
+    # ------------------------------------------------------------------ leader API
+    def submit(self, req: GenRequest) -> GenRequest:
+        if not self.leader:
+            raise RuntimeError("requests are submitted to the TP leader (rank 0) only")
+        if not req.prompt:
+            raise ValueError("empty prompt")
+        if len(req.prompt) >= self.max_context:
+            raise ValueError(f"prompt of {len(req.prompt)} tokens exceeds max_context {self.max_context}")
+        with self._qlock:
+            self._pending.append(req)
+        return req
+
+    def cancel(self, req: GenRequest) -> None:
+        with self._qlock:
+            if req in self._pending:   # never broadcast: drop locally
+                self._pending.remove(req)
+                req.done, req.error = True, "cancelled"
+                req.event.set()
+                return
+            self._cancels.append(req)
+
+    def has_work(self) -> bool:
+        return bool(self._pending or self._cancels) or super().has_work()
+
+    def step(self) -> list[GenRequest]:
+        if not self.leader:
+            raise RuntimeError("TP followers step from follow()")
+        with self._qlock:
+            new, canc = self._pending, self._cancels
+            self._pending, self._cancels = [], []
+        msg = [("s", list(r.prompt), r.max_tokens, r.temperature, r.seed, r.ignore_eos) for r in new] + \
+              [("c", r.rid) for r in canc]
+        self._bcast(msg)
+        self._apply(msg, new)
+        return self._step_and_forget()
+
+    def close(self) -> None:
+        """Release the followers (collective over the control group)."""
+        if self.leader and not self.closed and self.tp_group is not None and self.tp_group.world > 1:
+            self._bcast(None)
+        self.closed = True
+
+    # ------------------------------------------------------------------ follower loop
+    def follow(self) -> None:
+        if self.leader:
+            raise RuntimeError("the TP leader does not follow")
+        while True:
+            msg = self._bcast(None)
+            if msg is None:
+                self.closed = True
+                return
+            self._apply(msg, None)
+            self._step_and_forget()
+
+    # ------------------------------------------------------------------ shared
+    def _bcast(self, msg):
+        if self.tp_group is None or self.tp_group.world == 1:
+            return msg
+        box = [msg]
+        dist.broadcast_object_list(box, src=self._src, group=self.ctrl)
+        return box[0]
+
+    def _apply(self, msg, reqs: list[GenRequest] | None) -> None:
+        it = iter(reqs or [])
+        for m in msg:
+            if m[0] == "s":
+                r = next(it) if self.leader else GenRequest(m[1], max_tokens=m[2], temperature=m[3], seed=m[4],
+                                                            ignore_eos=m[5])
+                LLMEngine.submit(self, r)
+                self._by_rid[r.rid] = r
+            else:
+                r = self._by_rid.get(m[1])
+                if r is not None:
+                    LLMEngine.cancel(self, r)
+                    r.cancelled = True
+                    if r.done:   # was still waiting: never reaped
+                        self._by_rid.pop(r.rid, None)
+
+    def _step_and_forget(self) -> list[GenRequest]:
+        fin = LLMEngine.step(self)
+        for r in fin:
+            self._by_rid.pop(r.rid, None)
+        return fin

@@ -72,8 +72,21 @@ class Group:
         g.pg, g.rank, g.world, g.ranks = None, 0, 1, [0]
         return g
 
+    def enable_oneshot(self, device, max_bytes: int | None = None) -> bool:
+        """Route small GPU all-reduces through the one-shot IPC kernel (custom_ar.py).
+        Collective over the group; returns False (RCCL stays in use) on world 1 or CPU."""
+        if self.world <= 1 or torch.device(device).type != "cuda":
+            return False
+        from .custom_ar import DEFAULT_MAX_BYTES, OneShotAllReduce
+
+        self.oneshot = OneShotAllReduce(self, device, max_bytes or DEFAULT_MAX_BYTES)
+        return True
+
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
         if self.world > 1:
+            car = getattr(self, "oneshot", None)
+            if car is not None and car.fits(t):
+                return car.all_reduce_(t)
             dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.pg)
         return t
 

@@ -1,0 +1,70 @@
+"""One-shot all-reduce over peer-mapped HBM for tensor-parallel decode
+(kernel: csrc/kernels/allreduce.hip).
+
+RCCL's ring all-reduce over xGMI takes 2(n-1) dependent link hops; a TP decode
+all-reduce is only M x hidden x 2 B (16 KB per token at 70B), so those hops,
+not bandwidth, set its cost. Here each rank pushes its input straight into a
+slot of every peer's fine-grained receive buffer over the direct link to that
+peer, and reduces the n slots locally: one fabric hop, one kernel, no host
+involvement per call (device-side round counters), so it is capturable in the
+decode hipGraph.
+
+Set-up exchanges the 64-byte hipIpc handles over the process group (any
+backend: gloo in tests, RCCL in production). Above ``max_bytes`` — where
+bandwidth, not hop latency, dominates — ``Group.all_reduce_`` keeps using RCCL.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from operator_amd import ops
+
+DEFAULT_MAX_BYTES = 8 << 20   # 256 tokens x 8192 x 2 B (70B hidden) = 4 MB, with room
+DEFAULT_BLOCKS = 32
+
+
+class OneShotAllReduce:
+    def __init__(self, group, device: torch.device | str, max_bytes: int = DEFAULT_MAX_BYTES,
+                 blocks: int = DEFAULT_BLOCKS):
+        self.group = group
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError("OneShotAllReduce needs a GPU device")
+        self.world, self.rank = group.world, group.rank
+        if self.world > 8:
+            raise ValueError("one-shot all-reduce supports up to 8 ranks (one xGMI-connected node)")
+        self.max_bytes = (int(max_bytes) + 15) // 16 * 16
+        self.ext = ops.kernels().CustomAllReduce(self.max_bytes, self.rank, self.world, int(blocks),
+                                                 self.device.index or 0)
+        handles = [None] * self.world
+        if self.world > 1:
+            dist.all_gather_object(handles, self.ext.handle(), group=group.pg)
+        else:
+            handles = [self.ext.handle()]
+        self.ext.open([bytes(h) for h in handles])
+        self.calls = 0
+
+    def fits(self, t: torch.Tensor) -> bool:
+        nbytes = t.numel() * t.element_size()
+        return (t.is_cuda and t.is_contiguous() and t.dtype in (torch.bfloat16, torch.float32)
+                and nbytes % 16 == 0 and nbytes <= self.max_bytes)
+
+    def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
+        self.ext.all_reduce(t, t)
+        self.calls += 1
+        return t
+
+    def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
+        out = torch.empty_like(t)
+        self.ext.all_reduce(t, out)
+        self.calls += 1
+        return out
+
+    def check(self, clear: bool = True) -> None:
+        """Raise if any call timed out waiting for a peer since the last check."""
+        if self.ext.error(clear):
+            raise RuntimeError("one-shot all-reduce: a peer did not arrive within 2 s")
+
+    def close(self) -> None:
+        self.ext.close()

@@ -1,0 +1,111 @@
+"""One-shot IPC all-reduce (csrc/kernels/allreduce.hip) with 2 ranks.
+
+The gpurun box has one MI355X, so both ranks are processes on the SAME device:
+the kernel's peer path (hipIpc export/open, pushes into the peer's
+fine-grained buffer, system-scope flags) is exercised exactly as across xGMI,
+just over local HBM. The handle exchange runs over a gloo group (RCCL refuses
+two ranks on one device). Reference: fp32 sum of both ranks' inputs, rounded
+once — the kernel accumulates in fp32 in rank order, so results must be exact.
+"""
+import os
+import socket
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _inputs(rank: int, n: int, dtype, call: int) -> torch.Tensor:
+    g = torch.Generator().manual_seed(1000 * rank + 17 * call + n)
+    return torch.randn(n, generator=g, dtype=torch.float32).to(dtype)
+
+
+def _worker(rank: int, world: int, port: int, q) -> None:
+    try:
+        import torch.distributed as dist
+
+        from operator_amd.parallel.comm import Group
+
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        grp = Group()
+        assert grp.enable_oneshot(dev, max_bytes=4 << 20)
+        car = grp.oneshot
+        checked = 0
+        call = 0
+        for dtype in (torch.bfloat16, torch.float32):
+            for n in (8, 4096, 8192 * 3, 1 << 20 if dtype == torch.float32 else 2 << 20):
+                for _ in range(3):  # both parities of the receive buffer, repeated
+                    xs = [_inputs(r, n, dtype, call) for r in range(world)]
+                    want = sum(x.float() for x in xs).to(dtype)
+                    t = xs[rank].to(dev)
+                    grp.all_reduce_(t)
+                    torch.cuda.synchronize()
+                    assert torch.equal(t.cpu(), want), (dtype, n, (t.cpu().float() - want.float()).abs().max())
+                    call += 1
+                    checked += 1
+        # hipGraph capture: the round counter lives on the device, so replays stay in step
+        n = 16384
+        buf = torch.zeros(n, dtype=torch.bfloat16, device=dev)
+        out = torch.zeros_like(buf)
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            out.copy_(car.all_reduce(buf))
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            out.copy_(car.all_reduce(buf))
+        for rep in range(5):
+            xs = [_inputs(r, n, torch.bfloat16, 500 + rep) for r in range(world)]
+            buf.copy_(xs[rank].to(dev))
+            g.replay()
+            torch.cuda.synchronize()
+            assert torch.equal(out.cpu(), sum(x.float() for x in xs).to(torch.bfloat16)), rep
+            checked += 1
+        car.check()
+        dist.barrier()
+        car.close()
+        dist.destroy_process_group()
+        q.put((rank, "ok", checked))
+    except BaseException as e:  # noqa: BLE001
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc()))
+
+
+def test_oneshot_allreduce_two_ranks_one_gpu():
+    import torch.multiprocessing as mp
+
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from operator_amd.ops import kernels
+
+    assert hasattr(kernels(), "CustomAllReduce")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = []
+    try:
+        for _ in procs:
+            res.append(q.get(timeout=100))
+    finally:
+        for p in procs:
+            p.join(timeout=20)
+            if p.is_alive():
+                p.kill()
+    errs = [r for r in res if r[1] != "ok"]
+    assert not errs, errs[0][2]
+    assert all(r[2] >= 25 for r in res), res

@@ -105,3 +105,32 @@ def test_dp_shard_and_gather(tmp_path):
     merged = torch.load(tmp_path / "dp.pt", weights_only=True)
     assert sorted(x.split("@")[0] for x in merged) == sorted(f"pod-{i}" for i in range(11))
     assert {x.split("@")[1] for x in merged} == {"0", "1"}
+
+
+def test_bench_tp_script_two_ranks():
+    """tools/bench_tp.py (BASELINE config 5 launcher) under torch.distributed.run:
+    leader + follower lock-step through TPLLMEngine over gloo."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "tools", "bench_tp.py"),
+           "--model", "tiny-gqa4", "--dtype", "float32", "--batch", "3", "--prompt", "24", "--gen", "6",
+           "--kv-gb", "0.05"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(line) == 1, r.stdout
+    out = json.loads(line[0])
+    assert out["tp"] == 2 and out["decode_tok_s"] > 0
+
+
+def test_oneshot_disabled_without_gpu():
+    from operator_amd.parallel.comm import Group
+
+    g = Group.single()
+    assert g.enable_oneshot("cpu") is False
+    t = torch.ones(4)
+    assert g.all_reduce_(t) is t

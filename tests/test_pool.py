@@ -124,3 +124,39 @@ def test_pool_start_failure_is_fatal():
             p.submit_match(_data("x")).result(10)
     finally:
         p.close()
+
+
+def test_pool_tp2_replica_matches_tp1_engine():
+    """engine.tp=2: one explanation replica over two ranks (leader + follower,
+    lock-stepped through the control group, gloo collectives on the CPU tier)
+    gives the same tokens as the in-process TP=1 engine; a follower crash takes
+    the whole replica down and it is respawned."""
+    from operator_amd.engine import factory
+
+    ov = {"engine.dtype": "float32", "engine.model": "tiny-gqa4", "engine.tp": 2}
+    s1 = _settings(**{"engine.dtype": "float32", "engine.model": "tiny-gqa4"})
+    res = MatchEngine(catalog_library(), device="cpu").analyze([LOG_OOM.encode()], [("tp", "default")])[0]
+    cfgs = [AIProviderConfig(max_tokens=8, temperature=0.0), AIProviderConfig(max_tokens=8, temperature=0.3)]
+    ref = factory.build_explain_service(s1)
+    try:
+        want = [ref.explain(res, c).explanation for c in cfgs]
+    finally:
+        ref.ee.close(join_s=10)
+    p = EnginePool(_settings(**ov), catalog_library(), ["cpu", "cpu"], roles=("explain",), heartbeat_s=0.2,
+                   heartbeat_timeout_s=20.0, max_restarts=1)
+    try:
+        assert len(p.workers) == 1 and p.workers[0].follower_devices == ["cpu"]
+        assert p.wait_ready(600) == 1, p.health()
+        es = PoolExplainService(p, timeout_s=300)
+        got = [o.explanation for o in es.explain_many([(res, c) for c in cfgs])]
+        assert got == want
+        before = p.stats["deaths"]
+        p.workers[0].followers[0].kill()
+        deadline = time.time() + 120
+        while p.stats["deaths"] == before and time.time() < deadline:
+            time.sleep(0.1)
+        assert p.stats["deaths"] == before + 1
+        assert p.wait_ready(600) == 1, p.health()
+        assert es.explain(res, cfgs[0]).explanation == want[0]
+    finally:
+        p.close()
