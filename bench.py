@@ -88,7 +88,7 @@ def main() -> int:
         "engine.max_context": a.prompt_tokens + a.max_tokens + 64, "engine.max_prompt_tokens": a.prompt_tokens,
         "engine.kv_cache_gb": a.kv_gb or (96.0 if dev != "cpu" else 1.0), "engine.use_graphs": not a.no_graphs, "engine.ignore_eos": True,
         "engine.seed": 0, "health.enabled": False, "operator.workers": a.batch + 16, "operator.io_workers": 16,
-        "patterns.cache_dir": f"/tmp/oamd-bench-{os.getpid()}", "services.match_max_batch": max(a.batch, 64),
+        "patterns.cache_dir": f"/tmp/oamd-bench-{os.getpid()}", "services.match_max_batch": 64,
         "services.match_batch_wait_ms": 5.0})
 
     # ---- engines (weights, DFA, graphs) : not timed ----
@@ -113,7 +113,7 @@ def main() -> int:
 
     if a.mode == "pipeline":
         fk = FakeKube()
-        matcher = LocalMatchService(meng, max_batch=max(a.batch, 64), max_wait_ms=5.0)
+        matcher = LocalMatchService(meng, max_batch=64, max_wait_ms=5.0)
         op = Operator(fk, s, match_service=matcher, explain_service=explainer)
         fk.create(AIPROVIDERS, {"metadata": {"name": "local-llm", "namespace": "default"},
                                 "spec": {"providerId": "local", "modelId": a.model, "maxTokens": a.max_tokens,

@@ -28,7 +28,8 @@ namespace oamd {
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 
 constexpr int kBK = 64;     // K per stage: one 128-B line per row
-constexpr int kStages = 3;  // default LDS ring depth (2: two blocks per CU for the smaller tiles)
+constexpr int kStages = 3;  // default LDS ring depth (2: two blocks per CU for the smaller tiles; 4: three
+                            // stages in flight for tiles with BM + BN <= 320 rows, 160 KB of LDS at most)
 
 // 8 waves (2 per SIMD: one wave's LDS-read latency hides under the other's
 // MFMAs) laid out 4 (M) x 2 (N).
@@ -151,9 +152,12 @@ __global__ void __launch_bounds__(kWaves * 64, NS == 2 ? 2 : 1) gemm_tn_kernel(c
   // prologue: stages 0 .. NS-2 in flight; iteration t issues stage t + NS - 1
   // into the buffer compute(t - 1) just released (fenced by the barrier)
   issue(0, 0);
-  if (NS == 3 && T > 1) issue(1, 1);
+  if (NS >= 3 && T > 1) issue(1, 1);
+  if (NS >= 4 && T > 2) issue(2, 2);
   for (int t = 0; t < T; ++t) {
-    if (NS == 3 && t + 1 < T) wait_vmcnt<C::GL>();  // leave stage t+1 in flight
+    // stages issued so far: min(T, t + NS - 1); leave all but stage t in flight
+    if (NS >= 4 && t + 2 < T) wait_vmcnt<2 * C::GL>();
+    else if (NS >= 3 && t + 1 < T) wait_vmcnt<C::GL>();
     else wait_vmcnt<0>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -250,8 +254,14 @@ int gemm_decode(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, in
   if (S > 1) gemm_tn_kernel<BM, BNN, kEpiPartial, NSS><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, S,   \
                                                                                        w_tiled);              \
   else gemm_tn_kernel<BM, BNN, kEpiStore, NSS><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, S, w_tiled)
-#define OAMD_GEMM2(BM, BNN) \
-  if (stages == 2 && BM <= 128) { OAMD_GEMM3(BM, BNN, 2); } else { OAMD_GEMM3(BM, BNN, 3); }
+#define OAMD_GEMM2(BM, BNN)                                   \
+  if (stages == 2 && BM <= 128) {                              \
+    OAMD_GEMM3(BM, BNN, 2);                                    \
+  } else if (stages == 4 && BM + BNN <= 320) {                 \
+    OAMD_GEMM3(BM, BNN, (BM + BNN <= 320 ? 4 : 3));            \
+  } else {                                                     \
+    OAMD_GEMM3(BM, BNN, 3);                                    \
+  }
 #define OAMD_GEMM(BM) \
   if (BN == 64) { OAMD_GEMM2(BM, 64); } else { OAMD_GEMM2(BM, 128); }
   switch (BM) {

@@ -14,6 +14,16 @@ Race fix: all status writes for one Podmortem go through
 one ``StatusWriter`` lock, and the phase/message update is a merge patch of
 just those two fields on a fresh object, so it can never clobber
 ``recentFailures`` (the reference patches the whole status from a stale list).
+
+Group commit: a burst of failures for one monitor (hundreds of analyses
+finishing in the same decode window) would otherwise be hundreds of serialized
+GET+PATCH round trips on one object. Writers enqueue; whichever thread finds
+no flush in progress becomes the flusher and commits everything queued in ONE
+GET -> prepend-all -> PATCH (retried on 409 exactly as before), looping until
+the queue is empty; the others wait for the commit that carried their entry.
+The resulting ring is identical to one-at-a-time prepends in completion order.
+Phase/message updates coalesce the same way: each overwrites the previous, so
+only the latest queued one is written.
 """
 from __future__ import annotations
 
@@ -66,20 +76,75 @@ class Retrier:
         self.max_retries, self.initial_delay_s, self.sleep = max_retries, initial_delay_s, sleep
 
 
+class _Commit:
+    """Outcome of one queued write, filled in by whichever thread flushed it."""
+    __slots__ = ("done", "ok")
+
+    def __init__(self):
+        self.done, self.ok = False, False
+
+
+class _Queue:
+    """Per-Podmortem write queue + flusher flag (group commit)."""
+
+    def __init__(self):
+        self.cv = threading.Condition()
+        self.items: list = []
+        self.flushing = False
+
+
 class StatusWriter:
-    """Single writer per Podmortem (per-key lock)."""
+    """Single writer per Podmortem (per-key lock), with group commit of bursts."""
 
     def __init__(self, kube, retrier: Retrier | None = None, use_finished_at: bool = False):
         self.kube = kube
         self.retrier = retrier or Retrier()
         self.use_finished_at = use_finished_at
         self._locks: dict[tuple[str, str], threading.Lock] = defaultdict(threading.Lock)
+        self._queues: dict[tuple[str, str, str], _Queue] = defaultdict(_Queue)
         self._guard = threading.Lock()
+        self.commits = 0   # PATCHes actually issued (observability / tests)
+
+    def _key(self, monitor: dict) -> tuple[str, str]:
+        md = monitor.get("metadata") or {}
+        return (md.get("namespace") or "", md.get("name") or "")
 
     def _lock(self, monitor: dict) -> threading.Lock:
-        md = monitor.get("metadata") or {}
         with self._guard:
-            return self._locks[(md.get("namespace") or "", md.get("name") or "")]
+            return self._locks[self._key(monitor)]
+
+    def _group_commit(self, kind: str, monitor: dict, item, flush) -> bool:
+        """Queue ``item``; flush the queue (``flush(items) -> bool``) unless another
+        thread is already flushing it, and return the outcome of the commit that
+        carried ``item``."""
+        with self._guard:
+            q = self._queues[(kind, *self._key(monitor))]
+        mine = _Commit()
+        with q.cv:
+            q.items.append((item, mine))
+            if q.flushing:
+                while not mine.done:
+                    q.cv.wait()
+                return mine.ok
+            q.flushing = True
+        while True:
+            with q.cv:
+                batch, q.items = q.items, []
+                if not batch:
+                    q.flushing = False
+                    q.cv.notify_all()
+                    return mine.ok
+            try:
+                with self._lock(monitor):
+                    ok = bool(flush([it for it, _ in batch]))
+            except Exception as e:  # noqa: BLE001 - never leave waiters hanging
+                log.warning("status commit failed: %s", e)
+                ok = False
+            self.commits += 1
+            with q.cv:
+                for _, c in batch:
+                    c.ok, c.done = ok, True
+                q.cv.notify_all()
 
     def _with_retry(self, what: str, fn) -> bool:
         delay = self.retrier.initial_delay_s
@@ -107,15 +172,20 @@ class StatusWriter:
     def set_phase(self, monitor: dict, phase: str, message: str, observed_generation: bool = False) -> bool:
         md = monitor.get("metadata") or {}
 
-        def do():
-            patch = {"phase": phase, "message": message, "lastUpdate": instant_str()}
-            if observed_generation and md.get("generation") is not None:
+        def flush(items):
+            # each update overwrites the previous one: only the latest queued is written
+            ph, msg, og = items[-1]
+            patch = {"phase": ph, "message": msg, "lastUpdate": instant_str()}
+            if any(x[2] for x in items) and md.get("generation") is not None:
                 patch["observedGeneration"] = md.get("generation")
-            self.kube.patch_status(PODMORTEMS, md["name"], md.get("namespace"), patch)
-            return True
 
-        with self._lock(monitor):
+            def do():
+                self.kube.patch_status(PODMORTEMS, md["name"], md.get("namespace"), patch)
+                return True
+
             return self._with_retry(f"Podmortem {md.get('name')} status", do)
+
+        return self._group_commit("phase", monitor, (phase, message, observed_generation), flush)
 
     def update_pod_failure(self, monitor: dict, pod: dict, message: str) -> bool:
         """PodFailureWatcher.updatePodFailureStatusAsync (:452-502): phase Processing,
@@ -126,33 +196,34 @@ class StatusWriter:
     def append_failure(self, pod: dict, monitor: dict, result: AnalysisResult, ai_analysis: str | None) -> bool:
         md = monitor.get("metadata") or {}
         pmd = pod.get("metadata") or {}
+        when = instant_str()
+        if self.use_finished_at:
+            for cs in (pod.get("status") or {}).get("containerStatuses") or []:
+                t = ((cs or {}).get("state") or {}).get("terminated") or {}
+                if t.get("finishedAt"):
+                    when = t["finishedAt"]
+                    break
+        entry = {"podName": pmd.get("name"), "podNamespace": pmd.get("namespace"), "failureTime": when,
+                 "analysisStatus": "Completed",
+                 "explanation": ai_analysis if not is_blank(ai_analysis) else pattern_explanation(result)}
 
-        def do():
-            latest = self.kube.get(PODMORTEMS, md["name"], md.get("namespace"))
-            if latest is None:
-                log.warning("Podmortem not found: %s", md.get("name"))
-                return False
-            status = dict(latest.get("status") or {})
-            recent = list(status.get("recentFailures") or [])
-            when = instant_str()
-            if self.use_finished_at:
-                for cs in (pod.get("status") or {}).get("containerStatuses") or []:
-                    t = ((cs or {}).get("state") or {}).get("terminated") or {}
-                    if t.get("finishedAt"):
-                        when = t["finishedAt"]
-                        break
-            entry = {"podName": pmd.get("name"), "podNamespace": pmd.get("namespace"), "failureTime": when,
-                     "analysisStatus": "Completed",
-                     "explanation": ai_analysis if not is_blank(ai_analysis) else pattern_explanation(result)}
-            recent.insert(0, entry)
-            recent = recent[:MAX_RECENT_FAILURES]
-            self.kube.patch_status(PODMORTEMS, md["name"], md.get("namespace"),
-                                   {"recentFailures": recent, "lastUpdate": instant_str()},
-                                   resource_version=latest["metadata"]["resourceVersion"])
-            return True
+        def flush(entries):
+            def do():
+                latest = self.kube.get(PODMORTEMS, md["name"], md.get("namespace"))
+                if latest is None:
+                    log.warning("Podmortem not found: %s", md.get("name"))
+                    return False
+                recent = list((latest.get("status") or {}).get("recentFailures") or [])
+                # newest first: the same ring as prepending each entry in completion order
+                recent = (entries[::-1] + recent)[:MAX_RECENT_FAILURES]
+                self.kube.patch_status(PODMORTEMS, md["name"], md.get("namespace"),
+                                       {"recentFailures": recent, "lastUpdate": instant_str()},
+                                       resource_version=latest["metadata"]["resourceVersion"])
+                return True
 
-        with self._lock(monitor):
             return self._with_retry(f"Podmortem {md.get('name')} status", do)
+
+        return self._group_commit("ring", monitor, entry, flush)
 
 
 class AnalysisStorage:

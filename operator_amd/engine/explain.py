@@ -19,6 +19,7 @@ loop thread that owns the GPU (LLMEngine.step).
 from __future__ import annotations
 
 import hashlib
+import sys
 import threading
 import time
 from collections import OrderedDict
@@ -55,9 +56,17 @@ class EngineLoop(threading.Thread):
             self._stopping = True
             self._cv.notify()
 
+    # GIL hand-off interval while this thread feeds the GPU: at CPython's default
+    # (5 ms) every kernel-launch burst of a prefill step can wait that long behind the
+    # operator's worker threads, leaving the GPU idle (measured: ~0.3-0.5 s of idle
+    # per 256-failure wave). 0.5 ms bounds that wait at a small context-switch cost.
+    GIL_SWITCH_S = 0.0005
+
     def run(self) -> None:
         if self.llm.device.type == "cuda":
             torch.cuda.set_device(self.llm.device)
+            if sys.getswitchinterval() > self.GIL_SWITCH_S:
+                sys.setswitchinterval(self.GIL_SWITCH_S)
         while True:
             with self._cv:
                 while not self._stopping and not self.llm.has_work():
@@ -88,6 +97,61 @@ class _Pending:
     attempt: int = 0
 
 
+class PromptBatcher(threading.Thread):
+    """Coalesces prompt building of concurrent ``explain()`` callers.
+
+    The pipeline calls ``explain`` from one worker thread per failure; building
+    each prompt there (render + shrink-ladder tokenization, ~2-4 ms of
+    GIL-holding ``encode`` per prompt at 1k tokens) starved the engine-loop
+    thread that launches the GPU work. Callers instead enqueue and wait; this
+    thread takes everything queued (after ``wait_s`` for stragglers) and
+    tokenizes it with ``render_bounded_batch`` (Rust ``encode_batch``, GIL
+    released, parallel)."""
+
+    def __init__(self, build_many, wait_s: float = 0.002, max_batch: int = 32):
+        super().__init__(name="prompt-batcher", daemon=True)
+        import queue as _queue
+
+        self.build_many, self.wait_s, self.max_batch = build_many, wait_s, max_batch
+        self.q: _queue.Queue = _queue.Queue()
+        self._empty = _queue.Empty
+
+    def build(self, result: AnalysisResult, cfg: AIProviderConfig) -> list[int]:
+        from concurrent.futures import Future
+
+        f: Future = Future()
+        self.q.put((result, cfg, f))
+        return f.result()
+
+    def stop(self) -> None:
+        self.q.put(None)
+
+    def run(self) -> None:
+        while True:
+            item = self.q.get()
+            if item is None:
+                return
+            batch = [item]
+            deadline = time.perf_counter() + self.wait_s
+            while len(batch) < self.max_batch:
+                try:
+                    nxt = self.q.get(timeout=max(0.0, deadline - time.perf_counter()))
+                except self._empty:
+                    break
+                if nxt is None:
+                    self.q.put(None)
+                    break
+                batch.append(nxt)
+            try:
+                ids = self.build_many([(r, c) for r, c, _ in batch])
+                for (_, _, f), x in zip(batch, ids):
+                    f.set_result(x)
+            except BaseException as e:  # noqa: BLE001 - delivered to every caller
+                for _, _, f in batch:
+                    if not f.done():
+                        f.set_exception(e)
+
+
 class ExplainEngine:
     def __init__(self, llm: LLMEngine, tokenizer, model_id: str = "local", max_prompt_tokens: int = 1024,
                  cache_size: int = 4096, ignore_eos: bool = False, start_loop: bool = True):
@@ -99,10 +163,13 @@ class ExplainEngine:
         self._cache_size = cache_size
         self._lock = threading.Lock()
         self.loop = EngineLoop(llm)
+        self.prompts = PromptBatcher(self.build_prompts)
+        self.prompts.start()
         if start_loop:
             self.loop.start()
 
     def close(self, join_s: float = 0.0) -> None:
+        self.prompts.stop()
         self.loop.stop()
         if join_s and self.loop.is_alive():
             self.loop.join(join_s)
@@ -110,6 +177,10 @@ class ExplainEngine:
     # ------------------------------------------------------------------ helpers
     def build_prompt(self, result: AnalysisResult, cfg: AIProviderConfig) -> list[int]:
         return prompt_mod.render_bounded(result, self.tok, self.max_prompt_tokens, cfg.prompt_template)
+
+    def build_prompts(self, items: list[tuple[AnalysisResult, AIProviderConfig]]) -> list[list[int]]:
+        return prompt_mod.render_bounded_batch([(r, c.prompt_template) for r, c in items], self.tok,
+                                               self.max_prompt_tokens)
 
     def _key(self, ids: list[int], cfg: AIProviderConfig) -> str:
         h = hashlib.sha256()
@@ -131,8 +202,11 @@ class ExplainEngine:
     def explain_many(self, items: list[tuple[AnalysisResult, AIProviderConfig]]) -> list[AIResponse | ExplainError]:
         """Explain a batch concurrently (continuous batching); per-item errors are returned, not raised."""
         pend: list[_Pending | AIResponse | ExplainError] = []
-        for res, cfg in items:
-            ids = self.build_prompt(res, cfg)
+        if len(items) == 1 and self.prompts.is_alive():   # one caller of many: coalesced with the others
+            prompts = [self.prompts.build(*items[0])]
+        else:
+            prompts = self.build_prompts(items)
+        for (res, cfg), ids in zip(items, prompts):
             key = self._key(ids, cfg) if cfg.caching_enabled else None
             if key is not None:
                 with self._lock:

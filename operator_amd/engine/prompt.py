@@ -66,10 +66,35 @@ def render(result: AnalysisResult, template: str | None = None, top_k: int = 5, 
     return _PH.sub(sub, tpl)
 
 
+# Shrink ladder: (events kept, context lines kept on each side of the match; None = all)
+LADDER = ((5, None), (5, 2), (5, 1), (3, 0), (1, 0), (0, 0))
+
+
 def render_bounded(result: AnalysisResult, tokenizer, max_tokens: int, template: str | None = None) -> list[int]:
     """Token ids of the rendered prompt, shrunk (context, then events) to fit ``max_tokens``."""
-    for top_k, ctx in ((5, None), (5, 2), (5, 1), (3, 0), (1, 0), (0, 0)):
-        ids = tokenizer.encode(render(result, template, top_k, ctx))
-        if len(ids) <= max_tokens:
-            return ids
-    return ids[: max_tokens]
+    return render_bounded_batch([(result, template)], tokenizer, max_tokens)[0]
+
+
+def render_bounded_batch(items: list[tuple[AnalysisResult, str | None]], tokenizer, max_tokens: int) -> list[list[int]]:
+    """``render_bounded`` for many prompts at once: every rung of the shrink ladder is
+    ONE ``encode_batch`` call over the prompts still too long (the tokenizer's Rust
+    core encodes them in parallel without the GIL), instead of one or more
+    GIL-holding ``encode`` calls per prompt. Same result as the per-prompt loop."""
+    out: list[list[int] | None] = [None] * len(items)
+    todo = list(range(len(items)))
+    last: dict[int, list[int]] = {}
+    for top_k, ctx in LADDER:
+        if not todo:
+            break
+        enc = tokenizer.encode_batch([render(items[i][0], items[i][1], top_k, ctx) for i in todo])
+        nxt = []
+        for i, ids in zip(todo, enc):
+            if len(ids) <= max_tokens:
+                out[i] = ids
+            else:
+                last[i] = ids
+                nxt.append(i)
+        todo = nxt
+    for i in todo:
+        out[i] = last[i][:max_tokens]
+    return out  # type: ignore[return-value]

@@ -86,6 +86,7 @@ class FakeKube:
     def __init__(self):
         self._lock = threading.RLock()
         self._objs: dict[tuple[str, str, str], dict] = {}  # (plural-key, ns, name) -> obj
+        self._by_kind: dict[str, dict[tuple[str, str], dict]] = {}
         self._rv = itertools.count(1)
         self._history: list[tuple[int, str, str, dict]] = []  # (rv, plural-key, type, obj)
         self._watches: list[FakeWatch] = []
@@ -116,9 +117,22 @@ class FakeKube:
     def _key(res: Resource) -> str:
         return f"{res.api_version}/{res.plural}"
 
+    def _kind(self, key: str) -> dict:
+        """Per-resource index {(ns, name): obj} over the same objects as ``_objs``."""
+        d = self._by_kind.get(key)
+        if d is None:
+            d = self._by_kind[key] = {}
+        return d
+
+    def _store(self, k: tuple[str, str, str], obj: dict) -> None:
+        self._objs[k] = obj
+        self._kind(k[0])[k[1:]] = obj
+
     def _emit(self, res: Resource, typ: str, obj: dict) -> None:
         rv = int(obj["metadata"]["resourceVersion"])
-        self._history.append((rv, self._key(res), typ, copy.deepcopy(obj)))
+        # stored objects are never mutated after they are stored (every update stores a
+        # new dict), so the history can hold them by reference
+        self._history.append((rv, self._key(res), typ, obj))
         for w in list(self._watches):
             if w.res == res and (w.namespace is None or w.namespace == obj["metadata"].get("namespace")):
                 w.push(typ, copy.deepcopy(obj))
@@ -148,8 +162,8 @@ class FakeKube:
         key = self._key(res)
         with self._lock:
             out = []
-            for (k, ns, _), o in sorted(self._objs.items()):
-                if k != key or (namespace is not None and ns != namespace):
+            for (ns, _), o in sorted(self._kind(key).items()):
+                if namespace is not None and ns != namespace:
                     continue
                 if sel is not None and not match_selector(sel, o["metadata"].get("labels")):
                     continue
@@ -183,7 +197,7 @@ class FakeKube:
             md.setdefault("creationTimestamp", instant_str())
             o.setdefault("apiVersion", res.api_version)
             o.setdefault("kind", res.kind)
-            self._objs[k] = o
+            self._store(k, o)
             self._emit(res, "ADDED", o)
             return copy.deepcopy(o)
 
@@ -197,14 +211,23 @@ class FakeKube:
             if resource_version is not None and str(resource_version) != cur["metadata"]["resourceVersion"]:
                 raise ApiError(409, f"the object has been modified; resourceVersion {resource_version} is stale",
                                "Conflict")
-            new = fn(copy.deepcopy(cur))
+            if status:
+                # only status may change: copy status deeply, share the rest (never mutated)
+                base = dict(cur)
+                base["metadata"] = dict(cur["metadata"])
+                if "status" in cur:
+                    base["status"] = copy.deepcopy(cur["status"])
+                new = fn(base)
+            else:
+                new = fn(copy.deepcopy(cur))
             new["metadata"]["uid"] = cur["metadata"]["uid"]
             new["metadata"]["name"] = name
             if res.namespaced:
                 new["metadata"]["namespace"] = namespace
             if status:
                 # status subresource: only status may change
-                kept = copy.deepcopy(cur)
+                kept = dict(cur)
+                kept["metadata"] = dict(cur["metadata"])
                 kept["status"] = new.get("status")
                 if kept["status"] is None:
                     kept.pop("status", None)
@@ -214,7 +237,7 @@ class FakeKube:
             else:
                 new["metadata"]["generation"] = cur["metadata"].get("generation", 1)
             new["metadata"]["resourceVersion"] = str(next(self._rv))
-            self._objs[k] = new
+            self._store(k, new)
             self._emit(res, "MODIFIED", new)
             return copy.deepcopy(new)
 
@@ -257,9 +280,13 @@ class FakeKube:
         self._log_call("delete", res, namespace, name)
         self._fault("delete", res)
         with self._lock:
-            o = self._objs.pop((self._key(res), namespace or "", name), None)
+            k = (self._key(res), namespace or "", name)
+            o = self._objs.pop(k, None)
             if o is None:
                 return False
+            self._kind(k[0]).pop(k[1:], None)
+            o = dict(o)
+            o["metadata"] = dict(o["metadata"])
             o["metadata"]["resourceVersion"] = str(next(self._rv))
             self._emit(res, "DELETED", o)
             return True

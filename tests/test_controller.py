@@ -362,3 +362,39 @@ def test_readiness_check(tmp_path):
     (tmp_path / "cache" / "a.yaml").unlink()
     t[0] = 301
     assert chk()[1] is True  # grace period exceeded
+
+
+def test_status_group_commit_coalesces_bursts():
+    """Concurrent ring appends for one Podmortem are committed in batches: fewer
+    PATCHes than entries, and the ring equals one-by-one prepends in commit order."""
+    import threading
+
+    fk = FakeKube()
+    fk.create(PODMORTEMS, {"metadata": {"name": "m", "namespace": "default"}, "spec": {}})
+    order = []
+    real_patch = fk.patch_status
+
+    def slow_patch(res, name, ns, patch, **kw):
+        time.sleep(0.01)
+        if "recentFailures" in patch:
+            order.append([e["podName"] for e in patch["recentFailures"]])
+        return real_patch(res, name, ns, patch, **kw)
+
+    fk.patch_status = slow_patch
+    w = st.StatusWriter(fk)
+    mon = fk.get(PODMORTEMS, "m", "default")
+    res = AnalysisResult(summary=AnalysisSummary(highest_severity="HIGH", significant_events=1), events=[])
+    oks = []
+    th = [threading.Thread(target=lambda i=i: oks.append(w.append_failure(failed_pod(f"p{i}"), mon, res, f"x{i}")))
+          for i in range(40)]
+    th += [threading.Thread(target=lambda i=i: w.update_pod_failure(mon, failed_pod(f"p{i}"), "done")) for i in range(40)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(30)
+    assert oks == [True] * 40
+    assert w.commits < 80   # both queues coalesced
+    rf = fk.get(PODMORTEMS, "m", "default")["status"]["recentFailures"]
+    assert len(rf) == 10 and [e["podName"] for e in rf] == order[-1]
+    assert len(order) < 40   # ring PATCHes: one per flushed batch, not one per entry
+    assert fk.get(PODMORTEMS, "m", "default")["status"]["message"].startswith("done (Pod: p")

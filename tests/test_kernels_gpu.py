@@ -154,7 +154,7 @@ def test_gemm_decode(M, N, K):
             for S in (1, 2, 4, 8):
                 if bm > M or K % (64 * S) or N % bn:
                     continue
-                for ns in ((2, 3) if bm <= 128 else (3,)):
+                for ns in ((2, 3, 4) if bm <= 128 else (3, 4) if bm + bn <= 320 else (3,)):
                     y = ops.linear(x, w, splits=S, bn=bn, bm=bm, stages=ns)
                     torch.testing.assert_close(y.float(), ref_, atol=2e-2, rtol=2e-2)
     # default split choice and the hipBLASLt fallback shape agree too

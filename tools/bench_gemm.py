@@ -73,7 +73,7 @@ for M in [int(x) for x in a.m.split(",")]:
             for bm in (64, 128, 256):
                 for bn in (64, 128):
                     for S in (1, 2, 4, 8):
-                        for ns in ((2, 3) if bm <= 128 else (3,)):
+                        for ns in ((2, 3, 4) if bm <= 128 else (3, 4) if bm + bn <= 320 else (3,)):
                             if bm > M or K % (64 * S) or N % bn:
                                 continue
                             got = ops.linear(x, ws[name][0], out=y, splits=S, partial=part, bn=bn, bm=bm,

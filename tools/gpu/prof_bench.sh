@@ -8,5 +8,5 @@ tail -1 gpurun_out/prof_bench.log
 f=$(find gpurun_out/prof -name '*kernel_trace.csv' | head -1)
 python3 tools/prof_summary.py "$f" --window-json gpurun_out/prof_bench.json --top 40 > gpurun_out/prof_summary.txt
 cp $(find gpurun_out/prof -name '*kernel_stats.csv' | head -1) gpurun_out/prof_kernel_stats.csv
-rm -f "$f"
+gzip -c "$f" > gpurun_out/kernel_trace.csv.gz; rm -f "$f"
 head -60 gpurun_out/prof_summary.txt
