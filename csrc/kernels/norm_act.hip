@@ -14,12 +14,16 @@ namespace oamd {
 // fp32 split-K slabs xp[s * slab + row * hidden + c] written by gemm_decode —
 // the GEMM's reduction pass is folded into this kernel (same numerics: the
 // projection output is rounded to bf16 once, then added to the residual).
-template <int NT, int MAXV>
+// SC = compile-time slab count (0: runtime S) so the S slab loads of a vector are
+// all issued before the first add (a runtime-trip-count loop waits for each load
+// in turn: S dependent L2/HBM round trips per vector).
+template <int NT, int MAXV, int SC>
 __global__ void __launch_bounds__(NT) rmsnorm_kernel(
     const bf16_t* __restrict__ x, bf16_t* __restrict__ residual,
     const bf16_t* __restrict__ w, bf16_t* __restrict__ y, int hidden,
     int64_t x_stride, int64_t r_stride, int64_t y_stride, float eps,
-    const float* __restrict__ xp, int S, int64_t slab) {
+    const float* __restrict__ xp, int S_rt, int64_t slab) {
+  const int S = SC > 0 ? SC : S_rt;
   __shared__ float scratch[NT / 64];
   const int row = blockIdx.x;
   const int nvec = hidden >> 3;
@@ -35,9 +39,23 @@ __global__ void __launch_bounds__(NT) rmsnorm_kernel(
       if (xp) {
         const float* pr = xp + (int64_t)row * hidden + vi * 8;
         f32x4 lo = *reinterpret_cast<const f32x4*>(pr), hi = *reinterpret_cast<const f32x4*>(pr + 4);
-        for (int sp = 1; sp < S; ++sp) {
-          lo += *reinterpret_cast<const f32x4*>(pr + sp * slab);
-          hi += *reinterpret_cast<const f32x4*>(pr + sp * slab + 4);
+        if constexpr (SC > 0) {
+          f32x4 pl[SC > 1 ? SC - 1 : 1], ph[SC > 1 ? SC - 1 : 1];
+#pragma unroll
+          for (int sp = 1; sp < SC; ++sp) {
+            pl[sp - 1] = *reinterpret_cast<const f32x4*>(pr + sp * slab);
+            ph[sp - 1] = *reinterpret_cast<const f32x4*>(pr + sp * slab + 4);
+          }
+#pragma unroll
+          for (int sp = 1; sp < SC; ++sp) {
+            lo += pl[sp - 1];
+            hi += ph[sp - 1];
+          }
+        } else {
+          for (int sp = 1; sp < S; ++sp) {
+            lo += *reinterpret_cast<const f32x4*>(pr + sp * slab);
+            hi += *reinterpret_cast<const f32x4*>(pr + sp * slab + 4);
+          }
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -92,16 +110,26 @@ int rmsnorm(const bf16_t* x, bf16_t* residual, const bf16_t* w, bf16_t* y,
   constexpr int NT = 256;
   const int nvec = hidden / 8;
   const int64_t slab = (int64_t)rows * hidden;
-  if (nvec <= NT * 2) {
-    rmsnorm_kernel<NT, 2><<<rows, NT, 0, stream>>>(x, residual, w, y, hidden, x_stride, r_stride, y_stride, eps,
-                                                   xp, S, slab);
-  } else if (nvec <= NT * 4) {
-    rmsnorm_kernel<NT, 4><<<rows, NT, 0, stream>>>(x, residual, w, y, hidden, x_stride, r_stride, y_stride, eps,
-                                                   xp, S, slab);
-  } else {
-    rmsnorm_kernel<NT, 8><<<rows, NT, 0, stream>>>(x, residual, w, y, hidden, x_stride, r_stride, y_stride, eps,
-                                                   xp, S, slab);
+  const int sc = xp == nullptr ? 1 : S;
+#define OAMD_RMS(MV, SCC) \
+  rmsnorm_kernel<NT, MV, SCC><<<rows, NT, 0, stream>>>(x, residual, w, y, hidden, x_stride, r_stride, y_stride, eps, xp, S, slab)
+#define OAMD_RMS_S(MV)                  \
+  switch (sc) {                         \
+    case 1: OAMD_RMS(MV, 1); break;     \
+    case 2: OAMD_RMS(MV, 2); break;     \
+    case 4: OAMD_RMS(MV, 4); break;     \
+    case 8: OAMD_RMS(MV, 8); break;     \
+    default: OAMD_RMS(MV, 0); break;    \
   }
+  if (nvec <= NT * 2) {
+    OAMD_RMS_S(2)
+  } else if (nvec <= NT * 4) {
+    OAMD_RMS_S(4)
+  } else {
+    OAMD_RMS_S(8)
+  }
+#undef OAMD_RMS_S
+#undef OAMD_RMS
   OAMD_LAUNCH_CHECK();
   return 0;
 }

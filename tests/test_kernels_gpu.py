@@ -217,7 +217,7 @@ def test_gemm_fp8(M, N, K):
     assert rel < 0.06, float(rel)
 
 
-@pytest.mark.parametrize("S", [2, 4, 8])
+@pytest.mark.parametrize("S", [1, 2, 3, 4, 8])
 def test_rmsnorm_sums_splitk_slabs(S):
     torch.manual_seed(11)
     M, N = 128, 1024
