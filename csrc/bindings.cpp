@@ -159,6 +159,37 @@ void gemm_decode(const at::Tensor& x, const at::Tensor& w, const c10::optional<a
                        (int)bn, (int)bm, silu_gu, w_tiled, (int)stages, cur_stream()));
 }
 
+void gemm_skinny(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& y_opt,
+                 const c10::optional<at::Tensor>& p, int64_t splits, bool silu_gu) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && w.size(1) == x.size(1), "x [M,K], w [N,K]");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(M >= 1 && M <= 32, "gemm_skinny: M must be 1..32");
+  TORCH_CHECK(N % (silu_gu ? 128 : 16) == 0, "gemm_skinny: N % 16 (128 for the fused SwiGLU)");
+  TORCH_CHECK(splits >= 1 && splits <= 8 && K % (128 * splits) == 0, "gemm_skinny: K % (128 * splits)");
+  TORCH_CHECK(!silu_gu || splits == 1, "fused SwiGLU needs splits = 1");
+  bf16_t* yp = nullptr;
+  if (y_opt.has_value()) {
+    CHECK_BF16(*y_opt); CHECK_CONTIG(*y_opt);
+    TORCH_CHECK(y_opt->dim() == 2 && y_opt->size(0) == M && y_opt->size(1) == (silu_gu ? N / 2 : N), "gemm shapes");
+    yp = ptr<bf16_t>(*y_opt);
+  } else {
+    TORCH_CHECK(splits > 1 && !silu_gu, "y may be omitted only for split-K slabs summed by the consumer");
+  }
+  float* pp = nullptr;
+  if (splits > 1) {
+    TORCH_CHECK(p.has_value(), "split-K needs a partial buffer");
+    CHECK_DT(*p, at::kFloat); CHECK_CONTIG(*p);
+    TORCH_CHECK(p->numel() >= splits * M * N, "partial buffer too small");
+    TORCH_CHECK((M * N) % 4 == 0 || yp == nullptr, "split-K reduce needs M * N % 4 == 0");
+    pp = p->data_ptr<float>();
+  }
+  TORCH_CHECK(N * K < (1LL << 40) && M * K < (1LL << 31), "gemm too large");
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  RC(oamd::gemm_skinny(ptr<bf16_t>(x), ptr<bf16_t>(w), yp, pp, (int)M, (int)N, (int)K, (int)splits, silu_gu,
+                       cur_stream()));
+}
+
 void quantize_fp8(const at::Tensor& x, at::Tensor& q, at::Tensor& sx) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_CONTIG(q); CHECK_CONTIG(sx); CHECK_DT(sx, at::kFloat);
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be [M, K] row-major");
@@ -315,6 +346,8 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("p") = pybind11::none(), pybind11::arg("splits") = 1, pybind11::arg("bn") = 64,
         pybind11::arg("bm") = 0, pybind11::arg("silu_gu") = false, pybind11::arg("w_tiled") = false,
         pybind11::arg("stages") = 3);
+  m.def("gemm_skinny", &gemm_skinny, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"),
+        pybind11::arg("p") = pybind11::none(), pybind11::arg("splits") = 1, pybind11::arg("silu_gu") = false);
   m.def("attn_prefill", &attn_prefill);
   m.def("sample", &sample, pybind11::arg("logits"), pybind11::arg("temperature"), pybind11::arg("seeds"),
         pybind11::arg("positions"), pybind11::arg("out"), pybind11::arg("col_offset") = 0,

@@ -227,6 +227,14 @@ __global__ void gemm_splitk_reduce_kernel(const float* __restrict__ P, bf16_t* _
   *reinterpret_cast<uint2*>(Y + i) = o;
 }
 
+int splitk_reduce(const float* P, bf16_t* Y, int64_t MN, int S, hipStream_t stream) {
+  if (MN % 4 != 0 || S < 1) return -1;
+  const int64_t threads = MN / 4;
+  gemm_splitk_reduce_kernel<<<(threads + 255) / 256, 256, 0, stream>>>(P, Y, MN, S);
+  OAMD_LAUNCH_CHECK();
+  return 0;
+}
+
 int gemm_decode(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, int N, int K, int S, int BN,
                 int BM, bool silu_gu, bool w_tiled_b, int stages, hipStream_t stream) {
   const int w_tiled = w_tiled_b ? 1 : 0;

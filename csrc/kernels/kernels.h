@@ -26,6 +26,14 @@ int rope_kv(const bf16_t* qkv, int64_t qkv_stride, const int64_t* pos, const flo
 int gemm_decode(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, int N, int K, int S, int BN,
                 int BM, bool silu_gu, bool w_tiled, int stages, hipStream_t stream);
 
+// Y[M, N] = bf16(sum_s P[s][M][N]) (fp32 split-K slabs).
+int splitk_reduce(const float* P, bf16_t* Y, int64_t MN, int S, hipStream_t stream);
+// Skinny-M decode GEMM (M <= 32, gemm_skinny.hip): N % 16 == 0, K % (128 S) == 0; S-way split-K slabs P
+// reduced into Y (Y == nullptr: left for the consumer); silu_gu: fused SwiGLU over the 64-row
+// interleaved gate|up weight, Y [M, N/2].
+int gemm_skinny(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, int N, int K, int S, bool silu_gu,
+                hipStream_t stream);
+
 // FP8 e4m3fn W8A8: Y = (X8 . W8^T) * sx[m] * sw[n]; any M (BM-row tiles), S | 8 split-K.
 int gemm_fp8(const uint8_t* X, const uint8_t* W, const float* sx, const float* sw, bf16_t* Y, float* P, int M,
              int N, int K, int S, int BN, int BM, hipStream_t stream);

@@ -93,6 +93,12 @@ def gate_up_silu(x: torch.Tensor, wgu: torch.Tensor, block: int | None) -> torch
     other shapes run the GEMM then the silu_mul kernel."""
     M, K = x.shape
     N = wgu.shape[0]
+    if (x.is_cuda and block == 64 and x.dtype == torch.bfloat16 and M <= SKINNY_MAX_M and N % 128 == 0
+            and K % 128 == 0 and x.is_contiguous() and wgu.is_contiguous()
+            and skinny_plan(M, N, K) is not None and _gemm_table_get().get(("silu", M, N, K)) != "blas"):
+        y = torch.empty(M, N // 2, dtype=x.dtype, device=x.device)
+        kernels().gemm_skinny(x, wgu, y, None, 1, True)
+        return y
     if (x.is_cuda and block == 64 and x.dtype == torch.bfloat16 and M % 64 == 0 and M <= 256 and N % 128 == 0
             and K % 64 == 0 and x.is_contiguous() and wgu.is_contiguous()):
         t = _gemm_table_get().get(("silu", M, N, K))
@@ -193,7 +199,7 @@ def _gemm_table_get() -> dict:
     if _gemm_table is None:
         try:
             with open(_GEMM_TABLE_PATH) as f:
-                _gemm_table = {tuple(x if x == "silu" else int(x) for x in k.split(",")): v
+                _gemm_table = {tuple(x if x in ("silu", "skinny") else int(x) for x in k.split(",")): v
                                for k, v in json.load(f).items()}
         except (OSError, ValueError):
             _gemm_table = {}
@@ -226,15 +232,48 @@ def gemm_plan(M: int, N: int, K: int):
     return (min(M, 256), 64, gemm_splits(M, N, K))
 
 
+SKINNY_MAX_M = 32
+
+
+def skinny_plan(M: int, N: int, K: int) -> int | None:
+    """Split-K count for the gfx950 gemm_skinny kernel (M <= 32 decode buckets), or None
+    for hipBLASLt: tuned table entry ``skinny,M,N,K`` if present, else split K until
+    the 16-row tiles give >= 512 blocks (K permitting)."""
+    if M > SKINNY_MAX_M or N % 16 or K % 128 or os.environ.get("OAMD_SKINNY", "1") == "0":
+        return None
+    t = _gemm_table_get().get(("skinny", M, N, K))
+    if t == "blas":
+        return None
+    if t is not None:
+        return int(t)
+    S = 1
+    while (N // 16) * S < 512 and S < 8 and K % (128 * S * 2) == 0:
+        S *= 2
+    return S
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None, splits: int | None = None,
            partial: torch.Tensor | None = None, bn: int | None = None, bm: int | None = None,
            defer_reduce: bool = False, stages: int | None = None):
-    """y = x @ w^T (bf16). Decode-bucket shapes (M a multiple of 64, <= 256) run on the
-    gfx950 gemm_decode kernel when it beats hipBLASLt for the shape (tuned table);
-    everything else (prefill, odd shapes, CPU) on hipBLASLt / torch."""
+    """y = x @ w^T (bf16). Decode-bucket shapes run on gfx950 kernels where they beat
+    hipBLASLt: M <= 32 on the weight-streaming gemm_skinny, M in {64, 128, 256} on the
+    LDS-staged gemm_decode (tuned tables); everything else (prefill, odd shapes, CPU)
+    on hipBLASLt / torch."""
     M, K = x.shape
     N = w.shape[0]
     plan = None
+    if (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous() and M <= SKINNY_MAX_M
+            and bm is None and bn is None):
+        S = splits or skinny_plan(M, N, K)
+        if S is not None:
+            if S > 1 and (partial is None or partial.numel() < S * M * N):
+                partial = torch.empty(S * M * N, dtype=torch.float32, device=x.device)
+            if defer_reduce and S > 1 and out is None:
+                kernels().gemm_skinny(x, w, None, partial, S, False)
+                return SplitK(partial, S, M, N)
+            y = out if out is not None else torch.empty(M, N, dtype=x.dtype, device=x.device)
+            kernels().gemm_skinny(x, w, y, partial if S > 1 else None, S, False)
+            return y
     if x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous():
         plan = gemm_plan(M, N, K)
         if plan is None and (splits or bn or bm) and M % 64 == 0 and N % 64 == 0 and K % 64 == 0:

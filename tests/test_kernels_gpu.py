@@ -162,7 +162,32 @@ def test_gemm_decode(M, N, K):
     torch.testing.assert_close(ops.linear(x[:M - 3].contiguous(), w).float(), ref_[:M - 3], atol=2e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("M", [64, 128, 256, 40])
+@pytest.mark.parametrize("M", [1, 2, 5, 16, 17, 32])
+@pytest.mark.parametrize("N,K", [(256, 512), (640, 2048), (128, 4096), (1024, 14336)])
+def test_gemm_skinny(M, N, K):
+    """Weight-streaming MFMA GEMM for M <= 32 decode buckets, every split count,
+    plain / deferred (slabs) / reduced outputs, against an fp32 reference."""
+    from operator_amd.ops import kernels
+
+    torch.manual_seed(12)
+    x = _rand(M, K)
+    w = _rand(N, K) * 0.05
+    ref_ = x.float() @ w.float().t()
+    for S in (1, 2, 4, 8):
+        if K % (128 * S):
+            continue
+        y = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        p = torch.empty(S * M * N, dtype=torch.float32, device=DEV) if S > 1 else None
+        kernels().gemm_skinny(x, w, y, p, S, False)
+        torch.testing.assert_close(y.float(), ref_, atol=2e-2, rtol=2e-2)
+        if S > 1:
+            torch.testing.assert_close(p.view(S, M, N).sum(0), ref_, atol=1e-3, rtol=1e-3)
+            d = ops.linear(x, w, splits=S, defer_reduce=True)
+            torch.testing.assert_close(d.materialize().float(), ref_, atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(ops.linear(x, w).float(), ref_, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M", [64, 128, 256, 40, 1, 7, 16, 32])
 def test_gate_up_silu_fused(M):
     torch.manual_seed(8)
     K, inter = 1024, 640
