@@ -43,6 +43,7 @@ def timeit(fn, wl, it=48):
     return e0.elapsed_time(e1) / it * 1e3
 
 
+DEFERRED = ("o", "down")  # models/llama.py: defer=True projections (split-K slabs summed by rmsnorm)
 table = {}
 for M in [int(x) for x in a.m.split(",")]:
     tot = {"hipblaslt": 0.0, "best": 0.0}
@@ -61,7 +62,9 @@ for M in [int(x) for x in a.m.split(",")]:
             if err > 0.1:
                 print("BAD", name, M, S, err, flush=True)
                 continue
-            res[f"s{S}"] = timeit(lambda w: kernels().gemm_skinny(x, w, y, part if S > 1 else None, S, False),
+            # o / down hand their slabs to the next rmsnorm in the model: no reduce kernel
+            yy = None if (S > 1 and name in DEFERRED) else y
+            res[f"s{S}"] = timeit(lambda w: kernels().gemm_skinny(x, w, yy, part if S > 1 else None, S, False),
                                   ws[name])
         best = min(res, key=res.get)
         if best != "hipblaslt" and res[best] < 0.97 * res["hipblaslt"]:
