@@ -88,6 +88,7 @@ class ServicesCfg(BaseModel):
     ai_interface_connect_timeout_s: float = 120.0
     match_batch_wait_ms: float = 2.0
     match_max_batch: int = 1024
+    external_providers: bool = True   # AIProviders with providerId openai/ollama call their apiUrl directly
 
 
 class EngineCfg(BaseModel):

@@ -6,7 +6,9 @@ never written. Here the provider is validated against the on-node engine:
 * the referenced auth Secret (if any) must exist and contain the key;
 * the explain service must be ready (model weights loaded / engine loop alive);
 * ``modelId`` is informational (the local engine serves its configured model);
-  a mismatch is reported in the message, not treated as a failure.
+  a mismatch is reported in the message, not treated as a failure;
+* a provider routed to an external API (``providerId`` openai / ollama, see
+  engine/providers.py) is Ready when it names an ``apiUrl``.
 """
 from __future__ import annotations
 
@@ -38,11 +40,22 @@ class AIProviderReconciler:
                     problems.append(f"key {auth.get('secretKey')} missing in secret {auth.get('secretName')}")
             except ApiError as e:
                 problems.append(f"secret lookup failed: {e}")
-        ready = self.explainer is not None and getattr(self.explainer, "ready", lambda: True)()
-        if not ready:
-            problems.append("explanation engine not ready")
+        from operator_amd.api.models import AIProviderConfig
+
+        route = getattr(self.explainer, "route", lambda c: "local")(AIProviderConfig(provider_id=spec.get("providerId")))
+        if route != "local":   # external API (engine/providers.py): needs an endpoint
+            if not spec.get("apiUrl"):
+                problems.append(f"providerId {spec.get('providerId')} needs spec.apiUrl")
+        else:
+            ready = self.explainer is not None and getattr(self.explainer, "ready", lambda: True)() \
+                and getattr(self.explainer, "local", True) is not None
+            if not ready:
+                problems.append("explanation engine not ready")
         if problems:
             phase, msg = "Failed", "; ".join(problems)
+        elif route != "local":
+            phase = "Ready"
+            msg = f"Served by the external {route} API at {spec.get('apiUrl')} (model {spec.get('modelId')})"
         else:
             phase = "Ready"
             mid = spec.get("modelId")

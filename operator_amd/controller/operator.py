@@ -72,7 +72,11 @@ class Operator:
         self.events = EventEmitter(kube, self.io_pool, self.metrics)
         self.match_engine_factory = match_engine_factory
         self.matcher = match_service
-        self.explainer = explain_service
+        # providerId routing: on-node engine by default, external OpenAI / Ollama APIs for
+        # AIProviders that name them (engine/providers.py)
+        from operator_amd.engine.providers import ProviderRouter
+
+        self.explainer = ProviderRouter(explain_service, enabled=s.services.external_providers)
         self.pipeline = AnalysisPipeline(kube, self.matcher, self.explainer, self.events, self.storage, self.status,
                                          self.pool, self.metrics, log_container=s.watch.log_container,
                                          log_previous=s.watch.log_previous, log_limit_bytes=s.watch.log_limit_bytes)
@@ -142,7 +146,7 @@ class Operator:
             return len(ps)
 
     def _engine_ready(self) -> tuple[str, bool]:
-        ok = self.matcher is not None and (self.explainer is None or getattr(self.explainer, "ready", lambda: True)())
+        ok = self.matcher is not None and self.explainer.ready()
         return "analysis-engine", bool(ok)
 
     # ------------------------------------------------------------------ lifecycle
