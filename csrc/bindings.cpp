@@ -286,7 +286,7 @@ void attn_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tenso
 
 void attn_prefill(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor& o,
                   const at::Tensor& cu_seqlens, const at::Tensor& work_seq, const at::Tensor& work_q0,
-                  double scale) {
+                  double scale, int64_t block_q) {
   CHECK_DEV(q); for (auto* t : {&q, &k, &v}) { CHECK_BF16(*t); CHECK_CONTIG(*t); }
   CHECK_BF16(o); CHECK_CONTIG(o);
   for (auto* t : {&cu_seqlens, &work_seq, &work_q0}) { CHECK_DT(*t, at::kInt); CHECK_CONTIG(*t); }
@@ -297,7 +297,7 @@ void attn_prefill(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
   const c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
   RC(oamd::attn_prefill(ptr<bf16_t>(q), ptr<bf16_t>(k), ptr<bf16_t>(v), ptr<bf16_t>(o), ptr<int>(cu_seqlens),
                         ptr<int>(work_seq), ptr<int>(work_q0), (int)work_seq.numel(), (int)q.size(1),
-                        (int)k.size(1), 128, (float)scale, cur_stream()));
+                        (int)k.size(1), 128, (float)scale, (int)block_q, cur_stream()));
 }
 
 void sample(const at::Tensor& logits, const at::Tensor& temperature, const at::Tensor& seeds,
@@ -348,7 +348,10 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("stages") = 3);
   m.def("gemm_skinny", &gemm_skinny, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"),
         pybind11::arg("p") = pybind11::none(), pybind11::arg("splits") = 1, pybind11::arg("silu_gu") = false);
-  m.def("attn_prefill", &attn_prefill);
+  m.def("attn_prefill", &attn_prefill, pybind11::arg("q"), pybind11::arg("k"), pybind11::arg("v"),
+        pybind11::arg("o"), pybind11::arg("cu_seqlens"), pybind11::arg("work_seq"), pybind11::arg("work_q0"),
+        pybind11::arg("scale"), pybind11::arg("block_q") = 64);
+  m.def("attn_prefill_block_q", &oamd::attn_prefill_block_q);
   m.def("sample", &sample, pybind11::arg("logits"), pybind11::arg("temperature"), pybind11::arg("seeds"),
         pybind11::arg("positions"), pybind11::arg("out"), pybind11::arg("col_offset") = 0,
         pybind11::arg("out_val") = pybind11::none());

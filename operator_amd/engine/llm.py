@@ -319,12 +319,13 @@ class LLMEngine:
             slots.extend(self.kv.slots_for(r.pages, 0, n))
             lens.append(n)
             last.append(len(ids) - 1)
-        ws, wq = ops.prefill_work_list(lens)
+        bq = ops.prefill_block_q(self.model.hq, self.model.hkv)
+        ws, wq = ops.prefill_work_list(lens, bq)
         cu = [0]
         for L in lens:
             cu.append(cu[-1] + L)
         t = lambda x, dt=torch.long: torch.tensor(x, dtype=dt).to(dev, non_blocking=True)  # noqa: E731
-        work = (t(cu, torch.int32), t(ws, torch.int32), t(wq, torch.int32)) if dev.type == "cuda" else None
+        work = (t(cu, torch.int32), t(ws, torch.int32), t(wq, torch.int32), bq) if dev.type == "cuda" else None
         fb = ForwardBatch(t(ids), t(pos), t(slots), True, t(last), seq_lens=lens, prefill_work=work)
         logits = self.model.forward(fb, self.kv)
         toks = self.model.sample(logits, t([r.temperature for r in batch], torch.float32),

@@ -102,6 +102,8 @@ class FakeKube:
             self._faults[(verb, plural)].extend([code] * times)
 
     def _fault(self, verb: str, res: Resource) -> None:
+        if not self._faults.get((verb, res.plural)):   # fast path: nothing injected (no lock round trip)
+            return
         with self._lock:
             lst = self._faults.get((verb, res.plural))
             if lst:

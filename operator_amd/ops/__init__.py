@@ -17,7 +17,7 @@ from ._native import kernels, native_available, patterns
 
 __all__ = [
     "rmsnorm", "silu_mul", "embedding", "rope_kv", "attn_prefill", "attn_decode", "sample",
-    "kernels", "patterns", "native_available", "reference", "prefill_work_list", "decode_splits",
+    "kernels", "patterns", "native_available", "reference", "prefill_work_list", "prefill_block_q", "decode_splits",
     "decode_workspace", "linear", "gemm_splits", "gemm_plan", "gate_up_silu", "interleave_gate_up",
     "quantize_fp8", "linear_fp8", "fp8_plan", "SplitK",
 ]
@@ -155,8 +155,18 @@ def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, cos: torch.Tensor, sin: torch.
     return q, k, v
 
 
+def prefill_block_q(Hq: int, Hkv: int) -> int:
+    """Query rows per attn_prefill work item: 16 x (8 / G) for the GQA-grouped kernel
+    (G = Hq / Hkv in 1, 2, 4, 8: one block per KV head, all G query heads), else 64
+    (the per-query-head kernel; also forced by OAMD_PREFILL_ATTN=v1)."""
+    G = Hq // Hkv if Hkv and Hq % Hkv == 0 else 0
+    if G in (1, 2, 4, 8) and os.environ.get("OAMD_PREFILL_ATTN", "v2") != "v1":
+        return 16 * (8 // G)
+    return 64
+
+
 def prefill_work_list(seq_lens: list[int], block_q: int = 64) -> tuple[list[int], list[int]]:
-    """(work_seq, work_q0) for attn_prefill: one item per 64-row query block; longest first."""
+    """(work_seq, work_q0) for attn_prefill: one item per ``block_q``-row query block; longest first."""
     items = []
     for s, L in enumerate(seq_lens):
         for q0 in range(0, L, block_q):
@@ -179,11 +189,12 @@ def attn_prefill(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, seq_lens: li
         return r
     o = out if out is not None else torch.empty_like(q)
     if work is None:
-        ws, wq = prefill_work_list([int(x) for x in seq_lens])
+        bq = prefill_block_q(q.shape[1], k.shape[1])
+        ws, wq = prefill_work_list([int(x) for x in seq_lens], bq)
         dev = q.device
         work = (torch.tensor(cu, dtype=torch.int32, device=dev), torch.tensor(ws, dtype=torch.int32, device=dev),
-                torch.tensor(wq, dtype=torch.int32, device=dev))
-    kernels().attn_prefill(q, k, v, o, work[0], work[1], work[2], scale)
+                torch.tensor(wq, dtype=torch.int32, device=dev), bq)
+    kernels().attn_prefill(q, k, v, o, work[0], work[1], work[2], scale, work[3] if len(work) > 3 else 64)
     return o
 
 
