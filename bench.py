@@ -54,6 +54,8 @@ def parse_args():
     ap.add_argument("--prefill-tokens", type=int, default=16384, help="max tokens per prefill batch")
     ap.add_argument("--mode", choices=["pipeline", "engine"], default="pipeline")
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--serial-waves", action="store_true",
+                    help="wait for every sink write of a wave before writing the next one")
     ap.add_argument("--kv-gb", type=float, default=None, help="KV-cache budget (default 96 GB on GPU, 1 GB on CPU)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
@@ -114,7 +116,30 @@ def main() -> int:
     if a.mode == "pipeline":
         fk = FakeKube()
         matcher = LocalMatchService(meng, max_batch=64, max_wait_ms=5.0)
-        op = Operator(fk, s, match_service=matcher, explain_service=explainer)
+        explained = {"n": 0}
+        exp_cv = threading.Condition()
+
+        def count_explained() -> None:
+            with exp_cv:
+                explained["n"] += 1
+                exp_cv.notify_all()
+
+        class CountingExplainer:
+            """Counts generated explanations: the hand-off point between pipelined waves."""
+
+            def __init__(self, inner):
+                self.inner = inner
+
+            def explain(self, result, cfg):
+                try:
+                    return self.inner.explain(result, cfg)
+                finally:
+                    count_explained()
+
+            def ready(self):
+                return self.inner.ready()
+
+        op = Operator(fk, s, match_service=matcher, explain_service=CountingExplainer(explainer))
         fk.create(AIPROVIDERS, {"metadata": {"name": "local-llm", "namespace": "default"},
                                 "spec": {"providerId": "local", "modelId": a.model, "maxTokens": a.max_tokens,
                                          "temperature": 0.3, "cachingEnabled": False,
@@ -125,6 +150,8 @@ def main() -> int:
 
         def on_done(monitor, pod, outcome):
             name = pod["metadata"]["name"]
+            if outcome not in ("ai-complete", "ai-failed"):   # never reached the explainer
+                count_explained()
             with lock:
                 lat.append(time.perf_counter() - t_inject.get(name, time.perf_counter()))
                 counter["n"] += 1
@@ -137,20 +164,44 @@ def main() -> int:
         while not op.monitors.list():
             time.sleep(0.01)
 
-        def run_wave(w: int) -> None:
-            with lock:
-                counter["n"], counter["target"] = 0, a.batch
-                done_ev.clear()
+        def inject(w: int) -> None:
             names = [f"app-r{rank}-w{w}-{i}" for i in range(a.batch)]
             for name, log in zip(names, logs[w]):
                 fk.create(PODS, running_pod(name, labels={"app": "bench"}))
                 fk.set_log("default", name, log)
-            now = time.perf_counter()
             for name in names:
                 cur = fk.get(PODS, name, "default")
                 cur["status"] = failed_pod(name, finished_at=f"2025-08-29T10:{w % 60:02d}:00Z")["status"]
                 t_inject[name] = time.perf_counter()
                 fk.replace(PODS, cur)
+
+        def run_wave(w: int) -> None:
+            with lock:
+                counter["n"], counter["target"] = 0, a.batch
+                done_ev.clear()
+            inject(w)
+            done_ev.wait()
+            op.drain(600)
+
+        def run_timed(ws: list[int]) -> None:
+            """Pipelined waves (default): wave w+1 is written to the API server as soon as
+            every explanation of wave w has been generated, so its scan / prefill overlap
+            wave w's result sinks (annotations, status ring, Events) instead of waiting
+            behind them, as under a steady stream of failures. Every wave still completes
+            (all analyses stored, kube writes drained) inside the timed region."""
+            if a.serial_waves:
+                for w in ws:
+                    run_wave(w)
+                return
+            with lock:
+                counter["n"], counter["target"] = 0, a.batch * len(ws)
+                done_ev.clear()
+            base = explained["n"]
+            for j, w in enumerate(ws):
+                inject(w)
+                if j + 1 < len(ws):
+                    with exp_cv:
+                        exp_cv.wait_for(lambda: explained["n"] >= base + (j + 1) * a.batch)
             done_ev.wait()
             op.drain(600)
     else:
@@ -169,6 +220,10 @@ def main() -> int:
                 lat.append(time.perf_counter() - t0)
             counter["outcomes"]["ai-complete"] = counter["outcomes"].get("ai-complete", 0) + len(outs)
 
+        def run_timed(ws: list[int]) -> None:
+            for w in ws:
+                run_wave(w)
+
     for w in range(a.warmup):
         run_wave(w)
     lat.clear()
@@ -184,8 +239,7 @@ def main() -> int:
     sync()
     t0 = time.perf_counter()
     mono0 = time.monotonic_ns()  # same clock as rocprofv3 timestamps: lets a trace be cut to the timed region
-    for w in range(a.warmup, waves):
-        run_wave(w)
+    run_timed(list(range(a.warmup, waves)))
     sync()
     elapsed = time.perf_counter() - t0
     mono1 = time.monotonic_ns()
@@ -210,7 +264,8 @@ def main() -> int:
         "config": {"model": a.model, "global_batch": a.batch * world, "seq_len": a.prompt_tokens + a.max_tokens,
                    "parallelism": f"dp{world}", "tp": 1, "max_tokens": a.max_tokens,
                    "prompt_tokens_cap": a.prompt_tokens, "log_kib": a.log_kb, "patterns": a.patterns,
-                   "mode": a.mode, "hipgraph": bool(llm.use_graphs)},
+                   "mode": a.mode, "hipgraph": bool(llm.use_graphs),
+                   "waves": "serial" if (a.serial_waves or a.mode != "pipeline") else "pipelined"},
         "detail": {"init_s": round(init_s, 1), "prefill_tokens_per_gpu": ptoks, "decode_tokens_per_gpu": dtoks,
                    "decode_tok_s_per_gpu": round(dtoks / elapsed, 1), "outcomes": counter["outcomes"],
                    "dfa_states": getattr(meng, "dfa_states", None), "timed_monotonic_ns": [mono0, mono1]},

@@ -39,14 +39,32 @@ __global__ void __launch_bounds__(1024) sample_kernel(const T* __restrict__ logi
                        (static_cast<uint64_t>(positions[row]) << 32);
   float bv = -INFINITY;
   int bi = 0x7fffffff;
-  for (int i = threadIdx.x; i < vocab; i += blockDim.x) {
-    float x = load_logit<T>(lr, i);
+  auto visit = [&](float x, int i) {
     if (!greedy) {
       const float u = uniform01(key + static_cast<uint64_t>(i + col_offset));
       x = x * inv_t - __logf(-__logf(u));
     }
     argmax_merge(bv, bi, x, i);
+  };
+  // 16-B loads over the aligned body of the row (8 bf16 / 4 fp32 per lane), scalar tail.
+  // argmax_merge is a total order (value, then smaller index), so the visiting order
+  // does not change the result.
+  constexpr int VEC = 16 / static_cast<int>(sizeof(T));
+  const int nv = (reinterpret_cast<uintptr_t>(lr) & 15) == 0 ? vocab / VEC : 0;
+  for (int v = threadIdx.x; v < nv; v += blockDim.x) {
+    const uint4 raw = reinterpret_cast<const uint4*>(lr)[v];
+    const uint32_t wv[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if constexpr (sizeof(T) == 2) {
+        visit(__uint_as_float(wv[k] << 16), VEC * v + 2 * k);
+        visit(__uint_as_float(wv[k] & 0xffff0000u), VEC * v + 2 * k + 1);
+      } else {
+        visit(__uint_as_float(wv[k]), VEC * v + k);
+      }
+    }
   }
+  for (int i = nv * VEC + threadIdx.x; i < vocab; i += blockDim.x) visit(load_logit<T>(lr, i), i);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const float ov = __shfl_xor(bv, o, kWave);

@@ -106,7 +106,9 @@ class EventEmitter:
         pod_ns = (pod.get("metadata") or {}).get("namespace")
         self._submit(self._emit, pod, pod_ns, reason, message, typ)
         self._submit(self._emit, monitor, (monitor.get("metadata") or {}).get("namespace"), reason, message, typ)
-        self._submit(self._emit_to_deployment, pod, pod_ns, reason, message, typ)
+        owners = (pod.get("metadata") or {}).get("ownerReferences") or []
+        if any((o or {}).get("kind") == "ReplicaSet" for o in owners):   # else no Deployment to find
+            self._submit(self._emit_to_deployment, pod, pod_ns, reason, message, typ)
 
     def _emit_to_deployment(self, pod: dict, ns: str, reason: str, message: str, typ: str) -> None:
         dep = self.find_owning_deployment(pod)

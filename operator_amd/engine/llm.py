@@ -24,6 +24,7 @@ import time
 from collections import deque
 from dataclasses import dataclass, field
 
+import numpy as np
 import torch
 
 from operator_amd import ops
@@ -311,20 +312,20 @@ class LLMEngine:
     def _prefill_impl(self, batch: list[GenRequest]) -> None:
         t0 = time.perf_counter()
         dev = self.device
-        ids, pos, slots, lens, last = [], [], [], [], []
-        for r in batch:
-            n = len(r.prompt)
-            ids.extend(r.prompt)
-            pos.extend(range(n))
-            slots.extend(self.kv.slots_for(r.pages, 0, n))
-            lens.append(n)
-            last.append(len(ids) - 1)
+        # packed token ids / positions / cache slots built with numpy: this runs on the
+        # engine thread between prefill batches, while the GPU waits for it
+        P = self.kv.page_size
+        lens = [len(r.prompt) for r in batch]
+        ar = [np.arange(n, dtype=np.int64) for n in lens]
+        ids = np.concatenate([np.asarray(r.prompt, dtype=np.int64) for r in batch])
+        pos = np.concatenate(ar)
+        slots = np.concatenate([np.asarray(r.pages, dtype=np.int64)[a // P] * P + a % P for r, a in zip(batch, ar)])
+        cu = np.zeros(len(lens) + 1, dtype=np.int64)
+        cu[1:] = np.cumsum(lens)
+        last = cu[1:] - 1
         bq = ops.prefill_block_q(self.model.hq, self.model.hkv)
         ws, wq = ops.prefill_work_list(lens, bq)
-        cu = [0]
-        for L in lens:
-            cu.append(cu[-1] + L)
-        t = lambda x, dt=torch.long: torch.tensor(x, dtype=dt).to(dev, non_blocking=True)  # noqa: E731
+        t = lambda x, dt=torch.long: torch.as_tensor(np.asarray(x)).to(dtype=dt).to(dev, non_blocking=True)  # noqa: E731
         work = (t(cu, torch.int32), t(ws, torch.int32), t(wq, torch.int32), bq) if dev.type == "cuda" else None
         fb = ForwardBatch(t(ids), t(pos), t(slots), True, t(last), seq_lens=lens, prefill_work=work)
         logits = self.model.forward(fb, self.kv)

@@ -14,6 +14,7 @@ CPU path: the same post-processing fed by the pure-Python oracle.
 """
 from __future__ import annotations
 
+import contextlib
 import threading
 import time
 import uuid
@@ -117,6 +118,15 @@ class MatchEngine:
         self._verify = np.asarray(self.cp.matcher_verify + [False], dtype=bool)
         if self.device.type == "cuda" and self.cp.factors:
             self._upload_dfa()
+        # Scans run on a stream of their own: the LLM engine keeps the default stream
+        # busy with prefill/decode work, and a scan (and its result read-back) queued
+        # behind that would wait for the whole queue before the prompt can be built.
+        self._stream = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
+        if self._stream is not None:
+            torch.cuda.synchronize(self.device)   # DFA tables uploaded before the first scan
+
+    def _on_stream(self):
+        return torch.cuda.stream(self._stream) if self._stream is not None else contextlib.nullcontext()
 
     # ------------------------------------------------------------------ DFA upload
     def _upload_dfa(self) -> None:
@@ -148,7 +158,7 @@ class MatchEngine:
         """Raw factor hits as int64 array [n, 4] = (doc, factor, line, end_offset_in_doc)."""
         from operator_amd.utils.tracing import trace_range
 
-        with trace_range(f"scan[{len(docs)}]"):
+        with trace_range(f"scan[{len(docs)}]"), self._on_stream():
             return self._scan_gpu(docs)
 
     def _scan_gpu(self, docs: list[bytes]) -> np.ndarray:
@@ -323,7 +333,8 @@ class MatchEngine:
         hits, offs = self.hits(docs)
         cp = self.cp
         if self.gpu_scorer and self.device.type == "cuda":
-            return self._events_gpu(hits, len(docs)), offs
+            with self._on_stream():
+                return self._events_gpu(hits, len(docs)), offs
         if self.use_native_scorer:
             from operator_amd.ops import patterns
 
