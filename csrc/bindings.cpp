@@ -286,7 +286,7 @@ void attn_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tenso
 
 void attn_prefill(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor& o,
                   const at::Tensor& cu_seqlens, const at::Tensor& work_seq, const at::Tensor& work_q0,
-                  double scale, int64_t block_q) {
+                  double scale, int64_t variant) {
   CHECK_DEV(q); for (auto* t : {&q, &k, &v}) { CHECK_BF16(*t); CHECK_CONTIG(*t); }
   CHECK_BF16(o); CHECK_CONTIG(o);
   for (auto* t : {&cu_seqlens, &work_seq, &work_q0}) { CHECK_DT(*t, at::kInt); CHECK_CONTIG(*t); }
@@ -297,7 +297,7 @@ void attn_prefill(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
   const c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
   RC(oamd::attn_prefill(ptr<bf16_t>(q), ptr<bf16_t>(k), ptr<bf16_t>(v), ptr<bf16_t>(o), ptr<int>(cu_seqlens),
                         ptr<int>(work_seq), ptr<int>(work_q0), (int)work_seq.numel(), (int)q.size(1),
-                        (int)k.size(1), 128, (float)scale, (int)block_q, cur_stream()));
+                        (int)k.size(1), 128, (float)scale, (int)variant, cur_stream()));
 }
 
 void sample(const at::Tensor& logits, const at::Tensor& temperature, const at::Tensor& seeds,

@@ -1,7 +1,10 @@
 // Causal flash attention for prefill, variable-length packed sequences, GQA,
-// on MFMA.
+// on MFMA. Three variants share the work-list contract
+// (attn_prefill_block_q): v1 per-query-head (below), v2 GQA-grouped 16-row waves
+// with a software-pipelined K/V tile, v3 GQA-grouped swapped-operand 32x32 MFMA
+// waves (S^T = K Q^T, P stays in registers as the next MFMA's B operand).
 //
-// Work item = (64-row query block of one sequence, query head). 4 waves; each
+// v1 work item = (64-row query block of one sequence, query head). 4 waves; each
 // wave owns 16 query rows. Per 64-key tile:
 //   S = Q K^T      16 x v_mfma_f32_16x16x32_bf16 per wave (Q in registers)
 //   online softmax in the C-fragment layout (row max/sum over 16 lanes)
@@ -366,37 +369,240 @@ __global__ void __launch_bounds__(512) attn_prefill_gqa_kernel(
   }
 }
 
-int attn_prefill_block_q(int Hq, int Hkv) {
-  if (Hkv <= 0 || Hq % Hkv != 0) return 64;
+// ---------------------------------------------------------------------------
+// v3: swapped-operand 32x32 MFMA kernel (cdna_hip_programming.md §3
+// "accumulator tile as the next MFMA's operand", §5.5 T10/T12). Block = (32 x RG
+// query rows, one KV head), 8 waves; wave w computes query head kvh * G + (w % G)
+// for 32 rows starting 32 (w / G). Per 64-key tile:
+//   S^T = K Q^T   v_mfma_f32_32x32x16_bf16, A = K rows from LDS, B = Q^T held in
+//                 registers; the result has the query row on the lane and the keys
+//                 in the 16 accumulator registers, so the softmax row max/sum is
+//                 lane-local (one lane^32 exchange per tile for the max, none for
+//                 the sum, which stays a per-lane partial until the epilogue)
+//   O^T += V^T P^T  the S^T accumulator converted to bf16 IS the B operand (no LDS
+//                 bounce for P); V^T comes from the row-major V tile with
+//                 ds_read_b64_tr_b16 (hardware transpose)
+// A 32-row wave reads each staged K/V byte from LDS once per 32 rows instead of
+// once per 16 (v2), halving LDS read traffic per MFMA, and both tiles are staged
+// with plain 16-B row writes (v2 scattered V with 2-B transposing writes).
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+
+// K tile image: 256-B rows, chunk ch of row r at 16 * (ch ^ (r & 15)) -> the
+// ds_read_b128 of 16 consecutive rows at one chunk hits 16 distinct chunk slots.
+__device__ __forceinline__ int k_img(int r, int ch) { return 256 * r + 16 * (ch ^ (r & 15)); }
+// V tile image (§5.5 T10 image (b)): conflict-free for the 32x32x16 transposed reads.
+__device__ __forceinline__ int v_img(int r, int ch) { return 256 * r + 16 * (ch ^ (((r & 3) << 2) | ((r >> 2) & 3))); }
+
+__device__ __forceinline__ s16x4 ds_read_tr16(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
+}
+
+template <int G>
+__global__ void __launch_bounds__(512) attn_prefill_mfma32_kernel(
+    const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+    bf16_t* __restrict__ o, const int* __restrict__ cu_seqlens, const int* __restrict__ work_seq,
+    const int* __restrict__ work_q0, int Hq, int Hkv, float scale_log2) {
+  constexpr int D = 128, BK = 64, RG = 8 / G, BQ = 32 * RG;
+  __shared__ __attribute__((aligned(16))) char Ks[BK * 256];
+  __shared__ __attribute__((aligned(16))) char Vs[BK * 256];
+
+  const int wi = blockIdx.x, kvh = blockIdx.y;
+  const int seq = work_seq[wi];
+  const int s0 = cu_seqlens[seq];
+  const int slen = cu_seqlens[seq + 1] - s0;
+  const int q0 = work_q0[wi];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r32 = lane & 31, h = lane >> 5;
+  const int hq = kvh * G + (w % G);
+  const int rbase = q0 + 32 * (w / G);  // this wave's first query row
+  const int qrow = rbase + r32;          // this lane's query row (C column)
+
+  // Q^T as the B operand: k-step s covers d = 16s .. 16s+15; lane holds d = 16s + 8h + j
+  u16x8 qb[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s)
+    qb[s] = qrow < slen ? *reinterpret_cast<const u16x8*>(q + ((int64_t)(s0 + qrow) * Hq + hq) * D + 16 * s + 8 * h)
+                        : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  f32x16 oacc[4];
+#pragma unroll
+  for (int dd = 0; dd < 4; ++dd)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) oacc[dd][i] = 0.f;
+  float mrow = -INFINITY, lpart = 0.f;
+
+  const int kend = min(slen, q0 + BQ);
+  const int ntiles = (kend + BK - 1) / BK;
+  const bool active = rbase < slen;
+  const int wend = min(slen, rbase + 32);  // keys this wave can see: < wend
+
+  // transposed-read addressing: 16-lane group g reads rows r0 + q (q = i >> 2) at
+  // columns d0 + 4p .. +3 (p = i & 3), d0 = 32 dd + 16 (g & 1); lane i gets column d0 + i
+  const int gi = lane & 15, g = lane >> 4;
+  const int trq = gi >> 2, trp = gi & 3;
+
+  u16x8 kr[2], vr[2];
+  auto load_tile = [&](int kb) {
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int c = tid + r * 512;
+      const int key = c >> 4, ch = c & 15;
+      kr[r] = vr[r] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (kb + key < slen) {
+        const int64_t off = ((int64_t)(s0 + kb + key) * Hkv + kvh) * D + ch * 8;
+        kr[r] = *reinterpret_cast<const u16x8*>(k + off);
+        vr[r] = *reinterpret_cast<const u16x8*>(v + off);
+      }
+    }
+  };
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int c = tid + r * 512;
+      const int key = c >> 4, ch = c & 15;
+      *reinterpret_cast<u16x8*>(Ks + k_img(key, ch)) = kr[r];
+      *reinterpret_cast<u16x8*>(Vs + v_img(key, ch)) = vr[r];
+    }
+  };
+
+  load_tile(0);
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const int kb = kt * BK;
+    __syncthreads();  // previous tile fully consumed
+    store_tile();
+    __syncthreads();
+    if (kt + 1 < ntiles) load_tile(kb + BK);  // in flight during this tile's MFMAs
+    if (!active || kb >= wend) continue;      // wave-uniform: no visible key for this wave
+
+    // ---- S^T = K Q^T (two 32-key blocks) ----
+    f32x16 sacc[2];
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sacc[b][i] = 0.f;
+      const int key = 32 * b + r32;
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const u16x8 ka = *reinterpret_cast<const u16x8*>(Ks + k_img(key, 2 * s + h));
+        sacc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(ka), as_bf8(qb[s]), sacc[b], 0, 0, 0);
+      }
+    }
+    // ---- online softmax: register i of block b is key kb + 32b + (i&3) + 8(i>>2) + 4h ----
+    const bool mask = (kb + BK > rbase + 1) || (kb + BK > slen);
+    float mx = -INFINITY;
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float sv = sacc[b][i] * scale_log2;
+        if (mask) {
+          const int key = kb + 32 * b + (i & 3) + 8 * (i >> 2) + 4 * h;
+          if (key > qrow || key >= slen) sv = -INFINITY;
+        }
+        sacc[b][i] = sv;
+        mx = fmaxf(mx, sv);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
+    const float mnew = fmaxf(mrow, mx);
+    const float msafe = (mnew == -INFINITY) ? 0.f : mnew;
+    const float alpha = exp2f(mrow - msafe);
+    mrow = mnew;
+    float rs = 0.f;
+    u16x8 pb[2][2];
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        f32x8 p;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          p[j] = exp2f(sacc[b][8 * s + j] - msafe);
+          rs += p[j];
+        }
+        pb[b][s] = __builtin_bit_cast(u16x8, __builtin_convertvector(p, bf16x8_t));
+      }
+    lpart = lpart * alpha + rs;
+#pragma unroll
+    for (int dd = 0; dd < 4; ++dd)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) oacc[dd][i] *= alpha;
+
+    // ---- O^T += V^T P^T: B element j of half h is key 32b + 16s + 8(j>>2) + 4h + (j&3) ----
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int r0 = 32 * b + 16 * s + 4 * h + trq;
+#pragma unroll
+        for (int dd = 0; dd < 4; ++dd) {
+          const int d = 32 * dd + 16 * (g & 1) + 4 * trp;
+          const s16x4 lo = ds_read_tr16(Vs + v_img(r0, d >> 3) + 8 * ((d >> 2) & 1));
+          const s16x4 hi = ds_read_tr16(Vs + v_img(r0 + 8, d >> 3) + 8 * ((d >> 2) & 1));
+          const s16x8 va = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+          oacc[dd] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, va),
+                                                            as_bf8(pb[b][s]), oacc[dd], 0, 0, 0);
+        }
+      }
+  }
+  if (!active) return;
+  const float lsum = lpart + __shfl_xor(lpart, 32, kWave);
+  if (qrow >= slen) return;
+  const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+  bf16_t* dst = o + ((int64_t)(s0 + qrow) * Hq + hq) * D;
+  // O^T register i of d-block dd is d = 32 dd + (i&3) + 8(i>>2) + 4h: 4 contiguous d per 8-B store
+#pragma unroll
+  for (int dd = 0; dd < 4; ++dd)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      u16x4 st;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) st[e] = f2bf(oacc[dd][4 * c + e] * inv);
+      *reinterpret_cast<u16x4*>(dst + 32 * dd + 8 * c + 4 * h) = st;
+    }
+}
+
+// Query rows per work item of each variant: 1 = per-query-head (64 rows, any G),
+// 2 = GQA-grouped 16-row waves, 3 = GQA-grouped swapped 32x32 (32-row waves);
+// 2 and 3 need G = Hq / Hkv in {1, 2, 4, 8} (else -1).
+int attn_prefill_block_q(int Hq, int Hkv, int variant) {
+  if (variant == 1) return 64;
+  if (Hkv <= 0 || Hq % Hkv != 0) return -1;
   const int G = Hq / Hkv;
-  return (G == 1 || G == 2 || G == 4 || G == 8) ? 16 * (8 / G) : 64;
+  if (G != 1 && G != 2 && G != 4 && G != 8) return -1;
+  if (variant == 2) return 16 * (8 / G);
+  if (variant == 3) return 32 * (8 / G);
+  return -1;
 }
 
 int attn_prefill(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, const int* cu_seqlens,
                  const int* work_seq, const int* work_q0, int num_work, int Hq, int Hkv, int head_dim,
-                 float scale, int block_q, hipStream_t stream) {
+                 float scale, int variant, hipStream_t stream) {
   if (num_work == 0) return 0;
   if (head_dim != 128) return -1;
   if (Hq % Hkv != 0) return -3;
+  if (attn_prefill_block_q(Hq, Hkv, variant) < 0) return -4;
   const float sl2 = scale * 1.4426950408889634f;
   const int G = Hq / Hkv;
-  const bool gqa = (G == 1 || G == 2 || G == 4 || G == 8) && block_q == 16 * (8 / G);
-  if (gqa) {
-    dim3 grid(num_work, Hkv);
-#define OAMD_PF2(GG) \
-  attn_prefill_gqa_kernel<GG><<<grid, 512, 0, stream>>>(q, k, v, o, cu_seqlens, work_seq, work_q0, Hq, Hkv, sl2)
-    switch (G) {
-      case 1: OAMD_PF2(1); break;
-      case 2: OAMD_PF2(2); break;
-      case 4: OAMD_PF2(4); break;
-      default: OAMD_PF2(8); break;
-    }
-#undef OAMD_PF2
-  } else if (block_q == 64) {
+  if (variant == 1) {
     dim3 grid(num_work, Hq);
     attn_prefill_kernel<<<grid, 256, 0, stream>>>(q, k, v, o, cu_seqlens, work_seq, work_q0, Hq, Hkv, sl2);
   } else {
-    return -4;
+    dim3 grid(num_work, Hkv);
+#define OAMD_PF(KERN, GG) KERN<GG><<<grid, 512, 0, stream>>>(q, k, v, o, cu_seqlens, work_seq, work_q0, Hq, Hkv, sl2)
+#define OAMD_PF_G(KERN)            \
+  switch (G) {                     \
+    case 1: OAMD_PF(KERN, 1); break; \
+    case 2: OAMD_PF(KERN, 2); break; \
+    case 4: OAMD_PF(KERN, 4); break; \
+    default: OAMD_PF(KERN, 8); break; \
+  }
+    if (variant == 2) {
+      OAMD_PF_G(attn_prefill_gqa_kernel)
+    } else {
+      OAMD_PF_G(attn_prefill_mfma32_kernel)
+    }
+#undef OAMD_PF_G
+#undef OAMD_PF
   }
   OAMD_LAUNCH_CHECK();
   return 0;

@@ -51,13 +51,13 @@ int attn_decode(const bf16_t* q, const bf16_t* k_cache, const bf16_t* v_cache, c
                 const int* seq_lens, bf16_t* out, float* o_part, float* ml_part, int B, int Hq, int Hkv,
                 int head_dim, int page_size, int max_pages, int num_splits, float scale, int variant,
                 hipStream_t stream);
-// Causal prefill attention; the work list holds one item per block_q query rows of a sequence:
-// block_q == attn_prefill_block_q(Hq, Hkv) selects the GQA-grouped kernel (grid over KV heads),
-// block_q == 64 the per-query-head kernel.
-int attn_prefill_block_q(int Hq, int Hkv);
+// Causal prefill attention; the work list holds one item per attn_prefill_block_q(Hq, Hkv, variant)
+// query rows of a sequence. variant 1 = per-query-head kernel (64 rows), 2 = GQA-grouped 16-row
+// waves, 3 = GQA-grouped swapped-operand 32x32 MFMA waves (2 and 3 need Hq / Hkv in {1, 2, 4, 8}).
+int attn_prefill_block_q(int Hq, int Hkv, int variant);
 int attn_prefill(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, const int* cu_seqlens,
                  const int* work_seq, const int* work_q0, int num_work, int Hq, int Hkv, int head_dim,
-                 float scale, int block_q, hipStream_t stream);
+                 float scale, int variant, hipStream_t stream);
 int sample_tokens(const void* logits, bool logits_bf16, int64_t stride, int rows, int vocab,
                   const float* temperature, const int64_t* seeds, const int64_t* positions,
                   int64_t* out_tokens, int64_t col_offset, float* out_val, hipStream_t stream);

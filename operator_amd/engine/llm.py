@@ -323,10 +323,10 @@ class LLMEngine:
         cu = np.zeros(len(lens) + 1, dtype=np.int64)
         cu[1:] = np.cumsum(lens)
         last = cu[1:] - 1
-        bq = ops.prefill_block_q(self.model.hq, self.model.hkv)
-        ws, wq = ops.prefill_work_list(lens, bq)
+        var = ops.prefill_variant(self.model.hq, self.model.hkv)
+        ws, wq = ops.prefill_work_list(lens, ops.prefill_block_q(self.model.hq, self.model.hkv, var))
         t = lambda x, dt=torch.long: torch.as_tensor(np.asarray(x)).to(dtype=dt).to(dev, non_blocking=True)  # noqa: E731
-        work = (t(cu, torch.int32), t(ws, torch.int32), t(wq, torch.int32), bq) if dev.type == "cuda" else None
+        work = (t(cu, torch.int32), t(ws, torch.int32), t(wq, torch.int32), var) if dev.type == "cuda" else None
         fb = ForwardBatch(t(ids), t(pos), t(slots), True, t(last), seq_lens=lens, prefill_work=work)
         logits = self.model.forward(fb, self.kv)
         toks = self.model.sample(logits, t([r.temperature for r in batch], torch.float32),

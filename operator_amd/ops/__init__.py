@@ -17,7 +17,7 @@ from ._native import kernels, native_available, patterns
 
 __all__ = [
     "rmsnorm", "silu_mul", "embedding", "rope_kv", "attn_prefill", "attn_decode", "sample",
-    "kernels", "patterns", "native_available", "reference", "prefill_work_list", "prefill_block_q", "decode_splits",
+    "kernels", "patterns", "native_available", "reference", "prefill_work_list", "prefill_block_q", "prefill_variant", "decode_splits",
     "decode_workspace", "linear", "gemm_splits", "gemm_plan", "gate_up_silu", "interleave_gate_up",
     "quantize_fp8", "linear_fp8", "fp8_plan", "SplitK",
 ]
@@ -155,14 +155,26 @@ def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, cos: torch.Tensor, sin: torch.
     return q, k, v
 
 
-def prefill_block_q(Hq: int, Hkv: int) -> int:
-    """Query rows per attn_prefill work item: 16 x (8 / G) for the GQA-grouped kernel
-    (G = Hq / Hkv in 1, 2, 4, 8: one block per KV head, all G query heads), else 64
-    (the per-query-head kernel; also forced by OAMD_PREFILL_ATTN=v1)."""
+_PREFILL_VARIANTS = {"v1": 1, "v2": 2, "v3": 3}
+
+
+def prefill_variant(Hq: int, Hkv: int) -> int:
+    """attn_prefill kernel variant: 1 = per-query-head (any G), 2 = GQA-grouped 16-row waves,
+    3 = GQA-grouped swapped-operand 32x32 MFMA waves (2 and 3 need G = Hq / Hkv in 1, 2, 4, 8).
+    OAMD_PREFILL_ATTN=v1|v2|v3 overrides the default (v3); grouped variants fall back to v1
+    for other G."""
     G = Hq // Hkv if Hkv and Hq % Hkv == 0 else 0
-    if G in (1, 2, 4, 8) and os.environ.get("OAMD_PREFILL_ATTN", "v2") != "v1":
-        return 16 * (8 // G)
-    return 64
+    want = _PREFILL_VARIANTS.get(os.environ.get("OAMD_PREFILL_ATTN", "v3"), 3)
+    return want if G in (1, 2, 4, 8) else 1
+
+
+def prefill_block_q(Hq: int, Hkv: int, variant: int | None = None) -> int:
+    """Query rows per attn_prefill work item: 64 (v1), 16 x (8 / G) (v2), 32 x (8 / G) (v3)."""
+    v = prefill_variant(Hq, Hkv) if variant is None else variant
+    if v == 1:
+        return 64
+    G = Hq // Hkv
+    return (16 if v == 2 else 32) * (8 // G)
 
 
 def prefill_work_list(seq_lens: list[int], block_q: int = 64) -> tuple[list[int], list[int]]:
@@ -189,12 +201,13 @@ def attn_prefill(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, seq_lens: li
         return r
     o = out if out is not None else torch.empty_like(q)
     if work is None:
-        bq = prefill_block_q(q.shape[1], k.shape[1])
-        ws, wq = prefill_work_list([int(x) for x in seq_lens], bq)
+        var = prefill_variant(q.shape[1], k.shape[1])
+        ws, wq = prefill_work_list([int(x) for x in seq_lens], prefill_block_q(q.shape[1], k.shape[1], var))
         dev = q.device
         work = (torch.tensor(cu, dtype=torch.int32, device=dev), torch.tensor(ws, dtype=torch.int32, device=dev),
-                torch.tensor(wq, dtype=torch.int32, device=dev), bq)
-    kernels().attn_prefill(q, k, v, o, work[0], work[1], work[2], scale, work[3] if len(work) > 3 else 64)
+                torch.tensor(wq, dtype=torch.int32, device=dev), var)
+    # work = (cu_seqlens, work_seq, work_q0, variant); the work list must be cut at that variant's block_q
+    kernels().attn_prefill(q, k, v, o, work[0], work[1], work[2], scale, work[3] if len(work) > 3 else 1)
     return o
 
 

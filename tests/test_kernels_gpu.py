@@ -74,7 +74,7 @@ def test_rope_kv_and_cache(Hq, Hkv):
 
 @pytest.mark.parametrize("lens", [[1], [17, 64, 130], [300, 5, 64]])
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 8), (16, 2), (8, 4), (64, 8)])
-@pytest.mark.parametrize("variant", ["gqa", "per-head"])
+@pytest.mark.parametrize("variant", [3, 2, 1])
 def test_attn_prefill(lens, Hq, Hkv, variant):
     torch.manual_seed(2)
     T, D = sum(lens), 128
@@ -83,10 +83,9 @@ def test_attn_prefill(lens, Hq, Hkv, variant):
     cu = [0]
     for L in lens:
         cu.append(cu[-1] + L)
-    bq = ops.prefill_block_q(Hq, Hkv) if variant == "gqa" else 64
-    ws, wq = ops.prefill_work_list(lens, bq)
+    ws, wq = ops.prefill_work_list(lens, ops.prefill_block_q(Hq, Hkv, variant))
     it = lambda x: torch.tensor(x, dtype=torch.int32, device=DEV)  # noqa: E731
-    o = ops.attn_prefill(q, k, v, lens, scale, work=(it(cu), it(ws), it(wq), bq))
+    o = ops.attn_prefill(q, k, v, lens, scale, work=(it(cu), it(ws), it(wq), variant))
     o_r = ref.attn_prefill(q.cpu(), k.cpu(), v.cpu(), cu, scale)
     torch.testing.assert_close(o.cpu().float(), o_r.float(), atol=2e-2, rtol=3e-2)
 
