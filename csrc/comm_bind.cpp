@@ -16,8 +16,8 @@ namespace {
 
 class CustomAllReduce {
  public:
-  CustomAllReduce(int64_t cap_bytes, int64_t rank, int64_t world, int64_t blocks, int64_t device)
-      : cap_(cap_bytes), rank_(rank), world_(world), blocks_(blocks), device_(device) {
+  CustomAllReduce(int64_t cap_bytes, int64_t rank, int64_t world, int64_t blocks, int64_t device, double timeout_s)
+      : cap_(cap_bytes), rank_(rank), world_(world), blocks_(blocks), device_(device), timeout_s_(timeout_s) {
     TORCH_CHECK(world >= 1 && world <= 8, "CustomAllReduce: world must be 1..8");
     TORCH_CHECK(rank >= 0 && rank < world, "CustomAllReduce: bad rank");
     TORCH_CHECK(cap_bytes > 0 && cap_bytes % 16 == 0, "CustomAllReduce: capacity must be a positive multiple of 16 B");
@@ -27,6 +27,7 @@ class CustomAllReduce {
     const int rc = oamd::car_alloc((size_t)cap_bytes, (int)world, &base_, h);
     TORCH_CHECK(rc == 0, "CustomAllReduce: buffer allocation / IPC export failed rc=", rc);
     handle_.assign(h, 64);
+    TORCH_CHECK(oamd::car_host_flag(&herr_, &herr_dev_) == 0, "CustomAllReduce: host-mapped error word failed");
     bases_.assign(world, nullptr);
     bases_[rank] = base_;
   }
@@ -59,13 +60,19 @@ class CustomAllReduce {
     const c10::hip::HIPGuardMasqueradingAsCUDA g(in.device());
     const int rc = oamd::car_all_reduce(in.data_ptr(), out.data_ptr(), bytes, in.scalar_type() == at::kBFloat16,
                                         (int)rank_, (int)world_, bases_.data(), (size_t)cap_, (int)blocks_,
-                                        c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream());
+                                        herr_dev_, timeout_s_, c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream());
     TORCH_CHECK(rc == 0, "one-shot all-reduce launch failed rc=", rc);
   }
 
-  int64_t error(bool clear) {
+  // Host read of the mapped error word: no device synchronisation, so the engine
+  // can poll it after every decode window without draining its pipelined windows.
+  int64_t error() const { return herr_ != nullptr ? oamd::car_error(herr_) : 0; }
+
+  // Collective: every rank, between two barriers, with no call in flight.
+  void reset() {
+    TORCH_CHECK(base_ != nullptr, "CustomAllReduce: closed");
     const c10::hip::HIPGuardMasqueradingAsCUDA g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device_));
-    return oamd::car_error(base_, clear ? 1 : 0);
+    TORCH_CHECK(oamd::car_reset(base_, herr_) == 0, "CustomAllReduce.reset failed");
   }
 
   void close() {
@@ -75,6 +82,9 @@ class CustomAllReduce {
     for (int64_t p = 0; p < world_; ++p)
       if (p != rank_ && bases_[p] != nullptr) (void)oamd::car_close(bases_[p]);
     (void)oamd::car_free(base_);
+    oamd::car_free_host_flag(herr_);
+    herr_ = nullptr;
+    herr_dev_ = nullptr;
     base_ = nullptr;
     bases_.assign(world_, nullptr);
     opened_ = false;
@@ -84,7 +94,10 @@ class CustomAllReduce {
 
  private:
   int64_t cap_, rank_, world_, blocks_, device_;
+  double timeout_s_;
   void* base_ = nullptr;
+  uint32_t* herr_ = nullptr;
+  uint32_t* herr_dev_ = nullptr;
   std::string handle_;
   std::vector<void*> bases_;
   bool opened_ = false;
@@ -94,12 +107,14 @@ class CustomAllReduce {
 
 void register_comm_bindings(pybind11::module_& m) {
   pybind11::class_<CustomAllReduce>(m, "CustomAllReduce")
-      .def(pybind11::init<int64_t, int64_t, int64_t, int64_t, int64_t>(), pybind11::arg("cap_bytes"),
-           pybind11::arg("rank"), pybind11::arg("world"), pybind11::arg("blocks"), pybind11::arg("device"))
+      .def(pybind11::init<int64_t, int64_t, int64_t, int64_t, int64_t, double>(), pybind11::arg("cap_bytes"),
+           pybind11::arg("rank"), pybind11::arg("world"), pybind11::arg("blocks"), pybind11::arg("device"),
+           pybind11::arg("timeout_s") = 2.0)
       .def("handle", &CustomAllReduce::handle)
       .def("open", &CustomAllReduce::open)
       .def("all_reduce", &CustomAllReduce::all_reduce)
-      .def("error", &CustomAllReduce::error, pybind11::arg("clear") = false)
+      .def("error", &CustomAllReduce::error)
+      .def("reset", &CustomAllReduce::reset)
       .def("close", &CustomAllReduce::close)
       .def_property_readonly("capacity", &CustomAllReduce::capacity);
 }

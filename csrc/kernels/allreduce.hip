@@ -23,8 +23,15 @@
 // state per call. Parity buffers make slot reuse safe: a peer can be at most
 // one round ahead (it needs this rank's flag of round r+1 to finish r+1, and
 // that flag is raised only after this rank finished reading round r).
-// Every wait is bounded (wall clock, ~2 s): a missing peer sets `err` and the
-// kernel drains instead of spinning forever.
+// Every wait is bounded (wall clock, ~2 s by default): a missing peer sets
+// `err` and the kernel drains instead of spinning forever. A timed-out block
+// never leaves a partial sum behind: it writes NaN over its output slice, and
+// the error is STICKY — every later call sees `err` at entry, poisons its whole
+// output and touches no peer — because after a timeout the per-block round
+// counters of the ranks no longer agree, so the parity-buffer reuse invariant
+// above is gone. The error is mirrored into a host-mapped word, so the engine
+// polls it after each decode window with a plain host read (no device sync)
+// and fails the TP replica; the pool respawns it with fresh buffers.
 #include <cstring>
 
 #include "common.h"
@@ -40,7 +47,7 @@ constexpr size_t kFlagsOff = 0;
 constexpr size_t kRoundsOff = 8 << 10;
 constexpr size_t kErrOff = 12 << 10;
 constexpr size_t kDataOff = 64 << 10;
-constexpr uint64_t kTimeoutTicks = 200000000ull;  // wall_clock64 runs at 100 MHz: 2 s
+constexpr uint64_t kDefaultTimeoutTicks = 200000000ull;  // wall_clock64 runs at 100 MHz: 2 s
 }  // namespace car
 
 struct CarPeers {
@@ -63,25 +70,38 @@ __device__ __forceinline__ void acc8(float* a, uint4 v, bool is_bf16) {
   }
 }
 
+// NaN over out[v0, v1): a failed call must never look like a valid sum.
+template <bool BF16>
+__device__ __forceinline__ void poison(uint4* __restrict__ out, int64_t v0, int64_t v1, int tid) {
+  const uint32_t nan = BF16 ? 0x7FC07FC0u : 0x7FC00000u;
+  for (int64_t v = v0 + tid; v < v1; v += car::kThreads) out[v] = make_uint4(nan, nan, nan, nan);
+}
+
 // One 16-B vector = 8 bf16 or 4 fp32 elements.
 template <int W, bool BF16>
 __global__ void __launch_bounds__(car::kThreads) oneshot_allreduce_kernel(const uint4* __restrict__ in,
                                                                           uint4* __restrict__ out, int64_t nvec,
-                                                                          int64_t capvec, int rank, CarPeers peers) {
+                                                                          int64_t capvec, int rank, CarPeers peers,
+                                                                          uint32_t* herr, uint64_t timeout_ticks) {
   __shared__ uint32_t s_round;
   __shared__ uint32_t s_err;
   const int b = blockIdx.x, tid = threadIdx.x;
   char* mine = peers.base[rank];
   uint32_t* rounds = reinterpret_cast<uint32_t*>(mine + car::kRoundsOff);
+  uint32_t* err = reinterpret_cast<uint32_t*>(mine + car::kErrOff);
   if (tid == 0) {
     s_round = rounds[b] + 1;
-    s_err = 0;
+    s_err = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   __syncthreads();
   const uint32_t round = s_round;
   const int par = round & 1;
   const int64_t per = (nvec + gridDim.x - 1) / gridDim.x;
   const int64_t v0 = min(nvec, per * b), v1 = min(nvec, v0 + per);
+  if (s_err) {   // sticky: an earlier call timed out, the ranks are out of step
+    poison<BF16>(out, v0, v1, tid);
+    return;
+  }
 
   // ---- push: my slice of `in` into slot [par][rank] of every rank (me included)
   for (int64_t v = v0 + tid; v < v1; v += car::kThreads) {
@@ -104,7 +124,7 @@ __global__ void __launch_bounds__(car::kThreads) oneshot_allreduce_kernel(const 
     const uint64_t t0 = (uint64_t)wall_clock64();
     while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < round) {
       __builtin_amdgcn_s_sleep(2);
-      if ((uint64_t)wall_clock64() - t0 > car::kTimeoutTicks) {
+      if ((uint64_t)wall_clock64() - t0 > timeout_ticks) {
         s_err = 1;
         break;
       }
@@ -113,10 +133,11 @@ __global__ void __launch_bounds__(car::kThreads) oneshot_allreduce_kernel(const 
   __syncthreads();
   if (s_err) {
     if (tid == 0) {
-      __hip_atomic_store(reinterpret_cast<uint32_t*>(mine + car::kErrOff), 1u, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (herr != nullptr) __hip_atomic_store(herr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       rounds[b] = round;
     }
+    poison<BF16>(out, v0, v1, tid);
     return;
   }
   // ---- reduce the W slots from local HBM, fp32 accumulation in rank order
@@ -175,16 +196,31 @@ int car_close(void* ptr) { return (int)hipIpcCloseMemHandle(ptr); }
 
 int car_free(void* base) { return (int)hipFree(base); }
 
-int car_error(void* base, int clear) {
-  uint32_t v = 0;
-  char* p = static_cast<char*>(base) + car::kErrOff;
-  if (hipMemcpy(&v, p, 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
-  if (clear && v && hipMemset(p, 0, 4) != hipSuccess) return -1;
-  return (int)v;
+int car_host_flag(uint32_t** host, uint32_t** dev) {
+  hipError_t e = hipHostMalloc(reinterpret_cast<void**>(host), 4, hipHostMallocMapped | hipHostMallocCoherent);
+  if (e != hipSuccess) return (int)e;
+  **host = 0;
+  return (int)hipHostGetDevicePointer(reinterpret_cast<void**>(dev), *host, 0);
+}
+
+void car_free_host_flag(uint32_t* host) {
+  if (host != nullptr) (void)hipHostFree(host);
+}
+
+int car_error(const uint32_t* host) { return (int)__atomic_load_n(host, __ATOMIC_ACQUIRE); }
+
+int car_reset(void* base, uint32_t* host) {
+  // flags, rounds and err back to zero; only meaningful when EVERY rank resets
+  // between two barriers with no call in flight (a collective restart)
+  hipError_t e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemset(base, 0, car::kDataOff);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (host != nullptr) __atomic_store_n(host, 0u, __ATOMIC_RELEASE);
+  return (int)e;
 }
 
 int car_all_reduce(const void* in, void* out, int64_t bytes, bool bf16, int rank, int world, void* const* bases,
-                   size_t cap_bytes, int blocks, hipStream_t stream) {
+                   size_t cap_bytes, int blocks, uint32_t* herr_dev, double timeout_s, hipStream_t stream) {
   if (world < 1 || world > car::kMaxRanks || rank < 0 || rank >= world) return -1;
   if (bytes % 16 != 0 || (size_t)bytes > cap_bytes || cap_bytes % 16 != 0) return -2;
   if (blocks < 1 || blocks > car::kMaxBlocks) return -3;
@@ -194,10 +230,15 @@ int car_all_reduce(const void* in, void* out, int64_t bytes, bool bf16, int rank
   const int64_t nvec = bytes / 16, capvec = cap_bytes / 16;
   const uint4* i4 = static_cast<const uint4*>(in);
   uint4* o4 = static_cast<uint4*>(out);
+  const uint64_t ticks = timeout_s > 0 ? (uint64_t)(timeout_s * 1e8) : car::kDefaultTimeoutTicks;
 #define OAMD_CAR(W)                                                                                               \
   case W:                                                                                                         \
-    if (bf16) oneshot_allreduce_kernel<W, true><<<blocks, car::kThreads, 0, stream>>>(i4, o4, nvec, capvec, rank, peers); \
-    else oneshot_allreduce_kernel<W, false><<<blocks, car::kThreads, 0, stream>>>(i4, o4, nvec, capvec, rank, peers);     \
+    if (bf16)                                                                                                     \
+      oneshot_allreduce_kernel<W, true>                                                                           \
+          <<<blocks, car::kThreads, 0, stream>>>(i4, o4, nvec, capvec, rank, peers, herr_dev, ticks);             \
+    else                                                                                                          \
+      oneshot_allreduce_kernel<W, false>                                                                          \
+          <<<blocks, car::kThreads, 0, stream>>>(i4, o4, nvec, capvec, rank, peers, herr_dev, ticks);             \
     break;
   switch (world) {
     OAMD_CAR(1)

@@ -68,8 +68,11 @@ int car_alloc(size_t cap_bytes, int world, void** base, void* handle_out /* 64 B
 int car_open(const void* handle, void** ptr);
 int car_close(void* ptr);
 int car_free(void* base);
-int car_error(void* base, int clear);
+int car_host_flag(uint32_t** host, uint32_t** dev);   // host-mapped error word (read without a device sync)
+void car_free_host_flag(uint32_t* host);
+int car_error(const uint32_t* host);
+int car_reset(void* base, uint32_t* host);
 int car_all_reduce(const void* in, void* out, int64_t bytes, bool bf16, int rank, int world, void* const* bases,
-                   size_t cap_bytes, int blocks, hipStream_t stream);
+                   size_t cap_bytes, int blocks, uint32_t* herr_dev, double timeout_s, hipStream_t stream);
 
 }  // namespace oamd

@@ -59,6 +59,7 @@ class LeaderElector:
         self._stop = threading.Event()
         self._t: threading.Thread | None = None
         self._last_renew = 0.0
+        self._pending: threading.Event | None = None
 
     # ------------------------------------------------------------------ one attempt
     def try_acquire_or_renew(self) -> bool:
@@ -107,29 +108,72 @@ class LeaderElector:
             pass
 
     # ------------------------------------------------------------------ loop
+    def _bounded_attempt(self, timeout: float) -> bool:
+        """One acquire/renew, but never waited on past ``timeout``: a get/replace that
+        stalls (a slow apiserver; the client's own HTTP timeout is 30 s, longer than the
+        lease) must not keep this replica leading after a standby may have taken the
+        lease over. A stalled attempt is abandoned (its result ignored) and no second
+        one is started while it is still blocked."""
+        if self._pending is not None and not self._pending.is_set():
+            self._pending.wait(max(0.0, timeout))
+            if not self._pending.is_set():
+                return False
+        done, box = threading.Event(), [False]
+
+        def attempt():
+            try:
+                box[0] = self.try_acquire_or_renew()
+            except Exception as e:  # noqa: BLE001
+                log.warning("lease attempt failed: %s", e)
+            finally:
+                done.set()
+
+        self._pending = done
+        threading.Thread(target=attempt, name="lease-attempt", daemon=True).start()
+        if not done.wait(max(0.0, timeout)):
+            log.warning("%s: lease request still blocked after %.1fs; treating it as failed", self.identity,
+                        timeout)
+            return False
+        return box[0]
+
+    def _callback(self, fn, what: str) -> bool:
+        if fn is None:
+            return True
+        try:
+            fn()
+            return True
+        except Exception as e:  # noqa: BLE001 - the elector thread must survive its callbacks
+            log.exception("%s: %s callback failed: %s", self.identity, what, e)
+            return False
+
+    def _step_down(self, release: bool) -> None:
+        self.leading = False
+        if release:
+            self.release()
+        self._callback(self.on_stopped_leading, "on_stopped_leading")
+
     def run(self) -> None:
         while not self._stop.is_set():
-            ok = self.try_acquire_or_renew()
+            start = time.monotonic()
+            budget = (self.renew_deadline_s - (start - self._last_renew)) if self.leading else self.retry_period_s
+            ok = self._bounded_attempt(budget)
             now = time.monotonic()
             if ok:
-                self._last_renew = now
+                self._last_renew = start   # the lease counts from the renewTime stamped at the attempt's start
                 if not self.leading:
                     self.leading = True
                     self.transitions += 1
                     log.info("%s: became leader", self.identity)
-                    if self.on_started_leading:
-                        self.on_started_leading()
-            elif self.leading and now - self._last_renew > self.renew_deadline_s:
-                self.leading = False
+                    if not self._callback(self.on_started_leading, "on_started_leading"):
+                        # could not start leading (e.g. the first list failed): hand the lease
+                        # back at once and compete again after a retry period
+                        self._step_down(release=True)
+            elif self.leading and now - self._last_renew >= self.renew_deadline_s:
                 log.warning("%s: lost leadership (no renewal for %.1fs)", self.identity, now - self._last_renew)
-                if self.on_stopped_leading:
-                    self.on_stopped_leading()
-            self._stop.wait(self.retry_period_s)
+                self._step_down(release=False)
+            self._stop.wait(max(0.0, self.retry_period_s - (time.monotonic() - start)) if ok else self.retry_period_s)
         if self.leading:
-            self.leading = False
-            self.release()
-            if self.on_stopped_leading:
-                self.on_stopped_leading()
+            self._step_down(release=True)
 
     def start(self) -> "LeaderElector":
         self._t = threading.Thread(target=self.run, name="leader-elector", daemon=True)

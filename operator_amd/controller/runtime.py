@@ -22,7 +22,8 @@ from concurrent.futures import ThreadPoolExecutor
 from dataclasses import dataclass
 from typing import Callable
 
-from operator_amd.kube.resources import ApiError, Resource, WatchClosed
+from operator_amd.kube.informer import WatchLoop
+from operator_amd.kube.resources import Resource
 
 log = logging.getLogger(__name__)
 
@@ -93,8 +94,8 @@ class Controller:
         self._lock = threading.Lock()
         self._stop = threading.Event()
         self._threads: list[threading.Thread] = []
-        self._watch = None
-        self._rv: str | None = None
+        self._loop = WatchLoop(kube, res, None, self._on_event, relist=self._enqueue_all, name=f"{self.name}-watch",
+                               restart_delay_s=watch_restart_s, stop=self._stop)
         self.reconciles = 0
         self.errors = 0
 
@@ -102,7 +103,7 @@ class Controller:
     def start(self) -> None:
         self._stop.clear()
         self._initial_list()
-        t = threading.Thread(target=self._watch_loop, name=f"{self.name}-watch", daemon=True)
+        t = threading.Thread(target=self._loop.run, name=f"{self.name}-watch", daemon=True)
         t.start()
         self._threads.append(t)
         for i in range(self.workers):
@@ -117,11 +118,7 @@ class Controller:
     def stop(self) -> None:
         self._stop.set()
         self.queue.close()
-        if self._watch is not None:
-            try:
-                self._watch.close()
-            except Exception:  # noqa: BLE001
-                pass
+        self._loop.stop()
         for t in self._threads:
             t.join(timeout=2)
         self._threads.clear()
@@ -143,17 +140,15 @@ class Controller:
         self.queue.put(key, delay)
 
     def _initial_list(self) -> None:
-        for o in self.kube.list(self.res):
+        self._enqueue_all(self._loop.list_now())
+
+    def _enqueue_all(self, items: list[dict]) -> None:
+        for o in items:
             self.enqueue(self._key(o))
-            rv = (o.get("metadata") or {}).get("resourceVersion")
-            if rv and (self._rv is None or int(rv) > int(self._rv)):
-                self._rv = rv
 
     def _on_event(self, typ: str, obj: dict) -> None:
         key = self._key(obj)
         md = obj.get("metadata") or {}
-        if md.get("resourceVersion"):
-            self._rv = md["resourceVersion"]
         if typ == "DELETED":
             with self._lock:
                 self._gen.pop(key, None)
@@ -162,26 +157,6 @@ class Controller:
         if self.generation_aware and typ == "MODIFIED" and gen is not None and self._gen.get(key) == gen:
             return  # status-only change
         self.enqueue(key)
-
-    def _watch_loop(self) -> None:
-        backoff = self.watch_restart_s
-        while not self._stop.is_set():
-            try:
-                self._watch = self.kube.watch(self.res, None, resource_version=self._rv)
-                backoff = self.watch_restart_s
-                for typ, obj in self._watch:
-                    if self._stop.is_set():
-                        break
-                    self._on_event(typ, obj)
-                if self._stop.is_set():
-                    return
-            except (WatchClosed, ApiError, OSError) as e:
-                log.error("%s watch closed due to error: %s; restarting in %.1fs", self.name, e, backoff)
-            except Exception as e:  # noqa: BLE001
-                log.exception("%s watch failure: %s", self.name, e)
-            if self._stop.wait(backoff):
-                return
-            backoff = min(backoff * 2, 60.0)
 
     def _resync_loop(self) -> None:
         while not self._stop.wait(self.resync_s):

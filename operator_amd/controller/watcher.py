@@ -11,15 +11,19 @@ reference's hot path).
   de-duplicated on ns/name -> first terminated finishedAt (:169-200);
 * each (pod, Podmortem) pair goes to the shared AnalysisPipeline on the
   worker pool, so the watch thread never blocks on apiserver or GPU work;
-* when a watch closes with an error every watch is closed and restarted after
-  ``restart_delay_s`` (5 s, :562-583) — resuming from the last resourceVersion
-  seen instead of losing the events of the gap (fix), with backoff growth.
+* when a watch closes with an error it is restarted after ``restart_delay_s``
+  (5 s, :562-583) — resuming from the last resourceVersion seen instead of
+  losing the events of the gap (fix), with backoff growth; a stream the
+  apiserver ends on its own is reopened at once, and an expired (410)
+  resourceVersion triggers a relist whose failed pods go through the same
+  dedupe (kube/informer.WatchLoop).
 """
 from __future__ import annotations
 
 import logging
 import threading
 
+from operator_amd.kube.informer import WatchLoop
 from operator_amd.kube.resources import PODMORTEMS, PODS, ApiError, WatchClosed
 
 from .failures import FailureDeduper, failure_time, has_pod_failed, matches_monitor
@@ -35,64 +39,40 @@ def parse_namespaces(value: str | None) -> list[str]:
 
 
 class MonitorCache:
-    """Informer-style cache of Podmortem objects (list + watch)."""
+    """Informer-style cache of Podmortem objects (list + watch, kube/informer.WatchLoop)."""
 
-    def __init__(self, kube):
+    def __init__(self, kube, restart_delay_s: float = 1.0):
         self.kube = kube
         self._objs: dict[tuple, dict] = {}
         self._lock = threading.Lock()
-        self._stop = threading.Event()
+        self._loop = WatchLoop(kube, PODMORTEMS, None, self._on_event, relist=self._replace_all,
+                               name="podmortem-cache", restart_delay_s=restart_delay_s, max_delay_s=30.0)
         self._thread: threading.Thread | None = None
-        self._watch = None
-        self._rv = None
         self.synced = threading.Event()
 
+    @staticmethod
+    def _k(o: dict) -> tuple:
+        return ((o["metadata"].get("namespace") or ""), o["metadata"]["name"])
+
     def start(self) -> None:
-        self._relist()
-        self._thread = threading.Thread(target=self._loop, name="podmortem-cache", daemon=True)
+        self._replace_all(self._loop.list_now())
+        self._thread = threading.Thread(target=self._loop.run, name="podmortem-cache", daemon=True)
         self._thread.start()
 
-    def _relist(self) -> None:
-        items = self.kube.list(PODMORTEMS)
+    def _replace_all(self, items: list[dict]) -> None:
         with self._lock:
-            self._objs = {((o["metadata"].get("namespace") or ""), o["metadata"]["name"]): o for o in items}
-            rvs = [int(o["metadata"].get("resourceVersion", 0)) for o in items]
-            self._rv = str(max(rvs)) if rvs else None
+            self._objs = {self._k(o): o for o in items}
         self.synced.set()
 
-    def _loop(self) -> None:
-        delay = 1.0
-        while not self._stop.is_set():
-            try:
-                self._watch = self.kube.watch(PODMORTEMS, None, resource_version=self._rv)
-                delay = 1.0
-                for typ, o in self._watch:
-                    k = ((o["metadata"].get("namespace") or ""), o["metadata"]["name"])
-                    with self._lock:
-                        self._rv = o["metadata"].get("resourceVersion", self._rv)
-                        if typ == "DELETED":
-                            self._objs.pop(k, None)
-                        else:
-                            self._objs[k] = o
-                if self._stop.is_set():
-                    return
-            except Exception as e:  # noqa: BLE001
-                log.warning("Podmortem cache watch failed: %s", e)
-            if self._stop.wait(delay):
-                return
-            delay = min(delay * 2, 30.0)
-            try:
-                self._relist()
-            except Exception as e:  # noqa: BLE001
-                log.warning("Podmortem relist failed: %s", e)
+    def _on_event(self, typ: str, o: dict) -> None:
+        with self._lock:
+            if typ == "DELETED":
+                self._objs.pop(self._k(o), None)
+            else:
+                self._objs[self._k(o)] = o
 
     def stop(self) -> None:
-        self._stop.set()
-        if self._watch is not None:
-            try:
-                self._watch.close()
-            except Exception:  # noqa: BLE001
-                pass
+        self._loop.stop()
 
     def list(self) -> list[dict]:
         with self._lock:
@@ -108,71 +88,54 @@ class PodFailureWatcher:
         self.monitors = monitors
         self.restart_delay_s = restart_delay_s
         self.include_last_state, self.include_init = include_last_state, include_init
-        self._watches: list = []
+        self._loops: list[WatchLoop] = []
         self._threads: list[threading.Thread] = []
         self._stop = threading.Event()
-        self._lock = threading.Lock()
-        self._rv: dict[str | None, str | None] = {}
-        self.restarts = 0
         self.events_seen = 0
+
+    @property
+    def restarts(self) -> int:
+        return sum(lp.restarts for lp in self._loops)
+
+    @property
+    def reconnects(self) -> int:
+        return sum(lp.reconnects for lp in self._loops)
+
+    @property
+    def relists(self) -> int:
+        return sum(lp.relists for lp in self._loops)
 
     # ------------------------------------------------------------------ lifecycle
     def start(self) -> None:
         self._stop.clear()
         targets: list[str | None] = list(self.allowed) if self.allowed else [None]
+        self._loops = []
         for ns in targets:
+            lp = WatchLoop(self.kube, PODS, ns, self.on_event, relist=self._catch_up,
+                           name=f"pod-watch-{ns or 'all'}", restart_delay_s=self.restart_delay_s, stop=self._stop)
+            self._loops.append(lp)
             # open the first watch here, not in the thread: once start() returns, no pod update is missed
             # (a new leader's reconcile pass covers failures that happened before it)
             first = None
             try:
-                first = self.kube.watch(PODS, ns, resource_version=self._rv.get(ns))
-                with self._lock:
-                    self._watches.append(first)
-            except (ApiError, OSError) as e:
+                first = lp.open()
+            except (ApiError, WatchClosed, OSError) as e:
                 log.error("Pod watcher could not start: %s", e)
-            t = threading.Thread(target=self._run_watch, args=(ns, first), name=f"pod-watch-{ns or 'all'}",
-                                 daemon=True)
+            t = threading.Thread(target=lp.run, args=(first,), name=f"pod-watch-{ns or 'all'}", daemon=True)
             t.start()
             self._threads.append(t)
 
     def stop(self) -> None:
         self._stop.set()
-        with self._lock:
-            ws = list(self._watches)
-        for w in ws:
-            try:
-                w.close()
-            except Exception:  # noqa: BLE001
-                pass
+        for lp in self._loops:
+            lp.stop()
 
-    def _run_watch(self, ns: str | None, first=None) -> None:
-        delay = self.restart_delay_s
-        while not self._stop.is_set():
-            w, first = first, None
-            try:
-                if w is None:
-                    w = self.kube.watch(PODS, ns, resource_version=self._rv.get(ns))
-                    with self._lock:
-                        self._watches.append(w)
-                delay = self.restart_delay_s
-                for typ, pod in w:
-                    self._rv[ns] = (pod.get("metadata") or {}).get("resourceVersion", self._rv.get(ns))
-                    self.on_event(typ, pod)
-                if not self._stop.is_set():
-                    log.info("Pod watcher closed normally")
-                return  # normal close: no restart (PodFailureWatcher.java:132-134)
-            except (WatchClosed, ApiError, OSError) as e:
-                log.error("Pod watcher closed due to error: %s", e)
-            finally:
-                if w is not None:
-                    with self._lock:
-                        if w in self._watches:
-                            self._watches.remove(w)
-            if self._stop.wait(delay):
-                return
-            self.restarts += 1
-            log.info("Restarting pod failure watcher...")
-            delay = min(delay * 2, 60.0)
+    def _catch_up(self, pods: list[dict]) -> None:
+        """After 410 Gone the events of the gap are lost: the relisted pods stand in for
+        them. Failed ones go through the same dedupe, so a failure already analysed is
+        not analysed again and one that happened during the gap is."""
+        for pod in pods:
+            self.on_event("MODIFIED", pod)
 
     # ------------------------------------------------------------------ handling
     def on_event(self, action: str, pod: dict) -> None:

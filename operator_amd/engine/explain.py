@@ -29,6 +29,8 @@ import torch
 
 from operator_amd.api.models import AIProviderConfig, AIResponse, AnalysisResult
 
+from operator_amd.parallel.custom_ar import CollectiveTimeout
+
 from . import prompt as prompt_mod
 from .llm import GenRequest, LLMEngine
 
@@ -46,6 +48,7 @@ class EngineLoop(threading.Thread):
         self._cv = threading.Condition()
         self._stopping = False
         self.error: BaseException | None = None
+        self.fatal: BaseException | None = None
 
     def notify(self) -> None:
         with self._cv:
@@ -86,6 +89,11 @@ class EngineLoop(threading.Thread):
                     r.event.set()
                 self.llm.running.clear()
                 self.llm.waiting.clear()
+                if getattr(e, "fatal", False) or isinstance(e, CollectiveTimeout):
+                    # the replica's device state is inconsistent (e.g. a TP peer never
+                    # arrived): stop serving; the pool worker exits and is respawned
+                    self.fatal = e
+                    return
 
 
 @dataclass

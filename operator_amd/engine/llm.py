@@ -150,7 +150,7 @@ class _DecodeGraph:
         logits = e.model.forward(fb, e.kv)
         tok = e.model.sample(logits, st.temp, st.seeds, st.pos + 1)
         st.ids.copy_(tok)
-        st.hist.index_copy_(1, st.step, tok.unsqueeze(1))
+        st.hist.index_copy_(1, st.step % e.multi_step, tok.unsqueeze(1))   # wrap: a stray replay can never index past hist
         st.pos.add_(act.to(torch.long))
         st.ctx.add_(act.to(torch.int32))
         st.step.add_(1)
@@ -213,6 +213,9 @@ class LLMEngine:
         self.pipeline = self.use_graphs
         self._inflight: _Window | None = None
         self._hb = 0
+        # called after every engine step; raise to fail the engine (e.g. a TP collective
+        # that timed out: TPLLMEngine registers the one-shot all-reduce's check)
+        self.health_checks: list = []
         self._host_bufs = None
         if self.device.type == "cuda":
             self._host_bufs = [torch.empty(max_batch, self.multi_step, dtype=torch.long, pin_memory=True)
@@ -275,6 +278,8 @@ class LLMEngine:
             self._prefill(batch)
         elif self.running:
             self._decode()
+        for chk in self.health_checks:
+            chk()
         return self._reap()
 
     def _admittable(self) -> bool:

@@ -113,8 +113,15 @@ def _worker_main(idx: int, device: str, settings_obj: dict, patterns, roles: tup
         return
     stop = threading.Event()
 
+    loop = getattr(getattr(explainer, "ee", None), "loop", None)
+
     def beat():
         while not stop.wait(heartbeat_s):
+            if loop is not None and getattr(loop, "fatal", None) is not None:
+                # unrecoverable engine state (a TP collective timed out): die like a GPU
+                # fault so the health loop re-queues the in-flight work and respawns us
+                outq.put(("fatal", idx, f"engine failed: {loop.fatal}"))
+                os._exit(70)
             outq.put(("hb", idx, time.time()))
 
     threading.Thread(target=beat, daemon=True).start()

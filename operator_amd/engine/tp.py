@@ -51,6 +51,9 @@ class TPLLMEngine(LLMEngine):
         self._by_rid: dict[int, GenRequest] = {}
         self._qlock = threading.Lock()
         self.closed = False
+        car = getattr(tp_group, "oneshot", None)
+        if car is not None:   # a timed-out one-shot all-reduce fails the replica (NaN output, never partial sums)
+            self.health_checks.append(car.check)
 
     # ------------------------------------------------------------------ leader API
     def submit(self, req: GenRequest) -> GenRequest:

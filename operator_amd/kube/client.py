@@ -90,6 +90,8 @@ class HttpWatch:
         if self._resp.status_code >= 400:
             body = self._resp.read()
             self._cm.__exit__(None, None, None)
+            if self._resp.status_code == 410:   # resourceVersion too old: the caller must relist
+                raise WatchClosed(f"watch error: 410 {body[:200]!r}", 410)
             raise _error(self._resp.status_code, body)
         self._lines = self._resp.iter_lines()
         self.closed = False
@@ -106,9 +108,11 @@ class HttpWatch:
                 ev = json.loads(line)
                 typ, obj = ev.get("type"), ev.get("object") or {}
                 if typ == "ERROR":
-                    raise WatchClosed(f"watch error: {obj.get('code')} {obj.get('message')}")
-                if typ == "BOOKMARK":
-                    continue
+                    code = obj.get("code")
+                    raise WatchClosed(f"watch error: {code} {obj.get('message')}",
+                                      int(code) if isinstance(code, (int, str)) and str(code).isdigit() else None)
+                if typ == "BOOKMARK":   # only metadata.resourceVersion is meaningful: callers resume from it
+                    return typ, obj
                 obj.setdefault("apiVersion", self.res.api_version)
                 obj.setdefault("kind", self.res.kind)
                 return typ, obj
@@ -185,14 +189,22 @@ class KubeClient:
 
     def list(self, res: Resource, namespace: str | None = None, label_selector: dict | str | None = None,
              field_selector: str | None = None) -> list[dict]:
+        return self.list_rv(res, namespace, label_selector, field_selector)[0]
+
+    def list_rv(self, res: Resource, namespace: str | None = None, label_selector: dict | str | None = None,
+                field_selector: str | None = None) -> tuple[list[dict], str | None]:
+        """``list`` plus the list's own ``metadata.resourceVersion`` (an opaque string):
+        the point a following watch must resume from. The maximum of the items'
+        resourceVersions is NOT that point (it can be long compacted, or omit deletions)."""
         q = {}
         if label_selector:
             q["labelSelector"] = label_selector if isinstance(label_selector, str) else selector_to_string(label_selector)
         if field_selector:
             q["fieldSelector"] = field_selector
         url = res.base_path(namespace) + (f"?{urlencode(q)}" if q else "")
-        items = (self._req("GET", url) or {}).get("items") or []
-        return [self._with_kind(o, res) for o in items]
+        body = self._req("GET", url) or {}
+        items = [self._with_kind(o, res) for o in body.get("items") or []]
+        return items, (body.get("metadata") or {}).get("resourceVersion") or None
 
     def create(self, res: Resource, obj: dict, namespace: str | None = None) -> dict:
         ns = namespace or (obj.get("metadata") or {}).get("namespace")

@@ -9,8 +9,11 @@ behaviour the controllers depend on:
 * JSON merge patch (RFC 7386) on objects and on the ``status`` subresource
   (status writes never touch spec and do not bump generation);
 * list with label + field selectors; ``pods/log`` subresource;
-* watches (ADDED / MODIFIED / DELETED) with resourceVersion resume and
-  close-with-error injection;
+* watches (ADDED / MODIFIED / DELETED / BOOKMARK) with resourceVersion resume,
+  close-with-error injection, server-side clean close (``end_watches``: the
+  apiserver ends every watch after its min-request-timeout) and history
+  compaction (``compact``: a watch from a compacted resourceVersion fails with
+  410 Gone, as etcd compaction makes it on a real apiserver);
 * a fault matrix: ``inject(verb, plural, code, times)`` makes the next N
   matching calls raise ApiError(code) (409 / 403 / 500 ...);
 * a call journal (``calls``) so tests can assert on the exact verbs issued.
@@ -59,8 +62,8 @@ class FakeWatch:
         if not self.closed:
             self.q.put((typ, obj))
 
-    def fail(self, message: str = "watch stream error") -> None:
-        self.q.put(WatchClosed(message))
+    def fail(self, message: str = "watch stream error", code: int | None = None) -> None:
+        self.q.put(WatchClosed(message, code))
 
     def close(self) -> None:
         if not self.closed:
@@ -92,6 +95,8 @@ class FakeKube:
         self._watches: list[FakeWatch] = []
         self._faults: dict[tuple[str, str], list[int]] = defaultdict(list)
         self._logs: dict[tuple[str, str, str | None], str] = {}
+        self._compacted = 0
+        self._last_rv = 0
         self.calls: list[tuple[str, str, str | None, str | None]] = []
 
     # ------------------------------------------------------------------ faults
@@ -100,6 +105,10 @@ class FakeKube:
         on ``plural`` raise ApiError(code)."""
         with self._lock:
             self._faults[(verb, plural)].extend([code] * times)
+
+    def clear_faults(self) -> None:
+        with self._lock:
+            self._faults.clear()
 
     def _fault(self, verb: str, res: Resource) -> None:
         if not self._faults.get((verb, res.plural)):   # fast path: nothing injected (no lock round trip)
@@ -135,6 +144,7 @@ class FakeKube:
         # stored objects are never mutated after they are stored (every update stores a
         # new dict), so the history can hold them by reference
         self._history.append((rv, self._key(res), typ, obj))
+        self._last_rv = rv
         for w in list(self._watches):
             if w.res == res and (w.namespace is None or w.namespace == obj["metadata"].get("namespace")):
                 w.push(typ, copy.deepcopy(obj))
@@ -146,9 +156,16 @@ class FakeKube:
 
     def current_resource_version(self) -> str:
         with self._lock:
-            return str(max((int(o["metadata"]["resourceVersion"]) for o in self._objs.values()), default=0))
+            # the last resourceVersion handed out (deletions included), like etcd's revision
+            return str(self._last_rv)
 
     # ------------------------------------------------------------------ verbs
+    def list_rv(self, res: Resource, namespace: str | None = None, label_selector: dict | str | None = None,
+                field_selector: str | None = None) -> tuple[list[dict], str]:
+        """``list`` plus the list's resourceVersion (the store's current one), atomically."""
+        with self._lock:
+            return self.list(res, namespace, label_selector, field_selector), self.current_resource_version()
+
     def get(self, res: Resource, name: str, namespace: str | None = None) -> dict | None:
         self._log_call("get", res, namespace, name)
         self._fault("get", res)
@@ -298,6 +315,9 @@ class FakeKube:
         self._fault("watch", res)
         with self._lock:
             w = FakeWatch(self, res, namespace)
+            if resource_version and int(resource_version) < self._compacted:
+                w.fail(f"too old resource version: {resource_version} ({self._compacted})", 410)
+                return w
             if resource_version:
                 key = self._key(res)
                 for rv, k, typ, o in self._history:
@@ -314,6 +334,34 @@ class FakeKube:
         for w in ws:
             w.fail(message)
         return len(ws)
+
+    def end_watches(self, res: Resource | None = None) -> int:
+        """End every open watch cleanly from the server side (no ERROR event), as a
+        real apiserver does when a watch reaches its timeout (30-60 min)."""
+        with self._lock:
+            ws = [w for w in self._watches if res is None or w.res == res]
+        for w in ws:
+            w.close()
+        return len(ws)
+
+    def bookmark(self, res: Resource | None = None) -> int:
+        """Send a BOOKMARK (current resourceVersion only) to every open watch."""
+        with self._lock:
+            rv = self.current_resource_version()
+            ws = [w for w in self._watches if res is None or w.res == res]
+        for w in ws:
+            w.push("BOOKMARK", {"apiVersion": w.res.api_version, "kind": w.res.kind,
+                                "metadata": {"resourceVersion": rv}})
+        return len(ws)
+
+    def compact(self, resource_version: str | int | None = None) -> int:
+        """Forget the event history up to ``resource_version`` (default: everything so far);
+        later watches from an older resourceVersion fail with 410 Gone."""
+        with self._lock:
+            upto = int(resource_version) if resource_version is not None else int(self.current_resource_version())
+            self._history = [h for h in self._history if h[0] > upto]
+            self._compacted = max(self._compacted, upto)
+            return self._compacted
 
     def open_watches(self, res: Resource | None = None) -> int:
         with self._lock:

@@ -129,7 +129,9 @@ class FakeKubeServer:
                         chunk(json.dumps({"type": typ, "object": obj}).encode() + b"\n")
                 except WatchClosed as e:
                     try:
-                        chunk(json.dumps({"type": "ERROR", "object": {"code": 500, "message": str(e)}}).encode() + b"\n")
+                        chunk(json.dumps({"type": "ERROR", "object": {"code": e.code or 500, "message": str(e),
+                                                                      "reason": "Expired" if e.code == 410 else "Error"}}
+                                         ).encode() + b"\n")
                     except OSError:
                         pass
                 except OSError:

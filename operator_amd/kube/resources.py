@@ -58,7 +58,19 @@ class ApiError(Exception):
 
 
 class WatchClosed(Exception):
-    """Raised by a watch iterator when the stream closes with an error."""
+    """Raised by a watch iterator when the stream closes with an error.
+
+    ``code`` is the status of the apiserver's ERROR event when there was one:
+    410 (Gone / Expired) means the requested resourceVersion has been compacted
+    away, so resuming from it can never succeed: the caller must relist."""
+
+    def __init__(self, message: str = "", code: int | None = None):
+        super().__init__(message)
+        self.code = code
+
+    @property
+    def expired(self) -> bool:
+        return self.code == 410
 
 
 # ---------------------------------------------------------------- label selectors

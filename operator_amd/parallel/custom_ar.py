@@ -20,13 +20,19 @@ import torch.distributed as dist
 
 from operator_amd import ops
 
+
+class CollectiveTimeout(RuntimeError):
+    """A device-side collective gave up waiting for a peer: this replica's state is
+    no longer consistent across ranks and it must be restarted as a whole."""
+
+
 DEFAULT_MAX_BYTES = 8 << 20   # 256 tokens x 8192 x 2 B (70B hidden) = 4 MB, with room
 DEFAULT_BLOCKS = 32
 
 
 class OneShotAllReduce:
     def __init__(self, group, device: torch.device | str, max_bytes: int = DEFAULT_MAX_BYTES,
-                 blocks: int = DEFAULT_BLOCKS):
+                 blocks: int = DEFAULT_BLOCKS, timeout_s: float = 2.0):
         self.group = group
         self.device = torch.device(device)
         if self.device.type != "cuda":
@@ -36,7 +42,7 @@ class OneShotAllReduce:
             raise ValueError("one-shot all-reduce supports up to 8 ranks (one xGMI-connected node)")
         self.max_bytes = (int(max_bytes) + 15) // 16 * 16
         self.ext = ops.kernels().CustomAllReduce(self.max_bytes, self.rank, self.world, int(blocks),
-                                                 self.device.index or 0)
+                                                 self.device.index or 0, float(timeout_s))
         handles = [None] * self.world
         if self.world > 1:
             dist.all_gather_object(handles, self.ext.handle(), group=group.pg)
@@ -61,10 +67,21 @@ class OneShotAllReduce:
         self.calls += 1
         return out
 
-    def check(self, clear: bool = True) -> None:
-        """Raise if any call timed out waiting for a peer since the last check."""
-        if self.ext.error(clear):
-            raise RuntimeError("one-shot all-reduce: a peer did not arrive within 2 s")
+    @property
+    def failed(self) -> bool:
+        """A call timed out waiting for a peer. Sticky: every later call returns NaN
+        without touching a peer until ``reset()``. A host read, no device sync."""
+        return bool(self.ext.error())
+
+    def check(self) -> None:
+        """Raise if any call so far timed out waiting for a peer (its output, and that of
+        every later call, is NaN: never a partial sum)."""
+        if self.ext.error():
+            raise CollectiveTimeout("one-shot all-reduce: a peer did not arrive in time; the TP replica must restart")
+
+    def reset(self) -> None:
+        """Collective re-arm (every rank, between barriers, nothing in flight)."""
+        self.ext.reset()
 
     def close(self) -> None:
         self.ext.close()

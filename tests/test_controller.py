@@ -398,3 +398,106 @@ def test_status_group_commit_coalesces_bursts():
     assert len(rf) == 10 and [e["podName"] for e in rf] == order[-1]
     assert len(order) < 40   # ring PATCHes: one per flushed batch, not one per entry
     assert fk.get(PODMORTEMS, "m", "default")["status"]["message"].startswith("done (Pod: p")
+
+
+# ---------------------------------------------------------------- watch lifecycle
+def test_watch_reconnects_after_clean_server_close(env):
+    """The apiserver ends every watch after its min-request-timeout with no error:
+    the pod watcher must reopen it (fabric8 does), not stop for good."""
+    fk, op, _ = env
+    _pm(fk)
+    wait_for(lambda: op.monitors.list())
+    wait_for(lambda: fk.open_watches(PODS) == 1)
+    for _ in range(3):   # several server-side timeouts in a row
+        n = op.watcher.reconnects
+        assert fk.end_watches(PODS) == 1
+        wait_for(lambda: op.watcher.reconnects > n)
+        wait_for(lambda: fk.open_watches(PODS) == 1)
+    assert op.watcher.restarts == 0
+    _fail(fk, "after-timeout")
+    wait_for(lambda: "podmortem.io/analysis" in
+             (fk.get(PODS, "after-timeout", "default")["metadata"].get("annotations") or {}))
+    # the Podmortem cache reconnects too: a monitor created after its stream ended is seen
+    fk.end_watches(PODMORTEMS)
+    _pm(fk, name="second", labels={"app": "two"})
+    wait_for(lambda: len(op.monitors.list()) == 2)
+
+
+def test_watch_relists_after_410_and_catches_up(env):
+    """A watch resumed from a compacted resourceVersion fails with 410 Gone: the watcher
+    must not retry that resourceVersion forever but relist, and a failure that happened
+    while it was disconnected is still analysed (once)."""
+    fk, op, _ = env
+    _pm(fk)
+    wait_for(lambda: op.monitors.list())
+    _fail(fk, "before-gap")
+    wait_for(lambda: "podmortem.io/analysis" in
+             (fk.get(PODS, "before-gap", "default")["metadata"].get("annotations") or {}))
+    op.drain()
+    detected = len(_events(fk, "PodFailureDetected"))
+    # the watch errors out; while it waits to restart a pod fails and the history is compacted
+    fk.inject("watch", "pods", 503, times=10_000)   # hold the watcher off until the gap is set up
+    fk.fail_watches("connection reset", res=PODS)
+    wait_for(lambda: fk.open_watches(PODS) == 0)
+    _fail(fk, "during-gap")
+    fk.compact()
+    fk.clear_faults()
+    wait_for(lambda: op.watcher.relists >= 1)
+    wait_for(lambda: "podmortem.io/analysis" in
+             (fk.get(PODS, "during-gap", "default")["metadata"].get("annotations") or {}))
+    op.drain()
+    names = [e["regarding"]["name"] for e in _events(fk, "PodFailureDetected") if e["regarding"]["kind"] == "Pod"]
+    assert names.count("before-gap") == 1 and names.count("during-gap") == 1   # dedupe across the relist
+    assert len(_events(fk, "PodFailureDetected")) == detected + 2
+    wait_for(lambda: fk.open_watches(PODS) == 1)
+    _fail(fk, "after-relist")
+    wait_for(lambda: "podmortem.io/analysis" in
+             (fk.get(PODS, "after-relist", "default")["metadata"].get("annotations") or {}))
+
+
+def test_bookmarks_advance_the_resume_point():
+    from operator_amd.kube.informer import WatchLoop
+
+    fk = FakeKube()
+    seen = []
+    lp = WatchLoop(fk, PODS, None, lambda t, o: seen.append((t, o["metadata"]["name"])), restart_delay_s=0.01)
+    lp.list_now()
+    import threading
+
+    th = threading.Thread(target=lp.run, daemon=True)
+    th.start()
+    wait_for(lambda: fk.open_watches(PODS) == 1)
+    fk.create(PODS, running_pod("a"))
+    wait_for(lambda: seen == [("ADDED", "a")])
+    for i in range(5):   # unrelated churn elsewhere moves the store's resourceVersion
+        fk.create(PODMORTEMS, {"metadata": {"name": f"pm{i}", "namespace": "default"}, "spec": {}})
+    rv_before = lp.rv
+    fk.bookmark(PODS)
+    wait_for(lambda: lp.rv != rv_before)
+    assert lp.rv == fk.current_resource_version() and seen == [("ADDED", "a")]   # bookmarks are not events
+    # compaction up to the bookmark: resuming from it still works (no 410, no relist)
+    fk.compact()
+    fk.end_watches(PODS)
+    wait_for(lambda: lp.reconnects == 1 and fk.open_watches(PODS) == 1)
+    fk.create(PODS, running_pod("b"))
+    wait_for(lambda: seen[-1] == ("ADDED", "b"))
+    assert lp.relists == 0 and lp.restarts == 0
+    lp.stop()
+    th.join(5)
+    assert not th.is_alive()
+
+
+def test_list_resource_version_is_the_lists_own():
+    """The resume point after a LIST is the list's metadata.resourceVersion, not the
+    maximum of the items' (which misses deletions and can be long compacted)."""
+    fk = FakeKube()
+    fk.create(PODS, running_pod("a"))
+    fk.create(PODS, running_pod("b"))
+    fk.delete(PODS, "b", "default")
+    items, rv = fk.list_rv(PODS)
+    assert [o["metadata"]["name"] for o in items] == ["a"]
+    assert int(rv) > max(int(o["metadata"]["resourceVersion"]) for o in items)
+    w = fk.watch(PODS, None, resource_version=rv)   # nothing to replay: the DELETE is before rv
+    fk.create(PODS, running_pod("c"))
+    assert next(iter(w))[1]["metadata"]["name"] == "c"
+    w.close()

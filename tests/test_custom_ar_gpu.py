@@ -109,3 +109,96 @@ def test_oneshot_allreduce_two_ranks_one_gpu():
     errs = [r for r in res if r[1] != "ok"]
     assert not errs, errs[0][2]
     assert all(r[2] >= 25 for r in res), res
+
+
+def _missing_peer_worker(rank: int, world: int, port: int, q) -> None:
+    """Rank 1 skips one all-reduce: rank 0 must time out with an error and NaN output,
+    never return its own partial sum; after that the error is sticky on both ranks."""
+    try:
+        import time
+
+        import torch.distributed as dist
+
+        from operator_amd.parallel.comm import Group
+        from operator_amd.parallel.custom_ar import CollectiveTimeout, OneShotAllReduce
+
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        car = OneShotAllReduce(Group(), dev, max_bytes=1 << 20, timeout_s=0.2)
+        n = 8192
+        # one good call first: the protocol works with both ranks present
+        x = torch.full((n,), float(rank + 1), dtype=torch.bfloat16, device=dev)
+        y = car.all_reduce(x)
+        torch.cuda.synchronize()
+        assert torch.equal(y.cpu(), torch.full((n,), 3.0, dtype=torch.bfloat16)) and not car.failed
+        dist.barrier()
+        out = {}
+        if rank == 0:
+            t0 = time.perf_counter()
+            y = car.all_reduce(x)           # rank 1 never arrives
+            torch.cuda.synchronize()
+            out["wait_s"] = time.perf_counter() - t0
+            out["all_nan"] = bool(torch.isnan(y.float()).all())
+            out["failed"] = car.failed
+            try:
+                car.check()
+                out["raised"] = False
+            except CollectiveTimeout:
+                out["raised"] = True
+            t0 = time.perf_counter()
+            y = car.all_reduce(x)           # sticky: NaN at once, no wait, no peer touched
+            torch.cuda.synchronize()
+            out["sticky_nan"] = bool(torch.isnan(y.float()).all())
+            out["sticky_s"] = time.perf_counter() - t0
+        dist.barrier()
+        if rank == 1:
+            # rank 0 pushed its slice before it timed out, so rank 1's call of that round
+            # still completes with the true sum ...
+            y = car.all_reduce(x)
+            torch.cuda.synchronize()
+            out["late_ok"] = torch.equal(y.cpu(), torch.full((n,), 3.0, dtype=torch.bfloat16)) and not car.failed
+            y = car.all_reduce(x)           # ... but rank 0 now pushes nothing: timeout, NaN
+            torch.cuda.synchronize()
+            out["all_nan"] = bool(torch.isnan(y.float()).all())
+            out["failed"] = car.failed
+        dist.barrier()
+        car.close()
+        dist.destroy_process_group()
+        q.put((rank, "ok", out))
+    except BaseException:  # noqa: BLE001
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc()))
+
+
+def test_oneshot_allreduce_missing_peer_fails_loudly():
+    import torch.multiprocessing as mp
+
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_missing_peer_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in procs:
+            r = q.get(timeout=100)
+            res[r[0]] = r
+    finally:
+        for p in procs:
+            p.join(timeout=20)
+            if p.is_alive():
+                p.kill()
+    errs = [r for r in res.values() if r[1] != "ok"]
+    assert not errs, errs[0][2]
+    r0, r1 = res[0][2], res[1][2]
+    assert r0["failed"] and r0["raised"] and r0["all_nan"], r0
+    assert 0.15 < r0["wait_s"] < 5.0, r0
+    assert r0["sticky_nan"] and r0["sticky_s"] < 0.1, r0
+    assert r1["late_ok"] and r1["failed"] and r1["all_nan"], r1

@@ -154,3 +154,37 @@ def test_cli_manifests_and_scan(tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     out = json.loads(r.stdout)
     assert out[0]["summary"]["highestSeverity"] in ("CRITICAL", "HIGH")
+
+
+def test_watch_bookmark_410_and_list_rv_over_http(server):
+    """Wire level: BOOKMARK events reach the caller, an expired resourceVersion surfaces
+    as WatchClosed(code=410), and list_rv returns the list's metadata.resourceVersion."""
+    fk, srv, kc = server
+    kc.create(PODS, running_pod("a"))
+    items, rv = kc.list_rv(PODS, "default")
+    assert [o["metadata"]["name"] for o in items] == ["a"] and rv == fk.current_resource_version()
+    w = kc.watch(PODS, "default", resource_version=rv)
+    got = []
+
+    def reader():
+        try:
+            for typ, obj in w:
+                got.append((typ, obj["metadata"].get("resourceVersion")))
+        except WatchClosed as e:
+            got.append(("CLOSED", e.code))
+
+    t = threading.Thread(target=reader, daemon=True)
+    t.start()
+    wait_for(lambda: fk.open_watches(PODS) == 1)
+    fk.create(PODMORTEMS, {"metadata": {"name": "m", "namespace": "default"}, "spec": {}})
+    fk.bookmark(PODS)
+    wait_for(lambda: got)
+    assert got[0] == ("BOOKMARK", fk.current_resource_version())
+    fk.end_watches(PODS)          # clean server-side end: the iterator just stops
+    t.join(5)
+    assert not t.is_alive() and got[-1][0] == "BOOKMARK"
+    fk.compact()
+    w2 = kc.watch(PODS, "default", resource_version=rv)   # rv is now older than the compaction point
+    with pytest.raises(WatchClosed) as e:
+        next(iter(w2))
+    assert e.value.code == 410 and e.value.expired

@@ -93,3 +93,66 @@ def test_one_leader_and_failover(tmp_path):
     finally:
         a.stop()
         b.stop()
+
+
+class _StallingKube:
+    """FakeKube whose lease writes can be made to block (a stalled apiserver)."""
+
+    def __init__(self, fk):
+        self.fk = fk
+        self.stall_s = 0.0
+
+    def __getattr__(self, name):
+        return getattr(self.fk, name)
+
+    def replace(self, res, obj, namespace=None):
+        if self.stall_s and res == LEASES:
+            time.sleep(self.stall_s)
+        return self.fk.replace(res, obj, namespace)
+
+
+def test_stalled_renewal_stops_leading_within_deadline():
+    fk = FakeKube()
+    slow = _StallingKube(fk)
+    events = []
+    a = LeaderElector(slow, "l", "ns", identity="a", lease_duration_s=1.5, renew_deadline_s=0.8, retry_period_s=0.1,
+                      on_started_leading=lambda: events.append(("a", "start", time.monotonic())),
+                      on_stopped_leading=lambda: events.append(("a", "stop", time.monotonic()))).start()
+    b = LeaderElector(fk, "l", "ns", identity="b", lease_duration_s=1.5, renew_deadline_s=0.8, retry_period_s=0.1,
+                      on_started_leading=lambda: events.append(("b", "start", time.monotonic()))).start()
+    try:
+        wait_for(lambda: a.leading)
+        time.sleep(0.3)
+        assert not b.leading
+        t_stall = time.monotonic()
+        slow.stall_s = 30.0   # every renewal now blocks far longer than the lease
+        wait_for(lambda: not a.leading, timeout=5)
+        stop_t = next(t for who, what, t in events if who == "a" and what == "stop")
+        # stopped within renew_deadline (+ one retry period), long before the stalled call returns
+        assert stop_t - t_stall < 0.8 + 0.1 + 0.3
+        wait_for(lambda: b.leading, timeout=5)
+        start_b = next(t for who, what, t in events if who == "b" and what == "start")
+        assert start_b > stop_t    # never two leaders at once
+    finally:
+        slow.stall_s = 0.0
+        b.stop()
+        a.stop(timeout=1)
+
+
+def test_failing_start_callback_releases_lease_and_retries():
+    fk = FakeKube()
+    calls = {"n": 0}
+
+    def flaky_start():
+        calls["n"] += 1
+        if calls["n"] < 3:
+            raise RuntimeError("initial list failed")
+
+    a = LeaderElector(fk, "l", "ns", identity="a", lease_duration_s=1.0, renew_deadline_s=0.6, retry_period_s=0.05,
+                      on_started_leading=flaky_start).start()
+    try:
+        wait_for(lambda: a.leading and calls["n"] >= 3, timeout=5)
+        assert a._t.is_alive()
+        assert fk.get(LEASES, "l", "ns")["spec"]["holderIdentity"] == "a"
+    finally:
+        a.stop()

@@ -160,3 +160,37 @@ def test_pool_tp2_replica_matches_tp1_engine():
         assert es.explain(res, cfgs[0]).explanation == want[0]
     finally:
         p.close()
+
+
+def test_engine_loop_collective_timeout_is_fatal():
+    """A timed-out TP collective makes the engine loop stop serving (fatal), fail every
+    waiter, and exit its thread: the pool worker then dies and is respawned."""
+    import threading
+
+    from operator_amd.engine.explain import EngineLoop
+    from operator_amd.parallel.custom_ar import CollectiveTimeout
+
+    class _Req:
+        def __init__(self):
+            self.error, self.done, self.event = None, False, threading.Event()
+
+    class _LLM:
+        device = __import__("torch").device("cpu")
+
+        def __init__(self):
+            self.running, self.waiting = [_Req()], [_Req()]
+
+        def has_work(self):
+            return True
+
+        def step(self):
+            raise CollectiveTimeout("peer did not arrive")
+
+    llm = _LLM()
+    reqs = llm.running + llm.waiting
+    loop = EngineLoop(llm)
+    loop.start()
+    loop.join(5)
+    assert not loop.is_alive()
+    assert isinstance(loop.fatal, CollectiveTimeout)
+    assert all(r.done and r.event.is_set() and "engine failure" in r.error for r in reqs)
