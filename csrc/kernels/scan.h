@@ -7,7 +7,8 @@ namespace oamd {
 
 // Match record written by ac_scan (16 B):
 //   x = segment index, y = factor id, z = end byte offset inside the segment,
-//   w = newlines seen in the segment before the match.
+//   w = newlines seen in the segment before the match (v2: since the stream's start
+//       when bit 31 is set, i.e. the stream began inside this segment).
 // scan_fixup rewrites records in place as:
 //   x = doc index, y = factor id, z = 0-based line in doc, w = end byte offset in doc.
 struct MatchRec {
@@ -17,11 +18,19 @@ struct MatchRec {
 int ac_scan(const uint8_t* text, int64_t n_segs, int seg_bytes, const uint8_t* cls_map,
             const uint16_t* table, int num_states, int log2_classes, int hot_states,
             const uint32_t* out_off, const uint32_t* out_ids, MatchRec* matches, uint32_t* match_count,
-            uint32_t match_cap, uint32_t* seg_nl, int grid_blocks, hipStream_t stream);
+            uint32_t match_cap, uint32_t* seg_nl, int grid_blocks, const uint16_t* hot_table,
+            hipStream_t stream);
 
+// ac_scan v2's LDS image of the first min(num_states, 256) states: entry
+// [byte * kScanHotStride + state] = table[state][cls_map[byte]] (built on the host).
+constexpr int kScanHotStates = 256;
+constexpr int kScanHotStride = kScanHotStates + 2;
+
+// seg_head: per-segment newline count of the part scanned by the stream that ends
+// inside the segment (ac_scan v2; the second half of its seg_nl buffer).
 int scan_fixup(MatchRec* matches, const uint32_t* match_count, uint32_t match_cap,
                const int64_t* seg_nl_excl, const int64_t* doc_first_seg, int num_docs, int seg_bytes,
-               hipStream_t stream);
+               const uint32_t* seg_head, hipStream_t stream);
 
 int max_hot_states(int log2_classes);
 

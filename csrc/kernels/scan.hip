@@ -29,7 +29,13 @@ namespace oamd {
 constexpr int kScanThreads = 1024;
 constexpr int kHotTableBytes = 128 * 1024;
 
-int max_hot_states(int log2_classes) { return kHotTableBytes / (2 << log2_classes); }
+static int scan_v1_requested();
+constexpr int kHotWideStates = 256;  // ac_scan v2 hot set (full byte rows in LDS)
+
+// hot-state capacity of the scan kernel in use (v2 by default; OAMD_SCAN=v1)
+int max_hot_states(int log2_classes) {
+  return scan_v1_requested() ? kHotTableBytes / (2 << log2_classes) : kHotWideStates;
+}
 
 struct ScanStream {
   uint32_t s;     // DFA state
@@ -144,11 +150,283 @@ __global__ void __launch_bounds__(kScanThreads) ac_scan_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// ac_scan v2 ("wide"): the default kernel (OAMD_SCAN=v1 selects the one above).
+//
+// v1 runs at 1.16 TB/s on 1.19 GB x 1000 patterns, and not because of the
+// DFA: hipcc merges `s < H ? tl[i] : tg[i]` into ONE flat_load_ushort through a
+// selected LDS-or-global address, so every byte step of every wave waits
+// vmcnt(0) on a flat load. v2 (2.32 TB/s on the same input):
+//   * hot states (the 256 most-visited after MatchEngine's profile-guided
+//     renumbering: >= 99.9 % of visits on log text) are staged in LDS as FULL byte
+//     rows, so a byte step is one ds_read_u16 and no class-map read. Layout
+//     [byte][state], row stride 258 entries: the bank of (byte b, state s) is
+//     (b + s/2) mod 32, so lanes sitting in the same state spread by byte value.
+//     The image is built once on the host (MatchEngine.hot_table) and copied in
+//     with 16-B loads;
+//   * two passes per 64-byte chunk. The fast walk is branch-free: the state
+//     register holds the raw table entry (next | 0x8000 "has outputs"), its low
+//     byte indexes the hot row, and every entry is OR-ed into an accumulator. A
+//     chunk that started in or entered a cold state (>= 256: from there on the
+//     fast steps were wrong) or reached an output state is re-walked exactly from
+//     its saved start state (class map + global table, match emission) behind one
+//     wave-uniform branch per chunk: 3.7 % of wave-chunks on the synthetic corpus;
+//   * newlines are counted per 4-byte word (SWAR zero-byte test + popcount);
+//   * the text is cut into grid x 1024 equal streams (whole 64-byte chunks,
+//     >= seg_bytes) instead of fixed segments, so every lane does the same work and
+//     only a stream start replays the 64-byte look-back; a chunk is four
+//     consecutive 16-B loads, so each 128-B line is requested in two bursts;
+//   * per-segment newline counts are atomically accumulated (a segment is split
+//     between at most two streams, since streams are >= seg_bytes long); the
+//     stream that ends inside a segment also stores its part as seg_head[g], and
+//     matches found after such a split carry bit 31 in .w so scan_fixup adds it.
+// Measured alternatives (same input): 2 streams x 32-B chunks 2.02 TB/s; 2 x 64 B
+// and 1 x 128 B need > 128 VGPRs with the exact path inlined and spill; a
+// per-byte ballot branch for cold/output states instead of the two passes 1.95.
+constexpr int kHotWide = kScanHotStates;
+constexpr int kWideStride = kScanHotStride;
+static_assert(kHotWideStates == kScanHotStates, "hot set sizes");
+constexpr int kWideLds = 256 + kHotWide * kWideStride * 2;
+
+// 0x80 in each byte of w that is '\n' (exact: no carries between bytes)
+__device__ __forceinline__ uint32_t newline_bits(uint32_t w) {
+  const uint32_t x = w ^ 0x0a0a0a0au;
+  return ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x | 0x7f7f7f7fu);
+}
+
+template <int NS, int CH, int NT = kScanThreads>
+__global__ void __launch_bounds__(NT) ac_scan_wide_kernel(
+    const uint8_t* __restrict__ text, int64_t total, int64_t L, int64_t n_streams, int seg_shift,
+    const uint8_t* __restrict__ cls_map, const uint16_t* __restrict__ tg, const uint16_t* __restrict__ hot_table,
+    int log2C, int H, const uint32_t* __restrict__ out_off, const uint32_t* __restrict__ out_ids,
+    MatchRec* __restrict__ matches, uint32_t* __restrict__ count, uint32_t cap, uint32_t* __restrict__ seg_nl,
+    uint32_t* __restrict__ seg_head) {
+  constexpr int NV = CH / 16;  // 16-B loads per stream per chunk
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* cls = smem;
+  uint16_t* tl = reinterpret_cast<uint16_t*>(smem + 256);
+  const int tid = threadIdx.x;
+  // class map + the host-built [byte][state] hot table: plain 16-B copies
+  if (tid < 16) reinterpret_cast<uint4*>(cls)[tid] = reinterpret_cast<const uint4*>(cls_map)[tid];
+  for (int i = tid; i < kHotWide * kWideStride * 2 / 16; i += NT)
+    reinterpret_cast<uint4*>(tl)[i] = reinterpret_cast<const uint4*>(hot_table)[i];
+  __syncthreads();
+
+  const int64_t k0 = NS * ((int64_t)blockIdx.x * NT + tid);
+  if (k0 >= n_streams) return;  // no barrier follows
+  const uint32_t seg_mask = (1u << seg_shift) - 1;
+  const uint32_t cold_mask = (H >= kHotWide) ? 0x7f00u : 0xffffu;  // H < 256 only for tiny DFAs
+  const uint32_t Hs = static_cast<uint32_t>(H);
+
+  int64_t pos[NS], end[NS];
+  uint32_t st[NS], nl[NS], mid = 0, act = 0;
+#pragma unroll
+  for (int k = 0; k < NS; ++k) {
+    const int64_t b0 = (k0 + k) * L;
+    pos[k] = b0;
+    end[k] = b0 + L < total ? b0 + L : total;
+    act |= ((k0 + k) < n_streams && b0 < total) ? (1u << k) : 0u;
+    mid |= ((static_cast<uint64_t>(b0) & seg_mask) != 0) ? (1u << k) : 0u;
+    st[k] = 0;
+    nl[k] = 0;
+  }
+
+  typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+  // a chunk per stream as consecutive 16-B loads (plain, not nontemporal: the other
+  // half of each 128-B line is read by the next chunk, from L2; nt loads measured
+  // 1.6x slower)
+  auto load = [&](u32x4_t (&dst)[NS][NV], int64_t delta) {
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+      const int64_t o = pos[k] + delta;
+      if (o >= 0 && o < end[k] && (act >> k & 1u)) {
+        const u32x4_t* p = reinterpret_cast<const u32x4_t*>(text + o);
+#pragma unroll
+        for (int v = 0; v < NV; ++v) dst[k][v] = p[v];
+      } else {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) dst[k][v] = u32x4_t{0u, 0u, 0u, 0u};
+      }
+    }
+  };
+
+  // Exact walk of one chunk of stream k from state s (cold states through the
+  // global table) with match emission when `own`: the rare path. Rolled loop,
+  // bytes re-read from global memory (the chunk was just loaded: L2-resident).
+  auto slow = [&](int k, int64_t at, uint32_t s, uint32_t nl_now, bool own) -> uint32_t {
+    const uint8_t* tp = text + at;
+    const int lim = static_cast<int>(end[k] - at < CH ? end[k] - at : CH);  // bytes before the stream end
+#pragma unroll 1
+    for (int i = 0; i < CH; ++i) {
+      const uint32_t b = (at + i >= 0 && i < lim) ? tp[i] : 0u;
+      const uint32_t sk = s & 0x7fffu;
+      const uint32_t e = sk < Hs ? static_cast<uint32_t>(tl[b * kWideStride + sk])
+                                 : static_cast<uint32_t>(tg[(sk << log2C) | cls[b]]);
+      if (own && (e & 0x8000u)) {
+        const uint64_t p = static_cast<uint64_t>(at + i);
+        emit_matches(e & 0x7fffu, static_cast<uint32_t>(p >> seg_shift), static_cast<uint32_t>(p) & seg_mask,
+                     nl_now | ((mid >> k & 1u) << 31), out_off, out_ids, matches, count, cap);
+      }
+      nl_now += (own && b == 10u);
+      s = e;
+    }
+    return s;
+  };
+
+  // One chunk of every stream, the common case: one ds_read_u16 per byte and no
+  // branch. The state register holds the raw entry (next | 0x8000 outputs), its low
+  // byte indexes the hot row; `acc` ORs every entry, so one test per chunk finds a
+  // stream that entered a cold state (>= 256: every later fast step was wrong) or
+  // an output state. Those chunks are re-walked exactly by `slow`. Bit k of `own`:
+  // stream k's own range (count newlines, emit) rather than its look-back.
+  auto walk = [&](const u32x4_t (&cur)[NS][NV], uint32_t own, int64_t delta) {
+    uint32_t s0[NS], nl0[NS], acc[NS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+      s0[k] = st[k];
+      nl0[k] = nl[k];
+      acc[k] = st[k] & 0x7fffu;   // a chunk that STARTS in a cold state is re-walked too
+    }
+#pragma unroll
+    for (int w = 0; w < CH / 4; ++w) {
+      uint32_t wv[NS];
+#pragma unroll
+      for (int k = 0; k < NS; ++k) wv[k] = cur[k][w >> 2][w & 3];
+#pragma unroll
+      for (int by = 0; by < 4; ++by) {
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+          const uint32_t b = (wv[k] >> (8 * by)) & 0xffu;
+          st[k] = tl[b * kWideStride + (st[k] & 0xffu)];
+          acc[k] |= st[k];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < NS; ++k)
+        if (own >> k & 1u) nl[k] += __builtin_popcount(newline_bits(wv[k]));
+      // keep the scheduler from hoisting the state-independent byte-offset math of
+      // the whole chunk ahead of the chain (64 live VGPRs per stream, then spills)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    uint32_t flag = 0;
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+      const uint32_t m = (own >> k & 1u) ? (cold_mask | 0x8000u) : cold_mask;
+      flag |= (acc[k] & m) ? (1u << k) : 0u;
+    }
+    if (__ballot(flag != 0)) {
+#pragma unroll   // compile-time k: a runtime index would put st[]/pos[] in scratch
+      for (int k = 0; k < NS; ++k)
+        if (flag >> k & 1u) st[k] = slow(k, pos[k] + delta, s0[k], nl0[k], own >> k & 1u);
+    }
+  };
+
+  u32x4_t cur[NS][NV], nxt[NS][NV];
+  // look-back: the LB >= 64 bytes (the longest pattern) before each stream start,
+  // walked from the root without emitting
+  constexpr int LB = CH > 64 ? CH : 64;
+#pragma unroll
+  for (int lb = LB; lb > 0; lb -= CH) {
+    load(cur, -lb);
+    walk(cur, 0u, -lb);
+  }
+  load(cur, 0);
+  const int64_t chunks = (L + CH - 1) / CH;
+  for (int64_t c = 0; c < chunks; ++c) {
+    if (c + 1 < chunks) load(nxt, CH);
+    uint32_t own = 0;
+#pragma unroll
+    for (int k = 0; k < NS; ++k) own |= ((act >> k & 1u) && pos[k] < end[k]) ? (1u << k) : 0u;
+    walk(cur, own, 0);
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+      // segment part complete: at a segment boundary or at the stream end (CH <= seg_bytes
+      // and L % CH == 0, so a chunk ends at or before the next boundary)
+      pos[k] += CH;
+      if ((own >> k & 1u) && (((static_cast<uint64_t>(pos[k]) & seg_mask) == 0) || pos[k] >= end[k])) {
+        const uint32_t g = static_cast<uint32_t>(static_cast<uint64_t>(pos[k] - 1) >> seg_shift);
+        atomicAdd(seg_nl + g, nl[k]);
+        if ((static_cast<uint64_t>(pos[k]) & seg_mask) != 0) seg_head[g] = nl[k];  // ends mid-segment
+        nl[k] = 0;
+        mid &= ~(1u << k);
+      }
+    }
+    if (c + 1 < chunks) {
+#pragma unroll
+      for (int k = 0; k < NS; ++k)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) cur[k][v] = nxt[k][v];
+    }
+  }
+}
+
+static int scan_v1_requested() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("OAMD_SCAN");
+    v = (e && e[0] == 'v' && e[1] == '1') ? 1 : 0;
+  }
+  return v;
+}
+
+static int num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  }
+  return n;
+}
+
 int ac_scan(const uint8_t* text, int64_t n_segs, int seg_bytes, const uint8_t* cls_map, const uint16_t* table,
             int num_states, int log2_classes, int hot_states, const uint32_t* out_off, const uint32_t* out_ids,
             MatchRec* matches, uint32_t* match_count, uint32_t match_cap, uint32_t* seg_nl, int grid_blocks,
-            hipStream_t stream) {
+            const uint16_t* hot_table, hipStream_t stream) {
   if (n_segs == 0) return 0;
+  if (!scan_v1_requested()) {
+    if (hot_table == nullptr) return -8;
+    if (seg_bytes < 64 || (seg_bytes & (seg_bytes - 1)) != 0) return -1;
+    if (log2_classes < 3 || log2_classes > 8) return -2;
+    if (num_states > 32768) return -3;
+    int H = hot_states < num_states ? hot_states : num_states;
+    if (H > kHotWide) H = kHotWide;
+    if (H < 1) H = 1;
+    // one stream of 64-byte chunks per lane (measured on MI355X, 1.19 GB x 1000 patterns:
+    // 2.32 TB/s; 2 streams x 32 B 2.02, 1 x 128 B and 2 x 64 B spill registers)
+    constexpr int NSv = 1, CHv = 64;
+    const int threads = kScanThreads;
+    const void* fn = reinterpret_cast<const void*>(ac_scan_wide_kernel<NSv, CHv>);
+    static bool attr_set = false;
+    if (!attr_set) {
+      if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kWideLds) != hipSuccess) return -6;
+      attr_set = true;
+    }
+    const int64_t total = n_segs * (int64_t)seg_bytes;
+    const int64_t streams = (int64_t)(grid_blocks > 0 ? grid_blocks : num_cus()) * threads * NSv;
+    int64_t L = (total + streams - 1) / streams;
+    L = ((L + CHv - 1) / CHv) * CHv;   // whole chunks (CH = 64 <= seg_bytes)
+    if (L < seg_bytes) L = seg_bytes;
+    const int64_t n_streams = (total + L - 1) / L;
+    const int64_t per_block = (int64_t)threads * NSv;
+    const int64_t blocks = (n_streams + per_block - 1) / per_block;
+    int shift = 0;
+    while ((1 << shift) < seg_bytes) ++shift;
+    // seg_nl holds [n_segs] totals (atomically accumulated) then [n_segs] split-segment heads
+    if (hipMemsetAsync(seg_nl, 0, sizeof(uint32_t) * 2 * n_segs, stream) != hipSuccess) return -5;
+    uint32_t* seg_head = seg_nl + n_segs;
+    const uint8_t* txt = text;
+    const uint16_t* tgp = table;
+    int l2c = log2_classes;
+    void* args[] = {&txt, (void*)&total, &L, (void*)&n_streams, &shift, (void*)&cls_map, &tgp, (void*)&hot_table,
+                    &l2c, &H,
+                    (void*)&out_off, (void*)&out_ids, &matches, &match_count, &match_cap, &seg_nl, &seg_head};
+    if (hipLaunchKernel(fn, dim3(static_cast<unsigned>(blocks)), dim3(threads), args, kWideLds, stream) !=
+        hipSuccess)
+      return -7;
+    OAMD_LAUNCH_CHECK();
+    return 0;
+  }
   if (seg_bytes < 64 || (seg_bytes & (seg_bytes - 1)) != 0) return -1;
   if (log2_classes < 3 || log2_classes > 8) return -2;
   if (num_states > 32768) return -3;
@@ -176,7 +454,7 @@ int ac_scan(const uint8_t* text, int64_t n_segs, int seg_bytes, const uint8_t* c
 // doc_first_seg[num_docs + 1] = first segment of each doc (last = total).
 __global__ void scan_fixup_kernel(MatchRec* __restrict__ m, const uint32_t* __restrict__ count, uint32_t cap,
                                   const int64_t* __restrict__ nl_excl, const int64_t* __restrict__ doc_first_seg,
-                                  int num_docs, int seg_bytes) {
+                                  int num_docs, int seg_bytes, const uint32_t* __restrict__ seg_head) {
   const uint32_t n = min(*count, cap);
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     MatchRec r = m[i];
@@ -187,7 +465,10 @@ __global__ void scan_fixup_kernel(MatchRec* __restrict__ m, const uint32_t* __re
       if (doc_first_seg[mid] <= g) lo = mid; else hi = mid;
     }
     const int64_t fs = doc_first_seg[lo];
-    const int64_t line = nl_excl[g] - nl_excl[fs] + r.w;
+    // bit 31 of .w (ac_scan v2): the match's stream started inside segment g; the
+    // newlines of the segment's head part (the previous stream's) come first
+    const uint32_t head = (r.w & 0x80000000u) ? seg_head[g] : 0u;
+    const int64_t line = nl_excl[g] - nl_excl[fs] + (r.w & 0x7fffffffu) + head;
     const int64_t off = (g - fs) * seg_bytes + r.z;
     r.x = static_cast<uint32_t>(lo);
     r.z = static_cast<uint32_t>(line);
@@ -197,10 +478,11 @@ __global__ void scan_fixup_kernel(MatchRec* __restrict__ m, const uint32_t* __re
 }
 
 int scan_fixup(MatchRec* matches, const uint32_t* match_count, uint32_t match_cap, const int64_t* seg_nl_excl,
-               const int64_t* doc_first_seg, int num_docs, int seg_bytes, hipStream_t stream) {
+               const int64_t* doc_first_seg, int num_docs, int seg_bytes, const uint32_t* seg_head,
+               hipStream_t stream) {
   if (num_docs == 0 || match_cap == 0) return 0;
   scan_fixup_kernel<<<256, 256, 0, stream>>>(matches, match_count, match_cap, seg_nl_excl, doc_first_seg, num_docs,
-                                            seg_bytes);
+                                            seg_bytes, seg_head);
   OAMD_LAUNCH_CHECK();
   return 0;
 }

@@ -153,6 +153,73 @@ py::dict compile_dfa(const std::vector<std::string>& factors) {
   return d;
 }
 
+// Profile-guided state numbering for ac_scan's LDS hot set. Breadth-first order
+// is only a proxy for "often visited": on log text, 0.4 % of transitions leave
+// the first 1024 BFS states, but with 128 chains per wave that puts 42 % of the
+// wave's byte steps behind an L2 / Infinity-Cache round trip (measured on the
+// 1000-pattern synthetic library). Here the DFA is walked over a sample of the
+// text actually being scanned, states are ranked by visit count (root stays 0,
+// unvisited states keep BFS order after the visited ones), and the table and
+// output lists are permuted. Matches are invariant under renumbering; only the
+// hot prefix the kernel stages in LDS changes. Returns the permuted arrays and
+// the fraction of sampled transitions that land in the first `hot` states
+// before and after.
+py::dict reorder_dfa(const std::string& table_b, const std::string& out_off_b, const std::string& out_ids_b,
+                     int log2c, int64_t num_states, const std::string& cls_b, const std::string& sample, int hot) {
+  const int C = 1 << log2c;
+  const int64_t S = num_states;
+  if (static_cast<int64_t>(table_b.size()) != S * C * 2) throw std::invalid_argument("table size mismatch");
+  if (static_cast<int64_t>(out_off_b.size()) != (S + 1) * 4) throw std::invalid_argument("out_off size mismatch");
+  if (cls_b.size() != 256) throw std::invalid_argument("cls_map must have 256 entries");
+  const auto* tab = reinterpret_cast<const uint16_t*>(table_b.data());
+  const auto* off = reinterpret_cast<const uint32_t*>(out_off_b.data());
+  const auto* ids = reinterpret_cast<const uint32_t*>(out_ids_b.data());
+  const auto* cls = reinterpret_cast<const uint8_t*>(cls_b.data());
+  std::vector<uint64_t> visits(S, 0);
+  {
+    py::gil_scoped_release nogil;
+    uint32_t s = 0;
+    for (unsigned char b : sample) {
+      s = tab[(static_cast<size_t>(s) << log2c) | cls[b]] & 0x7fffu;
+      ++visits[s];
+    }
+  }
+  std::vector<uint32_t> order(S);
+  for (int64_t i = 0; i < S; ++i) order[i] = static_cast<uint32_t>(i);
+  // root first, then by visits (desc), ties in BFS order (stable)
+  std::stable_sort(order.begin() + 1, order.end(), [&](uint32_t a, uint32_t b) { return visits[a] > visits[b]; });
+  std::vector<uint32_t> rank(S);
+  for (int64_t i = 0; i < S; ++i) rank[order[i]] = static_cast<uint32_t>(i);
+  std::string nt(S * C * 2, '\0');
+  auto* ntab = reinterpret_cast<uint16_t*>(&nt[0]);
+  std::vector<uint32_t> noff(S + 1, 0), nids;
+  nids.reserve(off[S]);
+  for (int64_t i = 0; i < S; ++i) {
+    const uint32_t o = order[i];
+    for (int k = 0; k < C; ++k) {
+      const uint16_t e = tab[static_cast<size_t>(o) * C + k];
+      ntab[i * C + k] = static_cast<uint16_t>(rank[e & 0x7fffu] | (e & 0x8000u));
+    }
+    noff[i] = static_cast<uint32_t>(nids.size());
+    for (uint32_t k = off[o]; k < off[o + 1]; ++k) nids.push_back(ids[k]);
+  }
+  noff[S] = static_cast<uint32_t>(nids.size());
+  uint64_t total = 0, hot_before = 0, hot_after = 0;
+  for (int64_t i = 0; i < S; ++i) {
+    total += visits[i];
+    if (i < hot) hot_before += visits[i];
+    if (rank[i] < static_cast<uint32_t>(hot)) hot_after += visits[i];
+  }
+  py::dict d;
+  d["table"] = py::bytes(nt);
+  d["out_off"] = py::bytes(reinterpret_cast<const char*>(noff.data()), noff.size() * 4);
+  d["out_ids"] = py::bytes(reinterpret_cast<const char*>(nids.data()), std::max<size_t>(nids.size(), 1) * 4);
+  d["hot_before"] = total ? double(hot_before) / double(total) : 1.0;
+  d["hot_after"] = total ? double(hot_after) / double(total) : 1.0;
+  d["sampled"] = total;
+  return d;
+}
+
 // Layout: doc i occupies [first_seg[i]*seg, first_seg[i+1]*seg), content then NUL padding (>= 1 byte).
 py::tuple plan_docs(const std::vector<size_t>& lens, int64_t seg) {
   if (seg < 64 || (seg & (seg - 1))) throw std::invalid_argument("seg_bytes must be a power of two >= 64");
@@ -287,6 +354,8 @@ py::list score_events(const std::vector<int64_t>& hit_doc, const std::vector<int
 PYBIND11_MODULE(_patterns, m) {
   m.doc() = "operator_amd host pattern compiler / packer / scorer";
   m.def("compile_dfa", &compile_dfa, py::arg("factors"));
+  m.def("reorder_dfa", &reorder_dfa, py::arg("table"), py::arg("out_off"), py::arg("out_ids"), py::arg("log2_classes"),
+        py::arg("num_states"), py::arg("cls_map"), py::arg("sample"), py::arg("hot"));
   m.def("plan_docs", &plan_docs, py::arg("lens"), py::arg("seg_bytes"));
   m.def("pack_docs", &pack_docs, py::arg("docs"), py::arg("first_seg"), py::arg("seg_bytes"), py::arg("dst"),
         py::arg("threads") = 8);

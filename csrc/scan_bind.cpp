@@ -12,7 +12,8 @@ namespace {
 
 void ac_scan(const at::Tensor& text, int64_t seg_bytes, const at::Tensor& cls_map, const at::Tensor& table,
              int64_t log2_classes, int64_t hot_states, const at::Tensor& out_off, const at::Tensor& out_ids,
-             at::Tensor& matches, at::Tensor& match_count, at::Tensor& seg_nl, int64_t grid_blocks) {
+             at::Tensor& matches, at::Tensor& match_count, at::Tensor& seg_nl, int64_t grid_blocks,
+             const at::Tensor& hot_table) {
   CHECK_T(text, at::kByte);
   CHECK_T(cls_map, at::kByte);
   CHECK_T(table, at::kShort);
@@ -21,6 +22,9 @@ void ac_scan(const at::Tensor& text, int64_t seg_bytes, const at::Tensor& cls_ma
   CHECK_T(matches, at::kInt);
   CHECK_T(match_count, at::kInt);
   CHECK_T(seg_nl, at::kInt);
+  CHECK_T(hot_table, at::kShort);
+  TORCH_CHECK(hot_table.numel() == oamd::kScanHotStates * oamd::kScanHotStride,
+              "hot_table must be [256 bytes x 258] (MatchEngine builds it)");
   TORCH_CHECK(seg_bytes >= 64 && (seg_bytes & (seg_bytes - 1)) == 0, "seg_bytes must be a power of two >= 64");
   TORCH_CHECK(text.numel() % seg_bytes == 0, "text must be padded to a multiple of seg_bytes");
   TORCH_CHECK(cls_map.numel() == 256, "class map must have 256 entries");
@@ -35,7 +39,7 @@ void ac_scan(const at::Tensor& text, int64_t seg_bytes, const at::Tensor& cls_ma
   TORCH_CHECK(matches.dim() == 2 && matches.size(1) == 4, "matches must be [cap, 4] int32");
   TORCH_CHECK(match_count.numel() >= 1, "match_count needs one element");
   const int64_t n_segs = text.numel() / seg_bytes;
-  TORCH_CHECK(seg_nl.numel() >= n_segs, "seg_nl too small");
+  TORCH_CHECK(seg_nl.numel() >= 2 * n_segs, "seg_nl needs 2 x segments entries (totals, split heads)");
   TORCH_CHECK(n_segs < (int64_t(1) << 32), "too many segments");
   const c10::hip::HIPGuardMasqueradingAsCUDA g(text.device());
   const int rc = oamd::ac_scan(text.data_ptr<uint8_t>(), n_segs, (int)seg_bytes, cls_map.data_ptr<uint8_t>(),
@@ -45,24 +49,26 @@ void ac_scan(const at::Tensor& text, int64_t seg_bytes, const at::Tensor& cls_ma
                                reinterpret_cast<oamd::MatchRec*>(matches.data_ptr()),
                                reinterpret_cast<uint32_t*>(match_count.data_ptr()), (uint32_t)matches.size(0),
                                reinterpret_cast<uint32_t*>(seg_nl.data_ptr()), (int)grid_blocks,
-                               c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream());
+                               reinterpret_cast<const uint16_t*>(hot_table.data_ptr()), c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream());
   TORCH_CHECK(rc == 0, "ac_scan launch failed rc=", rc);
 }
 
 void scan_fixup(at::Tensor& matches, const at::Tensor& match_count, const at::Tensor& seg_nl_excl,
-                const at::Tensor& doc_first_seg, int64_t seg_bytes) {
+                const at::Tensor& doc_first_seg, int64_t seg_bytes, const at::Tensor& seg_head) {
   CHECK_T(matches, at::kInt);
   CHECK_T(match_count, at::kInt);
   CHECK_T(seg_nl_excl, at::kLong);
   CHECK_T(doc_first_seg, at::kLong);
   TORCH_CHECK(matches.dim() == 2 && matches.size(1) == 4, "matches must be [cap, 4]");
   TORCH_CHECK(doc_first_seg.numel() >= 2, "doc_first_seg must have num_docs+1 >= 2 entries");
+  CHECK_T(seg_head, at::kInt);
+  TORCH_CHECK(seg_head.numel() >= seg_nl_excl.numel(), "seg_head needs one entry per segment");
   const c10::hip::HIPGuardMasqueradingAsCUDA g(matches.device());
   const int rc = oamd::scan_fixup(reinterpret_cast<oamd::MatchRec*>(matches.data_ptr()),
                                   reinterpret_cast<const uint32_t*>(match_count.data_ptr()), (uint32_t)matches.size(0),
                                   seg_nl_excl.data_ptr<int64_t>(), doc_first_seg.data_ptr<int64_t>(),
                                   (int)doc_first_seg.numel() - 1, (int)seg_bytes,
-                                  c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream());
+                                  reinterpret_cast<const uint32_t*>(seg_head.data_ptr()), c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream());
   TORCH_CHECK(rc == 0, "scan_fixup launch failed rc=", rc);
 }
 
@@ -72,4 +78,5 @@ void register_scan_bindings(pybind11::module_& m) {
   m.def("ac_scan", &ac_scan);
   m.def("scan_fixup", &scan_fixup);
   m.def("max_hot_states", [](int64_t log2c) { return oamd::max_hot_states((int)log2c); });
+  m.attr("SCAN_HOT_STRIDE") = oamd::kScanHotStride;
 }

@@ -84,13 +84,21 @@ def _line_offsets(doc: bytes) -> list[int]:
 class MatchEngine:
     """Compile a PatternSet once, then analyze batches of logs on one device."""
 
+    SCAN_LANES = 256 * 1024   # ac_scan v2 streams on MI355X (256 CUs x 1024 threads)
+
     def __init__(self, patterns: PatternSet | CompiledPatterns, device: str | torch.device = "cuda",
                  seg_bytes: int = 1024, max_events: int = 50, significance: float = 0.5,
                  match_cap: int = 1 << 20, grid_blocks: int = 0, use_native_scorer: bool = True,
-                 gpu_scorer: bool | None = None):
+                 gpu_scorer: bool | None = None, profile_bytes: int = 1 << 20):
         self.cp = patterns if isinstance(patterns, CompiledPatterns) else compile_patterns(patterns)
+        # DFA states are renumbered by visit count over the first `profile_bytes` of
+        # text scanned (0: keep breadth-first numbering), see _profile_states
+        self.profile_bytes = int(profile_bytes)
+        self._profiled = False
+        self.hot_coverage: tuple[float, float] | None = None
         self.device = torch.device(device)
         self.seg_bytes = int(seg_bytes)
+        self.last_seg = self.seg_bytes   # segment size of the last scan (<= seg_bytes, see _scan_gpu)
         self.max_events = max_events
         self.significance = significance
         self.match_cap = int(match_cap)
@@ -141,6 +149,42 @@ class MatchEngine:
         self.out_off = torch.frombuffer(bytearray(d["out_off"]), dtype=torch.int32).to(dev)
         self.out_ids = torch.frombuffer(bytearray(d["out_ids"]), dtype=torch.int32).to(dev)
         self.hot_states = int(min(S, kernels().max_hot_states(log2c)))
+        self._build_hot_table(d["table"])
+
+    def _build_hot_table(self, table: bytes) -> None:
+        """ac_scan v2's LDS image: the first min(S, 256) states as full byte rows,
+        [byte][state] with a 258-entry row stride (csrc/kernels/scan.h)."""
+        from operator_amd.ops import kernels
+
+        d = self.cp.dfa
+        S, C = int(d["num_states"]), 1 << int(d["log2_classes"])
+        stride = int(kernels().SCAN_HOT_STRIDE)
+        H = min(S, stride - 2)
+        tab = np.frombuffer(table, dtype=np.uint16).reshape(S, C)
+        cls = np.frombuffer(d["cls_map"], dtype=np.uint8)
+        wide = np.zeros((256, stride), dtype=np.uint16)
+        wide[:, :H] = tab[:H][:, cls].T
+        self.hot_table = torch.from_numpy(wide.view(np.int16).reshape(-1).copy()).to(self.device)
+
+    def _profile_states(self, sample: bytes) -> None:
+        """Renumber DFA states by how often a walk over ``sample`` visits them, so the
+        hot prefix ac_scan stages in LDS holds the states the logs actually sit in
+        (breadth-first order leaves 42 % of wave byte-steps waiting on a global
+        table read on the synthetic library; see csrc/patterns/patterns.cpp
+        reorder_dfa). Match output does not depend on the numbering."""
+        from operator_amd.ops import patterns
+
+        d = self.cp.dfa
+        r = patterns().reorder_dfa(d["table"], d["out_off"], d["out_ids"], int(d["log2_classes"]),
+                                   int(d["num_states"]), d["cls_map"], sample, self.hot_states)
+        dev = self.device
+        S, C = int(d["num_states"]), 1 << int(d["log2_classes"])
+        self.table = torch.frombuffer(bytearray(r["table"]), dtype=torch.int16).reshape(S, C).to(dev)
+        self.out_off = torch.frombuffer(bytearray(r["out_off"]), dtype=torch.int32).to(dev)
+        self.out_ids = torch.frombuffer(bytearray(r["out_ids"]), dtype=torch.int32).to(dev)
+        self.hot_coverage = (float(r["hot_before"]), float(r["hot_after"]))
+        self._build_hot_table(r["table"])
+        self._profiled = True
 
     # ------------------------------------------------------------------ GPU scan
     def _ensure(self, name: str, numel: int, dtype, pinned: bool = False, device=None) -> torch.Tensor:
@@ -166,13 +210,22 @@ class MatchEngine:
 
         P = patterns()
         seg = self.seg_bytes
+        # ac_scan v2 cuts the text into (CUs x 1024) equal streams of >= seg bytes: a
+        # small batch (a 256-failure flagship wave is 16 MB) gets smaller segments so
+        # that every CU has lanes to run
+        approx = sum(len(d) + 1 for d in docs)
+        while seg > 64 and approx // seg < self.SCAN_LANES:
+            seg //= 2
+        self.last_seg = seg
         total, first = P.plan_docs([len(d) for d in docs], seg)
         n_segs = total // seg
         pinned = self._ensure("_pinned", total, torch.uint8, pinned=True)
         P.pack_docs(docs, first, seg, pinned.data_ptr(), 8)
+        if self.profile_bytes > 0 and not self._profiled:
+            self._profile_states(pinned[:min(total, self.profile_bytes)].numpy().tobytes())
         text = self._ensure("_text", total, torch.uint8)
         text[:total].copy_(pinned[:total], non_blocking=True)
-        seg_nl = self._ensure("_seg_nl", n_segs, torch.int32)
+        seg_nl = self._ensure("_seg_nl", 2 * n_segs, torch.int32)   # totals, then split-segment heads
         C = kernels()
         first_t = torch.tensor(first, dtype=torch.int64).to(self.device, non_blocking=True)
         while True:
@@ -182,10 +235,10 @@ class MatchEngine:
                 self._count = torch.zeros(1, dtype=torch.int32, device=self.device)
             self._count.zero_()
             C.ac_scan(text[:total], seg, self.cls_map, self.table, self.log2c, self.hot_states, self.out_off,
-                      self.out_ids, self._matches, self._count, seg_nl, self.grid_blocks)
+                      self.out_ids, self._matches, self._count, seg_nl, self.grid_blocks, self.hot_table)
             nl = seg_nl[:n_segs].to(torch.int64)
             excl = torch.cumsum(nl, 0) - nl
-            C.scan_fixup(self._matches, self._count, excl, first_t, seg)
+            C.scan_fixup(self._matches, self._count, excl, first_t, seg, seg_nl[n_segs:2 * n_segs])
             cnt = int(self._count.item())
             if cnt <= self._matches.shape[0]:
                 break

@@ -148,3 +148,27 @@ def test_case_sensitive_literal_is_verified():
     eng = MatchEngine(ps, device="cpu")
     evs, _ = eng.events([b"fatal\nFATAL\nFaTaL"])
     assert [e.line for e in evs[0]] == [1]
+
+
+def test_reorder_dfa_preserves_matches_and_raises_hot_coverage():
+    """Profile-guided renumbering (reorder_dfa) permutes states only: every match is
+    unchanged, the root stays state 0, and the sampled visits move into the hot prefix."""
+    ps = synthetic_library(200, seed=3)
+    cp = compile_patterns(ps)
+    d = cp.dfa
+    fac = LogFactory(n_patterns=200, seed=5)
+    sample = b"".join(fac.batch(4, 16 * 1024, n_failures=3)[0])
+    hot = 64
+    r = native_patterns().reorder_dfa(d["table"], d["out_off"], d["out_ids"], d["log2_classes"], d["num_states"],
+                                      d["cls_map"], sample, hot)
+    assert r["hot_after"] >= r["hot_before"]
+    assert r["sampled"] == len(sample)
+    d2 = dict(d, table=r["table"], out_off=r["out_off"], out_ids=r["out_ids"])
+    text = b"".join(LogFactory(n_patterns=200, seed=9).batch(3, 8 * 1024, n_failures=3)[0])
+    text += b" ".join(cp.factors[:50])  # every one of these must match
+    assert _dfa_scan(d2, text) == _dfa_scan(d, text)
+    # root row: transitions out of state 0 on the same byte class lead to the same factors
+    C = 1 << d["log2_classes"]
+    t1 = np.frombuffer(d["table"], np.uint16).reshape(-1, C)
+    t2 = np.frombuffer(r["table"], np.uint16).reshape(-1, C)
+    assert ((t1[0] & 0x8000) == (t2[0] & 0x8000)).all()

@@ -107,3 +107,16 @@ def test_gpu_scorer_matches_host_scorer():
     ra = [r.to_obj()["summary"] for r in g.analyze(docs)]
     rb = [r.to_obj()["summary"] for r in h.analyze(docs)]
     assert ra == rb
+
+
+def test_profiled_state_order_gives_identical_scan():
+    """MatchEngine renumbers DFA states by visit count on the first scan
+    (profile_bytes): the raw hits must equal the breadth-first-numbered DFA's."""
+    ps = synthetic_library(1000, seed=0)
+    docs, _ = LogFactory(n_patterns=1000, seed=4).batch(96, 32 * 1024, n_failures=3)
+    a = MatchEngine(ps, device="cuda", seg_bytes=1024, profile_bytes=0)
+    b = MatchEngine(ps, device="cuda", seg_bytes=1024, profile_bytes=1 << 20)
+    ra, rb = a.scan_gpu(docs), b.scan_gpu(docs)
+    assert b.hot_coverage is not None and b.hot_coverage[1] >= b.hot_coverage[0]
+    assert len(ra) > 0 and _rows(ra) == _rows(rb)
+    assert _rows(b.scan_gpu(docs[::-1])) == _rows(a.scan_gpu(docs[::-1]))

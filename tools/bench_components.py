@@ -58,7 +58,7 @@ def bench_scan(n_docs, doc_kb, n_patterns):
     # kernel-only timing
     from operator_amd.ops import kernels
     C = kernels()
-    seg = eng.seg_bytes
+    seg = eng.last_seg
     n_segs = eng._text.numel() // seg
     tot_pad = sum(((len(d) + 1 + seg - 1) // seg) * seg for d in docs)
     ev0, ev1 = torch.cuda.Event(True), torch.cuda.Event(True)
@@ -66,7 +66,7 @@ def bench_scan(n_docs, doc_kb, n_patterns):
     for _ in range(5):
         eng._count.zero_()
         C.ac_scan(eng._text[:tot_pad], seg, eng.cls_map, eng.table, eng.log2c, eng.hot_states, eng.out_off,
-                  eng.out_ids, eng._matches, eng._count, eng._seg_nl, 0)
+                  eng.out_ids, eng._matches, eng._count, eng._seg_nl, 0, eng.hot_table)
     ev1.record()
     torch.cuda.synchronize()
     ms = ev0.elapsed_time(ev1) / 5

@@ -1,0 +1,82 @@
+"""BASELINE config 2: PatternLibrary scan, ~1 GB of synthetic pod logs x 1000
+patterns on one MI355X (ac_scan).
+
+Arms (one JSON line each):
+  * bfs      - DFA states in breadth-first order (the compile-time numbering)
+  * profiled - states renumbered by visit count over the first MiB of text
+               (MatchEngine.profile_bytes, csrc/patterns/patterns.cpp reorder_dfa)
+Kernel-only time is the mean of ``--iters`` back-to-back ac_scan launches over
+the packed text (HIP events); ``analyze_s`` is one full MatchEngine.analyze
+(pack + H2D + scan + fixup + D2H + verify + score + results) of the same docs.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from operator_amd.engine.match import MatchEngine  # noqa: E402
+from operator_amd.ops import kernels  # noqa: E402
+from operator_amd.patterns.synth import LogFactory, synthetic_library  # noqa: E402
+
+
+def kernel_ms(eng, docs, iters):
+    C = kernels()
+    seg = eng.last_seg
+    tot_pad = sum(((len(d) + 1 + seg - 1) // seg) * seg for d in docs)
+    ev0, ev1 = torch.cuda.Event(True), torch.cuda.Event(True)
+    with torch.cuda.stream(eng._stream):
+        for _ in range(2):
+            eng._count.zero_()
+            C.ac_scan(eng._text[:tot_pad], seg, eng.cls_map, eng.table, eng.log2c, eng.hot_states, eng.out_off,
+                      eng.out_ids, eng._matches, eng._count, eng._seg_nl, eng.grid_blocks, eng.hot_table)
+        ev0.record()
+        for _ in range(iters):
+            eng._count.zero_()
+            C.ac_scan(eng._text[:tot_pad], seg, eng.cls_map, eng.table, eng.log2c, eng.hot_states, eng.out_off,
+                      eng.out_ids, eng._matches, eng._count, eng._seg_nl, eng.grid_blocks, eng.hot_table)
+        ev1.record()
+    torch.cuda.synchronize()
+    return ev0.elapsed_time(ev1) / iters, tot_pad, int(eng._count.item())
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--docs", type=int, default=4096)
+    ap.add_argument("--doc-kb", type=int, default=256)
+    ap.add_argument("--patterns", type=int, default=1000)
+    ap.add_argument("--seg", type=int, default=1024)
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--arms", default="bfs,profiled")
+    a = ap.parse_args()
+    ps = synthetic_library(a.patterns)
+    t0 = time.perf_counter()
+    docs, _ = LogFactory(n_patterns=a.patterns, seed=1).batch(a.docs, a.doc_kb * 1024, n_failures=3)
+    gen_s = time.perf_counter() - t0
+    total = sum(map(len, docs))
+    ref = None
+    for arm in a.arms.split(","):
+        eng = MatchEngine(ps, device="cuda", seg_bytes=a.seg, profile_bytes=(1 << 20) if arm == "profiled" else 0)
+        raw = eng.scan_gpu(docs)
+        torch.cuda.synchronize()
+        ms, tot_pad, cnt = kernel_ms(eng, docs, a.iters)
+        key = sorted(map(tuple, raw.tolist()))
+        same = None if ref is None else (key == ref)
+        ref = ref or key
+        t1 = time.perf_counter()
+        res = eng.analyze(docs)
+        t2 = time.perf_counter()
+        print(json.dumps({"bench": "scan", "arm": arm, "bytes": total, "padded_bytes": tot_pad,
+                          "patterns": a.patterns, "states": eng.dfa_states, "hot_states": eng.hot_states,
+                          "hot_coverage": eng.hot_coverage, "kernel_ms": round(ms, 3),
+                          "kernel_GBps": round(tot_pad / ms / 1e6, 1), "raw_matches": cnt,
+                          "same_matches_as_first_arm": same, "analyze_s": round(t2 - t1, 3),
+                          "analyses_per_s": round(len(res) / (t2 - t1), 1), "gen_s": round(gen_s, 1)}), flush=True)
+        del eng
+
+
+if __name__ == "__main__":
+    main()
