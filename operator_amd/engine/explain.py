@@ -65,6 +65,22 @@ class EngineLoop(threading.Thread):
     # per 256-failure wave). 0.5 ms bounds that wait at a small context-switch cost.
     GIL_SWITCH_S = 0.0005
 
+    def _gather_arrivals(self) -> None:
+        """Failures arrive in bursts that the pipeline feeds to the engine over tens of
+        ms (scan batches, prompt batches). An idle engine that admitted the first
+        arrival alone would run a 1-request prefill and queue everything behind it
+        (measured at the start of a 256-failure wave: a 1-request prefill stretched to
+        174 ms by the launch-side GIL contention of the burst, ahead of the first full
+        batch). So when idle, wait up to ``admit_wait_s`` for a full prefill batch."""
+        llm = self.llm
+        wait = getattr(llm, "admit_wait_s", 0.0)
+        if wait <= 0 or not llm.idle():
+            return
+        deadline = time.perf_counter() + wait
+        while (not self._stopping and time.perf_counter() < deadline
+               and llm.queued_prompt_tokens() < llm.max_prefill_tokens):
+            time.sleep(0.001)
+
     def run(self) -> None:
         if self.llm.device.type == "cuda":
             torch.cuda.set_device(self.llm.device)
@@ -79,6 +95,7 @@ class EngineLoop(threading.Thread):
                     if close is not None:   # TP leader: release the followers
                         close()
                     return
+            self._gather_arrivals()
             try:
                 self.llm.step()
             except BaseException as e:  # surface to every waiter

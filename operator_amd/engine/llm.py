@@ -186,8 +186,13 @@ class _DecodeGraph:
 
 class LLMEngine:
     def __init__(self, model: LlamaModel, kv: PagedKVCache, max_batch: int = 256, max_prefill_tokens: int = 16384,
-                 max_context: int | None = None, use_graphs: bool = True, multi_step: int = 8):
+                 max_context: int | None = None, use_graphs: bool = True, multi_step: int = 8,
+                 admit_wait_s: float = 0.0):
         self.model, self.kv = model, kv
+        # arrival batching window used by the loop that drives step() (EngineLoop):
+        # an idle engine given less than a full prefill batch waits this long for more
+        # requests. Not part of step() itself, which stays deterministic for TP.
+        self.admit_wait_s = admit_wait_s
         self.device = model.device
         self.max_batch = max_batch
         self.max_prefill_tokens = max_prefill_tokens
@@ -247,6 +252,20 @@ class LLMEngine:
 
     def has_work(self) -> bool:
         return bool(self.waiting or self.running)
+
+    def idle(self) -> bool:
+        """Nothing running or in flight on the device (the next step would be a prefill)."""
+        return not self.running and self._inflight is None
+
+    def queued_prompt_tokens(self) -> int:
+        """Prompt tokens waiting for admission (stops counting at one full prefill batch)."""
+        n = 0
+        with self._lock:
+            for r in self.waiting:
+                n += len(r.prompt)
+                if n >= self.max_prefill_tokens:
+                    break
+        return n
 
     def generate(self, reqs: list[GenRequest]) -> list[GenRequest]:
         for r in reqs:

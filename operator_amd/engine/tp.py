@@ -79,6 +79,11 @@ class TPLLMEngine(LLMEngine):
     def has_work(self) -> bool:
         return bool(self._pending or self._cancels) or super().has_work()
 
+    def queued_prompt_tokens(self) -> int:
+        with self._qlock:
+            n = sum(len(r.prompt) for r in self._pending)
+        return n + super().queued_prompt_tokens()
+
     def step(self) -> list[GenRequest]:
         if not self.leader:
             raise RuntimeError("TP followers step from follow()")

@@ -24,11 +24,15 @@ def _roctx():
     _tried = True
     if os.environ.get("OAMD_ROCTX", "1") == "0":
         return None
-    cands = ["libroctx64.so", "/opt/rocm/lib/libroctx64.so"]
+    # rocprofv3 (rocprofiler-sdk) intercepts the SDK's roctx; the legacy roctracer
+    # libroctx64 (also bundled with torch) is only a fallback for older tools
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    cands = [os.path.join(rocm, "lib", "librocprofiler-sdk-roctx.so"), "librocprofiler-sdk-roctx.so",
+             "libroctx64.so", os.path.join(rocm, "lib", "libroctx64.so")]
     try:
         import torch
 
-        cands.insert(0, os.path.join(os.path.dirname(torch.__file__), "lib", "libroctx64.so"))
+        cands.append(os.path.join(os.path.dirname(torch.__file__), "lib", "libroctx64.so"))
     except Exception:  # noqa: BLE001
         pass
     for c in cands:
