@@ -228,7 +228,7 @@ def main() -> int:
         run_wave(w)
     lat.clear()
     counter["outcomes"] = {}
-    stats0 = (llm.stats.prefill_tokens, llm.stats.decode_tokens)
+    stats0 = (llm.stats.prefill_tokens, llm.stats.decode_tokens, llm.stats.prefill_graph_replays)
 
     def sync():
         if torch.cuda.is_available():
@@ -237,12 +237,23 @@ def main() -> int:
             dist.barrier()
 
     sync()
+    # a progress line on stderr every 30 s (stdout stays the ONE JSON line)
+    prog_stop = threading.Event()
+
+    def progress():
+        t_start = time.perf_counter()
+        while not prog_stop.wait(30.0):
+            print(f"[bench rank {rank}] {time.perf_counter() - t_start:.0f} s, {counter['n']} analyses in the current "
+                  f"pass", file=sys.stderr, flush=True)
+
+    threading.Thread(target=progress, daemon=True).start()
     t0 = time.perf_counter()
     mono0 = time.monotonic_ns()  # same clock as rocprofv3 timestamps: lets a trace be cut to the timed region
     run_timed(list(range(a.warmup, waves)))
     sync()
     elapsed = time.perf_counter() - t0
     mono1 = time.monotonic_ns()
+    prog_stop.set()
 
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev if info.backend == "nccl" else "cpu")
     p50_local = statistics.median(lat) if lat else float("nan")
@@ -267,6 +278,8 @@ def main() -> int:
                    "mode": a.mode, "hipgraph": bool(llm.use_graphs),
                    "waves": "serial" if (a.serial_waves or a.mode != "pipeline") else "pipelined"},
         "detail": {"init_s": round(init_s, 1), "prefill_tokens_per_gpu": ptoks, "decode_tokens_per_gpu": dtoks,
+                   "prefill_graph_replays": llm.stats.prefill_graph_replays - stats0[2],
+                   "prefill_graph_buckets": sorted(getattr(llm, "_prefill_g", {})),
                    "decode_tok_s_per_gpu": round(dtoks / elapsed, 1), "outcomes": counter["outcomes"],
                    "dfa_states": getattr(meng, "dfa_states", None), "timed_monotonic_ns": [mono0, mono1]},
     }

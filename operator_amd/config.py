@@ -110,6 +110,7 @@ class EngineCfg(BaseModel):
     kv_cache_gb: float = 64.0
     page_size: int = 64
     use_graphs: bool = True
+    prefill_graphs: bool = True       # full-ish prefill batches replay a captured bucket graph
     multi_step: int = 8
     ignore_eos: bool = False
 

@@ -35,7 +35,8 @@ def build_llm(s: Settings, device: str | torch.device | None = None, tp=None):
                                           e.page_size, torch.finfo(dtype).bits // 8)
     kv = PagedKVCache(cfg.layers, pages, model.hkv, cfg.head_dim, e.page_size, device=dev, dtype=dtype)
     kw = dict(max_batch=e.max_batch, max_prefill_tokens=e.max_prefill_tokens, max_context=e.max_context,
-              use_graphs=e.use_graphs, multi_step=e.multi_step, admit_wait_s=e.admit_wait_ms / 1e3)
+              use_graphs=e.use_graphs, multi_step=e.multi_step, admit_wait_s=e.admit_wait_ms / 1e3,
+              prefill_graphs=e.prefill_graphs)
     if tp is not None and tp.world > 1:   # one replica over the TP group: lock-stepped engines
         from operator_amd.engine.tp import TPLLMEngine, control_group
 

@@ -66,6 +66,7 @@ class EngineStats:
     decode_s: float = 0.0
     steps: int = 0
     graph_replays: int = 0
+    prefill_graph_replays: int = 0
 
 
 @dataclass
@@ -184,15 +185,87 @@ class _DecodeGraph:
             self._run()
 
 
+class _PrefillGraph:
+    """A prefill of up to ``T`` packed tokens / ``S`` sequences captured as one
+    hipGraph: embedding -> 32 layers (hipBLASLt GEMMs, norms, RoPE + KV write,
+    flash prefill attention) -> last-token lm_head -> sampler.
+
+    Why: an eager prefill is ~400 launches from the engine thread, each needing
+    the GIL. At the start of a wave the operator's pipeline threads hold it for
+    most of ~0.4 s (watch events, log collection, scan post-processing, prompt
+    rendering) and the first prefill measured 1.9x its GPU time. Inputs live at
+    fixed addresses: the real tokens are copied in, the tail is padding (id 0,
+    slot -1: no KV write, no attention work item, logits discarded), unused
+    attention work items are -1 (the kernel returns at once)."""
+
+    def __init__(self, eng: "LLMEngine", T: int, S: int, variant: int, block_q: int):
+        dev = eng.device
+        self.eng, self.T, self.S, self.variant = eng, T, S, variant
+        self.W = T // block_q + S               # work items: sum ceil(len / bq) <= T / bq + S
+        i64, i32 = torch.long, torch.int32
+        self.dev = {n: torch.zeros(k, dtype=dt, device=dev) for n, k, dt in (
+            ("ids", T, i64), ("pos", T, i64), ("slots", T, i64), ("last", S, i64), ("seeds", S, i64),
+            ("spos", S, i64), ("cu", S + 1, i32), ("ws", self.W, i32), ("wq", self.W, i32),
+            ("temp", S, torch.float32))}
+        self.host = {n: torch.zeros_like(t, device="cpu").pin_memory() for n, t in self.dev.items()}
+        self.graph: torch.cuda.CUDAGraph | None = None
+        self.tok: torch.Tensor | None = None
+
+    def _run(self) -> None:
+        e, d = self.eng, self.dev
+        fb = ForwardBatch(d["ids"], d["pos"], d["slots"], True, d["last"], seq_lens=[],
+                          prefill_work=(d["cu"], d["ws"], d["wq"], self.variant))
+        logits = e.model.forward(fb, e.kv)
+        self.tok = e.model.sample(logits, d["temp"], d["seeds"], d["spos"])
+
+    def capture(self, pool) -> None:
+        # every work item padding and every slot -1 while warming up: no KV writes
+        self.dev["slots"].fill_(-1)
+        self.dev["ws"].fill_(-1)
+        s = torch.cuda.Stream(device=self.eng.device)
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                self._run()
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, pool=pool):
+            self._run()
+        self.graph = g
+
+    def run(self, ids, pos, slots, cu, ws, wq, last, temp, seeds, spos) -> list[int]:
+        """Inputs as numpy arrays of the real batch (<= T tokens, <= S sequences)."""
+        h = self.host
+        b = len(last)
+        for name, arr, fill in (("ids", ids, 0), ("pos", pos, 0), ("slots", slots, -1), ("last", last, 0),
+                                ("seeds", seeds, 0), ("spos", spos, 0), ("temp", temp, 0.0), ("ws", ws, -1),
+                                ("wq", wq, 0), ("cu", cu, int(cu[-1]))):
+            v = h[name].numpy()
+            v[:len(arr)] = arr
+            v[len(arr):] = fill
+        for name in h:
+            self.dev[name].copy_(h[name], non_blocking=True)
+        self.graph.replay()
+        return self.tok[:b].tolist()   # synchronises: the pinned inputs are free again after this
+
+
 class LLMEngine:
     def __init__(self, model: LlamaModel, kv: PagedKVCache, max_batch: int = 256, max_prefill_tokens: int = 16384,
                  max_context: int | None = None, use_graphs: bool = True, multi_step: int = 8,
-                 admit_wait_s: float = 0.0):
+                 admit_wait_s: float = 0.0, prefill_graphs: bool = True):
         self.model, self.kv = model, kv
         # arrival batching window used by the loop that drives step() (EngineLoop):
         # an idle engine given less than a full prefill batch waits this long for more
         # requests. Not part of step() itself, which stays deterministic for TP.
         self.admit_wait_s = admit_wait_s
+        # graph-captured prefill buckets (tokens): the largest is max_prefill_tokens; a
+        # batch runs in the smallest bucket >= its tokens when that pads it by <= 15 %,
+        # eagerly otherwise
+        self.prefill_graphs = use_graphs and model.device.type == "cuda" and prefill_graphs
+        self.prefill_buckets = sorted({max_prefill_tokens} | {1024 << i for i in range(8)
+                                                              if (1024 << i) < max_prefill_tokens})
+        self._prefill_g: dict[int, _PrefillGraph] = {}
+        self._prefill_pool = None
         self.device = model.device
         self.max_batch = max_batch
         self.max_prefill_tokens = max_prefill_tokens
@@ -283,6 +356,9 @@ class LLMEngine:
         for bp in bs:
             for ns in (splits or self.split_options(bp)):
                 self._graph(bp, ns)
+        if self.prefill_graphs:
+            for T in sorted(self.prefill_buckets, reverse=True):
+                self._prefill_graph(T)
         torch.cuda.synchronize(self.device)
 
     # ------------------------------------------------------------------ scheduling
@@ -349,13 +425,19 @@ class LLMEngine:
         last = cu[1:] - 1
         var = ops.prefill_variant(self.model.hq, self.model.hkv)
         ws, wq = ops.prefill_work_list(lens, ops.prefill_block_q(self.model.hq, self.model.hkv, var))
-        t = lambda x, dt=torch.long: torch.as_tensor(np.asarray(x)).to(dtype=dt).to(dev, non_blocking=True)  # noqa: E731
-        work = (t(cu, torch.int32), t(ws, torch.int32), t(wq, torch.int32), var) if dev.type == "cuda" else None
-        fb = ForwardBatch(t(ids), t(pos), t(slots), True, t(last), seq_lens=lens, prefill_work=work)
-        logits = self.model.forward(fb, self.kv)
-        toks = self.model.sample(logits, t([r.temperature for r in batch], torch.float32),
-                                 t([r.seed for r in batch]), t([len(r.prompt) for r in batch]))
-        toks = toks.tolist()
+        temps = [r.temperature for r in batch]
+        seeds = [r.seed for r in batch]
+        g = self._prefill_graph_for(len(ids), len(batch))
+        if g is not None:
+            toks = g.run(ids, pos, slots, cu, ws, wq, last, temps, seeds, lens)
+            self.stats.prefill_graph_replays += 1
+        else:
+            t = lambda x, dt=torch.long: torch.as_tensor(np.asarray(x)).to(dtype=dt).to(dev, non_blocking=True)  # noqa: E731
+            work = (t(cu, torch.int32), t(ws, torch.int32), t(wq, torch.int32), var) if dev.type == "cuda" else None
+            fb = ForwardBatch(t(ids), t(pos), t(slots), True, t(last), seq_lens=lens, prefill_work=work)
+            logits = self.model.forward(fb, self.kv)
+            toks = self.model.sample(logits, t(temps, torch.float32), t(seeds), t(lens))
+            toks = toks.tolist()
         now = time.perf_counter()
         for r, tk in zip(batch, toks):
             r.output.append(int(tk))
@@ -364,6 +446,27 @@ class LLMEngine:
         self._active = None  # new rows joined
         self.stats.prefill_tokens += len(ids)
         self.stats.prefill_s += now - t0
+
+    def _prefill_graph(self, T: int) -> _PrefillGraph:
+        g = self._prefill_g.get(T)
+        if g is None:
+            var = ops.prefill_variant(self.model.hq, self.model.hkv)
+            g = _PrefillGraph(self, T, self.max_batch, var, ops.prefill_block_q(self.model.hq, self.model.hkv, var))
+            if self._prefill_pool is None:   # its own pool: prefill and decode graphs never share memory
+                self._prefill_pool = torch.cuda.graph_pool_handle()
+            g.capture(self._prefill_pool)
+            self._prefill_g[T] = g
+        return g
+
+    def _prefill_graph_for(self, tokens: int, seqs: int) -> _PrefillGraph | None:
+        """Graph bucket for a prefill of ``tokens`` tokens: the smallest bucket that
+        holds it, if the padding is <= 15 % (else None: run eagerly)."""
+        if not self.prefill_graphs or seqs > self.max_batch:
+            return None
+        for T in self.prefill_buckets:
+            if T >= tokens:
+                return self._prefill_graph(T) if tokens >= 0.85 * T else None
+        return None
 
     def _state(self, bp: int) -> _BucketState:
         st = self._states.get(bp)

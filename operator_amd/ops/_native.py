@@ -27,6 +27,26 @@ def _try_build() -> None:
     _build.build()
 
 
+def _check_fresh(mod_name: str, src_globs: tuple[str, ...]) -> None:
+    """Refuse an in-tree extension older than any of its sources: a GPU run of stale
+    kernels (e.g. a host-side contract the old binary does not implement) can fault the
+    device. OAMD_ALLOW_STALE=1 skips the check."""
+    if os.environ.get("OAMD_ALLOW_STALE"):
+        return
+    import glob
+
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    so = glob.glob(os.path.join(root, "operator_amd", mod_name + ".*.so"))
+    if not so:
+        return
+    built = min(os.path.getmtime(f) for f in so)
+    srcs = [f for g in src_globs for f in glob.glob(os.path.join(root, g))]
+    newer = [os.path.relpath(f, root) for f in srcs if os.path.getmtime(f) > built + 1.0]
+    if newer:
+        raise RuntimeError(f"operator_amd.{mod_name} is older than {newer[:4]}: rebuild with "
+                           "`python -m operator_amd._build` (or set OAMD_ALLOW_STALE=1)")
+
+
 def kernels():
     """Return the compiled gfx950 kernel module, building it in-tree if needed."""
     global _C, _err
@@ -35,6 +55,7 @@ def kernels():
     with _lock:
         if _C is not None:
             return _C
+        _check_fresh("_C", ("csrc/kernels/*", "csrc/*.cpp"))
         try:
             _C = importlib.import_module("operator_amd._C")
         except ImportError as e:  # not built yet
@@ -54,6 +75,7 @@ def patterns():
         return _P
     with _lock:
         if _P is None:
+            _check_fresh("_patterns", ("csrc/patterns/*",))
             try:
                 _P = importlib.import_module("operator_amd._patterns")
             except ImportError:

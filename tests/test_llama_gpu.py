@@ -121,3 +121,34 @@ def test_fp8_weights_model_runs_and_tracks_bf16():
         assert len(reqs[0].output) == 9
     cos = torch.nn.functional.cosine_similarity(outs["fp8"].flatten(), outs["bfloat16"].flatten(), dim=0)
     assert cos > 0.98, float(cos)
+
+
+def test_graph_prefill_equals_eager_prefill():
+    """A prefill replayed from a captured bucket graph (tokens padded to the bucket,
+    padding slots -1, padding attention items -1) writes the same KV cache and samples
+    the same tokens as the eager prefill; a batch too small for any bucket runs eagerly."""
+    cfg = get_config("tiny-gqa4")
+    m = LlamaModel(cfg, device="cuda").init_random(seed=7)
+    lens = [400, 350, 30, 170]          # 950 tokens: bucket 1024 (7 % padding)
+    outs, caches, replays = [], [], []
+    for pg in (False, True):
+        kv = PagedKVCache(cfg.layers, 256, cfg.kv_heads, 128, 16, device="cuda")
+        eng = LLMEngine(m, kv, max_batch=8, max_prefill_tokens=1024, max_context=1024, use_graphs=True,
+                        prefill_graphs=pg)
+        eng.warmup([8])
+        reqs = [GenRequest(list(range(3, 3 + n)), max_tokens=12, temperature=t, seed=i, ignore_eos=True)
+                for i, (n, t) in enumerate(zip(lens, (0.0, 0.5, 0.0, 1.0)))]
+        for r in reqs:
+            eng.submit(r)
+        eng.step()                       # the one prefill of all four
+        caches.append(torch.stack([kv.layer(i)[0].float() for i in range(cfg.layers)]).cpu())
+        while any(not r.done for r in reqs):
+            eng.step()
+        outs.append([r.output for r in reqs])
+        replays.append(eng.stats.prefill_graph_replays)
+        small = [GenRequest([5, 6, 7], max_tokens=2, ignore_eos=True)]   # 3 tokens: eager
+        eng.generate(small)
+        assert eng.stats.prefill_graph_replays == replays[-1]
+    assert replays == [0, 1]
+    assert outs[0] == outs[1]
+    assert torch.equal(caches[0], caches[1])
