@@ -83,13 +83,14 @@ def main() -> int:
     from operator_amd.kube.fake import FakeKube, failed_pod, running_pod
     from operator_amd.kube.resources import AIPROVIDERS, PODMORTEMS, PODS
     from operator_amd.patterns.synth import LogFactory, synthetic_library
+    from operator_amd.utils.tracing import trace_range
 
     s = load_settings(env={}, overrides={
         "engine.model": a.model, "engine.device": dev, "engine.max_batch": a.max_batch,
         "engine.max_prefill_tokens": a.prefill_tokens,
         "engine.max_context": a.prompt_tokens + a.max_tokens + 64, "engine.max_prompt_tokens": a.prompt_tokens,
         "engine.kv_cache_gb": a.kv_gb or (96.0 if dev != "cpu" else 1.0), "engine.use_graphs": not a.no_graphs, "engine.ignore_eos": True,
-        "engine.seed": 0, "health.enabled": False, "operator.workers": a.batch + 16, "operator.io_workers": 16,
+        "engine.seed": 0, "health.enabled": False, "operator.workers": 2 * a.batch + 16, "operator.io_workers": 16,
         "patterns.cache_dir": f"/tmp/oamd-bench-{os.getpid()}", "services.match_max_batch": 64,
         "services.match_batch_wait_ms": 5.0})
 
@@ -164,16 +165,27 @@ def main() -> int:
         while not op.monitors.list():
             time.sleep(0.01)
 
-        def inject(w: int) -> None:
-            names = [f"app-r{rank}-w{w}-{i}" for i in range(a.batch)]
-            for name, log in zip(names, logs[w]):
+        # The pods (running, with their logs) exist before the benchmark, as in a cluster
+        # where a pod runs for a while before it fails: creating them is cluster state,
+        # not operator work, and is done here, untimed. A wave is the FAILURE of its
+        # pods: each pod's status flips to a terminated, non-zero exit (the MODIFIED
+        # watch event the operator reacts to), and its latency is timed from there.
+        def wave_names(w: int) -> list[str]:
+            return [f"app-r{rank}-w{w}-{i}" for i in range(a.batch)]
+
+        for w in range(waves):
+            for name, log in zip(wave_names(w), logs[w]):
                 fk.create(PODS, running_pod(name, labels={"app": "bench"}))
                 fk.set_log("default", name, log)
-            for name in names:
-                cur = fk.get(PODS, name, "default")
-                cur["status"] = failed_pod(name, finished_at=f"2025-08-29T10:{w % 60:02d}:00Z")["status"]
-                t_inject[name] = time.perf_counter()
-                fk.replace(PODS, cur)
+        logs.clear()
+
+        def inject(w: int) -> None:
+            with trace_range(f"inject[{w}]"):
+                for name in wave_names(w):
+                    cur = fk.get(PODS, name, "default")
+                    cur["status"] = failed_pod(name, finished_at=f"2025-08-29T10:{w % 60:02d}:00Z")["status"]
+                    t_inject[name] = time.perf_counter()
+                    fk.replace(PODS, cur)
 
         def run_wave(w: int) -> None:
             with lock:

@@ -322,6 +322,20 @@ void sample(const at::Tensor& logits, const at::Tensor& temperature, const at::T
 
 }  // namespace
 
+// Launch an instantiated hipGraph `count` times back to back on `stream` with the
+// GIL released (decode windows: one call per window instead of one Python
+// replay per step, so host threads contending for the GIL cannot stall the feed).
+void graph_launch(int64_t exec, int64_t count, int64_t stream) {
+  TORCH_CHECK(exec != 0 && count >= 0, "graph_launch: bad graph / count");
+  hipError_t err = hipSuccess;
+  {
+    pybind11::gil_scoped_release nogil;
+    for (int64_t i = 0; i < count && err == hipSuccess; ++i)
+      err = hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(exec), reinterpret_cast<hipStream_t>(stream));
+  }
+  TORCH_CHECK(err == hipSuccess, "hipGraphLaunch failed: ", hipGetErrorString(err));
+}
+
 void register_scan_bindings(pybind11::module_& m);
 void register_comm_bindings(pybind11::module_& m);
 
@@ -355,6 +369,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("sample", &sample, pybind11::arg("logits"), pybind11::arg("temperature"), pybind11::arg("seeds"),
         pybind11::arg("positions"), pybind11::arg("out"), pybind11::arg("col_offset") = 0,
         pybind11::arg("out_val") = pybind11::none());
+  m.def("graph_launch", &graph_launch, pybind11::arg("graph_exec"), pybind11::arg("count"), pybind11::arg("stream"));
   register_scan_bindings(m);
   register_comm_bindings(m);
   m.attr("ARCH") = "gfx950";

@@ -36,6 +36,7 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(
   const int wi = blockIdx.x, hq = blockIdx.y;
   const int kvh = hq / (Hq / Hkv);
   const int seq = work_seq[wi];
+  if (seq < 0) return;  // padding item of a graph-captured prefill (fixed grid)
   const int s0 = cu_seqlens[seq];
   const int slen = cu_seqlens[seq + 1] - s0;
   const int q0 = work_q0[wi];
@@ -207,6 +208,7 @@ __global__ void __launch_bounds__(512) attn_prefill_gqa_kernel(
 
   const int wi = blockIdx.x, kvh = blockIdx.y;
   const int seq = work_seq[wi];
+  if (seq < 0) return;  // padding item of a graph-captured prefill (fixed grid)
   const int s0 = cu_seqlens[seq];
   const int slen = cu_seqlens[seq + 1] - s0;
   const int q0 = work_q0[wi];
@@ -409,6 +411,7 @@ __global__ void __launch_bounds__(512) attn_prefill_mfma32_kernel(
 
   const int wi = blockIdx.x, kvh = blockIdx.y;
   const int seq = work_seq[wi];
+  if (seq < 0) return;  // padding item of a graph-captured prefill (fixed grid)
   const int s0 = cu_seqlens[seq];
   const int slen = cu_seqlens[seq + 1] - s0;
   const int q0 = work_q0[wi];

@@ -32,7 +32,9 @@ from pydantic import BaseModel, Field
 
 class OperatorCfg(BaseModel):
     name: str = "podmortem-operator"
-    workers: int = 16                 # analysis pipeline thread pool
+    workers: int = 0                  # analysis pipeline threads; 0 = auto: a failure holds one through its
+                                      # explanation, so 2 x engine.max_batch x GPUs (+16) keep the engines'
+                                      # batches full while the previous batch's results are written
     io_workers: int = 8               # kube write pool (annotations, status, events)
     leader_election: bool = False     # reference: 1 replica, no lease; true = HA replicas behind a Lease
     lease_name: str = "podmortem-operator-leader"

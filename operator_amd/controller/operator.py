@@ -59,13 +59,22 @@ def load_patterns(settings: Settings, kube) -> PatternSet:
 
 
 class Operator:
+    @staticmethod
+    def pipeline_workers(s: Settings) -> int:
+        """operator.workers, or (0 = auto) enough threads for two engine batches per GPU in
+        flight: the one being explained and the previous one whose results are being
+        stored (a pipeline task holds its thread from detection to its last Event)."""
+        if s.operator.workers > 0:
+            return s.operator.workers
+        return 2 * s.engine.max_batch * max(1, s.engine.gpus) + 16
+
     def __init__(self, kube, settings: Settings, match_service=None, explain_service=None, metrics: Metrics | None = None,
                  match_engine_factory=None):
         s = self.settings = settings
         self.kube = kube
         self.metrics = metrics or Metrics()
         self.io_pool = TrackedExecutor(s.operator.io_workers, thread_name_prefix="kube-io")
-        self.pool = TrackedExecutor(s.operator.workers, thread_name_prefix="analysis")
+        self.pool = TrackedExecutor(self.pipeline_workers(s), thread_name_prefix="analysis")
         retrier = Retrier(s.storage.max_retries, s.storage.initial_backoff_s)
         self.status = StatusWriter(kube, retrier, s.storage.failure_time_from_pod)
         self.storage = AnalysisStorage(kube, self.status, self.io_pool)

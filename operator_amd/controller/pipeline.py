@@ -24,6 +24,8 @@ from concurrent.futures import Executor, Future
 from operator_amd.api.models import AnalysisResult, PodFailureData
 from operator_amd.kube.resources import CORE_EVENTS
 
+from operator_amd.utils.tracing import trace_range
+
 from . import ai_client
 from .events import EventEmitter
 from .storage import AnalysisStorage, StatusWriter
@@ -50,7 +52,8 @@ class AnalysisPipeline:
 
     # ------------------------------------------------------------------ entry points
     def submit(self, monitor: dict, pod: dict) -> Future | None:
-        self.events.emit_failure_detected(pod, monitor)
+        with trace_range("detected"):
+            self.events.emit_failure_detected(pod, monitor)
         if self.metrics:
             self.metrics.failures_detected.inc()
         if self.executor is None:
@@ -68,7 +71,8 @@ class AnalysisPipeline:
     def process(self, monitor: dict, pod: dict) -> str:
         t0 = time.perf_counter()
         try:
-            data = self.collect(pod)
+            with trace_range("collect"):
+                data = self.collect(pod)
         except Exception as e:  # noqa: BLE001
             log.error("Error processing pod failure for pod %s: %s", (pod.get("metadata") or {}).get("name"), e)
             self._fail(monitor, pod, "Processing failed: " + _msg(e))
@@ -139,7 +143,8 @@ class AnalysisPipeline:
             return "ai-failed"
         if self.metrics:
             self.metrics.stage_seconds.labels(stage="explain").observe(time.perf_counter() - t0)
-        self.storage.store(pod, monitor, result, text)
-        self.status.update_pod_failure(monitor, pod, "Analysis completed with AI analysis")
-        self.events.emit_analysis_complete(pod, monitor, result, text)
+        with trace_range("sinks"):
+            self.storage.store(pod, monitor, result, text)
+            self.status.update_pod_failure(monitor, pod, "Analysis completed with AI analysis")
+            self.events.emit_analysis_complete(pod, monitor, result, text)
         return "ai-complete"

@@ -204,8 +204,11 @@ class ExplainEngine:
         return prompt_mod.render_bounded(result, self.tok, self.max_prompt_tokens, cfg.prompt_template)
 
     def build_prompts(self, items: list[tuple[AnalysisResult, AIProviderConfig]]) -> list[list[int]]:
-        return prompt_mod.render_bounded_batch([(r, c.prompt_template) for r, c in items], self.tok,
-                                               self.max_prompt_tokens)
+        from operator_amd.utils.tracing import trace_range
+
+        with trace_range(f"prompts[{len(items)}]"):
+            return prompt_mod.render_bounded_batch([(r, c.prompt_template) for r, c in items], self.tok,
+                                                   self.max_prompt_tokens)
 
     def _key(self, ids: list[int], cfg: AIProviderConfig) -> str:
         h = hashlib.sha256()

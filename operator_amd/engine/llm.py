@@ -33,6 +33,13 @@ from operator_amd.models.llama import ForwardBatch, LlamaModel
 from operator_amd.utils.tracing import trace_range
 
 
+def _launch_graph(graph: "torch.cuda.CUDAGraph", count: int, device) -> None:
+    """Launch a captured graph ``count`` times on the current stream without holding
+    the GIL (operator_amd._C.graph_launch; torch's replay() is the same hipGraphLaunch
+    plus RNG bookkeeping that these graphs do not use)."""
+    ops.kernels().graph_launch(graph.raw_cuda_graph_exec(), count, torch.cuda.current_stream(device).cuda_stream)
+
+
 @dataclass(eq=False)  # identity semantics: two requests are never "equal"
 class GenRequest:
     prompt: list[int]
@@ -245,7 +252,7 @@ class _PrefillGraph:
             v[len(arr):] = fill
         for name in h:
             self.dev[name].copy_(h[name], non_blocking=True)
-        self.graph.replay()
+        _launch_graph(self.graph, 1, self.eng.device)
         return self.tok[:b].tolist()   # synchronises: the pinned inputs are free again after this
 
 
@@ -506,8 +513,15 @@ class LLMEngine:
             self._active = st
         st.step.zero_()
         with trace_range(f"decode[{bp}x{k}]"):
-            for _ in range(k):
-                g.run(self.use_graphs)
+            if self.use_graphs and g.graph is not None:
+                # the whole window from C++ with the GIL released: ROCm feeds a graph's
+                # kernels from the launching thread, and Python-level replays beside
+                # GIL-holding operator threads measured 2.2x slower per step
+                # (tools/bench_graph_contention.py)
+                _launch_graph(g.graph, k, self.device)
+            else:
+                for _ in range(k):
+                    g.run(False)
         if self._host_bufs is not None:
             self._hb ^= 1
             host = self._host_bufs[self._hb]

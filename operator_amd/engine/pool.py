@@ -126,7 +126,9 @@ def _worker_main(idx: int, device: str, settings_obj: dict, patterns, roles: tup
 
     threading.Thread(target=beat, daemon=True).start()
     outq.put(("ready", idx, {"device": device, "pid": os.getpid(), "roles": list(roles)}))
-    pool = ThreadPoolExecutor(max_workers=max(4, s.operator.workers))
+    # one thread per in-flight request (an explain blocks its thread until generated):
+    # as many as the engine can batch, twice, like the controller's own pipeline pool
+    pool = ThreadPoolExecutor(max_workers=max(4, s.operator.workers or 2 * s.engine.max_batch + 16))
 
     def run(rid, kind, payload):
         try:

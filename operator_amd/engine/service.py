@@ -89,6 +89,12 @@ class LocalMatchService:
             self._run(batch)
 
     def _run(self, batch) -> None:
+        from operator_amd.utils.tracing import trace_range
+
+        with trace_range(f"match.batch[{len(batch)}]"):
+            self._run_batch(batch)
+
+    def _run_batch(self, batch) -> None:
         docs = [(d.logs or "").encode("utf-8", "replace") for d, _ in batch]
         pods = [_pod_id(d.pod) for d, _ in batch]
         try:
