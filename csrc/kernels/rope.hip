@@ -14,8 +14,15 @@
 
 namespace oamd {
 
+// One 64-lane workgroup per (token, 64 work items): a token's (Hq + Hkv) x D/16
+// rotation items and Hkv x D/8 copy items are spread over ceil(items / 64)
+// workgroups, so a decode batch of 256 tokens is ~1.8k workgroups instead of 256
+// (the split-K form, which sums S fp32 slabs per element, was latency-bound at
+// one 256-thread workgroup per token: 7.8 us + a separate 5.5 us reduce kernel).
+constexpr int kRopeItems = 64;
+
 template <int D>
-__global__ void __launch_bounds__(256) rope_kv_kernel(
+__global__ void __launch_bounds__(kRopeItems) rope_kv_kernel(
     const bf16_t* __restrict__ qkv, int64_t qkv_stride, const int64_t* __restrict__ pos,
     const float* __restrict__ cos_t, const float* __restrict__ sin_t, int Hq, int Hkv,
     bf16_t* __restrict__ q_out, bf16_t* __restrict__ k_out, bf16_t* __restrict__ v_out,
@@ -61,7 +68,9 @@ __global__ void __launch_bounds__(256) rope_kv_kernel(
   }
   const int rot_items = (Hq + Hkv) * GPH;
   const int copy_items = Hkv * (D / 8);
-  for (int it = threadIdx.x; it < rot_items + copy_items; it += blockDim.x) {
+  {
+    const int it = blockIdx.y * kRopeItems + threadIdx.x;
+    if (it >= rot_items + copy_items) return;
     if (it < rot_items) {
       const int h = it / GPH, g = (it % GPH) * 8;
       const u16x8 x1 = ld8(h * D + g);
@@ -118,8 +127,11 @@ int rope_kv(const bf16_t* qkv, int64_t qkv_stride, const int64_t* pos, const flo
   if (tokens == 0) return 0;
   if (head_dim != 128) return -1;
   const int64_t slab = (int64_t)tokens * (Hq + 2 * Hkv) * head_dim;
-  rope_kv_kernel<128><<<tokens, 256, 0, stream>>>(qkv, qkv_stride, pos, cos_t, sin_t, Hq, Hkv, q_out, k_out,
-                                                 v_out, k_cache, v_cache, slots, page_size, max_pos, xp, S, slab);
+  const int items = (Hq + Hkv) * (head_dim / 16) + Hkv * (head_dim / 8);
+  const dim3 grid(tokens, (items + kRopeItems - 1) / kRopeItems);
+  rope_kv_kernel<128><<<grid, kRopeItems, 0, stream>>>(qkv, qkv_stride, pos, cos_t, sin_t, Hq, Hkv, q_out, k_out,
+                                                       v_out, k_cache, v_cache, slots, page_size, max_pos, xp, S,
+                                                       slab);
   OAMD_LAUNCH_CHECK();
   return 0;
 }

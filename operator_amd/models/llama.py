@@ -230,9 +230,9 @@ class LlamaModel:
             ws = ops.decode_workspace(T, self.hq, fb.num_splits, h.device)
         for i, lw in enumerate(self.layers):
             kc, vc = kv.layer(i)
-            # (rope_kv can also sum split-K slabs, but one block per token reading S fp32
-            # rows measured slower than the grid-wide reduce at B = 256: not deferred)
-            qkv = self._lin(x, lw.wqkv, lw.sqkv)
+            # a split-K decode QKV projection hands its fp32 slabs to rope_kv, which sums
+            # them per element (no separate reduce kernel)
+            qkv = self._lin(x, lw.wqkv, lw.sqkv, defer=True)
             q, k, v = ops.rope_kv(qkv, fb.positions, self.cos, self.sin, self.hq, self.hkv, kc, vc, fb.slots,
                                   want_kv=fb.is_prefill)
             if fb.is_prefill:

@@ -2,11 +2,14 @@
 prefill tokens/s, and the log-scan GB/s. Writes JSON lines to stdout."""
 import argparse
 import json
+import os
+import sys
 import time
 
 import torch
 
-from operator_amd.engine.llm import GenRequest, LLMEngine
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from operator_amd.engine.llm import GenRequest, LLMEngine  # noqa: E402
 from operator_amd.models.config import get_config
 from operator_amd.models.kv_cache import PagedKVCache
 from operator_amd.models.llama import LlamaModel
