@@ -84,7 +84,7 @@ void rope_kv(const at::Tensor& qkv, const at::Tensor& pos, const at::Tensor& cos
              int64_t Hq, int64_t Hkv, at::Tensor& q_out, const c10::optional<at::Tensor>& k_out,
              const c10::optional<at::Tensor>& v_out, const c10::optional<at::Tensor>& k_cache,
              const c10::optional<at::Tensor>& v_cache, const c10::optional<at::Tensor>& slots,
-             const c10::optional<at::Tensor>& partial, int64_t splits) {
+             const c10::optional<at::Tensor>& partial, int64_t splits, const c10::optional<at::Tensor>& bias) {
   CHECK_DT(pos, at::kLong); CHECK_CONTIG(pos); CHECK_DEV(pos);
   CHECK_DT(cos_t, at::kFloat); CHECK_DT(sin_t, at::kFloat); CHECK_CONTIG(cos_t); CHECK_CONTIG(sin_t);
   const int64_t T = pos.numel();
@@ -118,11 +118,15 @@ void rope_kv(const at::Tensor& qkv, const at::Tensor& pos, const at::Tensor& cos
     TORCH_CHECK(slots->numel() == T, "slots shape");
     page = (int)k_cache->size(2);
   }
+  if (bias.has_value()) {
+    CHECK_BF16(*bias); CHECK_CONTIG(*bias); CHECK_DEV(*bias);
+    TORCH_CHECK(bias->numel() == (Hq + 2 * Hkv) * D, "rope_kv: bias must be [(Hq + 2 Hkv) * D]");
+  }
   const c10::hip::HIPGuardMasqueradingAsCUDA g(pos.device());
   RC(oamd::rope_kv(qp, qstride, ptr<int64_t>(pos), ptr<float>(cos_t), ptr<float>(sin_t),
                    (int)T, (int)Hq, (int)Hkv, (int)D, ptr<bf16_t>(q_out), optr<bf16_t>(k_out), optr<bf16_t>(v_out),
                    optr<bf16_t>(k_cache), optr<bf16_t>(v_cache), optr<int64_t>(slots), page, cos_t.size(0),
-                   xp, (int)splits, cur_stream()));
+                   xp, (int)splits, optr<bf16_t>(bias), cur_stream()));
 }
 
 void gemm_decode(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& y_opt,
@@ -349,7 +353,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("rope_kv", &rope_kv, pybind11::arg("qkv"), pybind11::arg("pos"), pybind11::arg("cos"),
         pybind11::arg("sin"), pybind11::arg("Hq"), pybind11::arg("Hkv"), pybind11::arg("q_out"),
         pybind11::arg("k_out"), pybind11::arg("v_out"), pybind11::arg("k_cache"), pybind11::arg("v_cache"),
-        pybind11::arg("slots"), pybind11::arg("partial") = pybind11::none(), pybind11::arg("splits") = 1);
+        pybind11::arg("slots"), pybind11::arg("partial") = pybind11::none(), pybind11::arg("splits") = 1,
+        pybind11::arg("bias") = pybind11::none());
   m.def("attn_decode", &attn_decode);
   m.def("quantize_fp8", &quantize_fp8);
   m.def("score_events", &score_events);

@@ -322,6 +322,11 @@ int attn_decode(const bf16_t* q, const bf16_t* k_cache, const bf16_t* v_cache, c
     case 1: if (nt2) OAMD_DEC(1, 2); else OAMD_DEC(1, 1); break;
     case 2: if (nt2) OAMD_DEC(2, 2); else OAMD_DEC(2, 1); break;
     case 4: if (nt2) OAMD_DEC(4, 2); else OAMD_DEC(4, 1); break;
+    // groups of Llama-3.2-3B (24/8), Qwen2.5-32B (40/8), Qwen2.5-7B (28/4)
+    case 3: OAMD_DEC(3, 1); break;
+    case 5: OAMD_DEC(5, 1); break;
+    case 6: OAMD_DEC(6, 1); break;
+    case 7: OAMD_DEC(7, 1); break;
     case 8: OAMD_DEC(8, 1); break;
     default: return -3;
   }

@@ -20,7 +20,8 @@ int embedding(const int64_t* ids, const bf16_t* table, bf16_t* out, int tokens, 
 int rope_kv(const bf16_t* qkv, int64_t qkv_stride, const int64_t* pos, const float* cos_t,
             const float* sin_t, int tokens, int Hq, int Hkv, int head_dim, bf16_t* q_out,
             bf16_t* k_out, bf16_t* v_out, bf16_t* k_cache, bf16_t* v_cache, const int64_t* slots,
-            int page_size, int64_t max_pos, const float* xp, int S, hipStream_t stream);
+            int page_size, int64_t max_pos, const float* xp, int S, const bf16_t* bias,
+            hipStream_t stream);
 // Y[M,N] = X[M,K] W[N,K]^T for decode buckets (M a multiple of the BM-row tile, BM in {64,128,256}); S-way split-K
 // (S | 8) with fp32 slabs P[S][M][N] reduced into Y; BN in {64, 128} columns per tile.
 int gemm_decode(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, int N, int K, int S, int BN,

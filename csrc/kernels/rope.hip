@@ -9,6 +9,9 @@
 //   k_out/v_out [T, Hkv, D]      rotated k / copied v (optional, prefill path)
 //   k_cache/v_cache [pages, Hkv, P, D] at slot_mapping[t] (optional; slot<0 skips);
 //   K is stored in 16-token MFMA tiles (see attn_decode.hip), V row-major
+// An optional bf16 bias [(Hq + 2Hkv) D] (Qwen2's q/k/v projection bias) is added
+// in fp32 before the one bf16 rounding of the split-K slab sum (HF numerics:
+// bf16(x W^T + b)); on a bf16 qkv row it is added after that row's rounding.
 #include "common.h"
 #include "kernels.h"
 
@@ -28,7 +31,7 @@ __global__ void __launch_bounds__(kRopeItems) rope_kv_kernel(
     bf16_t* __restrict__ q_out, bf16_t* __restrict__ k_out, bf16_t* __restrict__ v_out,
     bf16_t* __restrict__ k_cache, bf16_t* __restrict__ v_cache,
     const int64_t* __restrict__ slots, int page_size, int64_t max_pos,
-    const float* __restrict__ xp, int S, int64_t slab) {
+    const float* __restrict__ xp, int S, int64_t slab, const bf16_t* __restrict__ bias) {
   constexpr int HALF = D / 2;
   constexpr int GPH = HALF / 8;  // 8-element groups per half-head
   const int t = blockIdx.x;
@@ -37,12 +40,31 @@ __global__ void __launch_bounds__(kRopeItems) rope_kv_kernel(
   // 8 consecutive qkv values of this row: from the bf16 row, or (xp set) the bf16
   // rounding of the sum of S fp32 split-K slabs of the QKV projection
   auto ld8 = [&](int col) -> u16x8 {
-    if (!xp) return *reinterpret_cast<const u16x8*>(row + col);
-    const float* pr = xp + (int64_t)t * ncol + col;
-    f32x4 lo = *reinterpret_cast<const f32x4*>(pr), hi = *reinterpret_cast<const f32x4*>(pr + 4);
-    for (int sp = 1; sp < S; ++sp) {
-      lo += *reinterpret_cast<const f32x4*>(pr + sp * slab);
-      hi += *reinterpret_cast<const f32x4*>(pr + sp * slab + 4);
+    if (!xp && !bias) return *reinterpret_cast<const u16x8*>(row + col);
+    f32x4 lo, hi;
+    if (xp) {
+      const float* pr = xp + (int64_t)t * ncol + col;
+      lo = *reinterpret_cast<const f32x4*>(pr);
+      hi = *reinterpret_cast<const f32x4*>(pr + 4);
+      for (int sp = 1; sp < S; ++sp) {
+        lo += *reinterpret_cast<const f32x4*>(pr + sp * slab);
+        hi += *reinterpret_cast<const f32x4*>(pr + sp * slab + 4);
+      }
+    } else {
+      const u16x8 r = *reinterpret_cast<const u16x8*>(row + col);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        lo[j] = bf2f(r[j]);
+        hi[j] = bf2f(r[4 + j]);
+      }
+    }
+    if (bias) {
+      const u16x8 bb = *reinterpret_cast<const u16x8*>(bias + col);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        lo[j] += bf2f(bb[j]);
+        hi[j] += bf2f(bb[4 + j]);
+      }
     }
     u16x8 o;
 #pragma unroll
@@ -123,7 +145,7 @@ int rope_kv(const bf16_t* qkv, int64_t qkv_stride, const int64_t* pos, const flo
             const float* sin_t, int tokens, int Hq, int Hkv, int head_dim, bf16_t* q_out,
             bf16_t* k_out, bf16_t* v_out, bf16_t* k_cache, bf16_t* v_cache,
             const int64_t* slots, int page_size, int64_t max_pos, const float* xp, int S,
-            hipStream_t stream) {
+            const bf16_t* bias, hipStream_t stream) {
   if (tokens == 0) return 0;
   if (head_dim != 128) return -1;
   const int64_t slab = (int64_t)tokens * (Hq + 2 * Hkv) * head_dim;
@@ -131,7 +153,7 @@ int rope_kv(const bf16_t* qkv, int64_t qkv_stride, const int64_t* pos, const flo
   const dim3 grid(tokens, (items + kRopeItems - 1) / kRopeItems);
   rope_kv_kernel<128><<<grid, kRopeItems, 0, stream>>>(qkv, qkv_stride, pos, cos_t, sin_t, Hq, Hkv, q_out, k_out,
                                                        v_out, k_cache, v_cache, slots, page_size, max_pos, xp, S,
-                                                       slab);
+                                                       slab, bias);
   OAMD_LAUNCH_CHECK();
   return 0;
 }

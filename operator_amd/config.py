@@ -97,7 +97,8 @@ class EngineCfg(BaseModel):
     gpus: int = 1                     # engine processes (one per GPU) behind the controller
     pool: bool = False                # run the engines out of process even with one GPU
     model: str = "llama3-8b"
-    model_path: Optional[str] = None  # HF safetensors dir; random init when absent
+    model_path: Optional[str] = None  # HF safetensors dir (its config.json wins over `model`); random init when absent
+    chat_template: str = "auto"       # auto = the checkpoint's tokenizer_config.json template; none; a file; Jinja
     seed: int = 0
     dtype: str = "bfloat16"
     weight_dtype: str = "bfloat16"   # bfloat16 | fp8 (W8A8 e4m3fn projections, e.g. Llama-3-70B)

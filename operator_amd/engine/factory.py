@@ -2,6 +2,7 @@
 from __future__ import annotations
 
 import logging
+import os
 
 import torch
 
@@ -14,14 +15,18 @@ log = logging.getLogger(__name__)
 def build_llm(s: Settings, device: str | torch.device | None = None, tp=None):
     """(model, kv, LLMEngine, Tokenizer) for the configured explanation model."""
     from operator_amd.engine.llm import LLMEngine
-    from operator_amd.engine.tokenizer import Tokenizer
-    from operator_amd.models.config import get_config
+    from operator_amd.engine.tokenizer import Tokenizer, load_chat_template
+    from operator_amd.models.config import config_from_hf, get_config
     from operator_amd.models.kv_cache import PagedKVCache
     from operator_amd.models.llama import LlamaModel
 
     e = s.engine
     dev = torch.device(device or e.device)
-    cfg = get_config(e.model)
+    # a checkpoint's own config.json defines the architecture (llama / mistral / qwen2)
+    if e.model_path and os.path.exists(os.path.join(e.model_path, "config.json")):
+        cfg = config_from_hf(e.model_path, name=e.model)
+    else:
+        cfg = get_config(e.model)
     dtype = getattr(torch, e.dtype)
     if tp is not None and tp.world > 1 and dev.type == "cuda" and e.oneshot_allreduce_mb > 0 \
             and getattr(tp, "oneshot", None) is None:
@@ -44,7 +49,8 @@ def build_llm(s: Settings, device: str | torch.device | None = None, tp=None):
     else:
         llm = LLMEngine(model, kv, **kw)
     tok = Tokenizer(cfg.vocab_size, cfg.bos_id, cfg.eos_ids[0],
-                    path=(f"{e.model_path}/tokenizer.json" if e.model_path else None))
+                    path=(f"{e.model_path}/tokenizer.json" if e.model_path else None), add_bos=cfg.add_bos,
+                    chat_template=load_chat_template(e.chat_template, e.model_path))
     log.info("explanation model %s: %.1f GB weights, %d KV pages (%d tokens)", cfg.name,
              model.weight_bytes() / 1e9, pages, pages * e.page_size)
     return model, kv, llm, tok

@@ -9,12 +9,22 @@ counts per log line are realistic (~3-4 bytes/token) instead of the 1 byte/token
 of a raw byte fallback. Special ids (BOS/EOS) come from the model config, and
 ids the trained vocabulary does not cover (a random-weight model can sample
 any id < vocab_size) are folded into range for decoding.
+
+A checkpoint tokenizer is used the way HF ``apply_chat_template`` uses it: its
+own post-processor's special tokens are NOT added (Llama-3's tokenizer.json
+would otherwise put a second <|begin_of_text|> in front of ours); BOS comes from
+the model config (``add_bos``: Qwen2 has none), and with a chat template (the
+checkpoint's ``tokenizer_config.json`` ``chat_template``, or an explicit one)
+each prompt is rendered as one user turn plus the assistant generation prompt,
+which also supplies BOS.
 """
 from __future__ import annotations
 
 import hashlib
+import json
 import os
 import threading
+import time
 from pathlib import Path
 
 _CACHE = Path(os.environ.get("OAMD_CACHE_DIR", Path(__file__).resolve().parent.parent / ".cache"))
@@ -49,17 +59,64 @@ def _corpus(n_lines: int = 40000):
             yield line
 
 
+def load_chat_template(spec: str | None, model_dir: str | None) -> str | None:
+    """Resolve ``engine.chat_template``: "none"/"" -> None; "auto" -> the checkpoint's
+    ``tokenizer_config.json`` chat_template (None without one); a path -> that file;
+    anything else is the Jinja template itself."""
+    if not spec or spec == "none":
+        return None
+    if spec == "auto":
+        if not model_dir:
+            return None
+        f = os.path.join(model_dir, "tokenizer_config.json")
+        if not os.path.exists(f):
+            return None
+        with open(f) as fh:
+            t = json.load(fh).get("chat_template")
+        if isinstance(t, list):  # named templates: take "default"
+            t = next((x.get("template") for x in t if x.get("name") == "default"), None)
+        return t or None
+    if os.path.exists(spec):
+        with open(spec) as fh:
+            return fh.read()
+    return spec
+
+
+def _compile_template(src: str):
+    from jinja2.exceptions import TemplateError
+    from jinja2.sandbox import ImmutableSandboxedEnvironment
+
+    def raise_exception(msg):
+        raise TemplateError(msg)
+
+    env = ImmutableSandboxedEnvironment(trim_blocks=True, lstrip_blocks=True)
+    env.globals["raise_exception"] = raise_exception
+    env.globals["strftime_now"] = lambda fmt: time.strftime(fmt)
+    return env.from_string(src)
+
+
 class Tokenizer:
-    def __init__(self, vocab_limit: int, bos_id: int, eos_id: int, path: str | None = None):
+    def __init__(self, vocab_limit: int, bos_id: int, eos_id: int, path: str | None = None,
+                 add_bos: bool = True, chat_template: str | None = None):
         import tokenizers
 
         self.bos_id, self.eos_id = bos_id, eos_id
+        self.add_bos = add_bos and bos_id >= 0
         path = path or os.environ.get("OAMD_TOKENIZER")
-        if path and os.path.exists(path):
+        self.from_checkpoint = bool(path and os.path.exists(path))
+        if self.from_checkpoint:
             self.tk = tokenizers.Tokenizer.from_file(path)
         else:
             self.tk = self._trained(min(32000, max(256 + 8, vocab_limit - 16)))
         self.n_vocab = self.tk.get_vocab_size()
+        self.chat = _compile_template(chat_template) if chat_template else None
+        if self.chat is not None:
+            tok = lambda i: (self.tk.id_to_token(i) or "") if i >= 0 else ""  # noqa: E731
+            self._chat_vars = {"bos_token": tok(bos_id), "eos_token": tok(eos_id), "add_generation_prompt": True}
+
+    def render_chat(self, text: str) -> str:
+        """One user turn + the assistant generation prompt, through the chat template."""
+        return self.chat.render(messages=[{"role": "user", "content": text}], **self._chat_vars)
 
     @staticmethod
     def _trained(vocab: int):
@@ -84,13 +141,18 @@ class Tokenizer:
             return tk
 
     def encode(self, text: str, bos: bool = True) -> list[int]:
-        ids = self.tk.encode(text).ids
-        return ([self.bos_id] if bos else []) + ids
+        return self.encode_batch([text], bos)[0]
 
     def encode_batch(self, texts: list[str], bos: bool = True) -> list[list[int]]:
-        return [([self.bos_id] if bos else []) + e.ids for e in self.tk.encode_batch(texts)]
+        """Prompt token ids. ``bos`` prepends the config's BOS (when the model has one);
+        with a chat template the template places BOS and the turn markers instead."""
+        if self.chat is not None:
+            return [e.ids for e in self.tk.encode_batch([self.render_chat(t) for t in texts],
+                                                        add_special_tokens=False)]
+        pre = [self.bos_id] if (bos and self.add_bos) else []
+        return [pre + e.ids for e in self.tk.encode_batch(texts, add_special_tokens=False)]
 
     def decode(self, ids: list[int]) -> str:
         n = self.n_vocab
         keep = [i % n for i in ids if i != self.bos_id and i != self.eos_id]
-        return self.tk.decode(keep)
+        return self.tk.decode(keep, skip_special_tokens=self.from_checkpoint)

@@ -73,6 +73,7 @@ class LayerWeights:
     so: torch.Tensor | None = None
     sgu: torch.Tensor | None = None
     sd: torch.Tensor | None = None
+    bqkv: torch.Tensor | None = None   # q|k|v projection bias (Qwen2), bf16 [(hq + 2 hkv) D]
 
 
 def _seed_for(seed: int, name: str) -> int:
@@ -130,9 +131,13 @@ class LlamaModel:
             wg = self._randn(seed, f"l{i}.wg", (c.intermediate, H), std_in)
             wu = self._randn(seed, f"l{i}.wu", (c.intermediate, H), std_in)
             wd = self._randn(seed, f"l{i}.wd", (H, c.intermediate), 1.0 / math.sqrt(c.intermediate))
+            bias = None
+            if c.qkv_bias:  # Qwen2-style q/k/v bias (random, O(1) like trained ones)
+                bias = tuple(self._randn(seed, f"l{i}.b{n}", (rows * D,), 0.5)
+                             for n, rows in (("q", c.heads), ("k", c.kv_heads), ("v", c.kv_heads)))
             self.layers.append(self._shard_layer(wq, wk, wv, wo, wg, wu, wd,
                                                  torch.ones(H, dtype=self.dtype, device=self.device),
-                                                 torch.ones(H, dtype=self.dtype, device=self.device)))
+                                                 torch.ones(H, dtype=self.dtype, device=self.device), bias))
             del wq, wk, wv, wo, wg, wu, wd
         self.final_norm = torch.ones(H, dtype=self.dtype, device=self.device)
         lm = self.embed if c.tie_embeddings else self._randn(seed, "lm_head", (c.vocab_size, H), std_in)
@@ -157,14 +162,21 @@ class LlamaModel:
             return ops.linear_fp8(x, w, sc)
         return ops.linear(x, w, defer_reduce=defer and self.tp.world == 1)
 
-    def _shard_layer(self, wq, wk, wv, wo, wg, wu, wd, an, mn) -> LayerWeights:
+    def _shard_layer(self, wq, wk, wv, wo, wg, wu, wd, an, mn, bias=None) -> LayerWeights:
+        """One layer's weights, sharded for this TP rank; ``bias`` = (bq, bk, bv) or None."""
         r, D = self.tp.rank, self.cfg.head_dim
         q = wq[r * self.hq * D:(r + 1) * self.hq * D]
         k = wk[r * self.hkv * D:(r + 1) * self.hkv * D]
         v = wv[r * self.hkv * D:(r + 1) * self.hkv * D]
         g = wg[r * self.inter:(r + 1) * self.inter]
         u = wu[r * self.inter:(r + 1) * self.inter]
+        bqkv = None
+        if bias is not None:
+            bq, bk, bv = bias
+            bqkv = torch.cat([bq[r * self.hq * D:(r + 1) * self.hq * D], bk[r * self.hkv * D:(r + 1) * self.hkv * D],
+                              bv[r * self.hkv * D:(r + 1) * self.hkv * D]]).to(self.dtype).contiguous()
         return self._quantize_layer(LayerWeights(
+            bqkv=bqkv,
             wqkv=torch.cat([q, k, v], 0).contiguous(),
             wo=wo[:, r * self.hq * D:(r + 1) * self.hq * D].contiguous(),
             wgu=(ops.interleave_gate_up(g, u, self.gu_block) if self.gu_block else torch.cat([g, u], 0).contiguous()),
@@ -180,7 +192,8 @@ class LlamaModel:
         return v[:, 0].reshape(inter, -1), v[:, 1].reshape(inter, -1)
 
     def load_hf(self, path: str) -> "LlamaModel":
-        """Load a HuggingFace Llama checkpoint directory (safetensors) and shard it."""
+        """Load a HuggingFace checkpoint directory (safetensors; llama / mistral / qwen2
+        tensor names) and shard it. ``self.cfg`` must describe it (``config_from_hf``)."""
         from safetensors import safe_open
 
         files = sorted(f for f in os.listdir(path) if f.endswith(".safetensors"))
@@ -201,11 +214,14 @@ class LlamaModel:
         self.layers = []
         for i in range(c.layers):
             p = f"model.layers.{i}."
+            bias = None
+            if c.qkv_bias:
+                bias = tuple(get(p + f"self_attn.{n}_proj.bias") for n in "qkv")
             self.layers.append(self._shard_layer(
                 get(p + "self_attn.q_proj.weight"), get(p + "self_attn.k_proj.weight"),
                 get(p + "self_attn.v_proj.weight"), get(p + "self_attn.o_proj.weight"),
                 get(p + "mlp.gate_proj.weight"), get(p + "mlp.up_proj.weight"), get(p + "mlp.down_proj.weight"),
-                get(p + "input_layernorm.weight"), get(p + "post_attention_layernorm.weight")))
+                get(p + "input_layernorm.weight"), get(p + "post_attention_layernorm.weight"), bias))
         self.final_norm = get("model.norm.weight")
         lm = get("lm_head.weight") if "lm_head.weight" in tensors else self.embed
         self.lm_head = lm[r * self.vocab_local:(r + 1) * self.vocab_local].contiguous()
@@ -215,7 +231,7 @@ class LlamaModel:
         n = sum(t.numel() * t.element_size() for t in (self.embed, self.final_norm, self.lm_head))
         for lw in self.layers:
             n += sum(t.numel() * t.element_size() for t in (lw.wqkv, lw.wo, lw.wgu, lw.wd, lw.attn_norm, lw.mlp_norm,
-                                                            lw.sqkv, lw.so, lw.sgu, lw.sd) if t is not None)
+                                                            lw.sqkv, lw.so, lw.sgu, lw.sd, lw.bqkv) if t is not None)
         return n
 
     # ------------------------------------------------------------------ forward
@@ -231,10 +247,15 @@ class LlamaModel:
         for i, lw in enumerate(self.layers):
             kc, vc = kv.layer(i)
             # a split-K decode QKV projection hands its fp32 slabs to rope_kv, which sums
-            # them per element (no separate reduce kernel)
-            qkv = self._lin(x, lw.wqkv, lw.sqkv, defer=True)
+            # them per element (no separate reduce kernel) and adds a Qwen2 bias before
+            # rounding; a prefill bias rides hipBLASLt's epilogue
+            bias = lw.bqkv
+            if bias is not None and fb.is_prefill and lw.sqkv is None:
+                qkv, bias = F.linear(x, lw.wqkv, bias), None
+            else:
+                qkv = self._lin(x, lw.wqkv, lw.sqkv, defer=True)
             q, k, v = ops.rope_kv(qkv, fb.positions, self.cos, self.sin, self.hq, self.hkv, kc, vc, fb.slots,
-                                  want_kv=fb.is_prefill)
+                                  want_kv=fb.is_prefill, bias=bias)
             if fb.is_prefill:
                 o = ops.attn_prefill(q, k, v, fb.seq_lens, self.scale, work=fb.prefill_work)
             else:

@@ -126,8 +126,10 @@ def embedding(ids: torch.Tensor, table: torch.Tensor, out: torch.Tensor | None =
 def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, Hq: int, Hkv: int,
             k_cache: torch.Tensor | None = None, v_cache: torch.Tensor | None = None,
             slots: torch.Tensor | None = None, want_kv: bool = True,
-            q_out: torch.Tensor | None = None):
+            q_out: torch.Tensor | None = None, bias: torch.Tensor | None = None):
     """Rotate q/k of the packed qkv rows and scatter k/v into the paged cache.
+    ``bias`` [(Hq + 2 Hkv) D] is added to the projection first (Qwen2); with split-K
+    slabs it is added before the single bf16 rounding.
 
     Returns (q [T,Hq,D], k [T,Hkv,D] | None, v [T,Hkv,D] | None).
     """
@@ -138,9 +140,11 @@ def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, cos: torch.Tensor, sin: torch.
         q = q_out if q_out is not None else torch.empty(T, Hq, D, dtype=torch.bfloat16, device=dev)
         k = torch.empty(T, Hkv, D, dtype=torch.bfloat16, device=dev) if want_kv else None
         v = torch.empty(T, Hkv, D, dtype=torch.bfloat16, device=dev) if want_kv else None
-        kernels().rope_kv(q, pos, cos, sin, Hq, Hkv, q, k, v, k_cache, v_cache, slots, qkv.p, qkv.S)
+        kernels().rope_kv(q, pos, cos, sin, Hq, Hkv, q, k, v, k_cache, v_cache, slots, qkv.p, qkv.S, bias)
         return q, k, v
     if not qkv.is_cuda:
+        if bias is not None:
+            qkv = (qkv.float() + bias.float()).to(qkv.dtype)
         q, k, v = reference.rope_kv(qkv, pos, cos, sin, Hq, Hkv, k_cache, v_cache, slots)
         if q_out is not None:
             q_out.copy_(q.reshape(q_out.shape))
@@ -151,7 +155,7 @@ def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, cos: torch.Tensor, sin: torch.
     q = q_out if q_out is not None else torch.empty(T, Hq, D, dtype=qkv.dtype, device=qkv.device)
     k = torch.empty(T, Hkv, D, dtype=qkv.dtype, device=qkv.device) if want_kv else None
     v = torch.empty(T, Hkv, D, dtype=qkv.dtype, device=qkv.device) if want_kv else None
-    kernels().rope_kv(qkv, pos, cos, sin, Hq, Hkv, q, k, v, k_cache, v_cache, slots)
+    kernels().rope_kv(qkv, pos, cos, sin, Hq, Hkv, q, k, v, k_cache, v_cache, slots, None, 1, bias)
     return q, k, v
 
 

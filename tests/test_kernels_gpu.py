@@ -102,7 +102,8 @@ def test_attn_prefill_large_scores():
 
 
 @pytest.mark.parametrize("lens", [[1, 5, 300], [1000, 0, 2049], [4096]])
-@pytest.mark.parametrize("Hq,Hkv,P", [(32, 8, 64), (8, 1, 16), (16, 16, 32)])
+@pytest.mark.parametrize("Hq,Hkv,P", [(32, 8, 64), (8, 1, 16), (16, 16, 32), (24, 8, 64), (28, 4, 64), (5, 1, 16),
+                                      (12, 2, 32)])
 def test_attn_decode(lens, Hq, Hkv, P):
     torch.manual_seed(4)
     B, D = len(lens), 128
@@ -301,3 +302,27 @@ def test_rope_kv_from_splitk_slabs():
     q2, k2, v2 = ops.rope_kv(sk.materialize(), pos, cos, sin, Hq, Hkv, kc2, vc2, slots)
     for a, b in ((q1, q2), (k1, k2), (v1, v2), (kc1, kc2), (vc1, vc2)):
         torch.testing.assert_close(a.float(), b.float(), atol=3e-2, rtol=2e-2)
+
+
+def test_rope_kv_bias_slabs_and_rows():
+    """Qwen2 q/k/v bias: added in fp32 to the split-K slab sum before the one bf16
+    rounding, and to a bf16 qkv row otherwise; equal to bias-then-rope in fp32."""
+    torch.manual_seed(13)
+    T, Hq, Hkv, D, S = 64, 7, 1, 128, 2
+    W = (Hq + 2 * Hkv) * D
+    P = torch.randn(S * T * W, device=DEV, dtype=torch.float32)
+    sk = ops.SplitK(P, S, T, W)
+    bias = (torch.randn(W, device=DEV) * 2).to(torch.bfloat16)
+    cos, sin = ref.rope_tables(4096, D, 1e6)
+    cos, sin = cos.to(DEV), sin.to(DEV)
+    pos = torch.randint(0, 4000, (T,), device=DEV)
+    slots = torch.randperm(128, device=DEV)[:T]
+    exact = (P.view(S, T, W).sum(0) + bias.float()).to(torch.bfloat16)
+    kc_r, vc_r = torch.zeros(8, Hkv, 16, D, dtype=torch.bfloat16), torch.zeros(8, Hkv, 16, D, dtype=torch.bfloat16)
+    q_r, k_r, v_r = ref.rope_kv(exact.cpu(), pos.cpu(), cos.cpu(), sin.cpu(), Hq, Hkv, kc_r, vc_r, slots.cpu())
+    for src in (sk, sk.materialize()):
+        kc = torch.zeros(8, Hkv, 16, D, device=DEV, dtype=torch.bfloat16)
+        vc = torch.zeros_like(kc)
+        q, k, v = ops.rope_kv(src, pos, cos, sin, Hq, Hkv, kc, vc, slots, bias=bias)
+        for a, b in ((q, q_r), (k, k_r), (v, v_r), (kc, kc_r), (vc, vc_r)):
+            torch.testing.assert_close(a.cpu().float(), b.float(), atol=6e-2, rtol=2e-2)

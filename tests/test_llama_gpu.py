@@ -15,13 +15,15 @@ def _cpu_copy(m: LlamaModel) -> LlamaModel:
     c = LlamaModel(m.cfg, device="cpu", dtype=torch.float32)
     c.embed, c.final_norm, c.lm_head = m.embed.float().cpu(), m.final_norm.float().cpu(), m.lm_head.float().cpu()
     from operator_amd.models.llama import LayerWeights
-    c.layers = [LayerWeights(*(t.float().cpu() for t in (l.wqkv, l.wo, l.wgu, l.wd, l.attn_norm, l.mlp_norm)))
+    c.layers = [LayerWeights(*(t.float().cpu() for t in (l.wqkv, l.wo, l.wgu, l.wd, l.attn_norm, l.mlp_norm)),
+                             bqkv=None if l.bqkv is None else l.bqkv.float().cpu())
                 for l in m.layers]
     return c
 
 
-def test_prefill_logits_match_cpu_reference():
-    cfg = get_config("tiny-gqa4")
+@pytest.mark.parametrize("name", ["tiny-gqa4", "tiny-qwen"])
+def test_prefill_logits_match_cpu_reference(name):
+    cfg = get_config(name)
     g = LlamaModel(cfg, device="cuda").init_random(seed=3)
     c = _cpu_copy(g)
     kv_g = PagedKVCache(cfg.layers, 32, cfg.kv_heads, 128, 16, device="cuda")
@@ -152,3 +154,34 @@ def test_graph_prefill_equals_eager_prefill():
     assert replays == [0, 1]
     assert outs[0] == outs[1]
     assert torch.equal(caches[0], caches[1])
+
+
+@pytest.mark.parametrize("B", [3, 64])
+def test_qwen_decode_step_matches_cpu_reference(B):
+    """Qwen2-shaped decode (q/k/v bias, GQA group 7): one paged decode step after a
+    prefill, GPU kernels vs the fp32 CPU path. B = 64 takes the split-K decode GEMM
+    whose slabs carry the bias into rope_kv; B = 3 the skinny bf16 path."""
+    cfg = get_config("tiny-qwen")
+    g = LlamaModel(cfg, device="cuda").init_random(seed=9)
+    c = _cpu_copy(g)
+    P, per = 16, 4
+    lens = [(7 * i) % 50 + 3 for i in range(B)]
+    out = []
+    for m, dev, dt in ((g, "cuda", torch.bfloat16), (c, "cpu", torch.float32)):
+        kv = PagedKVCache(cfg.layers, B * per, cfg.kv_heads, 128, P, device=dev, dtype=dt)
+        bt = torch.arange(B * per, dtype=torch.int32).reshape(B, per)
+        ids = [torch.randint(0, cfg.vocab_size, (L,), generator=torch.Generator().manual_seed(i))
+               for i, L in enumerate(lens)]
+        pos = torch.cat([torch.arange(L) for L in lens])
+        slots = torch.cat([bt[i, torch.arange(L) // P].long() * P + torch.arange(L) % P for i, L in enumerate(lens)])
+        fb = ForwardBatch(torch.cat(ids).to(dev), pos.to(dev), slots.to(dev), True,
+                          torch.tensor([0]).to(dev), seq_lens=lens)
+        m.forward(fb, kv)
+        nxt = torch.tensor([int(x[-1]) for x in ids])
+        dpos = torch.tensor(lens)
+        dslots = torch.stack([bt[i, L // P].long() * P + L % P for i, L in enumerate(lens)])
+        fb = ForwardBatch(nxt.to(dev), dpos.to(dev), dslots.to(dev), False, None, block_tables=bt.to(dev),
+                          context_lens=(dpos + 1).int().to(dev), num_splits=1)
+        out.append(m.forward(fb, kv).float().cpu())
+    err = (out[0] - out[1]).abs().max() / out[1].abs().max()
+    assert err < 0.05, float(err)
