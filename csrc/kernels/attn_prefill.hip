@@ -420,6 +420,9 @@ __global__ void __launch_bounds__(512) attn_prefill_mfma32_kernel(
   const int hq = kvh * G + (w % G);
   const int rbase = q0 + 32 * (w / G);  // this wave's first query row
   const int qrow = rbase + r32;          // this lane's query row (C column)
+  // G = 3, 5, 6, 7: only G x RG of the 8 waves have a (head, row block); the rest
+  // stage K/V tiles with the others and compute nothing
+  const bool wave_used = w < G * RG;
 
   // Q^T as the B operand: k-step s covers d = 16s .. 16s+15; lane holds d = 16s + 8h + j
   u16x8 qb[8];
@@ -436,7 +439,7 @@ __global__ void __launch_bounds__(512) attn_prefill_mfma32_kernel(
 
   const int kend = min(slen, q0 + BQ);
   const int ntiles = (kend + BK - 1) / BK;
-  const bool active = rbase < slen;
+  const bool active = wave_used && rbase < slen;
   const int wend = min(slen, rbase + 32);  // keys this wave can see: < wend
 
   // transposed-read addressing: 16-lane group g reads rows r0 + q (q = i >> 2) at
@@ -565,15 +568,14 @@ __global__ void __launch_bounds__(512) attn_prefill_mfma32_kernel(
 }
 
 // Query rows per work item of each variant: 1 = per-query-head (64 rows, any G),
-// 2 = GQA-grouped 16-row waves, 3 = GQA-grouped swapped 32x32 (32-row waves);
-// 2 and 3 need G = Hq / Hkv in {1, 2, 4, 8} (else -1).
+// 2 = GQA-grouped 16-row waves (G = Hq / Hkv in {1, 2, 4, 8}), 3 = GQA-grouped
+// swapped 32x32 (32-row waves, any G <= 8: 8 / G row blocks per item); else -1.
 int attn_prefill_block_q(int Hq, int Hkv, int variant) {
   if (variant == 1) return 64;
   if (Hkv <= 0 || Hq % Hkv != 0) return -1;
   const int G = Hq / Hkv;
-  if (G != 1 && G != 2 && G != 4 && G != 8) return -1;
-  if (variant == 2) return 16 * (8 / G);
-  if (variant == 3) return 32 * (8 / G);
+  if (variant == 2 && (G == 1 || G == 2 || G == 4 || G == 8)) return 16 * (8 / G);
+  if (variant == 3 && G >= 1 && G <= 8) return 32 * (8 / G);
   return -1;
 }
 
@@ -602,7 +604,13 @@ int attn_prefill(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, c
     if (variant == 2) {
       OAMD_PF_G(attn_prefill_gqa_kernel)
     } else {
-      OAMD_PF_G(attn_prefill_mfma32_kernel)
+      switch (G) {  // groups of Llama-3.2-3B (3), Qwen2.5-32B (5), Qwen2.5-7B (7)
+        case 3: OAMD_PF(attn_prefill_mfma32_kernel, 3); break;
+        case 5: OAMD_PF(attn_prefill_mfma32_kernel, 5); break;
+        case 6: OAMD_PF(attn_prefill_mfma32_kernel, 6); break;
+        case 7: OAMD_PF(attn_prefill_mfma32_kernel, 7); break;
+        default: OAMD_PF_G(attn_prefill_mfma32_kernel)
+      }
     }
 #undef OAMD_PF_G
 #undef OAMD_PF

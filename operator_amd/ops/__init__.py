@@ -163,13 +163,15 @@ _PREFILL_VARIANTS = {"v1": 1, "v2": 2, "v3": 3}
 
 
 def prefill_variant(Hq: int, Hkv: int) -> int:
-    """attn_prefill kernel variant: 1 = per-query-head (any G), 2 = GQA-grouped 16-row waves,
-    3 = GQA-grouped swapped-operand 32x32 MFMA waves (2 and 3 need G = Hq / Hkv in 1, 2, 4, 8).
-    OAMD_PREFILL_ATTN=v1|v2|v3 overrides the default (v3); grouped variants fall back to v1
-    for other G."""
+    """attn_prefill kernel variant: 1 = per-query-head (any G), 2 = GQA-grouped 16-row waves
+    (G = Hq / Hkv in 1, 2, 4, 8), 3 = GQA-grouped swapped-operand 32x32 MFMA waves (G <= 8).
+    OAMD_PREFILL_ATTN=v1|v2|v3 overrides the default (v3); a grouped variant that cannot
+    take G falls back to v3, then v1."""
     G = Hq // Hkv if Hkv and Hq % Hkv == 0 else 0
     want = _PREFILL_VARIANTS.get(os.environ.get("OAMD_PREFILL_ATTN", "v3"), 3)
-    return want if G in (1, 2, 4, 8) else 1
+    if want == 2 and G not in (1, 2, 4, 8):
+        want = 3
+    return want if 1 <= G <= 8 else 1
 
 
 def prefill_block_q(Hq: int, Hkv: int, variant: int | None = None) -> int:
