@@ -68,8 +68,12 @@ def main() -> int:
 
     from operator_amd.parallel.comm import init_from_env
 
-    info = init_from_env()
-    rank, world, local = info.rank, info.world, info.local_rank
+    # OAMD_BENCH_SHARE_GPU=1: rehearsal of the multi-rank launch on a one-GPU box —
+    # every rank on cuda:0, gloo for the timing collectives (RCCL refuses two ranks
+    # on one device), KV budget split so the ranks fit one card. Not a scaling number.
+    share = os.environ.get("OAMD_BENCH_SHARE_GPU") == "1"
+    info = init_from_env(backend="gloo" if share else None)
+    rank, world, local = info.rank, info.world, (0 if share else info.local_rank)
     if torch.cuda.is_available():
         torch.cuda.set_device(local)
     dev = f"cuda:{local}" if torch.cuda.is_available() else "cpu"
@@ -89,12 +93,21 @@ def main() -> int:
         "engine.model": a.model, "engine.device": dev, "engine.max_batch": a.max_batch,
         "engine.max_prefill_tokens": a.prefill_tokens,
         "engine.max_context": a.prompt_tokens + a.max_tokens + 64, "engine.max_prompt_tokens": a.prompt_tokens,
-        "engine.kv_cache_gb": a.kv_gb or (96.0 if dev != "cpu" else 1.0), "engine.use_graphs": not a.no_graphs, "engine.ignore_eos": True,
+        "engine.kv_cache_gb": a.kv_gb or (1.0 if dev == "cpu" else 96.0 if not share else max(8.0, 200.0 / world - 16)), "engine.use_graphs": not a.no_graphs, "engine.ignore_eos": True,
         "engine.seed": 0, "health.enabled": False, "operator.workers": 2 * a.batch + 16, "operator.io_workers": 16,
         "patterns.cache_dir": f"/tmp/oamd-bench-{os.getpid()}", "services.match_max_batch": 64,
         "services.match_batch_wait_ms": 5.0})
 
+    def note(msg: str) -> None:   # stage progress on stderr (the JSON line stays alone on stdout)
+        print(f"[bench rank {rank}] {msg}", file=sys.stderr, flush=True)
+
+    if os.environ.get("OAMD_BENCH_STACKS_S"):   # debugging a stall: every thread's stack, then exit
+        import faulthandler
+
+        faulthandler.dump_traceback_later(float(os.environ["OAMD_BENCH_STACKS_S"]), exit=True)
+
     # ---- engines (weights, DFA, graphs) : not timed ----
+    note("init: patterns, weights, graphs")
     t_init = time.perf_counter()
     patset = synthetic_library(a.patterns, seed=0)
     meng = MatchEngine(patset, device=dev, seg_bytes=s.patterns.seg_bytes)
@@ -103,6 +116,7 @@ def main() -> int:
     ee = ExplainEngine(llm, tok, model_id=a.model, max_prompt_tokens=a.prompt_tokens, ignore_eos=True)
     explainer = LocalExplainService(ee)
     init_s = time.perf_counter() - t_init
+    note(f"init done in {init_s:.1f} s")
 
     fac = LogFactory(n_patterns=a.patterns, seed=rank)
     waves = a.warmup + a.steps
@@ -236,6 +250,17 @@ def main() -> int:
             for w in ws:
                 run_wave(w)
 
+    # a progress line on stderr every 30 s (stdout stays the ONE JSON line)
+    prog_stop = threading.Event()
+
+    def progress():
+        t_start = time.perf_counter()
+        while not prog_stop.wait(30.0):
+            print(f"[bench rank {rank}] {time.perf_counter() - t_start:.0f} s, {counter['n']} analyses in the current "
+                  f"pass", file=sys.stderr, flush=True)
+
+    threading.Thread(target=progress, daemon=True).start()
+    note(f"{a.warmup} warmup wave(s)")
     for w in range(a.warmup):
         run_wave(w)
     lat.clear()
@@ -249,16 +274,7 @@ def main() -> int:
             dist.barrier()
 
     sync()
-    # a progress line on stderr every 30 s (stdout stays the ONE JSON line)
-    prog_stop = threading.Event()
-
-    def progress():
-        t_start = time.perf_counter()
-        while not prog_stop.wait(30.0):
-            print(f"[bench rank {rank}] {time.perf_counter() - t_start:.0f} s, {counter['n']} analyses in the current "
-                  f"pass", file=sys.stderr, flush=True)
-
-    threading.Thread(target=progress, daemon=True).start()
+    note("timed waves")
     t0 = time.perf_counter()
     mono0 = time.monotonic_ns()  # same clock as rocprofv3 timestamps: lets a trace be cut to the timed region
     run_timed(list(range(a.warmup, waves)))
@@ -295,6 +311,8 @@ def main() -> int:
                    "decode_tok_s_per_gpu": round(dtoks / elapsed, 1), "outcomes": counter["outcomes"],
                    "dfa_states": getattr(meng, "dfa_states", None), "timed_monotonic_ns": [mono0, mono1]},
     }
+    if share:
+        out["detail"]["shared_gpu_rehearsal"] = True
     if rank == 0:
         print(json.dumps(out), flush=True)
         if a.json_out:

@@ -83,7 +83,8 @@ class EngineLoop(threading.Thread):
 
     def run(self) -> None:
         if self.llm.device.type == "cuda":
-            torch.cuda.set_device(self.llm.device)
+            if self.llm.device.index is not None:   # "cuda" alone: the thread's default device
+                torch.cuda.set_device(self.llm.device)
             if sys.getswitchinterval() > self.GIL_SWITCH_S:
                 sys.setswitchinterval(self.GIL_SWITCH_S)
         while True:

@@ -29,6 +29,9 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--ctx", type=int, default=1100)
     ap.add_argument("--steps", type=int, default=160)
+    ap.add_argument("--sync-start", type=int, default=0,
+                    help="N processes run together: each waits at a file barrier under /tmp before timing")
+    ap.add_argument("--only-alone", action="store_true")
     a = ap.parse_args()
     cfg = get_config("llama3-8b")
     m = LlamaModel(cfg, device="cuda").init_random(0)
@@ -79,7 +82,22 @@ def main():
                 x += i * i
 
     py_replays(8)
-    out = {"B": B, "bucket": bp, "ctx": a.ctx}
+    torch.cuda.synchronize()
+    if a.sync_start:   # crude cross-process start barrier: every process touches a file, waits for N
+        d = "/tmp/oamd_sync_start"
+        os.makedirs(d, exist_ok=True)
+        open(os.path.join(d, str(os.getpid())), "w").close()
+        t_end = time.time() + 120
+        while len(os.listdir(d)) < a.sync_start and time.time() < t_end:
+            time.sleep(0.01)
+    out = {"B": B, "bucket": bp, "ctx": a.ctx, "procs": max(1, a.sync_start)}
+    if a.sync_start:
+        t0 = time.perf_counter()
+        c_replays(a.steps * 2)
+        torch.cuda.synchronize()
+        out["together_c_ms"] = round((time.perf_counter() - t0) * 1e3 / (a.steps * 2), 3)
+        print(json.dumps(out), flush=True)
+        return
     out["alone_py_ms"] = round(timed(py_replays), 3)
     out["alone_c_ms"] = round(timed(c_replays), 3)
     th = [threading.Thread(target=spin, daemon=True) for _ in range(4)]
