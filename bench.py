@@ -57,6 +57,9 @@ def parse_args():
     ap.add_argument("--serial-waves", action="store_true",
                     help="wait for every sink write of a wave before writing the next one")
     ap.add_argument("--kv-gb", type=float, default=None, help="KV-cache budget (default 96 GB on GPU, 1 GB on CPU)")
+    ap.add_argument("--engine-procs", type=int, default=1,
+                    help="engine processes per GPU (EnginePool workers holding the scan + LLM engines, "
+                         "--max-batch split over them); 1 = engines inside this process")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -72,31 +75,57 @@ def main() -> int:
     # every rank on cuda:0, gloo for the timing collectives (RCCL refuses two ranks
     # on one device), KV budget split so the ranks fit one card. Not a scaling number.
     share = os.environ.get("OAMD_BENCH_SHARE_GPU") == "1"
+    procs = max(1, a.engine_procs)
+    if procs > 1 and a.mode != "pipeline":
+        raise SystemExit("--engine-procs > 1 runs the operator pipeline (--mode pipeline)")
+
+    from operator_amd.config import load_settings
+    from operator_amd.patterns.synth import LogFactory, synthetic_library
+
+    def settings(dev: str, max_batch: int, world_: int):
+        kv = a.kv_gb or (1.0 if dev == "cpu" else (96.0 if not share else max(8.0, 200.0 / world_ - 16)) / procs)
+        return load_settings(env={}, overrides={
+            "engine.model": a.model, "engine.device": dev, "engine.max_batch": max_batch,
+            "engine.max_prefill_tokens": a.prefill_tokens,
+            "engine.max_context": a.prompt_tokens + a.max_tokens + 64, "engine.max_prompt_tokens": a.prompt_tokens,
+            "engine.kv_cache_gb": kv, "engine.use_graphs": not a.no_graphs, "engine.ignore_eos": True,
+            "engine.seed": 0, "health.enabled": False, "operator.workers": 2 * a.batch + 16, "operator.io_workers": 16,
+            "patterns.cache_dir": f"/tmp/oamd-bench-{os.getpid()}", "services.match_max_batch": 64,
+            "services.match_batch_wait_ms": 5.0})
+
+    patset = synthetic_library(a.patterns, seed=0)
+    pool = None
+    t_pool = time.perf_counter()
+    if procs > 1:
+        # engine processes (spawned) start before this process touches the GPU; each
+        # holds the scan DFA and its own copy of the model, and serves max_batch / procs
+        from operator_amd.engine.pool import EnginePool
+
+        world_env = int(os.environ.get("WORLD_SIZE", "1"))
+        local_env = 0 if share else int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0")))
+        dev0 = f"cuda:{local_env}" if torch.cuda.device_count() > 0 else "cpu"
+        pool = EnginePool(settings(dev0, max(1, a.max_batch // procs), world_env), patset, devices=[dev0] * procs)
+
+    # OAMD_BENCH_SHARE_GPU=1: rehearsal of the multi-rank launch on a one-GPU box —
+    # every rank on cuda:0, gloo for the timing collectives (RCCL refuses two ranks
+    # on one device), KV budget split so the ranks fit one card. Not a scaling number.
     info = init_from_env(backend="gloo" if share else None)
     rank, world, local = info.rank, info.world, (0 if share else info.local_rank)
     if torch.cuda.is_available():
         torch.cuda.set_device(local)
     dev = f"cuda:{local}" if torch.cuda.is_available() else "cpu"
 
-    from operator_amd.config import load_settings
     from operator_amd.controller.operator import Operator
     from operator_amd.engine.explain import ExplainEngine
     from operator_amd.engine.factory import build_llm
     from operator_amd.engine.match import MatchEngine
+    from operator_amd.engine.pool import PoolExplainService, PoolMatchService
     from operator_amd.engine.service import LocalExplainService, LocalMatchService
     from operator_amd.kube.fake import FakeKube, failed_pod, running_pod
     from operator_amd.kube.resources import AIPROVIDERS, PODMORTEMS, PODS
-    from operator_amd.patterns.synth import LogFactory, synthetic_library
     from operator_amd.utils.tracing import trace_range
 
-    s = load_settings(env={}, overrides={
-        "engine.model": a.model, "engine.device": dev, "engine.max_batch": a.max_batch,
-        "engine.max_prefill_tokens": a.prefill_tokens,
-        "engine.max_context": a.prompt_tokens + a.max_tokens + 64, "engine.max_prompt_tokens": a.prompt_tokens,
-        "engine.kv_cache_gb": a.kv_gb or (1.0 if dev == "cpu" else 96.0 if not share else max(8.0, 200.0 / world - 16)), "engine.use_graphs": not a.no_graphs, "engine.ignore_eos": True,
-        "engine.seed": 0, "health.enabled": False, "operator.workers": 2 * a.batch + 16, "operator.io_workers": 16,
-        "patterns.cache_dir": f"/tmp/oamd-bench-{os.getpid()}", "services.match_max_batch": 64,
-        "services.match_batch_wait_ms": 5.0})
+    s = settings(dev, a.max_batch, world)
 
     def note(msg: str) -> None:   # stage progress on stderr (the JSON line stays alone on stdout)
         print(f"[bench rank {rank}] {msg}", file=sys.stderr, flush=True)
@@ -107,16 +136,38 @@ def main() -> int:
         faulthandler.dump_traceback_later(float(os.environ["OAMD_BENCH_STACKS_S"]), exit=True)
 
     # ---- engines (weights, DFA, graphs) : not timed ----
-    note("init: patterns, weights, graphs")
+    note("init: patterns, weights, graphs" + (f" in {procs} engine processes" if pool else ""))
     t_init = time.perf_counter()
-    patset = synthetic_library(a.patterns, seed=0)
-    meng = MatchEngine(patset, device=dev, seg_bytes=s.patterns.seg_bytes)
-    model, kv, llm, tok = build_llm(s, device=dev)
-    llm.warmup([b for b in llm.buckets if b <= a.max_batch])
-    ee = ExplainEngine(llm, tok, model_id=a.model, max_prompt_tokens=a.prompt_tokens, ignore_eos=True)
-    explainer = LocalExplainService(ee)
+    meng = llm = ee = None
+    if pool is not None:
+        ready = pool.wait_ready(900)
+        if ready < procs:
+            raise SystemExit(f"only {ready} of {procs} engine processes started: {pool.health()}")
+        t_init = t_pool
+    else:
+        meng = MatchEngine(patset, device=dev, seg_bytes=s.patterns.seg_bytes)
+        model, kv, llm, tok = build_llm(s, device=dev)
+        llm.warmup([b for b in llm.buckets if b <= a.max_batch])
+        ee = ExplainEngine(llm, tok, model_id=a.model, max_prompt_tokens=a.prompt_tokens, ignore_eos=True)
+        explainer = LocalExplainService(ee)
     init_s = time.perf_counter() - t_init
     note(f"init done in {init_s:.1f} s")
+
+    def engine_stats() -> dict:
+        """Prefill / decode token counters, prefill graph buckets and DFA size, summed
+        over the engine processes (or read from the in-process engines)."""
+        if pool is None:
+            st = llm.stats
+            return {"prefill_tokens": st.prefill_tokens, "decode_tokens": st.decode_tokens,
+                    "prefill_graph_replays": st.prefill_graph_replays, "use_graphs": bool(llm.use_graphs),
+                    "prefill_graph_buckets": sorted(getattr(llm, "_prefill_g", {})),
+                    "dfa_states": getattr(meng, "dfa_states", None)}
+        ws = pool.worker_stats()
+        out = {k: sum(w["llm"][k] for w in ws) for k in ("prefill_tokens", "decode_tokens", "prefill_graph_replays")}
+        out.update(use_graphs=all(w.get("use_graphs") for w in ws),
+                   prefill_graph_buckets=sorted({b for w in ws for b in w.get("prefill_graph_buckets", [])}),
+                   dfa_states=ws[0].get("dfa_states") if ws else None)
+        return out
 
     fac = LogFactory(n_patterns=a.patterns, seed=rank)
     waves = a.warmup + a.steps
@@ -130,7 +181,10 @@ def main() -> int:
 
     if a.mode == "pipeline":
         fk = FakeKube()
-        matcher = LocalMatchService(meng, max_batch=64, max_wait_ms=5.0)
+        if pool is not None:
+            matcher, explainer = PoolMatchService(pool), PoolExplainService(pool)
+        else:
+            matcher = LocalMatchService(meng, max_batch=64, max_wait_ms=5.0)
         explained = {"n": 0}
         exp_cv = threading.Condition()
 
@@ -265,7 +319,7 @@ def main() -> int:
         run_wave(w)
     lat.clear()
     counter["outcomes"] = {}
-    stats0 = (llm.stats.prefill_tokens, llm.stats.decode_tokens, llm.stats.prefill_graph_replays)
+    stats0 = engine_stats()
 
     def sync():
         if torch.cuda.is_available():
@@ -292,8 +346,9 @@ def main() -> int:
     elapsed = float(el.item())
     total = a.batch * a.steps * world
     value = total / elapsed
-    ptoks = llm.stats.prefill_tokens - stats0[0]
-    dtoks = llm.stats.decode_tokens - stats0[1]
+    stats1 = engine_stats()
+    ptoks = stats1["prefill_tokens"] - stats0["prefill_tokens"]
+    dtoks = stats1["decode_tokens"] - stats0["decode_tokens"]
     out = {
         "metric": METRIC, "value": round(value, 3), "unit": "analyses/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 2), "higher_is_better": True,
@@ -303,13 +358,13 @@ def main() -> int:
         "config": {"model": a.model, "global_batch": a.batch * world, "seq_len": a.prompt_tokens + a.max_tokens,
                    "parallelism": f"dp{world}", "tp": 1, "max_tokens": a.max_tokens,
                    "prompt_tokens_cap": a.prompt_tokens, "log_kib": a.log_kb, "patterns": a.patterns,
-                   "mode": a.mode, "hipgraph": bool(llm.use_graphs),
+                   "mode": a.mode, "hipgraph": stats1["use_graphs"], "engine_procs_per_gpu": procs,
                    "waves": "serial" if (a.serial_waves or a.mode != "pipeline") else "pipelined"},
         "detail": {"init_s": round(init_s, 1), "prefill_tokens_per_gpu": ptoks, "decode_tokens_per_gpu": dtoks,
-                   "prefill_graph_replays": llm.stats.prefill_graph_replays - stats0[2],
-                   "prefill_graph_buckets": sorted(getattr(llm, "_prefill_g", {})),
+                   "prefill_graph_replays": stats1["prefill_graph_replays"] - stats0["prefill_graph_replays"],
+                   "prefill_graph_buckets": stats1["prefill_graph_buckets"],
                    "decode_tok_s_per_gpu": round(dtoks / elapsed, 1), "outcomes": counter["outcomes"],
-                   "dfa_states": getattr(meng, "dfa_states", None), "timed_monotonic_ns": [mono0, mono1]},
+                   "dfa_states": stats1["dfa_states"], "timed_monotonic_ns": [mono0, mono1]},
     }
     if share:
         out["detail"]["shared_gpu_rehearsal"] = True
@@ -320,7 +375,10 @@ def main() -> int:
                 json.dump(out, f, indent=1)
     if a.mode == "pipeline":
         op.stop()
-    ee.close()
+    if ee is not None:
+        ee.close()
+    if pool is not None:
+        pool.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -114,6 +114,7 @@ class EngineCfg(BaseModel):
     page_size: int = 64
     use_graphs: bool = True
     prefill_graphs: bool = True       # full-ish prefill batches replay a captured bucket graph
+    warmup_graphs: bool = True        # engine processes capture their graphs before reporting ready
     multi_step: int = 8
     ignore_eos: bool = False
 

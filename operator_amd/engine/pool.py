@@ -108,6 +108,9 @@ def _worker_main(idx: int, device: str, settings_obj: dict, patterns, roles: tup
                                                 s.services.match_max_batch, s.services.match_batch_wait_ms)
         if "explain" in roles:
             explainer = factory.build_explain_service(s, tp=tp)
+            llm = getattr(getattr(explainer, "ee", None), "llm", None)
+            if llm is not None and tp is None and s.engine.warmup_graphs:
+                llm.warmup()   # capture the decode / prefill graphs before reporting ready
     except Exception as e:  # noqa: BLE001 - reported to the controller, which marks the worker dead
         outq.put(("fatal", idx, f"{type(e).__name__}: {e}"))
         return
@@ -156,6 +159,9 @@ def _worker_main(idx: int, device: str, settings_obj: dict, patterns, roles: tup
             if matcher is not None:
                 matcher.swap_engine(factory.build_match_engine(s, msg[1], device=device))
             continue
+        if kind == "stats":          # engine counters for the controller (bench, metrics)
+            outq.put(("ok", idx, msg[1], _worker_stats(matcher, explainer)))
+            continue
         if kind in ("match", "explain"):
             pool.submit(run, msg[1], kind, msg[2])
     stop.set()
@@ -165,6 +171,21 @@ def _worker_main(idx: int, device: str, settings_obj: dict, patterns, roles: tup
     ee = getattr(explainer, "ee", None)
     if ee is not None:   # stops the engine loop (a TP leader releases its followers)
         ee.close(join_s=30.0)
+
+
+def _worker_stats(matcher, explainer) -> dict:
+    from dataclasses import asdict
+
+    out: dict = {}
+    llm = getattr(getattr(explainer, "ee", None), "llm", None)
+    if llm is not None:
+        out["llm"] = asdict(llm.stats)
+        out["prefill_graph_buckets"] = sorted(getattr(llm, "_prefill_g", {}))
+        out["use_graphs"] = bool(getattr(llm, "use_graphs", False))
+    eng = getattr(matcher, "engine", None)
+    if eng is not None:
+        out["dfa_states"] = getattr(eng, "dfa_states", None)
+    return out
 
 
 # ---------------------------------------------------------------- controller side
@@ -296,6 +317,20 @@ class EnginePool:
         self._dispatch("explain", (result.to_obj(), cfg.model_dump(by_alias=True, exclude_none=True)), fut)
         return fut
 
+    def worker_stats(self, timeout: float = 30.0) -> list[dict]:
+        """Engine counters of every live worker (LLM EngineStats, prefill graph buckets,
+        DFA size), one dict per worker."""
+        futs = []
+        with self._lock:
+            for w in self.workers:
+                if w.alive and w.ready:
+                    fut: Future = Future()
+                    rid = next(self._ids)
+                    w.inflight[rid] = ("stats", None, fut)
+                    w.inq.put(("stats", rid))
+                    futs.append(fut)
+        return [f.result(timeout) for f in futs]
+
     def set_patterns(self, patterns) -> None:
         self.patterns = patterns
         with self._lock:
@@ -335,7 +370,9 @@ class EnginePool:
                 elif kind in ("ok", "err"):
                     item = w.inflight.pop(msg[2], None)
                     if item is not None and not item[2].done():
-                        if kind == "ok":
+                        if kind == "ok" and item[0] == "stats":
+                            item[2].set_result(msg[3])
+                        elif kind == "ok":
                             cls = AnalysisResult if item[0] == "match" else AIResponse
                             item[2].set_result(cls.model_validate(msg[3]))
                         else:

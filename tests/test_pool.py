@@ -68,6 +68,18 @@ def test_pool_explain_and_routing(pool):
     assert all(f.result(120).summary.highest_severity == res.summary.highest_severity for f in futs)
 
 
+def test_pool_worker_stats(pool):
+    es = PoolExplainService(pool)
+    before = pool.worker_stats()
+    assert len(before) == 2 and all("llm" in w for w in before)
+    res = PoolMatchService(pool).analyze(_data("stats"))
+    es.explain_many([(res, AIProviderConfig(max_tokens=4, temperature=0.0, caching_enabled=False))] * 3)
+    after = pool.worker_stats()
+    gen = sum(w["llm"]["decode_tokens"] for w in after) - sum(w["llm"]["decode_tokens"] for w in before)
+    assert gen >= 3 * 3                       # 4 tokens each: 1 from the prefill + 3 decode steps
+    assert all(len(w.inflight) == 0 for w in pool.workers)   # stats requests do not linger
+
+
 def test_pool_pattern_broadcast(pool):
     ms = PoolMatchService(pool)
     custom = PatternSet.from_yaml_text("""
