@@ -106,7 +106,7 @@ class EngineCfg(BaseModel):
     tp: int = 1
     oneshot_allreduce_mb: float = 8.0  # TP all-reduces up to this size use the one-shot IPC kernel; 0 = RCCL only
     max_batch: int = 256
-    max_prefill_tokens: int = 16384
+    max_prefill_tokens: int = 32768   # tokens per prefill batch (profiles/prefill_batch_sweep_8b.jsonl)
     admit_wait_ms: float = 20.0       # idle engine: gather arrivals this long before a partial prefill
     max_context: int = 4096
     max_prompt_tokens: int = 1536
