@@ -509,6 +509,12 @@ class LLMEngine:
         st = g.st
         if self._active is not st:
             assert ahead == 0, "device state must be current before it is reloaded"
+            # rows longest context first: decode attention dispatches its workgroups in
+            # row order, so the long rows start first and short ones fill the tail
+            # (-3 % attention time at +-45 % context spread, tools/bench_attn.py --sort desc).
+            # Deterministic (rid tie-break), so TP followers build the same order.
+            self.running.sort(key=lambda r: (-r.length, r.rid))
+            reqs = list(self.running)
             st.load(reqs, self.max_pages)
             self._active = st
         st.step.zero_()
