@@ -67,7 +67,14 @@ def parse_args():
 
 def main() -> int:
     a = parse_args()
+    # host thread pools sized to this rank's share of the node (N ranks on one host):
+    # the tokenizer's Rust pool and torch's intra-op pool default to every CPU each
+    share_cpus = max(2, min(16, (os.cpu_count() or 16) // max(1, int(os.environ.get("LOCAL_WORLD_SIZE",
+                                                                                    os.environ.get("WORLD_SIZE", "1"))))))
+    os.environ.setdefault("RAYON_RS_NUM_CPUS", str(share_cpus))
     import torch
+
+    torch.set_num_threads(min(torch.get_num_threads(), share_cpus))
     import torch.distributed as dist
 
     from operator_amd.parallel.comm import init_from_env
