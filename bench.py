@@ -58,6 +58,8 @@ def parse_args():
     ap.add_argument("--serial-waves", action="store_true",
                     help="wait for every sink write of a wave before writing the next one")
     ap.add_argument("--kv-gb", type=float, default=None, help="KV-cache budget (default 96 GB on GPU, 1 GB on CPU)")
+    ap.add_argument("--kv-dtype", choices=["auto", "fp8"], default="auto",
+                    help="fp8: e4m3fn KV cache (reduced precision: not the headline configuration)")
     ap.add_argument("--engine-procs", type=int, default=1,
                     help="engine processes per GPU (EnginePool workers holding the scan + LLM engines, "
                          "--max-batch split over them); 1 = engines inside this process")
@@ -96,7 +98,8 @@ def main() -> int:
             "engine.model": a.model, "engine.device": dev, "engine.max_batch": max_batch,
             "engine.max_prefill_tokens": a.prefill_tokens,
             "engine.max_context": a.prompt_tokens + a.max_tokens + 64, "engine.max_prompt_tokens": a.prompt_tokens,
-            "engine.kv_cache_gb": kv, "engine.use_graphs": not a.no_graphs, "engine.ignore_eos": True,
+            "engine.kv_cache_gb": kv, "engine.kv_dtype": a.kv_dtype, "engine.use_graphs": not a.no_graphs,
+            "engine.ignore_eos": True,
             "engine.seed": 0, "health.enabled": False, "operator.workers": 2 * a.batch + 16, "operator.io_workers": 16,
             "patterns.cache_dir": f"/tmp/oamd-bench-{os.getpid()}", "services.match_max_batch": 64,
             "services.match_batch_wait_ms": 5.0})
@@ -367,6 +370,7 @@ def main() -> int:
                    "parallelism": f"dp{world}", "tp": 1, "max_tokens": a.max_tokens,
                    "prompt_tokens_cap": a.prompt_tokens, "log_kib": a.log_kb, "patterns": a.patterns,
                    "mode": a.mode, "hipgraph": stats1["use_graphs"], "engine_procs_per_gpu": procs,
+                   "kv_cache_dtype": "fp8_e4m3fn" if a.kv_dtype == "fp8" else "bf16",
                    "waves": "serial" if (a.serial_waves or a.mode != "pipeline") else "pipelined"},
         "detail": {"init_s": round(init_s, 1), "prefill_tokens_per_gpu": ptoks, "decode_tokens_per_gpu": dtoks,
                    "prefill_graph_replays": stats1["prefill_graph_replays"] - stats0["prefill_graph_replays"],

@@ -80,11 +80,16 @@ void embedding(const at::Tensor& ids, const at::Tensor& table, at::Tensor& out) 
                      (int)table.size(1), table.size(0), cur_stream()));
 }
 
+static bool kv_is_fp8(const at::Tensor& t) {
+  return t.scalar_type() == at::kFloat8_e4m3fn || t.scalar_type() == at::kByte;
+}
+
 void rope_kv(const at::Tensor& qkv, const at::Tensor& pos, const at::Tensor& cos_t, const at::Tensor& sin_t,
              int64_t Hq, int64_t Hkv, at::Tensor& q_out, const c10::optional<at::Tensor>& k_out,
              const c10::optional<at::Tensor>& v_out, const c10::optional<at::Tensor>& k_cache,
              const c10::optional<at::Tensor>& v_cache, const c10::optional<at::Tensor>& slots,
-             const c10::optional<at::Tensor>& partial, int64_t splits, const c10::optional<at::Tensor>& bias) {
+             const c10::optional<at::Tensor>& partial, int64_t splits, const c10::optional<at::Tensor>& bias,
+             double k_scale, double v_scale) {
   CHECK_DT(pos, at::kLong); CHECK_CONTIG(pos); CHECK_DEV(pos);
   CHECK_DT(cos_t, at::kFloat); CHECK_DT(sin_t, at::kFloat); CHECK_CONTIG(cos_t); CHECK_CONTIG(sin_t);
   const int64_t T = pos.numel();
@@ -111,7 +116,11 @@ void rope_kv(const at::Tensor& qkv, const at::Tensor& pos, const at::Tensor& cos
   int page = 1;
   if (k_cache.has_value()) {
     TORCH_CHECK(v_cache.has_value() && slots.has_value(), "k_cache needs v_cache and slots");
-    CHECK_BF16(*k_cache); CHECK_BF16(*v_cache); CHECK_CONTIG(*k_cache); CHECK_CONTIG(*v_cache);
+    TORCH_CHECK(kv_is_fp8(*k_cache) ? kv_is_fp8(*v_cache)
+                                    : (k_cache->scalar_type() == at::kBFloat16 &&
+                                       v_cache->scalar_type() == at::kBFloat16),
+                "KV cache must be bf16 or float8_e4m3fn (both K and V)");
+    CHECK_DEV(*k_cache); CHECK_CONTIG(*k_cache); CHECK_CONTIG(*v_cache);
     CHECK_DT(*slots, at::kLong); CHECK_CONTIG(*slots);
     TORCH_CHECK(k_cache->dim() == 4 && k_cache->size(1) == Hkv && k_cache->size(3) == D &&
                     k_cache->sizes() == v_cache->sizes(), "cache must be [pages, Hkv, page, D]");
@@ -123,10 +132,13 @@ void rope_kv(const at::Tensor& qkv, const at::Tensor& pos, const at::Tensor& cos
     TORCH_CHECK(bias->numel() == (Hq + 2 * Hkv) * D, "rope_kv: bias must be [(Hq + 2 Hkv) * D]");
   }
   const c10::hip::HIPGuardMasqueradingAsCUDA g(pos.device());
+  const bool fp8 = k_cache.has_value() && kv_is_fp8(*k_cache);
+  TORCH_CHECK(k_scale > 0 && v_scale > 0, "KV scales must be positive");
   RC(oamd::rope_kv(qp, qstride, ptr<int64_t>(pos), ptr<float>(cos_t), ptr<float>(sin_t),
                    (int)T, (int)Hq, (int)Hkv, (int)D, ptr<bf16_t>(q_out), optr<bf16_t>(k_out), optr<bf16_t>(v_out),
-                   optr<bf16_t>(k_cache), optr<bf16_t>(v_cache), optr<int64_t>(slots), page, cos_t.size(0),
-                   xp, (int)splits, optr<bf16_t>(bias), cur_stream()));
+                   k_cache.has_value() ? k_cache->data_ptr() : nullptr,
+                   v_cache.has_value() ? v_cache->data_ptr() : nullptr, optr<int64_t>(slots), page, cos_t.size(0),
+                   xp, (int)splits, optr<bf16_t>(bias), fp8, (float)k_scale, (float)v_scale, cur_stream()));
 }
 
 void gemm_decode(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& y_opt,
@@ -263,9 +275,14 @@ void score_events(const at::Tensor& keys, const at::Tensor& hit_doc, const at::T
 
 void attn_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                  const at::Tensor& block_tables, const at::Tensor& seq_lens, at::Tensor& out,
-                 at::Tensor& o_part, at::Tensor& ml_part, int64_t num_splits, double scale, int64_t variant) {
+                 at::Tensor& o_part, at::Tensor& ml_part, int64_t num_splits, double scale, int64_t variant,
+                 double k_scale, double v_scale) {
   CHECK_DEV(q); CHECK_BF16(q); CHECK_CONTIG(q); CHECK_BF16(out); CHECK_CONTIG(out);
-  CHECK_BF16(k_cache); CHECK_BF16(v_cache); CHECK_CONTIG(k_cache); CHECK_CONTIG(v_cache);
+  const bool fp8 = kv_is_fp8(k_cache);
+  TORCH_CHECK(fp8 ? kv_is_fp8(v_cache) : (k_cache.scalar_type() == at::kBFloat16 &&
+                                          v_cache.scalar_type() == at::kBFloat16),
+              "KV cache must be bf16 or float8_e4m3fn (both K and V)");
+  CHECK_DEV(k_cache); CHECK_DEV(v_cache); CHECK_CONTIG(k_cache); CHECK_CONTIG(v_cache);
   CHECK_DT(block_tables, at::kInt); CHECK_CONTIG(block_tables); CHECK_DT(seq_lens, at::kInt); CHECK_CONTIG(seq_lens);
   CHECK_DT(o_part, at::kFloat); CHECK_DT(ml_part, at::kFloat); CHECK_CONTIG(o_part); CHECK_CONTIG(ml_part);
   TORCH_CHECK(q.dim() == 3, "q must be [B, Hq, D]");
@@ -281,11 +298,12 @@ void attn_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tenso
                   (o_part.numel() >= B * Hq * num_splits * D && ml_part.numel() >= B * Hq * num_splits * 2),
               "partial buffers too small");
   TORCH_CHECK(B * num_splits < (1LL << 31), "grid too large");
+  TORCH_CHECK(k_scale > 0 && v_scale > 0, "KV scales must be positive");
   const c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
-  RC(oamd::attn_decode(ptr<bf16_t>(q), ptr<bf16_t>(k_cache), ptr<bf16_t>(v_cache), ptr<int>(block_tables),
-                       ptr<int>(seq_lens), ptr<bf16_t>(out), ptr<float>(o_part), ptr<float>(ml_part), (int)B,
-                       (int)Hq, (int)Hkv, (int)D, (int)page, (int)block_tables.size(1), (int)num_splits,
-                       (float)scale, (int)variant, cur_stream()));
+  RC(oamd::attn_decode(ptr<bf16_t>(q), k_cache.data_ptr(), v_cache.data_ptr(), fp8, (float)k_scale, (float)v_scale,
+                       ptr<int>(block_tables), ptr<int>(seq_lens), ptr<bf16_t>(out), ptr<float>(o_part),
+                       ptr<float>(ml_part), (int)B, (int)Hq, (int)Hkv, (int)D, (int)page, (int)block_tables.size(1),
+                       (int)num_splits, (float)scale, (int)variant, cur_stream()));
 }
 
 void attn_prefill(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor& o,
@@ -354,8 +372,11 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("sin"), pybind11::arg("Hq"), pybind11::arg("Hkv"), pybind11::arg("q_out"),
         pybind11::arg("k_out"), pybind11::arg("v_out"), pybind11::arg("k_cache"), pybind11::arg("v_cache"),
         pybind11::arg("slots"), pybind11::arg("partial") = pybind11::none(), pybind11::arg("splits") = 1,
-        pybind11::arg("bias") = pybind11::none());
-  m.def("attn_decode", &attn_decode);
+        pybind11::arg("bias") = pybind11::none(), pybind11::arg("k_scale") = 1.0, pybind11::arg("v_scale") = 1.0);
+  m.def("attn_decode", &attn_decode, pybind11::arg("q"), pybind11::arg("k_cache"), pybind11::arg("v_cache"),
+        pybind11::arg("block_tables"), pybind11::arg("seq_lens"), pybind11::arg("out"), pybind11::arg("o_part"),
+        pybind11::arg("ml_part"), pybind11::arg("num_splits"), pybind11::arg("scale"), pybind11::arg("variant") = 0,
+        pybind11::arg("k_scale") = 1.0, pybind11::arg("v_scale") = 1.0);
   m.def("quantize_fp8", &quantize_fp8);
   m.def("score_events", &score_events);
   m.def("gemm_fp8", &gemm_fp8, pybind11::arg("x8"), pybind11::arg("w8"), pybind11::arg("sx"), pybind11::arg("sw"),

@@ -27,6 +27,11 @@
 // stored in 16-token tiles laid out [ks 4][lg 4][token 16][8 dims] (d = 32*lg +
 // 8*ks + j), so each K fragment load (fixed ks) is ONE contiguous 1 KB wave
 // access instead of 16 token rows x 64 B (written that way by rope_kv).
+// FP8 cache (OCP e4m3fn, per-tensor scales): the same layout with 1-byte elements,
+// so every load moves half the bytes. K fragments are widened to bf16 in registers
+// (exact) for the bf16 MFMA against the bf16 query; V
+// to fp32 (v_cvt_pk_f32_fp8) for the VALU P.V. k_scale rides in the softmax scale,
+// v_scale multiplies the output.
 #include "common.h"
 #include "kernels.h"
 
@@ -40,6 +45,61 @@ __device__ __forceinline__ u16x8 ld16(const bf16_t* p) {
   return __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(p));
 }
 
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+
+// Per-element-type access to the cache: a fragment is 8 consecutive elements
+// (16 B of bf16, 8 B of fp8).
+template <typename KV>
+struct KVT;
+template <>
+struct KVT<bf16_t> {
+  using frag = u16x8;
+  static __device__ __forceinline__ frag load(const bf16_t* p) { return ld16(p); }
+  static __device__ __forceinline__ u16x8 to_bf16(const frag& f) { return f; }
+  static __device__ __forceinline__ void to_f32(const frag& f, float (&o)[8]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = bf2f(f[j]);
+  }
+};
+template <>
+struct KVT<uint8_t> {
+  using frag = u32x2;
+  static __device__ __forceinline__ frag load(const uint8_t* p) {
+    return __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(p));
+  }
+  // fp8 -> fp32 (v_cvt_pk_f32_fp8) then the upper halves of two floats into one dword
+  // (v_perm_b32): exact, as every e4m3 value is a bf16 value. (The one-instruction
+  // v_cvt_scalef32_pk_bf16_fp8 form was mis-packed by hipcc: it duplicated the low
+  // half into both halves of the register.)
+  static __device__ __forceinline__ u16x8 to_bf16(const frag& f) {
+    u32x4 d;
+    const unsigned w[2] = {f[0], f[1]};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const f32x2_t lo = __builtin_amdgcn_cvt_pk_f32_fp8(w[h], false);
+      const f32x2_t hi = __builtin_amdgcn_cvt_pk_f32_fp8(w[h], true);
+      d[2 * h] = __builtin_amdgcn_perm(__float_as_uint(lo[1]), __float_as_uint(lo[0]), 0x07060302u);
+      d[2 * h + 1] = __builtin_amdgcn_perm(__float_as_uint(hi[1]), __float_as_uint(hi[0]), 0x07060302u);
+    }
+    return __builtin_bit_cast(u16x8, d);
+  }
+  static __device__ __forceinline__ void to_f32(const frag& f, float (&o)[8]) {
+    const unsigned w[2] = {f[0], f[1]};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const f32x2_t lo = __builtin_amdgcn_cvt_pk_f32_fp8(w[h], false);
+      const f32x2_t hi = __builtin_amdgcn_cvt_pk_f32_fp8(w[h], true);
+      o[4 * h + 0] = lo[0];
+      o[4 * h + 1] = lo[1];
+      o[4 * h + 2] = hi[0];
+      o[4 * h + 3] = hi[1];
+    }
+  }
+};
+
 // Token range of split s of a sequence of `len` tokens cut into at most
 // `num_splits` pieces of a multiple of `chunk` tokens. Shared with the combine
 // kernel so both agree on how many splits a sequence really has.
@@ -48,18 +108,20 @@ __device__ __forceinline__ int split_len(int len, int num_splits, int chunk) {
   return (per + chunk - 1) / chunk * chunk;
 }
 
-template <int NT>
+template <typename KV, int NT>
 struct KVRegs {
-  u16x8 k[NT][4];   // K tile i: token 16i + l15, dims 32*lg + 8*ks
-  u16x8 v[4 * NT];  // token 4*it + lg, dims 8*l15
+  typename KVT<KV>::frag k[NT][4];   // K tile i: token 16i + l15, dims 32*lg + 8*ks
+  typename KVT<KV>::frag v[4 * NT];  // token 4*it + lg, dims 8*l15
 };
 
-template <int G, int NT>
-__global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2) attn_decode_kernel(
-    const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
-    const int* __restrict__ block_tables, const int* __restrict__ seq_lens, bf16_t* __restrict__ out,
-    float* __restrict__ o_part, float* __restrict__ ml_part, int Hkv, int page_size, int log2_page,
-    int max_pages, int num_splits, float scale_log2) {
+template <int G, int NT, typename KV = bf16_t>
+__global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2)
+    attn_decode_kernel(const bf16_t* __restrict__ q, const KV* __restrict__ kc, const KV* __restrict__ vc,
+                       const int* __restrict__ block_tables, const int* __restrict__ seq_lens,
+                       bf16_t* __restrict__ out, float* __restrict__ o_part, float* __restrict__ ml_part, int Hkv,
+                       int page_size, int log2_page, int max_pages, int num_splits, float scale_log2,
+                       float v_scale) {
+  using T = KVT<KV>;
   constexpr int D = 128;
   constexpr int TW = 16 * NT;  // tokens per wave per chunk
   constexpr int CH = 4 * TW;   // tokens per workgroup per chunk
@@ -113,19 +175,19 @@ __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2) attn_decode_
     return page * page_stride + head_off + (int64_t)(tok & (page_size - 1)) * D;
   };
   // Branch-free chunk load: rows past `end` are clamped duplicates (masked later).
-  auto load = [&](KVRegs<NT>& r, int c) {
+  auto load = [&](KVRegs<KV, NT>& r, int c) {
     const int base = start + c * CH + w * TW;
 #pragma unroll
     for (int i = 0; i < NT; ++i) {
       const int tok = min(base + 16 * i + l15, end - 1);
       const int t16 = tok & 15;
       // tile of `tok`: its 16-token-aligned row, then (lg*16 + t16)*8 inside each ks block
-      const bf16_t* p = kc + row_off(tok) - (int64_t)t16 * D + (lg * 16 + t16) * 8;
+      const KV* p = kc + row_off(tok) - (int64_t)t16 * D + (lg * 16 + t16) * 8;
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) r.k[i][ks] = ld16(p + ks * 512);
+      for (int ks = 0; ks < 4; ++ks) r.k[i][ks] = T::load(p + ks * 512);
     }
 #pragma unroll
-    for (int it = 0; it < 4 * NT; ++it) r.v[it] = ld16(vc + row_off(min(base + 4 * it + lg, end - 1)) + 8 * l15);
+    for (int it = 0; it < 4 * NT; ++it) r.v[it] = T::load(vc + row_off(min(base + 4 * it + lg, end - 1)) + 8 * l15);
   };
 
   float m_run = -1e30f, l_run = 0.f;  // per lane: head l15 (finite start: no inf - inf)
@@ -136,7 +198,7 @@ __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2) attn_decode_
     for (int j = 0; j < 8; ++j) acc[h][j] = 0.f;
   float* pwv = pw[w];
 
-  auto consume = [&](const KVRegs<NT>& r, int c) {
+  auto consume = [&](const KVRegs<KV, NT>& r, int c) {
     const int base = start + c * CH + w * TW;
     float sc[NT][4];
     float cmax = -INFINITY;
@@ -145,7 +207,7 @@ __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2) attn_decode_
       f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks)
-        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, r.k[i][ks]),
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, T::to_bf16(r.k[i][ks])),
                                                   __builtin_bit_cast(bf16x8_t, qb[ks]), a, 0, 0, 0);
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
@@ -196,8 +258,7 @@ __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2) attn_decode_
         for (int h = 0; h < G; ++h) p[h] = pwv[t * GP + h];
       }
       float vv[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) vv[j] = bf2f(r.v[it][j]);
+      T::to_f32(r.v[it], vv);
 #pragma unroll
       for (int h = 0; h < G; ++h)
 #pragma unroll
@@ -211,7 +272,7 @@ __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2) attn_decode_
   // Double-buffered stream over the chunks: the next chunk's loads are always in
   // flight while the current one is consumed. Loads past the last chunk re-read
   // the last chunk (branch-free, L2 hits) so hipcc's wait counts stay exact.
-  KVRegs<NT> ra, rb;
+  KVRegs<KV, NT> ra, rb;
   load(ra, 0);
   for (int c = 0; c < nch; c += 2) {
     load(rb, min(c + 1, nch - 1));
@@ -255,6 +316,7 @@ __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2) attn_decode_
       o += f * red[ww][h][d];
       L += f * mls[ww][h][1];
     }
+    o *= v_scale;
     const int hq = kvh * G + h;
     if (ns_b == 1) {  // whole context in this workgroup: final output, no combine
       out[((int64_t)b * Hq + hq) * D + d] = f2bf(L > 0.f ? o / L : 0.f);
@@ -292,9 +354,9 @@ __global__ void attn_decode_combine_kernel(const float* __restrict__ o_part, con
   out[(int64_t)bh * D + d] = f2bf(L > 0.f ? o / L : 0.f);
 }
 
-int attn_decode(const bf16_t* q, const bf16_t* k_cache, const bf16_t* v_cache, const int* block_tables,
-                const int* seq_lens, bf16_t* out, float* o_part, float* ml_part, int B, int Hq, int Hkv,
-                int head_dim, int page_size, int max_pages, int num_splits, float scale, int variant,
+int attn_decode(const bf16_t* q, const void* k_cache, const void* v_cache, bool fp8, float k_scale, float v_scale,
+                const int* block_tables, const int* seq_lens, bf16_t* out, float* o_part, float* ml_part, int B,
+                int Hq, int Hkv, int head_dim, int page_size, int max_pages, int num_splits, float scale, int variant,
                 hipStream_t stream) {
   if (B == 0) return 0;
   if (head_dim != 128) return -1;
@@ -304,31 +366,45 @@ int attn_decode(const bf16_t* q, const bf16_t* k_cache, const bf16_t* v_cache, c
   int log2p = 0;
   while ((1 << log2p) < page_size) ++log2p;
   const int G = Hq / Hkv;
-  const float scale_log2 = scale * 1.4426950408889634f;
+  const float scale_log2 = scale * k_scale * 1.4426950408889634f;
   // variant: 0 = default (NT = 1: 16 tokens per wave per chunk, 164 VGPRs at
-  // G = 4 -> 3 workgroups/CU); 2 = NT = 2 (32 tokens per wave, 238 VGPRs,
-  // measured 4-10 % slower at B = 256; G = 8 spills, so it stays NT = 1).
+  // G = 4 -> 3 workgroups/CU); 2 = NT = 2 (32 tokens per wave, 2 workgroups/CU;
+  // bf16: 238 VGPRs, measured 4-10 % slower at B = 256). G > 4 stays NT = 1.
   int chunk = 0;
   dim3 grid(B * num_splits, Hkv, 1);
-#define OAMD_DEC(GG, NTT)                                                                               \
-  do {                                                                                                  \
-    attn_decode_kernel<GG, NTT><<<grid, 256, 0, stream>>>(q, k_cache, v_cache, block_tables, seq_lens, \
-                                                          out, o_part, ml_part, Hkv, page_size, log2p,  \
-                                                          max_pages, num_splits, scale_log2);           \
-    chunk = 64 * NTT;                                                                                   \
+#define OAMD_DEC(GG, NTT, KVT_)                                                                           \
+  do {                                                                                                    \
+    attn_decode_kernel<GG, NTT, KVT_><<<grid, 256, 0, stream>>>(                                         \
+        q, static_cast<const KVT_*>(k_cache), static_cast<const KVT_*>(v_cache), block_tables, seq_lens, \
+        out, o_part, ml_part, Hkv, page_size, log2p, max_pages, num_splits, scale_log2, v_scale);        \
+    chunk = 64 * NTT;                                                                                     \
   } while (0)
   const bool nt2 = variant == 2;
-  switch (G) {
-    case 1: if (nt2) OAMD_DEC(1, 2); else OAMD_DEC(1, 1); break;
-    case 2: if (nt2) OAMD_DEC(2, 2); else OAMD_DEC(2, 1); break;
-    case 4: if (nt2) OAMD_DEC(4, 2); else OAMD_DEC(4, 1); break;
-    // groups of Llama-3.2-3B (24/8), Qwen2.5-32B (40/8), Qwen2.5-7B (28/4)
-    case 3: OAMD_DEC(3, 1); break;
-    case 5: OAMD_DEC(5, 1); break;
-    case 6: OAMD_DEC(6, 1); break;
-    case 7: OAMD_DEC(7, 1); break;
-    case 8: OAMD_DEC(8, 1); break;
-    default: return -3;
+  if (fp8) {
+    switch (G) {
+      case 1: if (nt2) OAMD_DEC(1, 2, uint8_t); else OAMD_DEC(1, 1, uint8_t); break;
+      case 2: if (nt2) OAMD_DEC(2, 2, uint8_t); else OAMD_DEC(2, 1, uint8_t); break;
+      case 4: if (nt2) OAMD_DEC(4, 2, uint8_t); else OAMD_DEC(4, 1, uint8_t); break;
+      case 3: OAMD_DEC(3, 1, uint8_t); break;
+      case 5: OAMD_DEC(5, 1, uint8_t); break;
+      case 6: OAMD_DEC(6, 1, uint8_t); break;
+      case 7: OAMD_DEC(7, 1, uint8_t); break;
+      case 8: OAMD_DEC(8, 1, uint8_t); break;
+      default: return -3;
+    }
+  } else {
+    switch (G) {
+      case 1: if (nt2) OAMD_DEC(1, 2, bf16_t); else OAMD_DEC(1, 1, bf16_t); break;
+      case 2: if (nt2) OAMD_DEC(2, 2, bf16_t); else OAMD_DEC(2, 1, bf16_t); break;
+      case 4: if (nt2) OAMD_DEC(4, 2, bf16_t); else OAMD_DEC(4, 1, bf16_t); break;
+      // groups of Llama-3.2-3B (24/8), Qwen2.5-32B (40/8), Qwen2.5-7B (28/4)
+      case 3: OAMD_DEC(3, 1, bf16_t); break;
+      case 5: OAMD_DEC(5, 1, bf16_t); break;
+      case 6: OAMD_DEC(6, 1, bf16_t); break;
+      case 7: OAMD_DEC(7, 1, bf16_t); break;
+      case 8: OAMD_DEC(8, 1, bf16_t); break;
+      default: return -3;
+    }
   }
 #undef OAMD_DEC
   OAMD_LAUNCH_CHECK();

@@ -19,9 +19,9 @@ int embedding(const int64_t* ids, const bf16_t* table, bf16_t* out, int tokens, 
               int64_t vocab, hipStream_t stream);
 int rope_kv(const bf16_t* qkv, int64_t qkv_stride, const int64_t* pos, const float* cos_t,
             const float* sin_t, int tokens, int Hq, int Hkv, int head_dim, bf16_t* q_out,
-            bf16_t* k_out, bf16_t* v_out, bf16_t* k_cache, bf16_t* v_cache, const int64_t* slots,
+            bf16_t* k_out, bf16_t* v_out, void* k_cache, void* v_cache, const int64_t* slots,
             int page_size, int64_t max_pos, const float* xp, int S, const bf16_t* bias,
-            hipStream_t stream);
+            bool fp8_cache, float k_scale, float v_scale, hipStream_t stream);  // cache: bf16 or e4m3fn
 // Y[M,N] = X[M,K] W[N,K]^T for decode buckets (M a multiple of the BM-row tile, BM in {64,128,256}); S-way split-K
 // (S | 8) with fp32 slabs P[S][M][N] reduced into Y; BN in {64, 128} columns per tile.
 int gemm_decode(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, int N, int K, int S, int BN,
@@ -48,9 +48,10 @@ int score_events(const int64_t* keys, const int* hit_doc, const int* doc_ptr, in
                  const double* conf, const int* severity, int num_matchers, double significance, double* ev_score,
                  int* ev_pat, int* ev_line, int* order, int* summary, hipStream_t stream);
 
-int attn_decode(const bf16_t* q, const bf16_t* k_cache, const bf16_t* v_cache, const int* block_tables,
-                const int* seq_lens, bf16_t* out, float* o_part, float* ml_part, int B, int Hq, int Hkv,
-                int head_dim, int page_size, int max_pages, int num_splits, float scale, int variant,
+// k_cache / v_cache: bf16, or (fp8) OCP e4m3fn bytes holding x / k_scale, x / v_scale
+int attn_decode(const bf16_t* q, const void* k_cache, const void* v_cache, bool fp8, float k_scale, float v_scale,
+                const int* block_tables, const int* seq_lens, bf16_t* out, float* o_part, float* ml_part, int B,
+                int Hq, int Hkv, int head_dim, int page_size, int max_pages, int num_splits, float scale, int variant,
                 hipStream_t stream);
 // Causal prefill attention; the work list holds one item per attn_prefill_block_q(Hq, Hkv, variant)
 // query rows of a sequence. variant 1 = per-query-head kernel (64 rows), 2 = GQA-grouped 16-row

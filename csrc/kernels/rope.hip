@@ -9,6 +9,8 @@
 //   k_out/v_out [T, Hkv, D]      rotated k / copied v (optional, prefill path)
 //   k_cache/v_cache [pages, Hkv, P, D] at slot_mapping[t] (optional; slot<0 skips);
 //   K is stored in 16-token MFMA tiles (see attn_decode.hip), V row-major
+// With an fp8 cache (OCP e4m3fn) K and V are stored as e4m3(bf16(x) / scale),
+// saturated to +-448, 8 bytes per 8-element group (same layouts as bf16).
 // An optional bf16 bias [(Hq + 2Hkv) D] (Qwen2's q/k/v projection bias) is added
 // in fp32 before the one bf16 rounding of the split-K slab sum (HF numerics:
 // bf16(x W^T + b)); on a bf16 qkv row it is added after that row's rounding.
@@ -24,14 +26,37 @@ namespace oamd {
 // one 256-thread workgroup per token: 7.8 us + a separate 5.5 us reduce kernel).
 constexpr int kRopeItems = 64;
 
-template <int D>
+// 8 bf16 values -> the cache element type (bf16: as is; fp8: e4m3(x * inv_scale))
+template <typename KV>
+struct CacheStore;
+template <>
+struct CacheStore<bf16_t> {
+  static __device__ __forceinline__ void put(bf16_t* dst, const u16x8& v, float) {
+    *reinterpret_cast<u16x8*>(dst) = v;
+  }
+};
+template <>
+struct CacheStore<uint8_t> {
+  static __device__ __forceinline__ void put(uint8_t* dst, const u16x8& v, float inv) {
+    auto f = [&](int j) { return fminf(fmaxf(bf2f(v[j]) * inv, -448.f), 448.f); };
+    int lo = 0, hi = 0;
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(f(0), f(1), lo, false);
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(f(2), f(3), lo, true);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(f(4), f(5), hi, false);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(f(6), f(7), hi, true);
+    *reinterpret_cast<uint2*>(dst) = uint2{(unsigned)lo, (unsigned)hi};
+  }
+};
+
+template <int D, typename KV>
 __global__ void __launch_bounds__(kRopeItems) rope_kv_kernel(
     const bf16_t* __restrict__ qkv, int64_t qkv_stride, const int64_t* __restrict__ pos,
     const float* __restrict__ cos_t, const float* __restrict__ sin_t, int Hq, int Hkv,
     bf16_t* __restrict__ q_out, bf16_t* __restrict__ k_out, bf16_t* __restrict__ v_out,
-    bf16_t* __restrict__ k_cache, bf16_t* __restrict__ v_cache,
+    KV* __restrict__ k_cache, KV* __restrict__ v_cache,
     const int64_t* __restrict__ slots, int page_size, int64_t max_pos,
-    const float* __restrict__ xp, int S, int64_t slab, const bf16_t* __restrict__ bias) {
+    const float* __restrict__ xp, int S, int64_t slab, const bf16_t* __restrict__ bias, float k_inv,
+    float v_inv) {
   constexpr int HALF = D / 2;
   constexpr int GPH = HALF / 8;  // 8-element groups per half-head
   const int t = blockIdx.x;
@@ -124,10 +149,10 @@ __global__ void __launch_bounds__(kRopeItems) rope_kv_kernel(
         if (cache_base_k >= 0) {
           // tiled K layout (attn_decode.hip): [16-token tile][ks][lg][token][8 dims],
           // dim d = 32*lg + 8*ks + j
-          bf16_t* tile = k_cache + tile_base_k + (int64_t)kh * page_size * D;
+          KV* tile = k_cache + tile_base_k + (int64_t)kh * page_size * D;
           const int d1 = g, d2 = HALF + g;
-          *reinterpret_cast<u16x8*>(tile + ((((d1 & 31) >> 3) * 4 + (d1 >> 5)) * 16 + t16) * 8) = o1;
-          *reinterpret_cast<u16x8*>(tile + ((((d2 & 31) >> 3) * 4 + (d2 >> 5)) * 16 + t16) * 8) = o2;
+          CacheStore<KV>::put(tile + ((((d1 & 31) >> 3) * 4 + (d1 >> 5)) * 16 + t16) * 8, o1, k_inv);
+          CacheStore<KV>::put(tile + ((((d2 & 31) >> 3) * 4 + (d2 >> 5)) * 16 + t16) * 8, o2, k_inv);
         }
       }
     } else {
@@ -135,25 +160,29 @@ __global__ void __launch_bounds__(kRopeItems) rope_kv_kernel(
       const int kh = ci / (D / 8), g = (ci % (D / 8)) * 8;
       const u16x8 v = ld8((Hq + Hkv + kh) * D + g);
       if (v_out) *reinterpret_cast<u16x8*>(v_out + ((int64_t)t * Hkv + kh) * D + g) = v;
-      if (cache_base_k >= 0)
-        *reinterpret_cast<u16x8*>(v_cache + cache_base_k + (int64_t)kh * page_size * D + g) = v;
+      if (cache_base_k >= 0) CacheStore<KV>::put(v_cache + cache_base_k + (int64_t)kh * page_size * D + g, v, v_inv);
     }
   }
 }
 
 int rope_kv(const bf16_t* qkv, int64_t qkv_stride, const int64_t* pos, const float* cos_t,
             const float* sin_t, int tokens, int Hq, int Hkv, int head_dim, bf16_t* q_out,
-            bf16_t* k_out, bf16_t* v_out, bf16_t* k_cache, bf16_t* v_cache,
+            bf16_t* k_out, bf16_t* v_out, void* k_cache, void* v_cache,
             const int64_t* slots, int page_size, int64_t max_pos, const float* xp, int S,
-            const bf16_t* bias, hipStream_t stream) {
+            const bf16_t* bias, bool fp8_cache, float k_scale, float v_scale, hipStream_t stream) {
   if (tokens == 0) return 0;
   if (head_dim != 128) return -1;
   const int64_t slab = (int64_t)tokens * (Hq + 2 * Hkv) * head_dim;
   const int items = (Hq + Hkv) * (head_dim / 16) + Hkv * (head_dim / 8);
   const dim3 grid(tokens, (items + kRopeItems - 1) / kRopeItems);
-  rope_kv_kernel<128><<<grid, kRopeItems, 0, stream>>>(qkv, qkv_stride, pos, cos_t, sin_t, Hq, Hkv, q_out, k_out,
-                                                       v_out, k_cache, v_cache, slots, page_size, max_pos, xp, S,
-                                                       slab, bias);
+  if (fp8_cache)
+    rope_kv_kernel<128, uint8_t><<<grid, kRopeItems, 0, stream>>>(
+        qkv, qkv_stride, pos, cos_t, sin_t, Hq, Hkv, q_out, k_out, v_out, static_cast<uint8_t*>(k_cache),
+        static_cast<uint8_t*>(v_cache), slots, page_size, max_pos, xp, S, slab, bias, 1.f / k_scale, 1.f / v_scale);
+  else
+    rope_kv_kernel<128, bf16_t><<<grid, kRopeItems, 0, stream>>>(
+        qkv, qkv_stride, pos, cos_t, sin_t, Hq, Hkv, q_out, k_out, v_out, static_cast<bf16_t*>(k_cache),
+        static_cast<bf16_t*>(v_cache), slots, page_size, max_pos, xp, S, slab, bias, 1.f, 1.f);
   OAMD_LAUNCH_CHECK();
   return 0;
 }

@@ -111,6 +111,8 @@ class EngineCfg(BaseModel):
     max_context: int = 4096
     max_prompt_tokens: int = 1536
     kv_cache_gb: float = 64.0
+    kv_dtype: str = "auto"            # auto = the compute dtype; fp8 = OCP e4m3fn cache (half the bytes; not the default)
+    kv_scale: float = 1.0             # fp8 cache: stored value = x / kv_scale (keys and values)
     page_size: int = 64
     use_graphs: bool = True
     prefill_graphs: bool = True       # full-ish prefill batches replay a captured bucket graph

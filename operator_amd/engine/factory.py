@@ -36,9 +36,14 @@ def build_llm(s: Settings, device: str | torch.device | None = None, tp=None):
         model.load_hf(e.model_path)
     else:
         model.init_random(e.seed)
+    # KV cache: the compute dtype, or OCP fp8 (e4m3fn, per-tensor scales) with engine.kv_dtype=fp8
+    if e.kv_dtype not in ("auto", "fp8"):
+        raise ValueError(f"engine.kv_dtype must be auto or fp8, not {e.kv_dtype!r}")
+    kv_dtype = torch.float8_e4m3fn if e.kv_dtype == "fp8" else dtype
     pages = PagedKVCache.pages_for_budget(int(e.kv_cache_gb * 1e9), cfg.layers, model.hkv, cfg.head_dim,
-                                          e.page_size, torch.finfo(dtype).bits // 8)
-    kv = PagedKVCache(cfg.layers, pages, model.hkv, cfg.head_dim, e.page_size, device=dev, dtype=dtype)
+                                          e.page_size, torch.finfo(kv_dtype).bits // 8)
+    kv = PagedKVCache(cfg.layers, pages, model.hkv, cfg.head_dim, e.page_size, device=dev, dtype=kv_dtype,
+                      k_scale=e.kv_scale, v_scale=e.kv_scale)
     kw = dict(max_batch=e.max_batch, max_prefill_tokens=e.max_prefill_tokens, max_context=e.max_context,
               use_graphs=e.use_graphs, multi_step=e.multi_step, admit_wait_s=e.admit_wait_ms / 1e3,
               prefill_graphs=e.prefill_graphs)

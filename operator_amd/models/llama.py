@@ -255,12 +255,12 @@ class LlamaModel:
             else:
                 qkv = self._lin(x, lw.wqkv, lw.sqkv, defer=True)
             q, k, v = ops.rope_kv(qkv, fb.positions, self.cos, self.sin, self.hq, self.hkv, kc, vc, fb.slots,
-                                  want_kv=fb.is_prefill, bias=bias)
+                                  want_kv=fb.is_prefill, bias=bias, k_scale=kv.k_scale, v_scale=kv.v_scale)
             if fb.is_prefill:
                 o = ops.attn_prefill(q, k, v, fb.seq_lens, self.scale, work=fb.prefill_work)
             else:
                 o = ops.attn_decode(q, kc, vc, fb.block_tables, fb.context_lens, self.scale, fb.num_splits,
-                                    workspace=ws)
+                                    workspace=ws, k_scale=kv.k_scale, v_scale=kv.v_scale)
             a = self._lin(o.view(T, self.hq * c.head_dim), lw.wo, lw.so, defer=True)
             self.tp.all_reduce_(a)
             x = ops.rmsnorm(a, lw.mlp_norm, c.rms_eps, residual=h)

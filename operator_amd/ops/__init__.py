@@ -126,10 +126,12 @@ def embedding(ids: torch.Tensor, table: torch.Tensor, out: torch.Tensor | None =
 def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, Hq: int, Hkv: int,
             k_cache: torch.Tensor | None = None, v_cache: torch.Tensor | None = None,
             slots: torch.Tensor | None = None, want_kv: bool = True,
-            q_out: torch.Tensor | None = None, bias: torch.Tensor | None = None):
+            q_out: torch.Tensor | None = None, bias: torch.Tensor | None = None,
+            k_scale: float = 1.0, v_scale: float = 1.0):
     """Rotate q/k of the packed qkv rows and scatter k/v into the paged cache.
     ``bias`` [(Hq + 2 Hkv) D] is added to the projection first (Qwen2); with split-K
-    slabs it is added before the single bf16 rounding.
+    slabs it is added before the single bf16 rounding. An e4m3fn cache stores
+    x / k_scale, x / v_scale.
 
     Returns (q [T,Hq,D], k [T,Hkv,D] | None, v [T,Hkv,D] | None).
     """
@@ -140,12 +142,13 @@ def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, cos: torch.Tensor, sin: torch.
         q = q_out if q_out is not None else torch.empty(T, Hq, D, dtype=torch.bfloat16, device=dev)
         k = torch.empty(T, Hkv, D, dtype=torch.bfloat16, device=dev) if want_kv else None
         v = torch.empty(T, Hkv, D, dtype=torch.bfloat16, device=dev) if want_kv else None
-        kernels().rope_kv(q, pos, cos, sin, Hq, Hkv, q, k, v, k_cache, v_cache, slots, qkv.p, qkv.S, bias)
+        kernels().rope_kv(q, pos, cos, sin, Hq, Hkv, q, k, v, k_cache, v_cache, slots, qkv.p, qkv.S, bias,
+                          k_scale, v_scale)
         return q, k, v
     if not qkv.is_cuda:
         if bias is not None:
             qkv = (qkv.float() + bias.float()).to(qkv.dtype)
-        q, k, v = reference.rope_kv(qkv, pos, cos, sin, Hq, Hkv, k_cache, v_cache, slots)
+        q, k, v = reference.rope_kv(qkv, pos, cos, sin, Hq, Hkv, k_cache, v_cache, slots, k_scale, v_scale)
         if q_out is not None:
             q_out.copy_(q.reshape(q_out.shape))
             q = q_out
@@ -155,7 +158,7 @@ def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, cos: torch.Tensor, sin: torch.
     q = q_out if q_out is not None else torch.empty(T, Hq, D, dtype=qkv.dtype, device=qkv.device)
     k = torch.empty(T, Hkv, D, dtype=qkv.dtype, device=qkv.device) if want_kv else None
     v = torch.empty(T, Hkv, D, dtype=qkv.dtype, device=qkv.device) if want_kv else None
-    kernels().rope_kv(qkv, pos, cos, sin, Hq, Hkv, q, k, v, k_cache, v_cache, slots, None, 1, bias)
+    kernels().rope_kv(qkv, pos, cos, sin, Hq, Hkv, q, k, v, k_cache, v_cache, slots, None, 1, bias, k_scale, v_scale)
     return q, k, v
 
 
@@ -392,11 +395,13 @@ def decode_workspace(B: int, Hq: int, num_splits: int, device, D: int = 128):
 
 def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
                 seq_lens: torch.Tensor, scale: float, num_splits: int, out: torch.Tensor | None = None,
-                workspace: tuple[torch.Tensor, torch.Tensor] | None = None, variant: int = 0) -> torch.Tensor:
+                workspace: tuple[torch.Tensor, torch.Tensor] | None = None, variant: int = 0,
+                k_scale: float = 1.0, v_scale: float = 1.0) -> torch.Tensor:
     """Paged decode attention; ``num_splits`` workgroups per (sequence, kv-head)
-    (``decode_splits``). Any value >= 1 is correct; it only changes the schedule."""
+    (``decode_splits``). Any value >= 1 is correct; it only changes the schedule.
+    The cache is bf16, or e4m3fn holding x / k_scale and x / v_scale."""
     if not q.is_cuda:
-        r = reference.attn_decode(q, k_cache, v_cache, block_tables, seq_lens, scale)
+        r = reference.attn_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, k_scale, v_scale)
         if out is not None:
             out.copy_(r)
             return out
@@ -406,7 +411,7 @@ def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, b
     if workspace is None:
         workspace = decode_workspace(B, Hq, num_splits, q.device)
     kernels().attn_decode(q, k_cache, v_cache, block_tables, seq_lens, o, workspace[0], workspace[1],
-                          num_splits, scale, variant)
+                          num_splits, scale, variant, k_scale, v_scale)
     return o
 
 

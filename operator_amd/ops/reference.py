@@ -100,9 +100,24 @@ def k_cache_write(k_cache: torch.Tensor, page: int, off: int, k: torch.Tensor) -
     k_cache.view(pages, Hkv, P // K_TILE, K_TILE * D)[page, :, off // K_TILE, idx] = k
 
 
+FP8_KV_MAX = 448.0  # OCP e4m3fn
+
+
+def kv_store(x: torch.Tensor, cache_dtype: torch.dtype, scale: float) -> torch.Tensor:
+    """Value as held by a cache of ``cache_dtype``: as is, or e4m3fn(x / scale) saturated."""
+    if cache_dtype == torch.float8_e4m3fn:
+        return (x.float() / scale).clamp(-FP8_KV_MAX, FP8_KV_MAX).to(torch.float8_e4m3fn)
+    return x.to(cache_dtype)
+
+
+def kv_load(c: torch.Tensor, scale: float) -> torch.Tensor:
+    """fp32 view of cache contents (fp8 caches dequantised by their scale)."""
+    return c.float() * scale if c.dtype == torch.float8_e4m3fn else c.float()
+
+
 def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, Hq: int, Hkv: int,
             k_cache: torch.Tensor | None = None, v_cache: torch.Tensor | None = None,
-            slots: torch.Tensor | None = None):
+            slots: torch.Tensor | None = None, k_scale: float = 1.0, v_scale: float = 1.0):
     """Split packed qkv, rotate q/k, optionally scatter k/v into the paged cache.
 
     Cache layout [pages, Hkv, page, D] (K tiled, see k_tile_index; V row-major);
@@ -122,8 +137,8 @@ def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, cos: torch.Tensor, sin: torch.
             s = int(slots[t])
             if s < 0:
                 continue
-            k_cache_write(k_cache, s // P, s % P, k[t])
-            v_cache[s // P, :, s % P] = v[t]
+            k_cache_write(k_cache, s // P, s % P, kv_store(k[t], k_cache.dtype, k_scale))
+            v_cache[s // P, :, s % P] = kv_store(v[t], v_cache.dtype, v_scale)
     return q, k.contiguous(), v.contiguous()
 
 
@@ -151,8 +166,9 @@ def attn_prefill(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cu_seqlens: 
 
 
 def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
-                seq_lens: torch.Tensor, scale: float) -> torch.Tensor:
-    """One query token per sequence over a paged cache [pages, Hkv, page, D] (K tiled)."""
+                seq_lens: torch.Tensor, scale: float, k_scale: float = 1.0, v_scale: float = 1.0) -> torch.Tensor:
+    """One query token per sequence over a paged cache [pages, Hkv, page, D] (K tiled;
+    bf16, or e4m3fn holding x / scale)."""
     B, Hq, D = q.shape
     Hkv, P = k_cache.shape[1], k_cache.shape[2]
     k_cache = k_cache_logical(k_cache)
@@ -164,8 +180,8 @@ def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, b
             continue
         npg = (L + P - 1) // P
         pages = block_tables[b, :npg].long()
-        ks = k_cache[pages].permute(1, 0, 2, 3).reshape(Hkv, npg * P, D)[:, :L].float()
-        vs = v_cache[pages].permute(1, 0, 2, 3).reshape(Hkv, npg * P, D)[:, :L].float()
+        ks = kv_load(k_cache[pages].permute(1, 0, 2, 3).reshape(Hkv, npg * P, D)[:, :L], k_scale)
+        vs = kv_load(v_cache[pages].permute(1, 0, 2, 3).reshape(Hkv, npg * P, D)[:, :L], v_scale)
         ks = ks.repeat_interleave(G, 0)
         vs = vs.repeat_interleave(G, 0)
         s = torch.einsum("hd,hld->hl", q[b].float(), ks) * scale

@@ -328,3 +328,51 @@ def test_rope_kv_bias_slabs_and_rows():
         q, k, v = ops.rope_kv(src, pos, cos, sin, Hq, Hkv, kc, vc, slots, bias=bias)
         for a, b in ((q, q_r), (k, k_r), (v, v_r), (kc, kc_r), (vc, vc_r)):
             torch.testing.assert_close(a.cpu().float(), b.float(), atol=6e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (28, 4), (16, 2)])
+@pytest.mark.parametrize("variant", [0, 2])
+def test_attn_decode_fp8_cache(Hq, Hkv, variant):
+    """e4m3fn KV cache (stored x / scale): the kernel equals the fp32 reference over
+    the dequantised cache (the fp8 -> bf16 widening is exact), for both tilings and
+    split schedules."""
+    torch.manual_seed(14)
+    lens, P, D = [1, 70, 300, 1029], 64, 128
+    B = len(lens)
+    maxp = (max(lens) + P - 1) // P + 1
+    pages = B * maxp + 2
+    k_scale, v_scale = 0.5, 2.0
+    kf, vf = torch.randn(pages, Hkv, P, D, device=DEV) * 3, torch.randn(pages, Hkv, P, D, device=DEV) * 3
+    kc = ref.kv_store(kf, torch.float8_e4m3fn, k_scale)
+    vc = ref.kv_store(vf, torch.float8_e4m3fn, v_scale)
+    bt = torch.randperm(pages, device=DEV)[: B * maxp].reshape(B, maxp).int()
+    sl = torch.tensor(lens, dtype=torch.int32, device=DEV)
+    q = _rand(B, Hq, D)
+    scale = 1 / math.sqrt(D)
+    o_r = ref.attn_decode(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), sl.cpu(), scale, k_scale, v_scale)
+    for ns in (1, 4):
+        o = ops.attn_decode(q, kc, vc, bt, sl, scale, ns, variant=variant, k_scale=k_scale, v_scale=v_scale)
+        torch.testing.assert_close(o.cpu().float(), o_r.float(), atol=3e-2, rtol=3e-2)
+
+
+def test_rope_kv_writes_fp8_cache():
+    """rope_kv into an e4m3fn cache stores e4m3(bf16(rotated k) / k_scale), v / v_scale."""
+    torch.manual_seed(15)
+    T, Hq, Hkv, D, P, pages = 40, 8, 2, 128, 16, 8
+    k_scale, v_scale = 0.25, 4.0
+    cos, sin = ref.rope_tables(4096, D, 500000.0, device=DEV)
+    qkv = _rand(T, (Hq + 2 * Hkv) * D)
+    pos = torch.randint(0, 4000, (T,), device=DEV)
+    slots = torch.randperm(pages * P, device=DEV)[:T]
+    kc = torch.zeros(pages, Hkv, P, D, dtype=torch.float8_e4m3fn, device=DEV)
+    vc = torch.zeros_like(kc)
+    ops.rope_kv(qkv, pos, cos, sin, Hq, Hkv, kc, vc, slots, k_scale=k_scale, v_scale=v_scale)
+    kb = torch.zeros(pages, Hkv, P, D, dtype=torch.bfloat16, device=DEV)
+    vb = torch.zeros_like(kb)
+    ops.rope_kv(qkv, pos, cos, sin, Hq, Hkv, kb, vb, slots)
+    # same rotated values as the bf16 cache, quantised: at most one e4m3 step apart
+    kd, vd = ref.kv_load(kc.cpu(), k_scale), ref.kv_load(vc.cpu(), v_scale)
+    torch.testing.assert_close(kd, kb.cpu().float(), atol=0.07 * k_scale, rtol=0.07)
+    torch.testing.assert_close(vd, vb.cpu().float(), atol=0.07 * v_scale, rtol=0.07)
+    exact = ref.kv_store(vb.cpu().float(), torch.float8_e4m3fn, v_scale)
+    assert torch.equal(vc.cpu().view(torch.uint8), exact.view(torch.uint8))

@@ -185,3 +185,35 @@ def test_qwen_decode_step_matches_cpu_reference(B):
         out.append(m.forward(fb, kv).float().cpu())
     err = (out[0] - out[1]).abs().max() / out[1].abs().max()
     assert err < 0.05, float(err)
+
+
+def test_fp8_kv_cache_engine_tracks_bf16_cache():
+    """Llama decode with an e4m3fn KV cache through the graph engine: the first decode
+    logits track the bf16 cache's and the engine runs windows with graphs."""
+    cfg = get_config("tiny-gqa4")
+    m = LlamaModel(cfg, device="cuda").init_random(seed=13)
+    lens = [37, 210, 5]
+    outs, toks = {}, {}
+    for dt in (torch.bfloat16, torch.float8_e4m3fn):
+        kv = PagedKVCache(cfg.layers, 64, cfg.kv_heads, 128, 16, device="cuda", dtype=dt)
+        P, per = 16, 16
+        B = len(lens)
+        bt = torch.arange(B * per, dtype=torch.int32).reshape(B, per)
+        ids = [torch.arange(3, 3 + L) for L in lens]
+        pos = torch.cat([torch.arange(L) for L in lens])
+        slots = torch.cat([bt[i, torch.arange(L) // P].long() * P + torch.arange(L) % P for i, L in enumerate(lens)])
+        m.forward(ForwardBatch(torch.cat(ids).cuda(), pos.cuda(), slots.cuda(), True, torch.tensor([0]).cuda(),
+                               seq_lens=lens), kv)
+        dpos = torch.tensor(lens)
+        dslots = torch.stack([bt[i, L // P].long() * P + L % P for i, L in enumerate(lens)])
+        fb = ForwardBatch(torch.tensor([7, 8, 9]).cuda(), dpos.cuda(), dslots.cuda(), False, None,
+                          block_tables=bt.cuda(), context_lens=(dpos + 1).int().cuda(), num_splits=1)
+        outs[dt] = m.forward(fb, kv).float()
+        kv2 = PagedKVCache(cfg.layers, 128, cfg.kv_heads, 128, 16, device="cuda", dtype=dt)
+        eng = LLMEngine(m, kv2, max_batch=4, max_context=1024, use_graphs=True)
+        r = eng.generate([GenRequest(list(range(2, 90)), max_tokens=20, temperature=0.0, ignore_eos=True)])[0]
+        assert len(r.output) == 20 and eng.stats.graph_replays > 0
+        toks[dt] = r.output
+    cos = torch.nn.functional.cosine_similarity(outs[torch.bfloat16].flatten(), outs[torch.float8_e4m3fn].flatten(),
+                                                dim=0)
+    assert cos > 0.99, float(cos)
