@@ -221,7 +221,8 @@ def attn_prefill(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, seq_lens: li
 
 
 GEMM_DECODE_M = (64, 128, 256)  # decode buckets the gfx950 gemm_decode kernel is tuned for
-_GEMM_TABLE_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_tuned.json")
+_GEMM_TABLE_PATH = os.environ.get("OAMD_GEMM_TABLE") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                                     "gemm_tuned.json")
 _gemm_table: dict | None = None
 
 
