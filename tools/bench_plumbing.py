@@ -1,0 +1,114 @@
+"""BASELINE.json config 1, "plumbing": the controller with stub engines, on the CPU.
+
+The reference's config 1 is one Podmortem CR reconciled in Quarkus dev mode with stub
+log-parser / ai-interface endpoints. Here: FakeKube (in-memory API server) + the
+operator (watcher, reconcilers, pipeline, sinks) with the CPU pattern matcher (Python
+oracle semantics, catalog library) and the echo explainer (no model). Reports
+
+* reconcile latency: Podmortem CR created -> status.phase Ready, over --crs CRs;
+* --match stub (default): a fixed pattern result, as the reference's stub log-parser —
+  the controller alone; --match cpu: the CPU pattern matcher over the pod log;
+* analyses/s: --failures pods fail at once (MODIFIED events) -> every analysis stored
+  (four pod annotations, recentFailures ring, Events), p50 / p99 per failure.
+
+One JSON line on stdout.
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from operator_amd.api.models import AnalysisEvent, AnalysisResult, AnalysisSummary, MatchedPattern  # noqa: E402
+from operator_amd.config import load_settings  # noqa: E402
+from operator_amd.controller.operator import Operator  # noqa: E402
+from operator_amd.engine.match import MatchEngine  # noqa: E402
+from operator_amd.engine.service import EchoExplainService, LocalMatchService  # noqa: E402
+from operator_amd.kube.fake import FakeKube, failed_pod, running_pod  # noqa: E402
+from operator_amd.kube.resources import AIPROVIDERS, PODMORTEMS, PODS  # noqa: E402
+from operator_amd.patterns.synth import catalog_library  # noqa: E402
+
+LOG = ("\n".join(["starting app", "loading config", "connected to db"] * 30 +
+                 ["java.lang.OutOfMemoryError: Java heap space", "\tat com.example.Cache.grow(Cache.java:42)"] +
+                 ["shutting down"] * 5)).encode()
+
+
+class StubMatch:
+    """The stub log-parser: one fixed CRITICAL OOM event for every pod."""
+
+    def analyze(self, data):
+        meta = data.pod.get("metadata") or {}
+        ev = AnalysisEvent(line_number=91, score=0.9, matched_line="java.lang.OutOfMemoryError: Java heap space",
+                           matched_pattern=MatchedPattern(id="oom", name="Java heap exhausted", severity="CRITICAL"))
+        return AnalysisResult(pod_name=meta.get("name"), pod_namespace=meta.get("namespace"), events=[ev],
+                              summary=AnalysisSummary(highest_severity="CRITICAL", significant_events=1,
+                                                      total_events=1))
+
+
+def wait(pred, timeout):
+    end = time.perf_counter() + timeout
+    while time.perf_counter() < end:
+        if pred():
+            return True
+        time.sleep(0.001)
+    return False
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--failures", type=int, default=2000)
+    ap.add_argument("--crs", type=int, default=20)
+    ap.add_argument("--workers", type=int, default=64)
+    ap.add_argument("--match", choices=["stub", "cpu"], default="stub")
+    a = ap.parse_args()
+    s = load_settings(env={}, overrides={"patterns.cache_dir": "/tmp/oamd-plumbing", "health.enabled": False,
+                                         "operator.workers": a.workers})
+    fk = FakeKube()
+    done = {}
+    match = StubMatch() if a.match == "stub" else LocalMatchService(MatchEngine(catalog_library(), device="cpu"),
+                                                                   max_wait_ms=2.0)
+    op = Operator(fk, s, match_service=match, explain_service=EchoExplainService())
+    op.pipeline.listeners.append(lambda monitor, pod, outcome: done.setdefault(pod["metadata"]["name"],
+                                                                                 time.perf_counter()))
+    op.start(http=False)
+    fk.create(AIPROVIDERS, {"metadata": {"name": "stub", "namespace": "default"},
+                            "spec": {"providerId": "stub", "modelId": "echo"}})
+    # reconcile latency of fresh Podmortem CRs (the first one is the monitor used below)
+    rec = []
+    for i in range(a.crs):
+        t0 = time.perf_counter()
+        fk.create(PODMORTEMS, {"metadata": {"name": f"m{i}", "namespace": "default"},
+                               "spec": {"podSelector": {"matchLabels": {"app": "demo" if i == 0 else f"x{i}"}},
+                                        "aiAnalysisEnabled": True, "aiProviderRef": {"name": "stub"}}})
+        ok = wait(lambda: (fk.get(PODMORTEMS, f"m{i}", "default").get("status") or {}).get("phase") == "Ready", 30)
+        assert ok, "reconcile timed out"
+        rec.append(time.perf_counter() - t0)
+    names = [f"p{i}" for i in range(a.failures)]
+    for n in names:
+        fk.create(PODS, running_pod(n, labels={"app": "demo"}))
+        fk.set_log("default", n, LOG)
+    t_fail = {}
+    t0 = time.perf_counter()
+    for n in names:
+        cur = fk.get(PODS, n, "default")
+        cur["status"] = failed_pod(n, finished_at="2025-08-29T10:00:00Z")["status"]
+        t_fail[n] = time.perf_counter()
+        fk.replace(PODS, cur)
+    assert wait(lambda: len(done) >= a.failures, 600), f"only {len(done)} of {a.failures} analysed"
+    op.drain(120)
+    elapsed = time.perf_counter() - t0
+    lat = sorted(done[n] - t_fail[n] for n in names)
+    op.stop()
+    print(json.dumps({"bench": "plumbing (BASELINE config 1)", "failures": a.failures,
+                      "analyses_per_s": round(a.failures / elapsed, 1),
+                      "p50_ms": round(statistics.median(lat) * 1e3, 1), "p99_ms": round(lat[int(0.99 * len(lat))] * 1e3, 1),
+                      "reconcile_p50_ms": round(statistics.median(rec) * 1e3, 2),
+                      "reconcile_max_ms": round(max(rec) * 1e3, 2), "crs": a.crs,
+                      "engines": ("stub log-parser" if a.match == "stub" else "CPU matcher (catalog)") +
+                      " + echo explainer", "pipeline_workers": a.workers}))
+
+
+if __name__ == "__main__":
+    main()
