@@ -63,12 +63,59 @@ def parse_args():
     ap.add_argument("--engine-procs", type=int, default=1,
                     help="engine processes per GPU (EnginePool workers holding the scan + LLM engines, "
                          "--max-batch split over them); 1 = engines inside this process")
+    ap.add_argument("--shards", type=int, default=None,
+                    help="operator shards per GPU (default 2 with a GPU, 1 without): independent operator "
+                         "processes (own API-server shard, controller and engines), each failing --batch / shards "
+                         "pods per step on its own closed loop; the rank process runs shard 0 and starts the "
+                         "others as child processes")
+    ap.add_argument("--shard-index", type=int, default=None, help=argparse.SUPPRESS)  # internal: child shard
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
 
+SHARD_TAG = "OAMD_SHARD"  # protocol lines on a child shard's stdout
+
+
+def spawn_shards(a) -> list:
+    """Child shard processes 1..shards-1 of this rank, started before this process
+    touches the GPU (plain child processes, no exec from a GPU-initialised process)."""
+    import subprocess
+
+    kids = []
+    for i in range(1, a.shards):
+        env = dict(os.environ)
+        env.update(OAMD_BENCH_RANK=os.environ.get("RANK", "0"),
+                   OAMD_BENCH_LOCAL=os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0")),
+                   WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+        kids.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), *sys.argv[1:],
+                                      "--shard-index", str(i)], stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                                     env=env, text=True, bufsize=1))
+    return kids
+
+
+def shard_read(kid, what: str) -> str:
+    """Next protocol line ``OAMD_SHARD <what> ...`` of a child shard (other stdout lines skipped)."""
+    while True:
+        line = kid.stdout.readline()
+        if not line:
+            raise SystemExit(f"shard process {kid.pid} exited (code {kid.poll()}) before {what}")
+        if line.startswith(f"{SHARD_TAG} {what}"):
+            return line[len(SHARD_TAG) + len(what) + 2:].strip()
+
+
 def main() -> int:
     a = parse_args()
+    child = a.shard_index is not None
+    if a.shards is None:   # device_count() does not initialise the GPU
+        import torch
+
+        # two shards measured 32.8 vs 28.1 analyses/s, p50 7.8 vs 9.2 s (profiles/bench_shards_8b.jsonl)
+        a.shards = 2 if torch.cuda.device_count() > 0 else 1
+    a.shards = max(1, a.shards)
+    kids = spawn_shards(a) if (a.shards > 1 and not child) else []
+    shard = a.shard_index or 0
+    a.batch = max(1, a.batch // a.shards)   # this shard's wave (--batch is per GPU, over all shards)
+    a.max_batch = max(1, a.max_batch // a.shards)
     # host thread pools sized to this rank's share of the node (N ranks on one host):
     # the tokenizer's Rust pool and torch's intra-op pool default to every CPU each
     share_cpus = max(2, min(16, (os.cpu_count() or 16) // max(1, int(os.environ.get("LOCAL_WORLD_SIZE",
@@ -93,7 +140,8 @@ def main() -> int:
     from operator_amd.patterns.synth import LogFactory, synthetic_library
 
     def settings(dev: str, max_batch: int, world_: int):
-        kv = a.kv_gb or (1.0 if dev == "cpu" else (96.0 if not share else max(8.0, 200.0 / world_ - 16)) / procs)
+        kv = a.kv_gb or (1.0 if dev == "cpu" else (96.0 if not share else max(8.0, 200.0 / world_ - 16)) / procs
+                         / a.shards)
         return load_settings(env={}, overrides={
             "engine.model": a.model, "engine.device": dev, "engine.max_batch": max_batch,
             "engine.max_prefill_tokens": a.prefill_tokens,
@@ -117,11 +165,10 @@ def main() -> int:
         dev0 = f"cuda:{local_env}" if torch.cuda.device_count() > 0 else "cpu"
         pool = EnginePool(settings(dev0, max(1, a.max_batch // procs), world_env), patset, devices=[dev0] * procs)
 
-    # OAMD_BENCH_SHARE_GPU=1: rehearsal of the multi-rank launch on a one-GPU box —
-    # every rank on cuda:0, gloo for the timing collectives (RCCL refuses two ranks
-    # on one device), KV budget split so the ranks fit one card. Not a scaling number.
     info = init_from_env(backend="gloo" if share else None)
     rank, world, local = info.rank, info.world, (0 if share else info.local_rank)
+    if child:   # a child shard: the parent rank's GPU, no process group of its own
+        rank, local = int(os.environ["OAMD_BENCH_RANK"]), (0 if share else int(os.environ["OAMD_BENCH_LOCAL"]))
     if torch.cuda.is_available():
         torch.cuda.set_device(local)
     dev = f"cuda:{local}" if torch.cuda.is_available() else "cpu"
@@ -139,7 +186,8 @@ def main() -> int:
     s = settings(dev, a.max_batch, world)
 
     def note(msg: str) -> None:   # stage progress on stderr (the JSON line stays alone on stdout)
-        print(f"[bench rank {rank}] {msg}", file=sys.stderr, flush=True)
+        tag = f"rank {rank}" + (f" shard {shard}" if a.shards > 1 else "")
+        print(f"[bench {tag}] {msg}", file=sys.stderr, flush=True)
 
     if os.environ.get("OAMD_BENCH_STACKS_S"):   # debugging a stall: every thread's stack, then exit
         import faulthandler
@@ -180,9 +228,10 @@ def main() -> int:
                    dfa_states=ws[0].get("dfa_states") if ws else None)
         return out
 
-    fac = LogFactory(n_patterns=a.patterns, seed=rank)
+    fac = LogFactory(n_patterns=a.patterns, seed=100 * rank + shard)
     waves = a.warmup + a.steps
-    logs = [fac.batch(a.batch, a.log_kb * 1024, n_failures=3, seed=1000 * rank + w)[0] for w in range(waves)]
+    logs = [fac.batch(a.batch, a.log_kb * 1024, n_failures=3, seed=1000 * rank + 100 * shard + w)[0]
+            for w in range(waves)]
 
     lat: list[float] = []
     t_inject: dict[str, float] = {}
@@ -250,7 +299,7 @@ def main() -> int:
         # pods: each pod's status flips to a terminated, non-zero exit (the MODIFIED
         # watch event the operator reacts to), and its latency is timed from there.
         def wave_names(w: int) -> list[str]:
-            return [f"app-r{rank}-w{w}-{i}" for i in range(a.batch)]
+            return [f"app-r{rank}-s{shard}-w{w}-{i}" for i in range(a.batch)]
 
         for w in range(waves):
             for name, log in zip(wave_names(w), logs[w]):
@@ -321,8 +370,7 @@ def main() -> int:
     def progress():
         t_start = time.perf_counter()
         while not prog_stop.wait(30.0):
-            print(f"[bench rank {rank}] {time.perf_counter() - t_start:.0f} s, {counter['n']} analyses in the current "
-                  f"pass", file=sys.stderr, flush=True)
+            note(f"{time.perf_counter() - t_start:.0f} s, {counter['n']} analyses in the current pass")
 
     threading.Thread(target=progress, daemon=True).start()
     note(f"{a.warmup} warmup wave(s)")
@@ -335,18 +383,58 @@ def main() -> int:
     def sync():
         if torch.cuda.is_available():
             torch.cuda.synchronize()
-        if world > 1:
+        if world > 1 and not child:
             dist.barrier()
 
+    if child:   # a child shard: report ready, start on the parent's signal, report the timed pass
+        print(f"{SHARD_TAG} READY", flush=True)
+        if sys.stdin.readline().strip() != "GO":
+            return 1
+        mono0 = time.monotonic_ns()
+        run_timed(list(range(a.warmup, waves)))
+        sync()
+        mono1 = time.monotonic_ns()
+        prog_stop.set()
+        st1 = engine_stats()
+        print(f"{SHARD_TAG} RESULT " + json.dumps({
+            "t0": mono0, "t1": mono1, "lat": lat, "outcomes": counter["outcomes"],
+            "ptoks": st1["prefill_tokens"] - stats0["prefill_tokens"],
+            "dtoks": st1["decode_tokens"] - stats0["decode_tokens"],
+            "replays": st1["prefill_graph_replays"] - stats0["prefill_graph_replays"]}), flush=True)
+        if a.mode == "pipeline":
+            op.stop()
+        if ee is not None:
+            ee.close()
+        if pool is not None:
+            pool.close()
+        return 0
+
+    for k in kids:   # every shard of this rank initialised and warmed up
+        shard_read(k, "READY")
     sync()
     note("timed waves")
-    t0 = time.perf_counter()
     mono0 = time.monotonic_ns()  # same clock as rocprofv3 timestamps: lets a trace be cut to the timed region
+    for k in kids:
+        k.stdin.write("GO\n")
+        k.stdin.flush()
     run_timed(list(range(a.warmup, waves)))
-    sync()
-    elapsed = time.perf_counter() - t0
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
     mono1 = time.monotonic_ns()
+    results = [json.loads(shard_read(k, "RESULT")) for k in kids]
+    for k in kids:
+        k.wait(120)
+    # the rank's timed pass: first shard start to last shard end (one host clock)
+    t_first = min([mono0] + [r["t0"] for r in results])
+    t_last = max([mono1] + [r["t1"] for r in results])
+    if world > 1:
+        dist.barrier()
+    elapsed = (t_last - t_first) / 1e9
     prog_stop.set()
+    for r in results:
+        lat.extend(r["lat"])
+        for o, n in r["outcomes"].items():
+            counter["outcomes"][o] = counter["outcomes"].get(o, 0) + n
 
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev if info.backend == "nccl" else "cpu")
     p50_local = statistics.median(lat) if lat else float("nan")
@@ -355,25 +443,28 @@ def main() -> int:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         dist.all_reduce(p50, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
-    total = a.batch * a.steps * world
+    total = a.batch * a.shards * a.steps * world
     value = total / elapsed
     stats1 = engine_stats()
-    ptoks = stats1["prefill_tokens"] - stats0["prefill_tokens"]
-    dtoks = stats1["decode_tokens"] - stats0["decode_tokens"]
+    ptoks = stats1["prefill_tokens"] - stats0["prefill_tokens"] + sum(r["ptoks"] for r in results)
+    dtoks = stats1["decode_tokens"] - stats0["decode_tokens"] + sum(r["dtoks"] for r in results)
+    replays = stats1["prefill_graph_replays"] - stats0["prefill_graph_replays"] + sum(r["replays"] for r in results)
     out = {
         "metric": METRIC, "value": round(value, 3), "unit": "analyses/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 2), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
         "data": "synthetic pod logs (LogFactory) + random-init weights",
         "p50_explanation_latency_ms": round(float(p50.item()) * 1e3, 1),
-        "config": {"model": a.model, "global_batch": a.batch * world, "seq_len": a.prompt_tokens + a.max_tokens,
+        "config": {"model": a.model, "global_batch": a.batch * a.shards * world,
+                   "seq_len": a.prompt_tokens + a.max_tokens,
                    "parallelism": f"dp{world}", "tp": 1, "max_tokens": a.max_tokens,
                    "prompt_tokens_cap": a.prompt_tokens, "log_kib": a.log_kb, "patterns": a.patterns,
                    "mode": a.mode, "hipgraph": stats1["use_graphs"], "engine_procs_per_gpu": procs,
+                   "operator_shards_per_gpu": a.shards,
                    "kv_cache_dtype": "fp8_e4m3fn" if a.kv_dtype == "fp8" else "bf16",
                    "waves": "serial" if (a.serial_waves or a.mode != "pipeline") else "pipelined"},
         "detail": {"init_s": round(init_s, 1), "prefill_tokens_per_gpu": ptoks, "decode_tokens_per_gpu": dtoks,
-                   "prefill_graph_replays": stats1["prefill_graph_replays"] - stats0["prefill_graph_replays"],
+                   "prefill_graph_replays": replays,
                    "prefill_graph_buckets": stats1["prefill_graph_buckets"],
                    "decode_tok_s_per_gpu": round(dtoks / elapsed, 1), "outcomes": counter["outcomes"],
                    "dfa_states": stats1["dfa_states"], "timed_monotonic_ns": [mono0, mono1]},
