@@ -42,6 +42,10 @@ class OperatorCfg(BaseModel):
     lease_duration_s: float = 15.0
     lease_renew_deadline_s: float = 10.0
     lease_retry_period_s: float = 2.0
+    # operator shards: shard_count processes split the pods by a stable hash of ns/name
+    # (each its own engines and, with leader election, its own lease); 1 = no sharding
+    shard_count: int = 1
+    shard_index: int = 0
 
 
 class KubeCfg(BaseModel):

@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import threading
 import time
+import zlib
 from collections import OrderedDict
 from typing import Any
 
@@ -44,6 +45,15 @@ def has_pod_failed(pod: dict, include_last_state: bool = False, include_init: bo
             if lt and _exit_code(lt) != 0:
                 return True
     return False
+
+
+def in_shard(pod: dict, index: int, count: int) -> bool:
+    """Operator sharding: pod ns/name -> shard crc32 % count (stable across processes
+    and restarts); every pod belongs to exactly one of ``count`` shards."""
+    if count <= 1:
+        return True
+    md = pod.get("metadata") or {}
+    return zlib.crc32(f"{md.get('namespace') or ''}/{md.get('name') or ''}".encode()) % count == index
 
 
 def failure_time(pod: dict, include_last_state: bool = False) -> str | None:

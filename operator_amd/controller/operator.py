@@ -104,10 +104,14 @@ class Operator:
         """Watcher, informer and reconcilers: what only the leader runs."""
         s, kube = self.settings, self.kube
         self.monitors = MonitorCache(kube)
+        shard = (s.operator.shard_index, s.operator.shard_count)
+        if not 0 <= shard[0] < max(1, shard[1]):
+            raise ValueError(f"operator.shard_index {shard[0]} outside 0..{shard[1] - 1}")
         self.watcher = PodFailureWatcher(kube, self.pipeline, self.deduper, s.watch.namespaces, self.monitors,
                                          s.watch.restart_delay_s, s.watch.include_last_state,
-                                         s.watch.include_init_containers)
-        self.pm_reconciler = PodmortemReconciler(kube, self.pipeline, self.deduper, s.watch.include_last_state)
+                                         s.watch.include_init_containers, shard=shard)
+        self.pm_reconciler = PodmortemReconciler(kube, self.pipeline, self.deduper, s.watch.include_last_state,
+                                                 shard=shard)
         self.pl_reconciler = PatternLibraryReconciler(kube, self.sync, on_synced=lambda lib: self.reload_patterns())
         self.aip_reconciler = AIProviderReconciler(kube, self.explainer, s.engine.model)
         self.controllers = [
@@ -171,7 +175,8 @@ class Operator:
         if o.leader_election:
             from operator_amd.controller.leader import LeaderElector
 
-            self.elector = LeaderElector(self.kube, o.lease_name, o.lease_namespace,
+            lease = o.lease_name if o.shard_count <= 1 else f"{o.lease_name}-shard{o.shard_index}"
+            self.elector = LeaderElector(self.kube, lease, o.lease_namespace,
                                          lease_duration_s=o.lease_duration_s,
                                          renew_deadline_s=o.lease_renew_deadline_s,
                                          retry_period_s=o.lease_retry_period_s,

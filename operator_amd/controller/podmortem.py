@@ -15,7 +15,7 @@ import logging
 
 from operator_amd.kube.resources import PODS, selector_is_empty
 
-from .failures import FailureDeduper, failure_time, has_pod_failed
+from .failures import FailureDeduper, failure_time, has_pod_failed, in_shard
 from .pipeline import AnalysisPipeline
 from .runtime import UpdateControl
 
@@ -23,9 +23,11 @@ log = logging.getLogger(__name__)
 
 
 class PodmortemReconciler:
-    def __init__(self, kube, pipeline: AnalysisPipeline, deduper: FailureDeduper, include_last_state: bool = False):
+    def __init__(self, kube, pipeline: AnalysisPipeline, deduper: FailureDeduper, include_last_state: bool = False,
+                 shard: tuple[int, int] = (0, 1)):
         self.kube, self.pipeline, self.deduper = kube, pipeline, deduper
         self.include_last_state = include_last_state
+        self.shard_index, self.shard_count = shard
 
     def find_matching_pods(self, monitor: dict) -> list[dict]:
         sel = (monitor.get("spec") or {}).get("podSelector")
@@ -38,6 +40,8 @@ class PodmortemReconciler:
         log.info("Reconciling Podmortem: %s", name)
         try:
             for pod in self.find_matching_pods(monitor):
+                if not in_shard(pod, self.shard_index, self.shard_count):
+                    continue
                 if has_pod_failed(pod, self.include_last_state):
                     if self.deduper.check_and_mark(pod, failure_time(pod, self.include_last_state)):
                         self.pipeline.submit(monitor, pod)

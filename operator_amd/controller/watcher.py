@@ -26,7 +26,7 @@ import threading
 from operator_amd.kube.informer import WatchLoop
 from operator_amd.kube.resources import PODMORTEMS, PODS, ApiError, WatchClosed
 
-from .failures import FailureDeduper, failure_time, has_pod_failed, matches_monitor
+from .failures import FailureDeduper, failure_time, has_pod_failed, in_shard, matches_monitor
 from .pipeline import AnalysisPipeline
 
 log = logging.getLogger(__name__)
@@ -82,8 +82,9 @@ class MonitorCache:
 class PodFailureWatcher:
     def __init__(self, kube, pipeline: AnalysisPipeline, deduper: FailureDeduper, namespaces: str | None = None,
                  monitors: MonitorCache | None = None, restart_delay_s: float = 5.0, include_last_state: bool = False,
-                 include_init: bool = False):
+                 include_init: bool = False, shard: tuple[int, int] = (0, 1)):
         self.kube, self.pipeline, self.deduper = kube, pipeline, deduper
+        self.shard_index, self.shard_count = shard
         self.allowed = parse_namespaces(namespaces)
         self.monitors = monitors
         self.restart_delay_s = restart_delay_s
@@ -145,6 +146,8 @@ class PodFailureWatcher:
                 return
             ns = (pod.get("metadata") or {}).get("namespace")
             if self.allowed and ns not in self.allowed:
+                return
+            if not in_shard(pod, self.shard_index, self.shard_count):   # another operator shard's pod
                 return
             if has_pod_failed(pod, self.include_last_state, self.include_init):
                 self.handle_failure(pod)

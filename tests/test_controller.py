@@ -501,3 +501,38 @@ def test_list_resource_version_is_the_lists_own():
     fk.create(PODS, running_pod("c"))
     assert next(iter(w))[1]["metadata"]["name"] == "c"
     w.close()
+
+
+def test_operator_shards_split_failures_exactly_once(tmp_path):
+    """Two operator shards on one API server (operator.shard_count=2): every failed pod
+    is analysed by exactly one of them, both take part, and both keep the CR status."""
+    from operator_amd.controller.failures import in_shard
+
+    fk = FakeKube()
+    ops_, echos = [], []
+    for i in range(2):
+        s = load_settings(env={}, overrides={"patterns.cache_dir": str(tmp_path / f"p{i}"), "health.enabled": False,
+                                             "operator.shard_count": 2, "operator.shard_index": i})
+        echo = EchoExplainService()
+        op = Operator(fk, s, match_service=LocalMatchService(MatchEngine(catalog_library(), device="cpu"),
+                                                             max_wait_ms=1), explain_service=echo)
+        ops_.append(op.start(http=False))
+        echos.append(echo)
+    try:
+        _pm(fk, ai=False)
+        wait_for(lambda: all(o.monitors.list() for o in ops_))
+        names = [f"sh-{i}" for i in range(24)]
+        for n in names:
+            _fail(fk, n)
+        wait_for(lambda: all("podmortem.io/analysis" in (fk.get(PODS, n, "default")["metadata"].get("annotations")
+                                                         or {}) for n in names), timeout=30)
+        for o in ops_:
+            o.drain()
+        per = [sum(1 for n in names if in_shard(fk.get(PODS, n, "default"), i, 2)) for i in range(2)]
+        assert per[0] > 0 and per[1] > 0 and sum(per) == len(names)
+        det = [e for e in _events(fk, "PodFailureDetected") if e["regarding"]["kind"] == "Pod"]
+        assert sorted(e["regarding"]["name"] for e in det) == sorted(names)   # exactly once each
+        assert len(fk.get(PODMORTEMS, "demo-monitor", "default")["status"]["recentFailures"]) == 10
+    finally:
+        for o in ops_:
+            o.stop()
