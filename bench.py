@@ -106,6 +106,16 @@ def shard_read(kid, what: str) -> str:
 def main() -> int:
     a = parse_args()
     child = a.shard_index is not None
+    if child:   # a child shard dies with its rank process (torchrun only signals its own workers)
+        try:
+            import ctypes
+            import signal
+
+            ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, int(signal.SIGTERM))   # PR_SET_PDEATHSIG
+        except OSError:
+            pass
+        if os.getppid() == 1:
+            return 1
     if a.shards is None:   # device_count() does not initialise the GPU
         import torch
 
