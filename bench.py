@@ -27,6 +27,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import resource
 import statistics
 import sys
 import threading
@@ -477,7 +478,10 @@ def main() -> int:
                    "prefill_graph_replays": replays,
                    "prefill_graph_buckets": stats1["prefill_graph_buckets"],
                    "decode_tok_s_per_gpu": round(dtoks / elapsed, 1), "outcomes": counter["outcomes"],
-                   "dfa_states": stats1["dfa_states"], "timed_monotonic_ns": [mono0, mono1]},
+                   "dfa_states": stats1["dfa_states"], "timed_monotonic_ns": [mono0, mono1],
+                   "host_max_rss_gb": {"rank": round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20, 2),
+                                       "child_shards": round(resource.getrusage(resource.RUSAGE_CHILDREN).ru_maxrss
+                                                             / 2**20, 2)}},
     }
     if share:
         out["detail"]["shared_gpu_rehearsal"] = True
