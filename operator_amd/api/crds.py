@@ -178,9 +178,11 @@ def rbac(namespace: str = "podmortem-system", name: str = "podmortem-operator") 
 
 
 def deployment(namespace: str = "podmortem-system", image: str = "ghcr.io/podmortem/operator-amd:latest",
-               gpus: int = 1, name: str = "podmortem-operator", replicas: int = 1) -> list[dict]:
+               gpus: int = 1, name: str = "podmortem-operator", replicas: int = 1, shards: int = 1) -> list[dict]:
     """PVC + operator Deployment + Service. ``replicas`` > 1 turns on Lease leader
-    election (one active replica, the others warm standbys)."""
+    election (one active replica, the others warm standbys); ``shards`` > 1 runs that
+    many operator processes in the pod, splitting the pods between them, each with
+    its own engines on the pod's GPUs (``run --shards``)."""
     labels = {"app.kubernetes.io/name": name}
     env = [{"name": "PODMORTEM_PATTERNS__CACHE_DIR", "value": "/shared/patterns"},
            {"name": "HSA_ENABLE_IPC_MODE_LEGACY", "value": "0"}]
@@ -201,11 +203,13 @@ def deployment(namespace: str = "podmortem-system", image: str = "ghcr.io/podmor
                       "securityContext": {"runAsNonRoot": True, "runAsUser": 1001},
                       "containers": [{
                           "name": "operator", "image": image,
-                          "command": ["python", "-m", "operator_amd", "run", "--gpus", str(gpus)],
+                          "command": ["python", "-m", "operator_amd", "run", "--gpus", str(gpus)] +
+                                     (["--shards", str(shards)] if shards > 1 else []),
                           "env": env,
                           "ports": [{"containerPort": 8080, "name": "http"}],
-                          "resources": {"limits": {"amd.com/gpu": gpus, "memory": "64Gi"},
-                                        "requests": {"cpu": "4", "memory": "32Gi"}},
+                          "resources": {"limits": {"amd.com/gpu": gpus, "memory": f"{64 * max(1, shards)}Gi"},
+                                        "requests": {"cpu": str(4 * max(1, shards)),
+                                                     "memory": f"{32 * max(1, shards)}Gi"}},
                           "livenessProbe": probe("/q/health/live", 30),
                           "readinessProbe": probe("/q/health/ready", 30),
                           "volumeMounts": [{"name": "pattern-cache", "mountPath": "/shared/patterns"},

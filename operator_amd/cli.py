@@ -44,7 +44,7 @@ def cmd_manifests(args) -> int:
     from operator_amd.api.crds import render_all
 
     text = render_all(namespace=args.namespace, image=args.image, gpus=args.gpus, replicas=args.replicas,
-                      compat=args.compat_services)
+                      shards=args.shards, compat=args.compat_services)
     if args.out:
         with open(args.out, "w") as f:
             f.write(text)
@@ -117,6 +117,42 @@ def _build_services(s, metrics):
     return matcher, factory, explainer
 
 
+def shard_env(base: dict, index: int, count: int, health_port: int) -> dict:
+    """Environment of operator shard ``index`` of ``count`` started by ``run --shards``:
+    its slice of the pods and its own health/metrics port (applied over the config and
+    the --set overrides by ``apply_shard_env``)."""
+    env = dict(base)
+    env.update({"OAMD_SHARD_CHILD": "1", "OAMD_SHARD_INDEX": str(index), "OAMD_SHARD_COUNT": str(count),
+                "OAMD_SHARD_PORT": str(health_port + index)})
+    return env
+
+
+def apply_shard_env(s, env: dict) -> None:
+    if env.get("OAMD_SHARD_CHILD"):
+        s.operator.shard_index = int(env["OAMD_SHARD_INDEX"])
+        s.operator.shard_count = int(env["OAMD_SHARD_COUNT"])
+        s.health.port = int(env["OAMD_SHARD_PORT"])
+
+
+def _spawn_shards(args, s) -> list:
+    """``run --shards K``: K-1 more operator processes on the same GPUs (K engine sets
+    per GPU), started before this process touches a GPU. One operator's kernel stream
+    does not fill an MI355X: two out-of-phase shards per GPU measured 32.8 vs 28.1
+    analyses/s at a lower p50 (bench.py, profiles/bench_shards_8b.jsonl)."""
+    import subprocess
+
+    argv = [a for a in sys.argv[1:]]
+    return [subprocess.Popen([sys.executable, "-m", "operator_amd", *argv],
+                             env=shard_env(os.environ, i, args.shards, s.health.port))
+            for i in range(1, args.shards)]
+
+
+def shard_sizing(s, count: int) -> None:
+    """Per-shard engine sizing: the GPU's batch and KV budget split over the shards."""
+    s.engine.max_batch = max(1, s.engine.max_batch // count)
+    s.engine.kv_cache_gb = s.engine.kv_cache_gb / count
+
+
 def cmd_run(args) -> int:
     from operator_amd.controller.operator import Operator
     from operator_amd.kube.client import KubeClient
@@ -124,6 +160,13 @@ def cmd_run(args) -> int:
     from operator_amd.utils.metrics import Metrics
 
     s = _settings(args)
+    apply_shard_env(s, os.environ)
+    kids = []
+    if args.shards and args.shards > 1:   # shards of this process's GPUs (config-only sharding: one pod each)
+        if not os.environ.get("OAMD_SHARD_CHILD"):
+            kids = _spawn_shards(args, s)
+            s.operator.shard_count, s.operator.shard_index = args.shards, 0
+        shard_sizing(s, args.shards)
     if args.gpus and args.gpus > 1:
         s.engine.gpus = args.gpus
     if args.tp and args.tp > 1:
@@ -158,6 +201,10 @@ def cmd_run(args) -> int:
     op.stop()
     if pool is not None:
         pool.close()
+    for k in kids:   # the other shards stop with this one
+        k.terminate()
+    for k in kids:
+        k.wait(60)
     return 0
 
 
@@ -204,11 +251,15 @@ def main(argv: list[str] | None = None) -> int:
     p.add_argument("--gpus", type=int, default=0, help="engine processes, one per GPU (engine.gpus)")
     p.add_argument("--tp", type=int, default=0,
                    help="GPUs per explanation-model replica (engine.tp); --gpus 8 --tp 8 = one 70B replica")
+    p.add_argument("--shards", type=int, default=0,
+                   help="operator shards (processes splitting the pods, each with its own engines on the same "
+                        "GPUs); 2 fills an MI355X better than 1 (operator.shard_count)")
     p = sub.add_parser("manifests")
     p.add_argument("--namespace", default="podmortem-system")
     p.add_argument("--image", default="ghcr.io/podmortem/operator-amd:latest")
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--replicas", type=int, default=1, help=">1 enables Lease leader election")
+    p.add_argument("--shards", type=int, default=1, help="operator shards per pod (run --shards)")
     p.add_argument("--compat-services", action="store_true",
                    help="also emit log-parser / ai-interface Deployments+Services backed by serve-compat")
     p.add_argument("--out", default=None)

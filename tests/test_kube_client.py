@@ -1,6 +1,7 @@
 """The HTTPS kube client against the FakeKube REST server (wire level), the
 operator running over it end to end, the compat REST server, and the CLI."""
 import json
+import os
 import subprocess
 import sys
 import threading
@@ -188,3 +189,48 @@ def test_watch_bookmark_410_and_list_rv_over_http(server):
     with pytest.raises(WatchClosed) as e:
         next(iter(w2))
     assert e.value.code == 410 and e.value.expired
+
+
+def test_cli_run_with_two_shards_starts_and_stops_both(tmp_path):
+    """`run --shards 2`: a second operator process (shard 1, health port + 1) comes up
+    beside the first and goes away when the first is stopped."""
+    import signal
+    import socket
+    import time as _t
+    import urllib.request
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = dict(os.environ, PODMORTEM_LOG_LEVEL="WARNING")
+    p = subprocess.Popen([sys.executable, "-m", "operator_amd", "run", "--fake", "--shards", "2",
+                          "--set", f"health.port={port}", "--set", "health.host=127.0.0.1",
+                          "--set", "services.explain=echo", "--set", "services.match=cpu",
+                          "--set", f"patterns.cache_dir={tmp_path}"], env=env)
+    try:
+        def up(pt):
+            try:
+                return urllib.request.urlopen(f"http://127.0.0.1:{pt}/q/health/live", timeout=1).status == 200
+            except OSError:
+                return False
+        end = _t.time() + 90
+        while _t.time() < end and not (up(port) and up(port + 1)):
+            _t.sleep(0.2)
+        assert up(port) and up(port + 1)
+    finally:
+        p.send_signal(signal.SIGTERM)
+        assert p.wait(60) == 0
+    _t.sleep(0.5)
+    assert not up(port + 1)
+
+
+def test_shard_env_and_sizing():
+    from operator_amd.cli import apply_shard_env, shard_env, shard_sizing
+    from operator_amd.config import load_settings
+
+    env = shard_env({"X": "1"}, 1, 2, 8080)
+    s = load_settings(env={}, overrides={"health.port": 9999})
+    apply_shard_env(s, env)
+    assert (s.operator.shard_index, s.operator.shard_count, s.health.port) == (1, 2, 8081) and env["X"] == "1"
+    shard_sizing(s, 2)
+    assert s.engine.max_batch == 128 and s.engine.kv_cache_gb == 32.0
