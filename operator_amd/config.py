@@ -103,6 +103,8 @@ class EngineCfg(BaseModel):
     model: str = "llama3-8b"
     model_path: Optional[str] = None  # HF safetensors dir (its config.json wins over `model`); random init when absent
     chat_template: str = "auto"       # auto = the checkpoint's tokenizer_config.json template; none; a file; Jinja
+    extra_models: list[str] = []      # more local models on the same GPU(s): "preset" or "name=/hf/dir"; an
+                                      # AIProvider whose modelId names one is served by it (KV budget split)
     seed: int = 0
     dtype: str = "bfloat16"
     weight_dtype: str = "bfloat16"   # bfloat16 | fp8 (W8A8 e4m3fn projections, e.g. Llama-3-70B)

@@ -5,8 +5,9 @@ never written. Here the provider is validated against the on-node engine:
 
 * the referenced auth Secret (if any) must exist and contain the key;
 * the explain service must be ready (model weights loaded / engine loop alive);
-* ``modelId`` is informational (the local engine serves its configured model);
-  a mismatch is reported in the message, not treated as a failure;
+* ``modelId`` picks among the on-node models (``engine.model`` + ``engine.extra_models``);
+  one that is not served is mapped to the default model, reported in the message,
+  not treated as a failure;
 * a provider routed to an external API (``providerId`` openai / ollama, see
   engine/providers.py) is Ready when it names an ``apiUrl``.
 """
@@ -59,8 +60,11 @@ class AIProviderReconciler:
         else:
             phase = "Ready"
             mid = spec.get("modelId")
-            msg = f"Served by on-node engine ({self.engine_model})"
-            if mid and mid != self.engine_model:
+            served = list(getattr(getattr(self.explainer, "local", self.explainer), "models", None) or
+                          [self.engine_model])
+            hit = next((m for m in served if mid and m.lower() == mid.lower()), None)
+            msg = f"Served by on-node engine ({hit or self.engine_model})"
+            if mid and hit is None:
                 msg += f"; requested modelId {mid} is mapped to {self.engine_model}"
         return UpdateControl.patch_status({"phase": phase, "message": msg, "lastValidated": instant_str(),
                                            "observedGeneration": md.get("generation")})

@@ -12,6 +12,12 @@ from operator_amd.patterns.schema import PatternSet
 log = logging.getLogger(__name__)
 
 
+def parse_model_spec(spec: str) -> tuple[str, str | None]:
+    """``engine.extra_models`` entry -> (name, HF checkpoint dir or None)."""
+    name, _, path = spec.partition("=")
+    return name.strip(), (path.strip() or None)
+
+
 def build_llm(s: Settings, device: str | torch.device | None = None, tp=None):
     """(model, kv, LLMEngine, Tokenizer) for the configured explanation model."""
     from operator_amd.engine.llm import LLMEngine
@@ -74,10 +80,24 @@ def build_explain_service(s: Settings, metrics=None, tp=None):
                                          s.services.ai_interface_connect_timeout_s)
     from operator_amd.engine.explain import ExplainEngine
 
-    _, _, llm, tok = build_llm(s, tp=tp)
-    ee = ExplainEngine(llm, tok, model_id=s.engine.model, max_prompt_tokens=s.engine.max_prompt_tokens,
-                       ignore_eos=s.engine.ignore_eos)
-    return service.LocalExplainService(ee, metrics)
+    extra = [parse_model_spec(x) for x in s.engine.extra_models] if (tp is None or tp.world == 1) else []
+    if not extra:
+        _, _, llm, tok = build_llm(s, tp=tp)
+        ee = ExplainEngine(llm, tok, model_id=s.engine.model, max_prompt_tokens=s.engine.max_prompt_tokens,
+                           ignore_eos=s.engine.ignore_eos)
+        return service.LocalExplainService(ee, metrics)
+    # several local models: each its own engine (weights, paged KV cache, graphs, loop
+    # thread) with an equal share of the KV budget; AIProviders pick one by modelId
+    services = {}
+    for name, path in [(s.engine.model, s.engine.model_path)] + extra:
+        sm = s.model_copy(deep=True)
+        sm.engine.model, sm.engine.model_path = name, path
+        sm.engine.kv_cache_gb = s.engine.kv_cache_gb / (1 + len(extra))
+        _, _, llm, tok = build_llm(sm, tp=tp)
+        ee = ExplainEngine(llm, tok, model_id=name, max_prompt_tokens=s.engine.max_prompt_tokens,
+                           ignore_eos=s.engine.ignore_eos)
+        services[name] = service.LocalExplainService(ee, metrics)
+    return service.MultiModelExplainService(services, default=s.engine.model)
 
 
 def build_match_engine(s: Settings, patterns: PatternSet, device: str | None = None):

@@ -137,6 +137,48 @@ class LocalExplainService:
         return self.ee.loop.is_alive() and self.ee.loop.error is None
 
 
+class MultiModelExplainService:
+    """Several on-node models behind one explain service (``engine.extra_models``): a
+    request goes to the engine serving ``AIProviderConfig.model_id`` (case-insensitive),
+    anything else to the default model — the reference forwards ``spec.modelId`` to its
+    ai-interface, which picks the model (J/service/AIInterfaceClient.java:76-84)."""
+
+    def __init__(self, services: dict, default: str):
+        if default not in services:
+            raise ValueError(f"default model {default!r} is not served")
+        self.services, self.default = dict(services), default
+        self._by_lower = {k.lower(): v for k, v in services.items()}
+        self.ee = services[default].ee      # the default model's engine (stats, health)
+
+    @property
+    def models(self) -> list[str]:
+        return list(self.services)
+
+    def pick(self, cfg: AIProviderConfig):
+        return self._by_lower.get((cfg.model_id or "").lower(), self.services[self.default])
+
+    def explain(self, result: AnalysisResult, cfg: AIProviderConfig) -> AIResponse:
+        return self.pick(cfg).explain(result, cfg)
+
+    def explain_many(self, items):
+        out = [None] * len(items)
+        groups: dict[int, tuple] = {}
+        for i, (r, c) in enumerate(items):
+            svc = self.pick(c)
+            groups.setdefault(id(svc), (svc, []))[1].append(i)
+        for svc, idx in groups.values():   # one continuous batch per model
+            for i, res in zip(idx, svc.explain_many([items[i] for i in idx])):
+                out[i] = res
+        return out
+
+    def ready(self) -> bool:
+        return all(getattr(v, "ready", lambda: True)() for v in self.services.values())
+
+    def close(self) -> None:
+        for v in self.services.values():
+            v.ee.close()
+
+
 class EchoExplainService:
     """Deterministic stand-in for the ai-interface (no model): renders a short
     Root Cause / Evidence / Fix text from the pattern result."""

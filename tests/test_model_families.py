@@ -175,3 +175,42 @@ def test_checkpoint_tokenizer_single_bos_and_chat_template(tmp_path):
     assert tc.encode("pod failed") == [0, vocab["<|user|>"], vocab["pod"], vocab["failed"], vocab["<|assistant|>"]]
     with pytest.raises(Exception):
         Tokenizer(100, 0, 1, path=str(f), chat_template="{{ raise_exception('no system role') }}").encode("x")
+
+
+def test_several_local_models_routed_by_model_id(tmp_path):
+    """engine.extra_models: each local model its own engine; an AIProvider's modelId
+    picks it (case-insensitive), anything else goes to engine.model; the AIProvider
+    controller reports which engine serves the provider."""
+    from operator_amd.api.models import AIProviderConfig, AnalysisResult, AnalysisSummary
+    from operator_amd.controller.aiprovider import AIProviderReconciler
+    from operator_amd.engine.factory import build_explain_service
+    from operator_amd.engine.providers import ProviderRouter
+    from operator_amd.kube.fake import FakeKube
+
+    s = load_settings(env={}, overrides={"engine.model": "tiny", "engine.extra_models": ["tiny-gqa4"],
+                                         "engine.device": "cpu", "engine.dtype": "float32",
+                                         "engine.kv_cache_gb": 0.04, "engine.use_graphs": False,
+                                         "engine.max_batch": 4, "engine.max_context": 512})
+    svc = build_explain_service(s)
+    try:
+        assert svc.models == ["tiny", "tiny-gqa4"]
+        res = AnalysisResult(pod_name="p", pod_namespace="default",
+                             summary=AnalysisSummary(highest_severity="HIGH", significant_events=1))
+        st = {m: svc.services[m].ee.llm.stats for m in svc.models}
+        before = {m: st[m].decode_tokens for m in svc.models}
+        svc.explain(res, AIProviderConfig(model_id="TINY-GQA4", max_tokens=5, caching_enabled=False))
+        assert st["tiny-gqa4"].decode_tokens > before["tiny-gqa4"] and st["tiny"].decode_tokens == before["tiny"]
+        svc.explain(res, AIProviderConfig(model_id="gpt-4o", max_tokens=5, caching_enabled=False))
+        assert st["tiny"].decode_tokens > before["tiny"]   # unknown model -> the default engine
+        out = svc.explain_many([(res, AIProviderConfig(model_id=m, max_tokens=3, caching_enabled=False))
+                                for m in ("tiny", "tiny-gqa4", "tiny")])
+        assert [o.tokens_generated for o in out] == [3, 3, 3]
+        rec = AIProviderReconciler(FakeKube(), ProviderRouter(svc), "tiny")
+        msg = rec.reconcile({"metadata": {"name": "a", "namespace": "default"},
+                             "spec": {"providerId": "local", "modelId": "tiny-gqa4"}}).status["message"]
+        assert msg == "Served by on-node engine (tiny-gqa4)"
+        msg = rec.reconcile({"metadata": {"name": "b", "namespace": "default"},
+                             "spec": {"providerId": "local", "modelId": "other"}}).status["message"]
+        assert msg.endswith("requested modelId other is mapped to tiny")
+    finally:
+        svc.close()
