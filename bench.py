@@ -129,8 +129,8 @@ def main() -> int:
     a.max_batch = max(1, a.max_batch // a.shards)
     # host thread pools sized to this rank's share of the node (N ranks on one host):
     # the tokenizer's Rust pool and torch's intra-op pool default to every CPU each
-    share_cpus = max(2, min(16, (os.cpu_count() or 16) // max(1, int(os.environ.get("LOCAL_WORLD_SIZE",
-                                                                                    os.environ.get("WORLD_SIZE", "1"))))))
+    procs_on_host = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))) * a.shards
+    share_cpus = max(2, min(16, (os.cpu_count() or 16) // procs_on_host))
     os.environ.setdefault("RAYON_RS_NUM_CPUS", str(share_cpus))
     import torch
 
