@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--sync-start", type=int, default=0,
                     help="N processes run together: each waits at a file barrier under /tmp before timing")
     ap.add_argument("--only-alone", action="store_true")
+    ap.add_argument("--order", default="py,c", help="arm order of the alone runs")
     a = ap.parse_args()
     cfg = get_config("llama3-8b")
     m = LlamaModel(cfg, device="cuda").init_random(0)
@@ -58,12 +59,16 @@ def main():
                 g.st.step.zero_()
             g.graph.replay()
 
-    def c_replays(n):
+    def c_replays(n, chunk=None):
         done = 0
         while done < n:
             k = min(eng.multi_step, n - done)
             g.st.step.zero_()
-            C.graph_launch(g.graph.raw_cuda_graph_exec(), k, stream)
+            if chunk is None:
+                C.graph_launch(g.graph.raw_cuda_graph_exec(), k, stream)
+            else:
+                for j in range(0, k, chunk):
+                    C.graph_launch(g.graph.raw_cuda_graph_exec(), min(chunk, k - j), stream)
             done += k
 
     def timed(fn):
@@ -98,8 +103,16 @@ def main():
         out["together_c_ms"] = round((time.perf_counter() - t0) * 1e3 / (a.steps * 2), 3)
         print(json.dumps(out), flush=True)
         return
-    out["alone_py_ms"] = round(timed(py_replays), 3)
-    out["alone_c_ms"] = round(timed(c_replays), 3)
+    for arm in a.order.split(","):
+        if arm == "py":
+            out["alone_py_ms"] = round(timed(py_replays), 3)
+        elif arm == "c":
+            out["alone_c_ms"] = round(timed(c_replays), 3)
+        elif arm == "c1":
+            out["alone_c1_ms"] = round(timed(lambda n: c_replays(n, 1)), 3)
+    if a.only_alone:
+        print(json.dumps(out), flush=True)
+        return
     th = [threading.Thread(target=spin, daemon=True) for _ in range(4)]
     for t in th:
         t.start()
