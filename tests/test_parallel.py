@@ -136,10 +136,12 @@ def test_oneshot_disabled_without_gpu():
     assert g.all_reduce_(t) is t
 
 
-def test_bench_two_ranks_gloo():
+@pytest.mark.parametrize("shards", [1, 2])
+def test_bench_two_ranks_gloo(shards):
     """bench.py as the driver launches it for N > 1 (torch.distributed.run, one rank per
     device, 127.0.0.1 rendezvous), on the CPU tier with gloo and a tiny model: rank 0
-    prints exactly one JSON line with whole-job numbers."""
+    prints exactly one JSON line with whole-job numbers; with 2 operator shards per
+    rank (a child process each) the counts cover both shards."""
     import json
     import subprocess
     import sys
@@ -147,12 +149,13 @@ def test_bench_two_ranks_gloo():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
-           "--gpus", "2", "--steps", "2", "--warmup", "1", "--model", "tiny", "--batch", "3", "--max-tokens", "4",
-           "--prompt-tokens", "128", "--log-kb", "4", "--patterns", "40"]
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--model", "tiny", "--batch", str(3 * shards),
+           "--max-tokens", "4", "--prompt-tokens", "128", "--log-kb", "4", "--patterns", "40", "--shards", str(shards)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=root)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, r.stdout
     out = json.loads(lines[0])
-    assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 6 and out["config"]["parallelism"] == "dp2"
-    assert out["detail"]["outcomes"] == {"ai-complete": 6} and out["value"] > 0
+    assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 6 * shards and out["config"]["parallelism"] == "dp2"
+    assert out["config"]["operator_shards_per_gpu"] == shards
+    assert out["detail"]["outcomes"] == {"ai-complete": 6 * shards} and out["value"] > 0
