@@ -71,16 +71,19 @@ def test_llama3_8b_architecture_smoke():
         assert len(r.output) == 6 and all(0 <= t < cfg.vocab_size for t in r.output)
 
 
-def test_pipelined_windows_eos_and_arrivals():
+@pytest.mark.parametrize("phase_streams", [False, True])
+def test_pipelined_windows_eos_and_arrivals(phase_streams):
     """Pipelined multi-step decode windows (graphs) must produce exactly the eager
     engine's tokens with staggered lengths, EOS inside a window and requests that
-    arrive while others decode."""
+    arrive while others decode — also with prefill / decode on their own priority
+    streams (engine.phase_streams)."""
     cfg = get_config("tiny-gqa4")
     m = LlamaModel(cfg, device="cuda").init_random(seed=6)
 
     def run(graphs, eos):
         kv = PagedKVCache(cfg.layers, 256, cfg.kv_heads, 128, 16, device="cuda")
-        eng = LLMEngine(m, kv, max_batch=8, max_context=1024, use_graphs=graphs, multi_step=4)
+        eng = LLMEngine(m, kv, max_batch=8, max_context=1024, use_graphs=graphs, multi_step=4,
+                        phase_streams=phase_streams and graphs)
         if eos is not None:
             eng.eos = {eos}
         first = [GenRequest(list(range(3, 3 + n)), max_tokens=mt, temperature=0.8, seed=s)
