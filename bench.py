@@ -70,6 +70,7 @@ def parse_args():
                          "pods per step on its own closed loop; the rank process runs shard 0 and starts the "
                          "others as child processes")
     ap.add_argument("--shard-index", type=int, default=None, help=argparse.SUPPRESS)  # internal: child shard
+    ap.add_argument("--multi-step", type=int, default=8, help="decode steps per graph window (engine.multi_step)")
     ap.add_argument("--phase-streams", action="store_true",
                     help="prefill on a normal-priority, decode on a high-priority HIP stream (engine.phase_streams)")
     ap.add_argument("--json-out", default=None)
@@ -161,6 +162,7 @@ def main() -> int:
             "engine.max_context": a.prompt_tokens + a.max_tokens + 64, "engine.max_prompt_tokens": a.prompt_tokens,
             "engine.kv_cache_gb": kv, "engine.kv_dtype": a.kv_dtype, "engine.use_graphs": not a.no_graphs,
             "engine.ignore_eos": True, "engine.phase_streams": a.phase_streams,
+            "engine.multi_step": a.multi_step,
             "engine.seed": 0, "health.enabled": False, "operator.workers": 2 * a.batch + 16, "operator.io_workers": 16,
             "patterns.cache_dir": f"/tmp/oamd-bench-{os.getpid()}", "services.match_max_batch": 64,
             "services.match_batch_wait_ms": 5.0})
