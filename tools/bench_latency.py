@@ -38,6 +38,11 @@ def main() -> int:
     ap.add_argument("--log-kb", type=int, default=64)
     ap.add_argument("--patterns", type=int, default=1000)
     ap.add_argument("--max-batch", type=int, default=256)
+    ap.add_argument("--kv-gb", type=float, default=96.0)
+    ap.add_argument("--seed", type=int, default=5, help="arrival process seed (one per shard)")
+    ap.add_argument("--dump-lat", default=None, help="write each rate's raw latencies (s) to this JSON file")
+    ap.add_argument("--start-at", type=float, default=0.0,
+                    help="time.time() to start the first rate at (aligns shard processes)")
     a = ap.parse_args()
 
     import torch
@@ -56,7 +61,7 @@ def main() -> int:
     s = load_settings(env={}, overrides={
         "engine.model": a.model, "engine.device": dev, "engine.max_batch": a.max_batch,
         "engine.max_context": a.prompt_tokens + a.max_tokens + 64, "engine.max_prompt_tokens": a.prompt_tokens,
-        "engine.kv_cache_gb": 96.0 if dev != "cpu" else 1.0, "engine.ignore_eos": True, "health.enabled": False,
+        "engine.kv_cache_gb": a.kv_gb if dev != "cpu" else 1.0, "engine.ignore_eos": True, "health.enabled": False,
         "operator.workers": 512, "operator.io_workers": 16, "patterns.cache_dir": f"/tmp/oamd-lat-{os.getpid()}"})
     meng = MatchEngine(synthetic_library(a.patterns, seed=0), device=dev, seg_bytes=s.patterns.seg_bytes)
     model, kv, llm, tok = build_llm(s, device=dev)
@@ -84,8 +89,11 @@ def main() -> int:
     while not op.monitors.list():
         time.sleep(0.01)
     pool = LogFactory(n_patterns=a.patterns, seed=7).batch(256, a.log_kb * 1024, n_failures=3, seed=11)[0]
-    rng = random.Random(5)
+    rng = random.Random(a.seed)
     seq = [0]
+    dump = {}
+    if a.start_at:
+        time.sleep(max(0.0, a.start_at - time.time()))
 
     def inject(prefix: str) -> str:
         i = seq[0]
@@ -125,6 +133,7 @@ def main() -> int:
         with lock:
             lat = [done[n] - t_inject[n] for n in names if n in done]
             span = (max(done[n] for n in names if n in done) - min(t_inject[n] for n in names)) if lat else 0
+        dump[f"{rate:g}"] = {"lat": lat, "span": span}
         print(json.dumps({"bench": "open-loop latency", "model": a.model, "offered_rate": rate,
                           "failures": len(names), "completed": len(lat),
                           "analyses_per_s": round(len(lat) / span, 2) if span > 0 else None,
@@ -135,6 +144,9 @@ def main() -> int:
         op.drain(120)
     op.stop()
     ee.close()
+    if a.dump_lat:
+        with open(a.dump_lat, "w") as f:
+            json.dump(dump, f)
     return 0
 
 
