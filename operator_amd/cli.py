@@ -129,12 +129,6 @@ def shard_env(base: dict, index: int, count: int, health_port: int) -> dict:
 
 def apply_shard_env(s, env: dict) -> None:
     if env.get("OAMD_SHARD_CHILD"):
-        try:   # a shard started by `run --shards` exits with the process that started it
-            import ctypes
-
-            ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, int(signal.SIGTERM))   # PR_SET_PDEATHSIG
-        except OSError:
-            pass
         s.operator.shard_index = int(env["OAMD_SHARD_INDEX"])
         s.operator.shard_count = int(env["OAMD_SHARD_COUNT"])
         s.health.port = int(env["OAMD_SHARD_PORT"])
@@ -167,6 +161,13 @@ def cmd_run(args) -> int:
 
     s = _settings(args)
     apply_shard_env(s, os.environ)
+    if os.environ.get("OAMD_SHARD_CHILD"):
+        try:   # a shard started by `run --shards` exits with the process that started it
+            import ctypes
+
+            ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, int(signal.SIGTERM))   # PR_SET_PDEATHSIG
+        except OSError:
+            pass
     kids = []
     if args.shards and args.shards > 1:   # shards of this process's GPUs (config-only sharding: one pod each)
         if not os.environ.get("OAMD_SHARD_CHILD"):
