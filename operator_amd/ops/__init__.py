@@ -103,7 +103,7 @@ def gate_up_silu(x: torch.Tensor, wgu: torch.Tensor, block: int | None) -> torch
             and K % 64 == 0 and x.is_contiguous() and wgu.is_contiguous()):
         t = _gemm_table_get().get(("silu", M, N, K))
         if t != "blas":
-            bm = t[0] if t else min(M, 256)
+            bm = t[0] if t else row_tile(M)
             ns = t[1] if t and len(t) > 1 else 3
             y = torch.empty(M, N // 2, dtype=x.dtype, device=x.device)
             kernels().gemm_decode(x, wgu, y, None, 1, 128, bm, True, False, ns)
@@ -240,6 +240,12 @@ def _gemm_table_get() -> dict:
     return _gemm_table
 
 
+def row_tile(M: int) -> int:
+    """Largest gemm_decode row tile (256, 128, 64) dividing M (M % 64 == 0): a bucket of
+    192 rows runs three 64-row tiles, not one 192-row tile the kernel has no variant for."""
+    return next(b for b in (256, 128, 64) if M % b == 0)
+
+
 def gemm_splits(M: int, N: int, K: int) -> int:
     """Heuristic split-K ways for gemm_decode (shapes not in the tuned table): the
     smallest S | 8 whose (N/64) x S blocks reach one block per CU (256)."""
@@ -263,7 +269,7 @@ def gemm_plan(M: int, N: int, K: int):
         return None
     if t is not None:
         return tuple(t)
-    return (min(M, 256), 64, gemm_splits(M, N, K))
+    return (row_tile(M), 64, gemm_splits(M, N, K))
 
 
 SKINNY_MAX_M = 32
@@ -310,8 +316,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None, sp
             return y
     if x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous():
         plan = gemm_plan(M, N, K)
-        if plan is None and (splits or bn or bm) and M % 64 == 0 and N % 64 == 0 and K % 64 == 0:
-            plan = (min(M, 256), 64, 1)  # explicit request (tests / tuning)
+        if plan is None and (splits or bn or bm) and M % 64 == 0 and M <= 256 and N % 64 == 0 and K % 64 == 0:
+            plan = (row_tile(M), 64, 1)  # explicit request (tests / tuning)
     if plan is None:
         return F.linear(x, w, out=out) if out is not None else F.linear(x, w)
     bm, bn, S = bm or plan[0], bn or plan[1], splits or plan[2]

@@ -148,7 +148,7 @@ def test_sample(dtype):
     assert torch.equal(ops.sample(logits, temp, seeds, pos).cpu(), tok)
 
 
-@pytest.mark.parametrize("M", [64, 128, 256])
+@pytest.mark.parametrize("M", [64, 128, 192, 256])
 @pytest.mark.parametrize("N,K", [(256, 512), (640, 2048), (128, 4096)])
 def test_gemm_decode(M, N, K):
     torch.manual_seed(7)
@@ -158,7 +158,7 @@ def test_gemm_decode(M, N, K):
     for bm in (64, 128, 256):
         for bn in (64, 128):
             for S in (1, 2, 4, 8):
-                if bm > M or K % (64 * S) or N % bn:
+                if M % bm or K % (64 * S) or N % bn:
                     continue
                 for ns in ((2, 3, 4) if bm <= 128 else (3, 4) if bm + bn <= 320 else (3,)):
                     y = ops.linear(x, w, splits=S, bn=bn, bm=bm, stages=ns)
@@ -193,7 +193,7 @@ def test_gemm_skinny(M, N, K):
     torch.testing.assert_close(ops.linear(x, w).float(), ref_, atol=2e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("M", [64, 128, 256, 40, 1, 7, 16, 32])
+@pytest.mark.parametrize("M", [64, 128, 192, 256, 40, 1, 7, 16, 32])
 def test_gate_up_silu_fused(M):
     torch.manual_seed(8)
     K, inter = 1024, 640

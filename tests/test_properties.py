@@ -204,3 +204,21 @@ def test_status_ring_newest_first_capped(_fk_status, n):
     assert len(ring) <= MAX_RECENT_FAILURES
     want = list(reversed(names))[:MAX_RECENT_FAILURES]
     assert [r["podName"] for r in ring][:len(want)] == want[:len(ring)]
+
+
+@settings(max_examples=200, deadline=None)
+@given(st.integers(1, 8).map(lambda m: 32 * m), st.sampled_from([128, 512, 1024, 6144, 14336, 28672]),
+       st.sampled_from([512, 1024, 4096, 14336]))
+def test_gemm_plans_are_launchable(M, N, K):
+    """Every gemm_decode plan satisfies the binding's launch checks: the row tile is
+    a kernel variant dividing M (a 192-row decode bucket included) and the split
+    count divides K in 64-column steps."""
+    from operator_amd import ops
+
+    p = ops.gemm_plan(M, N, K)
+    if p is None:
+        return
+    bm, bn, S = p[0], p[1], p[2]
+    assert bm in (64, 128, 256) and M % bm == 0
+    assert bn in (64, 128) and N % bn == 0
+    assert S >= 1 and K % (64 * S) == 0
