@@ -122,6 +122,7 @@ class FailureDeduper:
             if ftime is not None:
                 v = self._d.get(k)
                 if v is not None and v[0] == ftime and self.clock() - v[1] <= self.ttl_s:
+                    self._d.move_to_end(k)   # LRU: a repeat event keeps the entry recent (TTL unchanged)
                     return False
                 self._d[k] = (ftime, self.clock())
                 self._d.move_to_end(k)
