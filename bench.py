@@ -88,7 +88,7 @@ def spawn_shards(a) -> list:
     kids = []
     for i in range(1, a.shards):
         env = dict(os.environ)
-        env.update(OAMD_BENCH_RANK=os.environ.get("RANK", "0"),
+        env.update(OAMD_BENCH_RANK=os.environ.get("RANK", "0"), OAMD_BENCH_WORLD=os.environ.get("WORLD_SIZE", "1"),
                    OAMD_BENCH_LOCAL=os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0")),
                    WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
         kids.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), *sys.argv[1:],
@@ -154,8 +154,9 @@ def main() -> int:
     from operator_amd.patterns.synth import LogFactory, synthetic_library
 
     def settings(dev: str, max_batch: int, world_: int):
-        kv = a.kv_gb or (1.0 if dev == "cpu" else (96.0 if not share else max(8.0, 200.0 / world_ - 16)) / procs
-                         / a.shards)
+        on_gpu = procs * a.shards * (world_ if share else 1)   # operator / engine processes on this GPU
+        # each holds 16 GB of weights and up to ~8 GB of prefill workspace beside its KV
+        kv = a.kv_gb or (1.0 if dev == "cpu" else 96.0 / on_gpu if not share else max(8.0, 240.0 / on_gpu - 24))
         return load_settings(env={}, overrides={
             "engine.model": a.model, "engine.device": dev, "engine.max_batch": max_batch,
             "engine.max_prefill_tokens": a.prefill_tokens,
@@ -198,7 +199,7 @@ def main() -> int:
     from operator_amd.kube.resources import AIPROVIDERS, PODMORTEMS, PODS
     from operator_amd.utils.tracing import trace_range
 
-    s = settings(dev, a.max_batch, world)
+    s = settings(dev, a.max_batch, int(os.environ.get("OAMD_BENCH_WORLD", world)) if child else world)
 
     def note(msg: str) -> None:   # stage progress on stderr (the JSON line stays alone on stdout)
         tag = f"rank {rank}" + (f" shard {shard}" if a.shards > 1 else "")
