@@ -16,6 +16,7 @@ import os
 import signal
 import sys
 import threading
+import time
 
 
 def _settings(args):
@@ -134,17 +135,54 @@ def apply_shard_env(s, env: dict) -> None:
         s.health.port = int(env["OAMD_SHARD_PORT"])
 
 
-def _spawn_shards(args, s) -> list:
+class ShardSupervisor:
     """``run --shards K``: K-1 more operator processes on the same GPUs (K engine sets
     per GPU), started before this process touches a GPU. One operator's kernel stream
     does not fill an MI355X: two out-of-phase shards per GPU measured 32.8 vs 28.1
-    analyses/s at a lower p50 (bench.py, profiles/bench_shards_8b.jsonl)."""
-    import subprocess
+    analyses/s at a lower p50 (bench.py, profiles/bench_shards_8b.jsonl).
 
-    argv = [a for a in sys.argv[1:]]
-    return [subprocess.Popen([sys.executable, "-m", "operator_amd", *argv],
-                             env=shard_env(os.environ, i, args.shards, s.health.port))
-            for i in range(1, args.shards)]
+    A shard that exits is started again (its slice of the pods would otherwise go
+    unanalysed); more than ``max_restarts`` restarts within ``window_s`` makes
+    ``poll`` return False so the whole pod fails and Kubernetes restarts it."""
+
+    def __init__(self, argv: list[str], count: int, health_port: int, max_restarts: int = 5,
+                 window_s: float = 300.0, clock=time.monotonic):
+        self.argv, self.count, self.health_port = list(argv), count, health_port
+        self.max_restarts, self.window_s, self.clock = max_restarts, window_s, clock
+        self.restarts: list[float] = []
+        self.kids = {i: self._start(i) for i in range(1, count)}
+
+    def _start(self, index: int):
+        import subprocess
+
+        return subprocess.Popen([sys.executable, "-m", "operator_amd", *self.argv],
+                                env=shard_env(os.environ, index, self.count, self.health_port))
+
+    def poll(self) -> bool:
+        """Restart exited shards; False once they crash-loop."""
+        for i, k in list(self.kids.items()):
+            rc = k.poll()
+            if rc is None:
+                continue
+            now = self.clock()
+            self.restarts = [t for t in self.restarts if now - t < self.window_s] + [now]
+            if len(self.restarts) > self.max_restarts:
+                logging.getLogger(__name__).error("operator shard %d exited (code %s): %d restarts in %.0f s, "
+                                                  "giving up", i, rc, len(self.restarts) - 1, self.window_s)
+                return False
+            logging.getLogger(__name__).error("operator shard %d exited (code %s); starting it again", i, rc)
+            self.kids[i] = self._start(i)
+        return True
+
+    def stop(self, timeout_s: float = 60.0) -> None:
+        for k in self.kids.values():
+            if k.poll() is None:
+                k.terminate()
+        for k in self.kids.values():
+            try:
+                k.wait(timeout_s)
+            except Exception:  # noqa: BLE001 - a shard that ignores SIGTERM is killed
+                k.kill()
 
 
 def shard_sizing(s, count: int) -> None:
@@ -168,10 +206,10 @@ def cmd_run(args) -> int:
             ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, int(signal.SIGTERM))   # PR_SET_PDEATHSIG
         except OSError:
             pass
-    kids = []
+    sup = None
     if args.shards and args.shards > 1:   # shards of this process's GPUs (config-only sharding: one pod each)
         if not os.environ.get("OAMD_SHARD_CHILD"):
-            kids = _spawn_shards(args, s)
+            sup = ShardSupervisor(sys.argv[1:], args.shards, s.health.port)
             s.operator.shard_count, s.operator.shard_index = args.shards, 0
         shard_sizing(s, args.shards)
     if args.gpus and args.gpus > 1:
@@ -204,15 +242,17 @@ def cmd_run(args) -> int:
     signal.signal(signal.SIGTERM, lambda *_: stop.set())
     signal.signal(signal.SIGINT, lambda *_: stop.set())
     logging.getLogger(__name__).info("running; health on :%d", s.health.port)
-    stop.wait()
+    rc = 0
+    while not stop.wait(1.0):
+        if sup is not None and not sup.poll():
+            rc = 1
+            break
     op.stop()
     if pool is not None:
         pool.close()
-    for k in kids:   # the other shards stop with this one
-        k.terminate()
-    for k in kids:
-        k.wait(60)
-    return 0
+    if sup is not None:   # the other shards stop with this one
+        sup.stop()
+    return rc
 
 
 def cmd_serve_compat(args) -> int:

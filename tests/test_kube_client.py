@@ -193,7 +193,8 @@ def test_watch_bookmark_410_and_list_rv_over_http(server):
 
 def test_cli_run_with_two_shards_starts_and_stops_both(tmp_path):
     """`run --shards 2`: a second operator process (shard 1, health port + 1) comes up
-    beside the first and goes away when the first is stopped."""
+    beside the first, is started again when it dies, and goes away when the first is
+    stopped."""
     import signal
     import socket
     import time as _t
@@ -217,6 +218,18 @@ def test_cli_run_with_two_shards_starts_and_stops_both(tmp_path):
         while _t.time() < end and not (up(port) and up(port + 1)):
             _t.sleep(0.2)
         assert up(port) and up(port + 1)
+        # the shard process dies: the first one starts it again
+        import psutil
+
+        kids = psutil.Process(p.pid).children()
+        assert len(kids) == 1
+        kids[0].kill()
+        kids[0].wait(30)
+        end = _t.time() + 90
+        while _t.time() < end and not (up(port + 1) and psutil.Process(p.pid).children()):
+            _t.sleep(0.2)
+        again = psutil.Process(p.pid).children()
+        assert up(port + 1) and len(again) == 1 and again[0].pid != kids[0].pid
     finally:
         p.send_signal(signal.SIGTERM)
         assert p.wait(60) == 0
@@ -234,3 +247,23 @@ def test_shard_env_and_sizing():
     assert (s.operator.shard_index, s.operator.shard_count, s.health.port) == (1, 2, 8081) and env["X"] == "1"
     shard_sizing(s, 2)
     assert s.engine.max_batch == 128 and s.engine.kv_cache_gb == 32.0
+
+
+def test_shard_supervisor_restarts_then_gives_up(monkeypatch):
+    """A shard that exits is started again; more than max_restarts exits within the
+    window make poll() False (the pod fails and is restarted by Kubernetes)."""
+    from operator_amd import cli
+
+    class Dead:
+        def poll(self):
+            return 1
+
+    started = []
+    monkeypatch.setattr(cli.ShardSupervisor, "_start", lambda self, i: started.append(i) or Dead())
+    now = [0.0]
+    sup = cli.ShardSupervisor(["run"], 3, 8080, max_restarts=3, window_s=100.0, clock=lambda: now[0])
+    assert started == [1, 2]
+    assert sup.poll()              # restarts 1 and 2 (two restarts)
+    now[0] = 200.0                 # the earlier restarts leave the window
+    assert sup.poll()              # two more, two within the window
+    assert sup.poll() is False     # the fifth exit is the fourth within the window
