@@ -246,9 +246,13 @@ int gemm_decode(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, in
     switch (BM) {
       case 64:
         if (stages == 2) gemm_tn_kernel<64, 128, kEpiSiluGU, 2><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, 1, w_tiled);
+        else if (stages == 4) gemm_tn_kernel<64, 128, kEpiSiluGU, 4><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, 1, w_tiled);
         else gemm_tn_kernel<64, 128, kEpiSiluGU><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, 1, w_tiled);
         break;
-      case 128: gemm_tn_kernel<128, 128, kEpiSiluGU><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, 1, w_tiled); break;
+      case 128:
+        if (stages == 4) gemm_tn_kernel<128, 128, kEpiSiluGU, 4><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, 1, w_tiled);
+        else gemm_tn_kernel<128, 128, kEpiSiluGU><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, 1, w_tiled);
+        break;
       default: gemm_tn_kernel<256, 128, kEpiSiluGU><<<grid, kWaves * 64, 0, stream>>>(X, W, Y, P, M, N, K, 1, w_tiled); break;
     }
     OAMD_LAUNCH_CHECK();

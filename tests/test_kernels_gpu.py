@@ -208,6 +208,14 @@ def test_gate_up_silu_fused(M):
     # the unfused path over the same interleaved layout agrees
     un = ops.silu_mul(torch.nn.functional.linear(x, wgu), block=ops.GU_BLOCK)
     torch.testing.assert_close(un.float(), ref_.float(), atol=2e-2, rtol=2e-2)
+    if M in (64, 128, 256):   # every LDS ring depth of the fused kernel
+        for bm in (64, 128, 256):
+            for ns in (2, 3, 4):
+                if bm > M or M % bm or (ns == 2 and bm != 64) or (ns == 4 and bm == 256):
+                    continue
+                y = torch.empty(M, inter, dtype=x.dtype, device=x.device)
+                ops.kernels().gemm_decode(x, wgu, y, None, 1, 128, bm, True, False, ns)
+                torch.testing.assert_close(y.float(), ref_.float(), atol=2e-2, rtol=2e-2, msg=f"bm={bm} ns={ns}")
 
 
 def test_quantize_fp8_matches_torch():

@@ -24,6 +24,7 @@ ap.add_argument("--write-table", default=None, help="write the best (bm, bn, spl
 ap.add_argument("--tp", type=int, default=1, help="also cover the TP-sharded shapes of this degree")
 ap.add_argument("--fp8", action="store_true", help="also time the W8A8 e4m3fn gemm_fp8 path")
 ap.add_argument("--model", default="8b", choices=["8b", "70b"])
+ap.add_argument("--shapes", default=None, help="comma list of projections to time (default: all)")
 a = ap.parse_args()
 shapes = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336),
           "lm_head": (128256, 4096)}
@@ -34,6 +35,8 @@ if a.tp > 1:
     t = a.tp
     shapes = {f"{k}_tp{t}": ((n // t, kk) if k in ("qkv", "gate_up", "lm_head") else (n, kk // t))
               for k, (n, kk) in shapes.items()}
+if a.shapes:
+    shapes = {k: v for k, v in shapes.items() if k.split("_tp")[0] in a.shapes.split(",")}
 table = {}
 if a.tune:
     import torch.cuda.tunable as tun
@@ -124,7 +127,7 @@ for M in [int(x) for x in a.m.split(",")]:
         res = {"blas+silu": timeit(lambda w: ops.silu_mul(F.linear(x, w), block=64), ws["gate_up"])}
         yo = torch.empty(M, N // 2, device="cuda", dtype=torch.bfloat16)
         for bm in (64, 128, 256):
-            for ns in ((2, 3) if bm == 64 else (3,)):
+            for ns in ((2, 3, 4) if bm == 64 else (3, 4) if bm == 128 else (3,)):
                 if bm <= M:
                     res[f"fused_m{bm}x{ns}"] = timeit(
                         lambda w: ops.kernels().gemm_decode(x, w, yo, None, 1, 128, bm, True, False, ns), ws["gate_up"])
