@@ -7,7 +7,7 @@ import glob
 import json
 
 ap = argparse.ArgumentParser()
-ap.add_argument("dirs", nargs="+")
+ap.add_argument("dirs", nargs="+", help="rocprofv3 output dirs or kernel_trace.csv files, one per process")
 ap.add_argument("--window-json", required=True)
 ap.add_argument("--top", type=int, default=14)
 a = ap.parse_args()
@@ -15,7 +15,7 @@ t0, t1 = json.load(open(a.window_json))["detail"]["timed_monotonic_ns"]
 print(f"timed window {(t1 - t0) / 1e6:.1f} ms")
 ivs = []
 for d in a.dirs:
-    f = glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True)[0]
+    f = d if d.endswith(".csv") else glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True)[0]
     rows = [r for r in csv.DictReader(open(f)) if int(r["Start_Timestamp"]) >= t0 and int(r["End_Timestamp"]) <= t1]
     agg = collections.defaultdict(lambda: [0, 0.0])
     for r in rows:
