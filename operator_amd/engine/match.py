@@ -15,6 +15,7 @@ CPU path: the same post-processing fed by the pure-Python oracle.
 from __future__ import annotations
 
 import contextlib
+import os
 import threading
 import time
 import uuid
@@ -85,6 +86,7 @@ class MatchEngine:
     """Compile a PatternSet once, then analyze batches of logs on one device."""
 
     SCAN_LANES = 256 * 1024   # ac_scan v2 streams on MI355X (256 CUs x 1024 threads)
+    PACK_CHUNK = 64 << 20     # host pack / H2D pipelining granule (bytes; profiles/scan_config2_e2e.jsonl)
 
     def __init__(self, patterns: PatternSet | CompiledPatterns, device: str | torch.device = "cuda",
                  seg_bytes: int = 1024, max_events: int = 50, significance: float = 0.5,
@@ -103,6 +105,7 @@ class MatchEngine:
         self.significance = significance
         self.match_cap = int(match_cap)
         self.grid_blocks = grid_blocks
+        self.pack_threads = max(1, min(16, (os.cpu_count() or 8)))
         self.use_native_scorer = use_native_scorer
         # score + rank events on the GPU (score.hip) when scanning there
         self.gpu_scorer = (self.device.type == "cuda") if gpu_scorer is None else gpu_scorer
@@ -114,6 +117,7 @@ class MatchEngine:
         self._seg_nl: torch.Tensor | None = None
         self._matches: torch.Tensor | None = None
         self._count: torch.Tensor | None = None
+        self._doc_newlines: tuple[list[bytes], list[int]] | None = None   # (docs, newlines) of the last GPU scan
         # matcher -> list of (pattern) where it is primary, for quick checks
         self._nm = self.cp.num_matchers
         fm_ptr = [0]
@@ -220,11 +224,23 @@ class MatchEngine:
         total, first = P.plan_docs([len(d) for d in docs], seg)
         n_segs = total // seg
         pinned = self._ensure("_pinned", total, torch.uint8, pinned=True)
-        P.pack_docs(docs, first, seg, pinned.data_ptr(), 8)
-        if self.profile_bytes > 0 and not self._profiled:
-            self._profile_states(pinned[:min(total, self.profile_bytes)].numpy().tobytes())
         text = self._ensure("_text", total, torch.uint8)
-        text[:total].copy_(pinned[:total], non_blocking=True)
+        # pack and upload in doc-aligned chunks of >= PACK_CHUNK bytes: the host packs
+        # chunk k+1 (native threads) while chunk k's DMA runs, so a large batch pays
+        # max(pack, H2D) rather than the sum (BASELINE config 2: 1.2 GB)
+        ptr = pinned.data_ptr()
+        a = 0
+        while a < len(docs):
+            b = a + 1
+            while b < len(docs) and (first[b] - first[a]) * seg < self.PACK_CHUNK:
+                b += 1
+            lo, hi = first[a] * seg, first[b] * seg
+            threads = max(1, min(self.pack_threads, (hi - lo) >> 23))   # ~8 MB per packing thread
+            P.pack_docs(docs[a:b], [f - first[a] for f in first[a:b + 1]], seg, ptr + lo, threads)
+            if self.profile_bytes > 0 and not self._profiled:
+                self._profile_states(pinned[:min(total, self.profile_bytes, hi)].numpy().tobytes())
+            text[lo:hi].copy_(pinned[lo:hi], non_blocking=True)
+            a = b
         seg_nl = self._ensure("_seg_nl", 2 * n_segs, torch.int32)   # totals, then split-segment heads
         C = kernels()
         first_t = torch.tensor(first, dtype=torch.int64).to(self.device, non_blocking=True)
@@ -237,16 +253,23 @@ class MatchEngine:
             C.ac_scan(text[:total], seg, self.cls_map, self.table, self.log2c, self.hot_states, self.out_off,
                       self.out_ids, self._matches, self._count, seg_nl, self.grid_blocks, self.hot_table)
             nl = seg_nl[:n_segs].to(torch.int64)
-            excl = torch.cumsum(nl, 0) - nl
+            incl = torch.cumsum(nl, 0)
+            excl = incl - nl
             C.scan_fixup(self._matches, self._count, excl, first_t, seg, seg_nl[n_segs:2 * n_segs])
             cnt = int(self._count.item())
             if cnt <= self._matches.shape[0]:
                 break
             self.match_cap = int(cnt * 1.25) + 1024  # overflow: grow and rescan (rare)
             self._matches = None
+        # newlines per doc from the per-segment counts the scan already produced (the
+        # host would otherwise re-read every byte for AnalysisResult.metadata.totalLines)
+        pre = torch.cat([incl.new_zeros(1), incl])
+        doc_nl = pre[first_t[1:]] - pre[first_t[:-1]]
         self.stats.raw_matches += cnt
         self.stats.bytes_scanned += sum(len(d) for d in docs)
-        return self._matches[:cnt].cpu().numpy().astype(np.int64) if cnt else np.zeros((0, 4), np.int64)
+        hits = self._matches[:cnt].cpu().numpy().astype(np.int64) if cnt else np.zeros((0, 4), np.int64)
+        self._doc_newlines = (docs, doc_nl.cpu().tolist())
+        return hits
 
     def scan_cpu(self, docs: list[bytes]) -> np.ndarray:
         """Same contract as scan_gpu, computed with Python (used without a GPU)."""
@@ -409,15 +432,19 @@ class MatchEngine:
         """Full AnalysisResult per doc (pods = [(name, namespace)] for labelling)."""
         with self._lock:
             t0 = time.perf_counter()
+            self._doc_newlines = None
             evs, offs = self.events(docs)
+            nls = self._doc_newlines[1] if self._doc_newlines and self._doc_newlines[0] is docs else None
             out = []
             for di, (doc, ev) in enumerate(zip(docs, evs)):
                 out.append(self._result(di, doc, ev, offs, pods[di] if pods else (None, None),
-                                        (time.perf_counter() - t0) * 1e3))
+                                        (time.perf_counter() - t0) * 1e3, None if nls is None else nls[di]))
+            self._doc_newlines = None
             self.stats.docs += len(docs)
             return out
 
-    def _result(self, di: int, doc: bytes, ev: list[oracle.Event], offs: dict, pod, ms: float) -> AnalysisResult:
+    def _result(self, di: int, doc: bytes, ev: list[oracle.Event], offs: dict, pod, ms: float,
+                newlines: int | None = None) -> AnalysisResult:
         cp = self.cp
         pats = cp.patset.patterns
         dist = {s: 0 for s in SEVERITIES}
@@ -448,5 +475,6 @@ class MatchEngine:
         return AnalysisResult(analysis_id=str(uuid.uuid4()), pod_name=pod[0], pod_namespace=pod[1], events=events,
                               summary=summary,
                               metadata={"engine": "gpu-ac" if self.device.type == "cuda" else "cpu-oracle",
-                                        "patternsChecked": len(pats), "totalLines": doc.count(b"\n") + 1,
+                                        "patternsChecked": len(pats),
+                                        "totalLines": (doc.count(b"\n") if newlines is None else newlines) + 1,
                                         "bytes": len(doc), "processingTimeMs": round(ms, 3)})

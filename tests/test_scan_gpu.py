@@ -48,9 +48,25 @@ def test_engine_matches_oracle_1k_patterns():
         assert [(e.pattern, e.line) for e in a] == [(e.pattern, e.line) for e in b]
         assert np.allclose([e.score for e in a], [e.score for e in b])
     res = eng.analyze(docs)
-    for r, t in zip(res, truth):
+    for r, t, d in zip(res, truth, docs):
         ids = {e.matched_pattern.id for e in r.events}
         assert set(t) <= ids
+        assert r.metadata["totalLines"] == d.count(b"\n") + 1
+
+
+@pytest.mark.parametrize("seg", [64, 1024])
+def test_total_lines_from_gpu_newline_counts(seg):
+    """AnalysisResult.metadata.totalLines comes from the scan's per-segment newline
+    counts (no host re-read of the logs); it equals the host count for edge-case docs
+    and for a batch large enough to use full-size segments."""
+    eng = MatchEngine(catalog_library(), device="cuda", seg_bytes=seg)
+    docs = [b"", b"\n", b"no newline at all", b"\n" * (3 * seg + 5), b"OOMKilled\n" * 999 + b"tail",
+            (b"x" * (seg - 1) + b"\n") * 7, bytes(range(256)) * 9]
+    for r, d in zip(eng.analyze(docs), docs):
+        assert r.metadata["totalLines"] == d.count(b"\n") + 1
+    big, _ = LogFactory(n_patterns=len(catalog_library()), seed=3, pool_lines=512).batch(600, 64 * 1024, n_failures=2)
+    for r, d in zip(eng.analyze(big), big):
+        assert r.metadata["totalLines"] == d.count(b"\n") + 1
 
 
 def test_match_overflow_grows_and_rescans():
