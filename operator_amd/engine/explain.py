@@ -291,3 +291,28 @@ class ExplainEngine:
                 while len(self._cache) > self._cache_size:
                     self._cache.popitem(last=False)
         return resp
+
+    # ------------------------------------------------------------------ raw completions
+    def complete(self, ids: list[int], max_tokens: int = 500, temperature: float = 0.3, seed: int | None = None,
+                 timeout_s: float | None = None) -> dict:
+        """Generate from raw prompt token ids on the same continuous batch as the
+        explanations (the OpenAI / Ollama endpoints of engine/server.py). Raises
+        ExplainError on a timeout, an engine error or a prompt the engine cannot hold."""
+        req = GenRequest(list(ids), max_tokens=max(1, int(max_tokens)), temperature=max(0.0, float(temperature)),
+                         seed=self._seed(ids) if seed is None else int(seed), ignore_eos=self.ignore_eos)
+        want = req.max_tokens
+        t0 = time.perf_counter()
+        try:
+            self.llm.submit(req)
+        except ValueError as e:
+            raise ExplainError(str(e)) from None
+        self.loop.notify()
+        if not req.event.wait(timeout=timeout_s if timeout_s else None):
+            self.llm.cancel(req)
+            raise ExplainError(f"completion timed out after {timeout_s}s")
+        if req.error:
+            raise ExplainError(req.error)
+        return {"text": self.tok.decode(req.output), "prompt_tokens": len(req.prompt),
+                "completion_tokens": len(req.output),
+                "finish_reason": "length" if len(req.output) >= min(want, req.max_tokens) else "stop",
+                "latency_ms": round((req.t_done - t0) * 1e3, 3)}

@@ -133,6 +133,20 @@ class LocalExplainService:
     def explain_many(self, items):
         return self.ee.explain_many(items)
 
+    def complete(self, prompt=None, messages=None, model: str | None = None, **kw) -> dict:
+        """Raw completion (``prompt`` text) or chat (``messages``) on this engine."""
+        tok = self.ee.tok
+        ids = tok.encode_chat(messages) if messages is not None else tok.encode_text(prompt or "")
+        out = self.ee.complete(ids, **kw)
+        out["model"] = self.ee.model_id
+        if self.metrics:
+            self.metrics.tokens_generated.inc(out["completion_tokens"])
+        return out
+
+    @property
+    def models(self) -> list[str]:
+        return [self.ee.model_id]
+
     def ready(self) -> bool:
         return self.ee.loop.is_alive() and self.ee.loop.error is None
 
@@ -170,6 +184,10 @@ class MultiModelExplainService:
             for i, res in zip(idx, svc.explain_many([items[i] for i in idx])):
                 out[i] = res
         return out
+
+    def complete(self, prompt=None, messages=None, model: str | None = None, **kw) -> dict:
+        svc = self._by_lower.get((model or "").lower(), self.services[self.default])
+        return svc.complete(prompt=prompt, messages=messages, model=model, **kw)
 
     def ready(self) -> bool:
         return all(getattr(v, "ready", lambda: True)() for v in self.services.values())

@@ -140,6 +140,21 @@ class Tokenizer:
             os.replace(tmp, f)
             return tk
 
+    def encode_chat(self, messages: list[dict]) -> list[int]:
+        """Token ids of a chat (``[{"role", "content"}, ...]``) ending in the assistant's
+        turn: through the checkpoint's chat template when there is one, else as plain
+        ``role: content`` lines after BOS."""
+        msgs = [{"role": str(m.get("role", "user")), "content": str(m.get("content") or "")} for m in messages]
+        if self.chat is not None:
+            text = self.chat.render(messages=msgs, **self._chat_vars)
+            return self.tk.encode(text, add_special_tokens=False).ids
+        text = "".join(f"{m['role']}: {m['content']}\n" for m in msgs) + "assistant:"
+        return ([self.bos_id] if self.add_bos else []) + self.tk.encode(text, add_special_tokens=False).ids
+
+    def encode_text(self, text: str) -> list[int]:
+        """Token ids of a raw completion prompt (BOS when the model has one; no chat template)."""
+        return ([self.bos_id] if self.add_bos else []) + self.tk.encode(text, add_special_tokens=False).ids
+
     def encode(self, text: str, bos: bool = True) -> list[int]:
         return self.encode_batch([text], bos)[0]
 
