@@ -120,7 +120,9 @@ class AnalysisPipeline:
             return "pattern-only"
         try:
             provider = ai_client.get_provider(self.kube, monitor)
-        except Exception:  # noqa: BLE001 (executor-level failure)
+        except Exception as e:  # noqa: BLE001 (executor-level failure)
+            md = pod.get("metadata") or {}
+            log.warning("AI provider lookup for pod %s/%s failed: %s", md.get("namespace"), md.get("name"), e)
             self.status.update_pod_failure(monitor, pod, "Analysis completed, AI provider lookup failed")
             self.events.emit_analysis_complete(pod, monitor, result, "AI provider lookup failed")
             return "provider-lookup-failed"

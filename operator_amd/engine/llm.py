@@ -18,6 +18,8 @@ hipGraph-captured decode steps.
 """
 from __future__ import annotations
 
+import contextlib
+import gc
 import itertools
 import threading
 import time
@@ -139,6 +141,24 @@ class _BucketState:
             dst.copy_(src.pin_memory() if nb else src, non_blocking=nb)
 
 
+@contextlib.contextmanager
+def _no_gc():
+    """No Python garbage collection while a hipGraph is being captured. Recent PyTorch
+    no longer collects on entering ``torch.cuda.graph``, so a collection triggered by
+    an allocation inside the capture could free a dead cycle's GPU tensors there; a
+    tensor used on another stream (engine.phase_streams, the scan stream) then
+    records an event on that stream mid-capture, which aborts the process. Dead
+    cycles are collected first, then collection waits until the capture ends."""
+    gc.collect()
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
+
+
 class _DecodeGraph:
     """One decode step over a bucket's state, with ``splits`` decode-attention
     workgroups per (sequence, kv-head) (``ops.decode_splits``)."""
@@ -179,7 +199,7 @@ class _DecodeGraph:
         torch.cuda.current_stream().wait_stream(s)
         st.ctx.copy_(torch.zeros_like(saved_ctx))
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, pool=pool):
+        with _no_gc(), torch.cuda.graph(g, pool=pool):
             self._run()
         self.graph = g
         for t, v in zip((st.ids, st.pos, st.ctx, st.step), snap):
@@ -236,7 +256,7 @@ class _PrefillGraph:
                 self._run()
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, pool=pool):
+        with _no_gc(), torch.cuda.graph(g, pool=pool):
             self._run()
         self.graph = g
 

@@ -117,6 +117,45 @@ def test_llama3_8b_prefill_and_greedy_decode_track_fp32_reference():
     exact = (ref_rows.argmax(-1) == chosen).float().mean()
     assert float(gap.max() / scale) < 0.02, gap.tolist()
     assert exact >= 0.85, float(exact)
+    del c, kv_c, lc, lg
+    import gc
+
+    gc.collect()
+
+
+def test_graph_capture_with_dead_cycles_holding_multi_stream_tensors():
+    """Regression: a Python GC pass inside a hipGraph capture that frees a dead cycle's
+    tensor last used on another stream records an event on that stream mid-capture
+    (a process abort). The engine collects before capturing and holds GC off during
+    it; here collection is forced to run on almost every allocation."""
+    import gc
+
+    cfg = get_config("tiny-gqa4")
+    m = LlamaModel(cfg, device="cuda").init_random(seed=7)
+    side = torch.cuda.Stream()
+
+    class Node:
+        pass
+
+    for _ in range(64):   # dead cycles, each holding a tensor with a use on `side`
+        a, b = Node(), Node()
+        a.o, b.o = b, a
+        a.t = torch.ones(1 << 16, device="cuda")
+        with torch.cuda.stream(side):
+            a.t.mul_(2)
+        a.t.record_stream(side)
+    del a, b
+    old = gc.get_threshold()
+    gc.set_threshold(1, 1, 1)
+    try:
+        kv = PagedKVCache(cfg.layers, 64, cfg.kv_heads, 128, 16, device="cuda")
+        eng = LLMEngine(m, kv, max_batch=4, max_context=512, use_graphs=True, multi_step=2, phase_streams=True)
+        reqs = [GenRequest(list(range(2, 2 + n)), max_tokens=6, temperature=0.0, ignore_eos=True) for n in (7, 30)]
+        eng.generate(reqs)
+    finally:
+        gc.set_threshold(*old)
+    torch.cuda.synchronize()
+    assert all(len(r.output) == 6 for r in reqs) and eng.stats.graph_replays > 0
 
 
 @pytest.mark.parametrize("phase_streams", [False, True])
