@@ -65,7 +65,7 @@ def parse_args():
                     help="engine processes per GPU (EnginePool workers holding the scan + LLM engines, "
                          "--max-batch split over them); 1 = engines inside this process")
     ap.add_argument("--shards", type=int, default=None,
-                    help="operator shards per GPU (default 2 with a GPU, 1 without): independent operator "
+                    help="operator shards per GPU (default 1): independent operator "
                          "processes (own API-server shard, controller and engines), each failing --batch / shards "
                          "pods per step on its own closed loop; the rank process runs shard 0 and starts the "
                          "others as child processes")
@@ -120,11 +120,11 @@ def main() -> int:
             pass
         if os.getppid() == 1:
             return 1
-    if a.shards is None:   # device_count() does not initialise the GPU
-        import torch
-
-        # two shards measured 32.8 vs 28.1 analyses/s, p50 7.8 vs 9.2 s (profiles/bench_shards_8b.jsonl)
-        a.shards = 2 if torch.cuda.device_count() > 0 else 1
+    if a.shards is None:
+        # one operator per GPU: with every shard's logs equally heavy, 1 x 256 measured
+        # 28.2 analyses/s at p50 9.0 s vs 26.6 / 9.5 s for 2 x 128 and 26.8 / 14.1 s for
+        # 3 x 128 (profiles/shards_equal_work_8b.jsonl)
+        a.shards = 1
     a.shards = max(1, a.shards)
     kids = spawn_shards(a) if (a.shards > 1 and not child) else []
     shard = a.shard_index or 0

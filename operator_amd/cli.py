@@ -137,9 +137,10 @@ def apply_shard_env(s, env: dict) -> None:
 
 class ShardSupervisor:
     """``run --shards K``: K-1 more operator processes on the same GPUs (K engine sets
-    per GPU), started before this process touches a GPU. One operator's kernel stream
-    does not fill an MI355X: two out-of-phase shards per GPU measured 32.8 vs 28.1
-    analyses/s at a lower p50 (bench.py, profiles/bench_shards_8b.jsonl).
+    per GPU), started before this process touches a GPU. Shards scale the operator's
+    host side (watch, collection, sinks: one Python process per shard). On one GPU
+    they do not raise GPU throughput: 2 x 128 measured 26.6 analyses/s vs 28.2 for one
+    operator with equal work (profiles/shards_equal_work_8b.jsonl).
 
     A shard that exits is started again (its slice of the pods would otherwise go
     unanalysed); more than ``max_restarts`` restarts within ``window_s`` makes

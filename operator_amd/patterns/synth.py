@@ -158,10 +158,15 @@ def library_yaml(n_patterns: int = 1000, seed: int = 0, library_id: str = "synth
 class LogFactory:
     """Deterministic pod-log synthesizer with injected failure signatures."""
 
-    def __init__(self, n_patterns: int = 1000, seed: int = 0, pool_lines: int = 8192):
+    def __init__(self, n_patterns: int = 1000, seed: int = 0, pool_lines: int = 8192, library_seed: int = 0):
+        """``seed`` varies the background lines; the injected failure signatures are the
+        examples of ``synthetic_library(n_patterns, seed=library_seed)`` — the library
+        the logs are scanned with — whatever ``seed`` is. (They once followed ``seed``,
+        so a factory seeded differently from its library injected signatures that the
+        library does not contain: bench.py's extra shards and ranks got lighter logs.)"""
         self.seed = seed
         rng = random.Random(seed + 1)
-        gen_items, gen_examples = _gen_items(max(0, n_patterns - len(CATALOG)), seed)
+        gen_items, gen_examples = _gen_items(max(0, n_patterns - len(CATALOG)), library_seed)
         self.examples: dict[str, list[str]] = {c[0]: [c[6]] for c in CATALOG}
         self.examples.update(gen_examples)
         self.secondary_examples = {

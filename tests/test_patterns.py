@@ -172,3 +172,18 @@ def test_reorder_dfa_preserves_matches_and_raises_hot_coverage():
     t1 = np.frombuffer(d["table"], np.uint16).reshape(-1, C)
     t2 = np.frombuffer(r["table"], np.uint16).reshape(-1, C)
     assert ((t1[0] & 0x8000) == (t2[0] & 0x8000)).all()
+
+
+def test_log_factory_injects_signatures_of_the_scanned_library_for_any_seed():
+    """Benchmark workload invariance: whatever the factory's seed (bench.py seeds it per
+    rank and shard), every injected failure is a signature of synthetic_library(n, 0),
+    so each shard and rank analyses equally heavy failures."""
+    from operator_amd.engine.match import MatchEngine
+    from operator_amd.patterns.synth import LogFactory, synthetic_library
+
+    eng = MatchEngine(synthetic_library(1000, seed=0), device="cpu")
+    for seed in (0, 1, 3, 101):
+        docs, truth = LogFactory(n_patterns=1000, seed=seed, pool_lines=256).batch(3, 8 * 1024, n_failures=3,
+                                                                                  seed=seed + 7)
+        for r, t in zip(eng.analyze(docs), truth):
+            assert set(t) <= {e.matched_pattern.id for e in r.events}, (seed, t)
