@@ -73,6 +73,10 @@ def parse_args():
     ap.add_argument("--multi-step", type=int, default=8, help="decode steps per graph window (engine.multi_step)")
     ap.add_argument("--phase-streams", action="store_true",
                     help="prefill on a normal-priority, decode on a high-priority HIP stream (engine.phase_streams)")
+    ap.add_argument("--sink-concurrency", type=int, default=16,
+                    help="operator.sink_concurrency: analyses writing results at once (0 = unbounded); a bound "
+                         "keeps a finished wave's 256 result writers from starving the next wave's ramp "
+                         "(GPU gap before its first prefill 230-440 -> 140-170 ms, profiles/wave_timeline_sinks_8b.jsonl)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -165,6 +169,7 @@ def main() -> int:
             "engine.ignore_eos": True, "engine.phase_streams": a.phase_streams,
             "engine.multi_step": a.multi_step,
             "engine.seed": 0, "health.enabled": False, "operator.workers": 2 * a.batch + 16, "operator.io_workers": 16,
+            "operator.sink_concurrency": a.sink_concurrency,
             "patterns.cache_dir": f"/tmp/oamd-bench-{os.getpid()}", "services.match_max_batch": 64,
             "services.match_batch_wait_ms": 5.0})
 

@@ -36,6 +36,9 @@ class OperatorCfg(BaseModel):
                                       # explanation, so 2 x engine.max_batch x GPUs (+16) keep the engines'
                                       # batches full while the previous batch's results are written
     io_workers: int = 8               # kube write pool (annotations, status, events)
+    sink_concurrency: int = 0         # analyses writing their results at once (annotations, status ring,
+                                      # Events); 0 = unbounded. A bound keeps a wave of result writes from
+                                      # starving the next failures' watch -> collect -> scan -> prompt path
     leader_election: bool = False     # reference: 1 replica, no lease; true = HA replicas behind a Lease
     lease_name: str = "podmortem-operator-leader"
     lease_namespace: str = "podmortem-system"

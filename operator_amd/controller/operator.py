@@ -88,7 +88,8 @@ class Operator:
         self.explainer = ProviderRouter(explain_service, enabled=s.services.external_providers)
         self.pipeline = AnalysisPipeline(kube, self.matcher, self.explainer, self.events, self.storage, self.status,
                                          self.pool, self.metrics, log_container=s.watch.log_container,
-                                         log_previous=s.watch.log_previous, log_limit_bytes=s.watch.log_limit_bytes)
+                                         log_previous=s.watch.log_previous, log_limit_bytes=s.watch.log_limit_bytes,
+                                         sink_concurrency=s.operator.sink_concurrency)
         self.deduper = FailureDeduper(s.watch.dedupe_max_entries, s.watch.dedupe_ttl_s)
         self.sync = PatternSync(s.patterns.cache_dir)
         self._make_workers()

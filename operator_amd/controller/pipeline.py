@@ -17,7 +17,9 @@ AIProviderConfig). Per-stage timings feed the Prometheus histograms.
 """
 from __future__ import annotations
 
+import contextlib
 import logging
+import threading
 import time
 from concurrent.futures import Executor, Future
 
@@ -41,8 +43,10 @@ def _msg(e: BaseException) -> str:
 class AnalysisPipeline:
     def __init__(self, kube, matcher, explainer, events: EventEmitter, storage: AnalysisStorage,
                  status: StatusWriter, executor: Executor | None = None, metrics=None,
-                 log_container: str | None = None, log_previous: bool = False, log_limit_bytes: int | None = None):
+                 log_container: str | None = None, log_previous: bool = False, log_limit_bytes: int | None = None,
+                 sink_concurrency: int = 0):
         self.kube, self.matcher, self.explainer = kube, matcher, explainer
+        self._sinks = threading.BoundedSemaphore(sink_concurrency) if sink_concurrency > 0 else None
         self.events, self.storage, self.status = events, storage, status
         self.executor, self.metrics = executor, metrics
         self.log_container, self.log_previous, self.log_limit_bytes = log_container, log_previous, log_limit_bytes
@@ -96,6 +100,11 @@ class AnalysisPipeline:
         self._notify(monitor, pod, out)
         return out
 
+    def _sink_slot(self):
+        """One of ``sink_concurrency`` result-writing slots (annotations, status ring,
+        Events), or no bound."""
+        return self._sinks if self._sinks is not None else contextlib.nullcontext()
+
     def _notify(self, monitor: dict, pod: dict, outcome: str) -> None:
         for fn in self.listeners:
             try:
@@ -114,22 +123,25 @@ class AnalysisPipeline:
     # ------------------------------------------------------------------ branching (PodFailureWatcher.java:347-443)
     def handle_result(self, monitor: dict, pod: dict, result: AnalysisResult) -> str:
         if not ai_client.ai_enabled(monitor):
-            self.storage.store(pod, monitor, result, None)
-            self.status.update_pod_failure(monitor, pod, "Pattern analysis completed (AI disabled)")
-            self.events.emit_analysis_complete(pod, monitor, result, "AI disabled")
+            with self._sink_slot():
+                self.storage.store(pod, monitor, result, None)
+                self.status.update_pod_failure(monitor, pod, "Pattern analysis completed (AI disabled)")
+                self.events.emit_analysis_complete(pod, monitor, result, "AI disabled")
             return "pattern-only"
         try:
             provider = ai_client.get_provider(self.kube, monitor)
         except Exception as e:  # noqa: BLE001 (executor-level failure)
             md = pod.get("metadata") or {}
             log.warning("AI provider lookup for pod %s/%s failed: %s", md.get("namespace"), md.get("name"), e)
-            self.status.update_pod_failure(monitor, pod, "Analysis completed, AI provider lookup failed")
-            self.events.emit_analysis_complete(pod, monitor, result, "AI provider lookup failed")
+            with self._sink_slot():
+                self.status.update_pod_failure(monitor, pod, "Analysis completed, AI provider lookup failed")
+                self.events.emit_analysis_complete(pod, monitor, result, "AI provider lookup failed")
             return "provider-lookup-failed"
         if provider is None:
-            self.storage.store(pod, monitor, result, None)
-            self.status.update_pod_failure(monitor, pod, "Analysis completed, AI provider not found")
-            self.events.emit_analysis_complete(pod, monitor, result, "AI provider not found")
+            with self._sink_slot():
+                self.storage.store(pod, monitor, result, None)
+                self.status.update_pod_failure(monitor, pod, "Analysis completed, AI provider not found")
+                self.events.emit_analysis_complete(pod, monitor, result, "AI provider not found")
             return "provider-not-found"
         t0 = time.perf_counter()
         try:
@@ -139,13 +151,14 @@ class AnalysisPipeline:
         except Exception as e:  # noqa: BLE001
             m = _msg(e)
             log.error("AI analysis failed for pod %s: %s", (pod.get("metadata") or {}).get("name"), m)
-            self.status.update_pod_failure(monitor, pod, "Pattern analysis completed, AI failed: " + m)
-            self.events.emit_analysis_complete(pod, monitor, result, "AI failed: " + m)
-            self.events.emit_analysis_error(pod, monitor, "AI analysis failed: " + m)
+            with self._sink_slot():
+                self.status.update_pod_failure(monitor, pod, "Pattern analysis completed, AI failed: " + m)
+                self.events.emit_analysis_complete(pod, monitor, result, "AI failed: " + m)
+                self.events.emit_analysis_error(pod, monitor, "AI analysis failed: " + m)
             return "ai-failed"
         if self.metrics:
             self.metrics.stage_seconds.labels(stage="explain").observe(time.perf_counter() - t0)
-        with trace_range("sinks"):
+        with self._sink_slot(), trace_range("sinks"):
             self.storage.store(pod, monitor, result, text)
             self.status.update_pod_failure(monitor, pod, "Analysis completed with AI analysis")
             self.events.emit_analysis_complete(pod, monitor, result, text)

@@ -536,3 +536,49 @@ def test_operator_shards_split_failures_exactly_once(tmp_path):
     finally:
         for o in ops_:
             o.stop()
+
+
+def test_sink_concurrency_bounds_result_writers(monkeypatch):
+    """operator.sink_concurrency: at most N analyses write their results at once; every
+    analysis still stores its result."""
+    import threading
+    import time as _time
+
+    from operator_amd.api.models import AIProviderConfig, AIResponse, AnalysisResult
+    from operator_amd.controller import ai_client
+    from operator_amd.controller.pipeline import AnalysisPipeline
+
+    monkeypatch.setattr(ai_client, "get_provider", lambda kube, m: {"spec": {}})
+    monkeypatch.setattr(ai_client, "to_provider_config", lambda kube, p: AIProviderConfig())
+    state = {"now": 0, "max": 0, "stored": 0}
+    lock = threading.Lock()
+
+    class Storage:
+        def store(self, pod, monitor, result, text):
+            with lock:
+                state["now"] += 1
+                state["max"] = max(state["max"], state["now"])
+            _time.sleep(0.02)
+            with lock:
+                state["now"] -= 1
+                state["stored"] += 1
+
+    class Nop:
+        def __getattr__(self, name):
+            return lambda *a, **k: None
+
+    class Explainer:
+        def explain(self, result, cfg):
+            return AIResponse(explanation="x")
+
+    p = AnalysisPipeline(None, None, Explainer(), Nop(), Storage(), Nop(), sink_concurrency=3)
+    ai = {"metadata": {"name": "m", "namespace": "default"}, "spec": {"aiProviderRef": {"name": "p"}}}
+    off = {"metadata": {"name": "m", "namespace": "default"}, "spec": {"aiAnalysisEnabled": False}}
+    ts = [threading.Thread(target=p.handle_result,
+                           args=(ai if i % 2 else off, {"metadata": {"name": f"p{i}"}}, AnalysisResult()))
+          for i in range(12)]   # AI-explained and pattern-only results share the bound
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert state["stored"] == 12 and 1 <= state["max"] <= 3
