@@ -359,6 +359,28 @@ class LLMEngine:
                 req.error = "cancelled"
                 req.event.set()
 
+    def abort_all(self, reason: str) -> None:
+        """Fail every queued and running request after a step raised (e.g. out of
+        memory): their waiters are released with ``reason``, their KV pages go back to
+        the allocator and the next step starts from a clean batch. Work the failed step
+        left queued on the device is drained first, so no late kernel writes into pages
+        that are handed out again (if the device itself is broken, that sync raises and
+        the caller treats the engine as lost)."""
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        with self._lock:
+            reqs = list(self.running) + list(self.waiting)
+            self.running, self.waiting = [], deque()
+        for r in reqs:
+            if r.pages:
+                self.kv.allocator.release(r.pages)
+                r.pages = []
+            r.error = reason
+            r.done = True
+            r.event.set()
+        self._inflight = None
+        self._active = None
+
     def has_work(self) -> bool:
         return bool(self.waiting or self.running)
 
