@@ -101,22 +101,24 @@ class EngineLoop(threading.Thread):
                 self.llm.step()
             except BaseException as e:  # surface to every waiter
                 self.error = e
-                try:   # release the failed batch's KV pages so the engine keeps serving
-                    self.llm.abort_all(f"engine failure: {e}")
-                except BaseException as e2:  # noqa: BLE001 - the device is gone: stop serving
-                    for r in list(self.llm.running) + list(self.llm.waiting):
-                        r.error = f"engine failure: {e}"
-                        r.done = True
-                        r.event.set()
-                    self.llm.running.clear()
-                    self.llm.waiting.clear()
-                    self.fatal = e2
-                    return
-                if getattr(e, "fatal", False) or isinstance(e, CollectiveTimeout):
-                    # the replica's device state is inconsistent (e.g. a TP peer never
-                    # arrived): stop serving; the pool worker exits and is respawned
-                    self.fatal = e
-                    return
+                fatal = getattr(e, "fatal", False) or isinstance(e, CollectiveTimeout)
+                if not fatal:
+                    try:   # release the failed batch's KV pages so the engine keeps serving
+                        self.llm.abort_all(f"engine failure: {e}")
+                        continue
+                    except BaseException as e2:  # noqa: BLE001 - the device is gone: stop serving
+                        fatal, e = True, e2
+                # the replica's device state is inconsistent (e.g. a TP peer never arrived:
+                # no device sync, it could wait forever): fail every waiter and stop
+                # serving; the pool worker exits and is respawned
+                for r in list(self.llm.running) + list(self.llm.waiting):
+                    r.error = f"engine failure: {e}"
+                    r.done = True
+                    r.event.set()
+                self.llm.running.clear()
+                self.llm.waiting.clear()
+                self.fatal = e
+                return
 
 
 @dataclass
