@@ -485,6 +485,9 @@ def main() -> int:
                    "kv_cache_dtype": "fp8_e4m3fn" if a.kv_dtype == "fp8" else "bf16",
                    "waves": "serial" if (a.serial_waves or a.mode != "pipeline") else "pipelined"},
         "detail": {"init_s": round(init_s, 1), "prefill_tokens_per_gpu": ptoks, "decode_tokens_per_gpu": dtoks,
+                   # workload check: every failure carries three signatures of the scanned library, so
+                   # this stays ~895 whatever the rank / shard layout (README "Correction")
+                   "prompt_tokens_per_analysis": round(ptoks / max(1, a.batch * a.shards * a.steps), 1),
                    "prefill_graph_replays": replays,
                    "prefill_graph_buckets": stats1["prefill_graph_buckets"],
                    "decode_tok_s_per_gpu": round(dtoks / elapsed, 1), "outcomes": counter["outcomes"],
