@@ -61,6 +61,7 @@ class GenRequest:
     t_first: float = 0.0
     t_done: float = 0.0
     event: threading.Event = field(default_factory=threading.Event, repr=False)
+    text: str | None = None        # detokenized output, filled by LLMEngine.finish_hook when set
 
     @property
     def length(self) -> int:
@@ -311,6 +312,9 @@ class LLMEngine:
         self._pool = None
         self.buckets = _buckets(max_batch)
         self.eos = set(model.cfg.eos_ids)
+        # called with the requests a step finished, before their waiters wake (ExplainEngine
+        # detokenizes a whole finished batch in one GIL-free call there)
+        self.finish_hook = None
         self._lock = threading.Lock()
         # Decode windows are pipelined on the GPU: window w+1 is launched before the
         # host reads window w's tokens, so the device never idles on the host's
@@ -645,10 +649,16 @@ class LLMEngine:
                 self.kv.allocator.release(r.pages)
                 r.pages = []
                 fin.append(r)
-                r.event.set()
             else:
                 keep.append(r)
         if fin:
             self._active = None  # batch composition changed: reload device state next step
+            if self.finish_hook is not None:
+                try:
+                    self.finish_hook([r for r in fin if not r.cancelled])
+                except Exception:  # noqa: BLE001 - waiters fall back to their own detokenization
+                    pass
+            for r in fin:
+                r.event.set()
         self.running = keep
         return fin

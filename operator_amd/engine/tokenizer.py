@@ -167,7 +167,14 @@ class Tokenizer:
         pre = [self.bos_id] if (bos and self.add_bos) else []
         return [pre + e.ids for e in self.tk.encode_batch(texts, add_special_tokens=False)]
 
-    def decode(self, ids: list[int]) -> str:
+    def _keep(self, ids: list[int]) -> list[int]:
         n = self.n_vocab
-        keep = [i % n for i in ids if i != self.bos_id and i != self.eos_id]
-        return self.tk.decode(keep, skip_special_tokens=self.from_checkpoint)
+        return [i % n for i in ids if i != self.bos_id and i != self.eos_id]
+
+    def decode(self, ids: list[int]) -> str:
+        return self.tk.decode(self._keep(ids), skip_special_tokens=self.from_checkpoint)
+
+    def decode_batch(self, seqs: list[list[int]]) -> list[str]:
+        """``decode`` of many sequences in one call (the Rust core runs them in
+        parallel without the GIL)."""
+        return self.tk.decode_batch([self._keep(x) for x in seqs], skip_special_tokens=self.from_checkpoint)

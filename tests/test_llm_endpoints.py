@@ -114,3 +114,29 @@ def test_providers_client_round_trip(server):
         out = c.explain(res, AIProviderConfig(provider_id=pid, api_url=url, model_id="tiny", max_tokens=4,
                                               temperature=0.0, caching_enabled=False))
         assert isinstance(out.explanation, str) and 0 < out.tokens_generated <= 4
+
+
+def test_finished_batch_is_detokenized_once_before_waiters_wake(server):
+    """The engine loop detokenizes every request a step finished in one decode_batch
+    call (LLMEngine.finish_hook), and the text equals per-request decoding."""
+    from operator_amd.engine.llm import GenRequest
+
+    _, svc = server
+    ee = svc.services["tiny"].ee
+    assert ee.llm.finish_hook is not None
+    seqs = [[5, 6, 7, 300, 301], [], list(range(40, 90))]
+    assert ee.tok.decode_batch(seqs) == [ee.tok.decode(x) for x in seqs]
+    reqs = [GenRequest(list(range(3, 3 + n)), max_tokens=5, temperature=0.0, ignore_eos=True) for n in (4, 20)]
+    seen = []
+    real = ee.llm.finish_hook
+    ee.llm.finish_hook = lambda fin: (seen.append([r.event.is_set() for r in fin]), real(fin))
+    try:
+        for r in reqs:
+            ee.llm.submit(r)
+        ee.loop.notify()
+        for r in reqs:
+            assert r.event.wait(60)
+    finally:
+        ee.llm.finish_hook = real
+    assert seen and not any(any(x) for x in seen)          # hook ran before the waiters were released
+    assert all(r.text == ee.tok.decode(r.output) for r in reqs)
