@@ -45,12 +45,18 @@ def _sampling(body: dict, ollama: bool) -> dict:
     """max_tokens / temperature / seed of an OpenAI body or an Ollama ``options`` map
     (defaults: the AIProvider CRD's 500 tokens at T = 0.3)."""
     src = (body.get("options") or {}) if ollama else body
+    if not isinstance(src, dict):
+        raise BadRequest("'options' must be an object")
     n = src.get("num_predict") if ollama else (body.get("max_completion_tokens") or body.get("max_tokens"))
-    kw = {"max_tokens": int(n) if n is not None and int(n) > 0 else 500,
-          "temperature": float(src.get("temperature", 0.3)), "timeout_s": COMPLETION_TIMEOUT_S}
-    if src.get("seed") is not None:
-        kw["seed"] = int(src["seed"])
-    if not ollama and int(body.get("n", 1) or 1) != 1:
+    try:
+        kw = {"max_tokens": int(n) if n is not None and int(n) > 0 else 500,
+              "temperature": float(src.get("temperature", 0.3)), "timeout_s": COMPLETION_TIMEOUT_S}
+        if src.get("seed") is not None:
+            kw["seed"] = int(src["seed"])
+        n_choices = int(body.get("n", 1) or 1)
+    except (TypeError, ValueError) as e:
+        raise BadRequest(f"bad sampling parameter: {e}") from None
+    if not ollama and n_choices != 1:
         raise BadRequest("only n = 1 is supported")
     return kw
 

@@ -92,6 +92,8 @@ def test_bad_requests_are_400(server):
     assert _post(srv, "/v1/chat/completions", {"model": "tiny", "messages": []}).status_code == 400
     assert _post(srv, "/v1/completions", {"model": "tiny", "prompt": 5}).status_code == 400
     assert _post(srv, "/v1/chat/completions", {"n": 2, "messages": [{"role": "user", "content": "x"}]}).status_code == 400
+    assert _post(srv, "/v1/completions", {"prompt": "x", "max_tokens": "many"}).status_code == 400
+    assert _post(srv, "/api/generate", {"prompt": "x", "options": {"temperature": "hot"}}).status_code == 400
     long = " ".join(["word"] * 2000)   # more tokens than the engine's 512-token context
     r = _post(srv, "/v1/completions", {"model": "tiny", "prompt": long, "max_tokens": 4})
     assert r.status_code == 400 and "max_context" in r.json()["error"]["message"]
