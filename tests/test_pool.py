@@ -29,7 +29,7 @@ def _settings(**extra):
 
 @pytest.fixture(scope="module")
 def pool():
-    p = EnginePool(_settings(), catalog_library(), ["cpu", "cpu"], heartbeat_s=0.2, heartbeat_timeout_s=8.0,
+    p = EnginePool(_settings(), catalog_library(), ["cpu", "cpu"], heartbeat_s=0.2, heartbeat_timeout_s=20.0,
                    max_restarts=2)
     try:
         assert p.wait_ready(600) == 2, p.health()
