@@ -173,6 +173,9 @@ def test_dedupe_and_added_ignored(env):
     fk, op, _ = env
     _pm(fk)
     wait_for(lambda: op.monitors.list())
+    # the Podmortem's first reconcile (which analyses failed pods that already exist, §3.3)
+    # must be over before the ADDED-only pod appears, or it rightly analyses that pod too
+    wait_for(lambda: ((fk.get(PODMORTEMS, "demo-monitor", "default") or {}).get("status") or {}).get("phase") == "Ready")
     fk.create(PODS, failed_pod("added-only", labels={"app": "demo"}))  # ADDED: ignored by the watcher
     _fail(fk, "w2", finished="2025-08-29T10:00:00Z")
     wait_for(lambda: len(_events(fk, "PodmortemAnalysisComplete")) >= 2)
