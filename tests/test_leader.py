@@ -126,12 +126,12 @@ def test_stalled_renewal_stops_leading_within_deadline():
         assert not b.leading
         t_stall = time.monotonic()
         slow.stall_s = 30.0   # every renewal now blocks far longer than the lease
-        wait_for(lambda: not a.leading, timeout=5)
+        wait_for(lambda: not a.leading, timeout=15)
         stop_t = next(t for who, what, t in events if who == "a" and what == "stop")
         # stopped within renew_deadline (+ one retry period, + scheduling slack when the
         # test runs beside a loaded suite), long before the stalled call (30 s) returns
         assert stop_t - t_stall < 0.8 + 0.1 + 1.0
-        wait_for(lambda: b.leading, timeout=5)
+        wait_for(lambda: b.leading, timeout=15)
         start_b = next(t for who, what, t in events if who == "b" and what == "start")
         assert start_b > stop_t    # never two leaders at once
     finally:
