@@ -78,7 +78,46 @@ def parse_args():
                          "keeps a finished wave's 256 result writers from starving the next wave's ramp "
                          "(GPU gap before its first prefill 230-440 -> 140-170 ms, profiles/wave_timeline_sinks_8b.jsonl)")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--cpu", action="store_true",
+                    help="CPU rehearsal (gloo, tiny models): allows --gpus N > 1 on a host without N GPUs")
     return ap.parse_args()
+
+
+def launch_ranks(a) -> int:
+    """``--gpus N`` with no outer torchrun (WORLD_SIZE unset): start N rank processes
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* on 127.0.0.1) as plain children of this
+    process, which never touches the GPU itself (device_count() does not initialise HIP
+    here, and nothing is exec'd). Rank 0 prints the JSON line on the inherited stdout;
+    the exit code is the first non-zero rank exit code."""
+    import socket
+    import subprocess
+
+    if not a.cpu:
+        import torch
+
+        have = torch.cuda.device_count()
+        if have < a.gpus:
+            print(f"bench.py: --gpus {a.gpus} needs {a.gpus} visible GPUs, found {have} "
+                  "(--cpu for a gloo CPU rehearsal)", file=sys.stderr, flush=True)
+            return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    kids = []
+    for r in range(a.gpus):
+        env = dict(os.environ)
+        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus), LOCAL_WORLD_SIZE=str(a.gpus),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), OAMD_BENCH_LAUNCHED="1")
+        kids.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    rc = 0
+    for k in kids:
+        c = k.wait()
+        if c != 0 and rc == 0:
+            rc = c
+            for o in kids:   # one rank failed: the others would block in a collective
+                if o.poll() is None:
+                    o.terminate()
+    return rc
 
 
 SHARD_TAG = "OAMD_SHARD"  # protocol lines on a child shard's stdout
@@ -114,6 +153,8 @@ def shard_read(kid, what: str) -> str:
 def main() -> int:
     a = parse_args()
     child = a.shard_index is not None
+    if not child and a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(a)
     if child:   # a child shard dies with its rank process (torchrun only signals its own workers)
         try:
             import ctypes
@@ -188,6 +229,14 @@ def main() -> int:
 
     info = init_from_env(backend="gloo" if share else None)
     rank, world, local = info.rank, info.world, (0 if share else info.local_rank)
+    if not child:
+        # the job must really span --gpus ranks (one per GPU): a launch that silently
+        # measured one GPU, or ranks sharing a device, is an error, not a data point
+        pg_world = dist.get_world_size() if dist.is_initialized() else 1
+        if pg_world != a.gpus or world != a.gpus:
+            raise SystemExit(f"bench.py: --gpus {a.gpus} but the process group has {pg_world} ranks")
+        if info.backend == "nccl" and not share and torch.cuda.device_count() < world:
+            raise SystemExit(f"bench.py: {world} RCCL ranks but only {torch.cuda.device_count()} GPUs")
     if child:   # a child shard: the parent rank's GPU, no process group of its own
         rank, local = int(os.environ["OAMD_BENCH_RANK"]), (0 if share else int(os.environ["OAMD_BENCH_LOCAL"]))
     if torch.cuda.is_available():
@@ -460,7 +509,11 @@ def main() -> int:
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev if info.backend == "nccl" else "cpu")
     p50_local = statistics.median(lat) if lat else float("nan")
     p50 = torch.tensor([p50_local], dtype=torch.float64, device=el.device)
+    per_rank_s = [elapsed]
     if world > 1:
+        allel = [torch.zeros_like(el) for _ in range(world)]
+        dist.all_gather(allel, el)
+        per_rank_s = [float(t.item()) for t in allel]
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         dist.all_reduce(p50, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
@@ -492,6 +545,12 @@ def main() -> int:
                    "prefill_graph_buckets": stats1["prefill_graph_buckets"],
                    "decode_tok_s_per_gpu": round(dtoks / elapsed, 1), "outcomes": counter["outcomes"],
                    "dfa_states": stats1["dfa_states"], "timed_monotonic_ns": [mono0, mono1],
+                   "rccl_world": dist.get_world_size() if dist.is_initialized() else 1,
+                   "dist_backend": info.backend,
+                   "launcher": "bench.py" if os.environ.get("OAMD_BENCH_LAUNCHED") else
+                               ("torchrun" if world > 1 else "single"),
+                   "per_rank_elapsed_s": [round(x, 3) for x in per_rank_s],
+                   "per_rank_analyses_s": [round(a.batch * a.shards * a.steps / x, 3) for x in per_rank_s],
                    "host_max_rss_gb": {"rank": round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20, 2),
                                        "child_shards": round(resource.getrusage(resource.RUSAGE_CHILDREN).ru_maxrss
                                                              / 2**20, 2)}},

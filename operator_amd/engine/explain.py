@@ -111,12 +111,15 @@ class EngineLoop(threading.Thread):
                 # the replica's device state is inconsistent (e.g. a TP peer never arrived:
                 # no device sync, it could wait forever): fail every waiter and stop
                 # serving; the pool worker exits and is respawned
-                for r in list(self.llm.running) + list(self.llm.waiting):
+                for r in (list(self.llm.running) + list(getattr(self.llm, "_prefilling", []))
+                          + list(self.llm.waiting)):
                     r.error = f"engine failure: {e}"
                     r.done = True
                     r.event.set()
                 self.llm.running.clear()
                 self.llm.waiting.clear()
+                if hasattr(self.llm, "_prefilling"):
+                    self.llm._prefilling = []
                 self.fatal = e
                 return
 

@@ -81,8 +81,17 @@ def build_explain_service(s: Settings, metrics=None, tp=None):
     from operator_amd.engine.explain import ExplainEngine
 
     extra = [parse_model_spec(x) for x in s.engine.extra_models] if (tp is None or tp.world == 1) else []
+
+    def warm(llm):
+        # capture the decode / prefill graphs now, before the controller starts watching:
+        # a lazy capture mid-wave stalls the engine loop and runs under the global capture
+        # mode while the scan thread issues GPU work (as the pool worker does, pool.py)
+        if s.engine.warmup_graphs and (tp is None or tp.world == 1):
+            llm.warmup()
+
     if not extra:
         _, _, llm, tok = build_llm(s, tp=tp)
+        warm(llm)
         ee = ExplainEngine(llm, tok, model_id=s.engine.model, max_prompt_tokens=s.engine.max_prompt_tokens,
                            ignore_eos=s.engine.ignore_eos)
         return service.LocalExplainService(ee, metrics)
@@ -94,6 +103,7 @@ def build_explain_service(s: Settings, metrics=None, tp=None):
         sm.engine.model, sm.engine.model_path = name, path
         sm.engine.kv_cache_gb = s.engine.kv_cache_gb / (1 + len(extra))
         _, _, llm, tok = build_llm(sm, tp=tp)
+        warm(llm)
         ee = ExplainEngine(llm, tok, model_id=name, max_prompt_tokens=s.engine.max_prompt_tokens,
                            ignore_eos=s.engine.ignore_eos)
         services[name] = service.LocalExplainService(ee, metrics)

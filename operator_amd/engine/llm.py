@@ -305,6 +305,9 @@ class LLMEngine:
         self._active: _BucketState | None = None   # bucket whose device state matches self.running
         self.waiting: deque[GenRequest] = deque()
         self.running: list[GenRequest] = []
+        # the batch between _admit (pages allocated, off `waiting`) and its append to
+        # `running`: abort_all must release it too if the prefill raises
+        self._prefilling: list[GenRequest] = []
         self.stats = EngineStats()
         self._rid = itertools.count()
         self._graphs: dict[tuple[int, int], _DecodeGraph] = {}
@@ -373,8 +376,8 @@ class LLMEngine:
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
         with self._lock:
-            reqs = list(self.running) + list(self.waiting)
-            self.running, self.waiting = [], deque()
+            reqs = list({id(r): r for r in (*self.running, *self._prefilling, *self.waiting)}.values())
+            self.running, self.waiting, self._prefilling = [], deque(), []
         for r in reqs:
             if r.pages:
                 self.kv.allocator.release(r.pages)
@@ -474,12 +477,15 @@ class LLMEngine:
                 r.pages = self.kv.allocator.alloc(need)
                 self.waiting.popleft()
                 out.append(r)
+                self._prefilling = out
                 toks += len(r.prompt)
         return out
 
     def _prefill(self, batch: list[GenRequest]) -> None:
+        self._prefilling = batch
         with trace_range(f"prefill[{len(batch)}]"):
             self._prefill_impl(batch)
+        self._prefilling = []
 
     def _prefill_impl(self, batch: list[GenRequest]) -> None:
         t0 = time.perf_counter()

@@ -180,9 +180,24 @@ class MultiModelExplainService:
         for i, (r, c) in enumerate(items):
             svc = self.pick(c)
             groups.setdefault(id(svc), (svc, []))[1].append(i)
-        for svc, idx in groups.values():   # one continuous batch per model
-            for i, res in zip(idx, svc.explain_many([items[i] for i in idx])):
-                out[i] = res
+        gl = list(groups.values())
+        if len(gl) == 1:
+            svc, idx = gl[0]
+            return svc.explain_many(items)
+
+        def run(svc, idx):   # one continuous batch per model, all models at once
+            try:
+                for i, res in zip(idx, svc.explain_many([items[i] for i in idx])):
+                    out[i] = res
+            except Exception as e:  # noqa: BLE001 - reported per item, like the engines do
+                for i in idx:
+                    out[i] = e
+
+        ts = [threading.Thread(target=run, args=g, name="explain-group", daemon=True) for g in gl]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
         return out
 
     def complete(self, prompt=None, messages=None, model: str | None = None, **kw) -> dict:

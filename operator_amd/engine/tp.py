@@ -33,6 +33,10 @@ import torch.distributed as dist
 from .llm import GenRequest, LLMEngine
 
 
+class _FatalTPError(RuntimeError):
+    fatal = True
+
+
 def control_group(tp_group):
     """A gloo group over the TP ranks for host-side control messages."""
     ranks = getattr(tp_group, "ranks", None)
@@ -94,7 +98,20 @@ class TPLLMEngine(LLMEngine):
               [("c", r.rid) for r in canc]
         self._bcast(msg)
         self._apply(msg, new)
-        return self._step_and_forget()
+        try:
+            return self._step_and_forget()
+        except BaseException as e:
+            # A step that failed on this rank only (OOM, a kernel error) leaves the peers
+            # inside the same step's collectives, or one step ahead of a leader that would
+            # abort and prefill a fresh batch: RCCL has no device-side timeout, so a
+            # local abort_all could hang the replica. Every TP step error is fatal: the
+            # replica stops and the pool respawns it.
+            if self.tp_group is not None and self.tp_group.world > 1:
+                try:
+                    e.fatal = True
+                except AttributeError:
+                    raise _FatalTPError(str(e)) from e
+            raise
 
     def close(self) -> None:
         """Release the followers (collective over the control group)."""

@@ -112,6 +112,46 @@ def test_fp8_kv_cache_tracks_bf16_cache():
     assert sum(a == b for a, b in zip(outs["f32"], outs["fp8"])) >= 4, outs
 
 
+def test_engine_prefill_failure_releases_pages():
+    """A step that raises during the PREFILL (the batch is off `waiting`, pages
+    allocated, not yet `running`) still returns every page and fails the batch."""
+    from operator_amd.engine.explain import EngineLoop
+
+    cfg = get_config("tiny")
+    m = LlamaModel(cfg, device="cpu", dtype=torch.float32).init_random(seed=4)
+    kv = PagedKVCache(cfg.layers, 32, cfg.kv_heads, cfg.head_dim, 16, device="cpu", dtype=torch.float32)
+    eng = LLMEngine(m, kv, max_batch=4, max_context=256, use_graphs=False)
+    real, calls = m.forward, {"n": 0}
+
+    def flaky(fb, kv_):
+        calls["n"] += 1
+        if calls["n"] == 1:
+            assert fb.is_prefill
+            raise RuntimeError("HIP out of memory (injected in prefill)")
+        return real(fb, kv_)
+
+    m.forward = flaky
+    loop = EngineLoop(eng)
+    loop.start()
+    try:
+        first = [GenRequest(list(range(1, 30)), max_tokens=8, temperature=0.0, ignore_eos=True) for _ in range(3)]
+        for r in first:
+            eng.submit(r)
+        loop.notify()
+        for r in first:
+            assert r.event.wait(60)
+        assert all(r.error and "out of memory" in r.error for r in first)
+        assert kv.allocator.free == kv.num_pages and loop.fatal is None
+        again = GenRequest(list(range(1, 30)), max_tokens=4, temperature=0.0, ignore_eos=True)
+        eng.submit(again)
+        loop.notify()
+        assert again.event.wait(60) and again.error is None and len(again.output) == 4
+        assert kv.allocator.free == kv.num_pages
+    finally:
+        loop.stop()
+        loop.join(10)
+
+
 def test_engine_step_failure_releases_pages_and_keeps_serving():
     """A step that raises (e.g. out of memory) fails the requests it held, returns
     their KV pages and leaves the engine loop serving the next requests."""

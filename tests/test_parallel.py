@@ -80,33 +80,6 @@ def test_tp2_matches_tp1(tmp_path):
     assert got["out"] == [r.output for r in reqs]
 
 
-def _dp_worker(rank, world, port, out_dir):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank))
-    torch.set_num_threads(1)
-    from operator_amd.parallel.dp import DPRouter
-    from operator_amd.parallel.comm import init_from_env
-
-    init_from_env(backend="gloo")
-    router = DPRouter()
-    items = [f"pod-{i}" for i in range(11)]
-    mine = router.shard(items)
-    results = [f"{x}@{rank}" for x in mine]
-    merged = router.gather(results)
-    if rank == 0:
-        torch.save(merged, os.path.join(out_dir, "dp.pt"))
-    dist.barrier()
-    dist.destroy_process_group()
-
-
-def test_dp_shard_and_gather(tmp_path):
-    port = _free_port()
-    mp.start_processes(_dp_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True, start_method="spawn")
-    merged = torch.load(tmp_path / "dp.pt", weights_only=True)
-    assert sorted(x.split("@")[0] for x in merged) == sorted(f"pod-{i}" for i in range(11))
-    assert {x.split("@")[1] for x in merged} == {"0", "1"}
-
-
 def test_bench_tp_script_two_ranks():
     """tools/bench_tp.py (BASELINE config 5 launcher) under torch.distributed.run:
     leader + follower lock-step through TPLLMEngine over gloo."""
@@ -134,6 +107,46 @@ def test_oneshot_disabled_without_gpu():
     assert g.enable_oneshot("cpu") is False
     t = torch.ones(4)
     assert g.all_reduce_(t) is t
+
+
+def test_bench_self_launches_ranks():
+    """`python bench.py --gpus 2` with no outer torchrun starts its two rank processes
+    itself (127.0.0.1 rendezvous); the JSON line reports the 2-rank job, not one rank."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--cpu", "--steps", "1", "--warmup", "1",
+           "--model", "tiny", "--batch", "3", "--max-tokens", "4", "--prompt-tokens", "128", "--log-kb", "4",
+           "--patterns", "40"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=root, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
+    assert out["detail"]["rccl_world"] == 2 and out["detail"]["launcher"] == "bench.py"
+    assert len(out["detail"]["per_rank_elapsed_s"]) == 2
+    assert out["detail"]["outcomes"] == {"ai-complete": 3}   # rank 0's own wave
+
+
+def test_bench_refuses_missing_gpus():
+    """Without --cpu, --gpus N on a host with fewer than N GPUs fails instead of
+    measuring one device."""
+    import subprocess
+    import sys
+
+    import torch
+
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("host has the GPUs")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"], capture_output=True,
+                       text=True, timeout=120, cwd=root, env=env)
+    assert r.returncode != 0 and "visible GPUs" in r.stderr
 
 
 @pytest.mark.parametrize("shards", [1, 2])
