@@ -175,6 +175,27 @@ void gemm_decode(const at::Tensor& x, const at::Tensor& w, const c10::optional<a
                        (int)bn, (int)bm, silu_gu, w_tiled, (int)stages, cur_stream()));
 }
 
+void gemm_tile(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const c10::optional<at::Tensor>& bias,
+               bool silu_gu, int64_t variant) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(y); CHECK_CONTIG(x); CHECK_CONTIG(w);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 2, "x [M,K], w [N,K], y [M,N]");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K, "gemm_tile: w [N, K] must match x [M, K]");
+  TORCH_CHECK(M >= 1 && K >= 64 && K % 64 == 0 && N % 16 == 0, "gemm_tile: K % 64 == 0, N % 16 == 0");
+  TORCH_CHECK(y.size(0) == M && y.size(1) == (silu_gu ? N / 2 : N) && y.stride(1) == 1 && y.stride(0) % 4 == 0,
+              "gemm_tile: y [M, N] (N/2 with silu_gu), unit column stride, 8-B aligned rows");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(y.data_ptr()) % 8 == 0, "gemm_tile: y must be 8-B aligned");
+  TORCH_CHECK(!silu_gu || (N % 128 == 0 && !bias.has_value()), "gemm_tile: SwiGLU needs N % 128, no bias");
+  if (bias.has_value()) {
+    CHECK_BF16(*bias); CHECK_CONTIG(*bias);
+    TORCH_CHECK(bias->numel() == N, "gemm_tile: bias [N]");
+  }
+  TORCH_CHECK(M * K < (1LL << 40) && N * K < (1LL << 40) && M < (1LL << 31) && N < (1LL << 31), "gemm too large");
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  RC(oamd::gemm_tile(ptr<bf16_t>(x), ptr<bf16_t>(w), ptr<bf16_t>(y), optr<bf16_t>(bias), (int)M, (int)N, (int)K,
+                     (int)y.stride(0), silu_gu, (int)variant, cur_stream()));
+}
+
 void gemm_skinny(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& y_opt,
                  const c10::optional<at::Tensor>& p, int64_t splits, bool silu_gu) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
@@ -386,6 +407,8 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("p") = pybind11::none(), pybind11::arg("splits") = 1, pybind11::arg("bn") = 64,
         pybind11::arg("bm") = 0, pybind11::arg("silu_gu") = false, pybind11::arg("w_tiled") = false,
         pybind11::arg("stages") = 3);
+  m.def("gemm_tile", &gemm_tile, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"),
+        pybind11::arg("bias") = pybind11::none(), pybind11::arg("silu_gu") = false, pybind11::arg("variant") = 0);
   m.def("gemm_skinny", &gemm_skinny, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"),
         pybind11::arg("p") = pybind11::none(), pybind11::arg("splits") = 1, pybind11::arg("silu_gu") = false);
   m.def("attn_prefill", &attn_prefill, pybind11::arg("q"), pybind11::arg("k"), pybind11::arg("v"),

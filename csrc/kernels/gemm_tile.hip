@@ -1,0 +1,290 @@
+// Compute-bound GEMM for prefill projections and the lm_head:
+//   Y[M, N] = X[M, K] . W[N, K]^T     bf16 in, fp32 accumulate, bf16 out
+// (SURVEY.md §2.4 N7 "prefill is compute-bound tiles (256² 8-phase template)";
+// replaces the external LLM behind J/service/AIInterfaceRestClient.java:37-39).
+//
+// Structure (cdna_hip_programming.md §5 "The 256² 8-phase template", T1-T5):
+//   * one 256 x 256 output tile per 512-thread workgroup (8 waves, 2 per SIMD),
+//     BK = 64, both operands staged global -> LDS by LDS-DMA
+//     (global_load_lds_dwordx4) into two 64 KiB buffers; every tile is split
+//     into four 16 KiB regions (X rows 0-127, W rows 0-127, W rows 128-255,
+//     X rows 128-255) that are loaded, waited for and recycled one at a time;
+//   * the K-tile is computed in four phases, one per (X half, W half) quadrant,
+//     16 MFMA v_mfma_f32_16x16x32_bf16 per wave each; a phase issues one region
+//     of the NEXT K-tile, so 1.5 tiles stay in flight with only 2 buffers and
+//     the LDS-DMA never drains inside the loop (counted vmcnt, raw s_barrier);
+//   * ping-pong: waves 4-7 run one barrier segment behind waves 0-3, so on
+//     every SIMD one wave issues its LDS fragment reads + DMA while the other
+//     runs its MFMA cluster (s_setprio 1 around it, T5);
+//   * the LDS image is lane-linear (DMA) with the st_16x32-style XOR swizzle
+//     applied to the global SOURCE chunk and the read address (rule 21):
+//     slot = chunk ^ ((row >> 1) & 7), conflict-free for ds_read_b128;
+//   * operands swapped in the MFMA (A = W fragment, B = X fragment) so each
+//     lane's accumulator holds 4 consecutive OUTPUT FEATURES of one token:
+//     8-byte stores, and a fused SwiGLU epilogue in registers when the gate|up
+//     weight is interleaved in 64-row blocks (wave wc owns gate rows
+//     wc*16..+16 and the matching up rows 64 + wc*16..+16 of every 128 rows);
+//   * XCD-aware, grouped tile order (T1 bijective remap, then GROUP_M m-tiles
+//     per n-tile) so the 32 tiles an XCD runs at once share X/W panels in L2.
+// M and N tails are handled by clamped loads and masked stores; K % 64 == 0.
+#include "common.h"
+#include "kernels.h"
+
+namespace oamd {
+
+namespace {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+
+constexpr int kT = 256;          // tile rows / cols
+constexpr int kBK = 64;          // K per tile step (one 128-B line per row)
+constexpr int kRegion = 16384;   // 128 rows x 128 B
+constexpr int kBuf = 4 * kRegion;
+constexpr int kGroupM = 8;
+
+enum { kEpiStore = 0, kEpiBias = 1, kEpiSilu = 2 };
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void seg_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+__device__ __forceinline__ uint2 pack4(f32x4 v) {
+  return make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+}
+
+}  // namespace
+
+template <int EPI, int PH>
+__global__ void __launch_bounds__(512) gemm_tile256_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
+                                                           bf16_t* __restrict__ Y, const bf16_t* __restrict__ bias,
+                                                           int M, int N, int K, int ldy) {
+  __shared__ __attribute__((aligned(1024))) char lds[2 * kBuf];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = w >> 2, wc = w & 3;
+
+  // ---- tile order: XCD-contiguous chunks, GROUP_M-row groups inside them
+  const int mt = (M + kT - 1) / kT, nt = (N + kT - 1) / kT;
+  const int nwg = mt * nt;
+  const int lid = xcd_remap(blockIdx.x, nwg);
+  const int gsz = kGroupM * nt;
+  const int first_m = (lid / gsz) * kGroupM;
+  const int gm = min(mt - first_m, kGroupM);
+  const int tm = first_m + (lid % gsz) % gm;
+  const int tn = (lid % gsz) / gm;
+  const int m0 = tm * kT, n0 = tn * kT;
+
+  // ---- LDS-DMA sources: region r (issue order 0 = X rows 0-127, 1 = W rows 0-127,
+  // 2 = W rows 128-255, 3 = X rows 128-255); wave w issues instructions q = w, w + 8
+  // of each region, lane l -> region row 8q + l/8, LDS slot l%8, global chunk swz
+  const int lrow = lane >> 3, lslot = lane & 7;
+  const bf16_t* src[4][2];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = 8 * (w + 8 * i) + lrow;
+      const int chunk = lslot ^ ((row >> 1) & 7);
+      const bool isx = (r == 0 || r == 3);
+      const int half = (r == 2 || r == 3) ? 128 : 0;
+      const int64_t grow = isx ? min(m0 + half + row, M - 1) : min(n0 + half + row, N - 1);
+      src[r][i] = (isx ? X : W) + grow * K + chunk * 8;
+    }
+  auto issue = [&](int r, int buf, int kt) {
+    char* dst = lds + buf * kBuf + r * kRegion;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds(src[r][i] + kt * kBK, (__attribute__((address_space(3))) void*)(dst + (w + 8 * i) * 1024),
+                                       16, 0, 0);
+  };
+
+  // ---- fragment read offsets (bytes within a region); row & 15 == lane & 15 for
+  // every fragment, so the swizzle term depends on the lane only
+  const int l15 = lane & 15, lq = lane >> 4, sw = (l15 >> 1) & 7;
+  const int xo0 = (g * 64 + l15) * 128 + ((lq ^ sw) << 4);         // k-substep 0
+  const int xo1 = (g * 64 + l15) * 128 + (((4 + lq) ^ sw) << 4);   // k-substep 1
+  const int wo0 = (wc * 16 + l15) * 128 + ((lq ^ sw) << 4);
+  const int wo1 = (wc * 16 + l15) * 128 + (((4 + lq) ^ sw) << 4);
+
+  f32x4 acc[2][2][4][2];   // [X half][W half][token block][feature block (gate, up)]
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) acc[h][f][b][e] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  u16x8 xf[4][2], wf0[2][2], wf1[2][2];
+  auto read_x = [&](const char* reg) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      xf[b][0] = *reinterpret_cast<const u16x8*>(reg + xo0 + b * 2048);
+      xf[b][1] = *reinterpret_cast<const u16x8*>(reg + xo1 + b * 2048);
+    }
+  };
+  auto read_w = [&](const char* reg, u16x8 (&wf)[2][2]) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      wf[e][0] = *reinterpret_cast<const u16x8*>(reg + wo0 + e * 8192);
+      wf[e][1] = *reinterpret_cast<const u16x8*>(reg + wo1 + e * 8192);
+    }
+  };
+  auto mfma_q = [&](f32x4 (&a)[4][2], u16x8 (&wf)[2][2]) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+          a[b][e] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, wf[e][s]),
+                                                            __builtin_bit_cast(bf16x8_t, xf[b][s]), a[b][e], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  const int T = K / kBK;
+  // prologue: all four regions of K-tile 0; X0 and W0 retired before the first reads
+#pragma unroll
+  for (int r = 0; r < 4; ++r) issue(r, 0, 0);
+  if constexpr (PH == 2) vm_wait<2>(); else vm_wait<4>();
+  seg_barrier();
+  if (g == 1) seg_barrier();   // ping-pong: waves 4-7 one segment behind
+
+  if constexpr (PH == 2) {
+    // two phases per K-tile (32 MFMAs each): A = X0 x {W0, W1}, B = X1 x {W0, W1};
+    // A issues X0 / W0 of tile t+1, B issues W1 / X1; half the barriers of PH = 4
+    for (int t = 0; t < T; ++t) {
+      const char* cur = lds + (t & 1) * kBuf;
+      const int nb = (t + 1) & 1;
+      const bool more = t + 1 < T;
+      read_x(cur + 0 * kRegion);
+      read_w(cur + 1 * kRegion, wf0);
+      read_w(cur + 2 * kRegion, wf1);
+      if (more) { issue(0, nb, t + 1); issue(1, nb, t + 1); }
+      if (g == 1) { if (more) vm_wait<4>(); else vm_wait<0>(); }
+      seg_barrier();
+      mfma_q(acc[0][0], wf0);
+      mfma_q(acc[0][1], wf1);
+      if (g == 0) { if (more) vm_wait<4>(); else vm_wait<0>(); }
+      seg_barrier();
+      read_x(cur + 3 * kRegion);
+      if (more) { issue(2, nb, t + 1); issue(3, nb, t + 1); }
+      if (g == 1 && more) vm_wait<2>();
+      seg_barrier();
+      mfma_q(acc[1][0], wf0);
+      mfma_q(acc[1][1], wf1);
+      if (g == 0 && more) vm_wait<2>();
+      seg_barrier();
+    }
+  } else
+  for (int t = 0; t < T; ++t) {
+    const char* cur = lds + (t & 1) * kBuf;
+    const int nb = (t + 1) & 1;
+    const bool more = t + 1 < T;
+    // -- phase 1: quadrant (X0, W0); issue X0 of tile t+1
+    read_x(cur + 0 * kRegion);
+    read_w(cur + 1 * kRegion, wf0);
+    if (more) issue(0, nb, t + 1);
+    if (g == 1) { if (more) vm_wait<4>(); else vm_wait<2>(); }
+    seg_barrier();
+    mfma_q(acc[0][0], wf0);
+    if (g == 0) { if (more) vm_wait<4>(); else vm_wait<2>(); }
+    seg_barrier();
+    // -- phase 2: quadrant (X0, W1); issue W0 of tile t+1
+    read_w(cur + 2 * kRegion, wf1);
+    if (more) issue(1, nb, t + 1);
+    if (g == 1) { if (more) vm_wait<4>(); else vm_wait<0>(); }
+    seg_barrier();
+    mfma_q(acc[0][1], wf1);
+    if (g == 0) { if (more) vm_wait<4>(); else vm_wait<0>(); }
+    seg_barrier();
+    // -- phase 3: quadrant (X1, W0); issue W1 of tile t+1
+    read_x(cur + 3 * kRegion);
+    if (more) issue(2, nb, t + 1);
+    seg_barrier();
+    mfma_q(acc[1][0], wf0);
+    seg_barrier();
+    // -- phase 4: quadrant (X1, W1) from registers; issue X1 of tile t+1 and retire
+    // X0 / W0 of tile t+1 before phase 1 reads them
+    if (more) issue(3, nb, t + 1);
+    if (g == 1 && more) vm_wait<4>();
+    seg_barrier();
+    mfma_q(acc[1][1], wf1);
+    if (g == 0 && more) vm_wait<4>();
+    seg_barrier();
+  }
+  if (g == 0) seg_barrier();   // pairs with the waves 4-7 stagger barrier
+
+  // ---- epilogue: lane holds features 4*lq .. 4*lq+3 of token l15 per fragment
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int tok = m0 + h * 128 + g * 64 + b * 16 + l15;
+      if (tok >= M) continue;
+      bf16_t* yrow = Y + (int64_t)tok * ldy;
+#pragma unroll
+      for (int f = 0; f < 2; ++f) {
+        if constexpr (EPI == kEpiSilu) {
+          // interleaved gate|up: 128-row block f = 64 gate rows then their 64 up rows
+          const int col = (n0 >> 1) + f * 64 + wc * 16 + 4 * lq;
+          if (2 * col >= N) continue;
+          const f32x4 gt = acc[h][f][b][0], up = acc[h][f][b][1];
+          f32x4 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float gg = bf2f(f2bf(gt[r]));
+            const float uu = bf2f(f2bf(up[r]));
+            const float sg = bf2f(f2bf(gg / (1.f + __expf(-gg))));
+            o[r] = sg * uu;
+          }
+          *reinterpret_cast<uint2*>(yrow + col) = pack4(o);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int col = n0 + f * 128 + e * 64 + wc * 16 + 4 * lq;
+            if (col >= N) continue;
+            f32x4 v = acc[h][f][b][e];
+            if constexpr (EPI == kEpiBias) {
+              const uint2 bb = *reinterpret_cast<const uint2*>(bias + col);
+              v[0] += __uint_as_float(bb.x << 16);
+              v[1] += __uint_as_float(bb.x & 0xffff0000u);
+              v[2] += __uint_as_float(bb.y << 16);
+              v[3] += __uint_as_float(bb.y & 0xffff0000u);
+            }
+            *reinterpret_cast<uint2*>(yrow + col) = pack4(v);
+          }
+        }
+      }
+    }
+}
+
+int gemm_tile(const bf16_t* X, const bf16_t* W, bf16_t* Y, const bf16_t* bias, int M, int N, int K, int ldy,
+              bool silu_gu, int variant, hipStream_t stream) {
+  if (M < 1 || N < 16 || N % 16 != 0 || K < kBK || K % kBK != 0) return -1;
+  if (silu_gu && (N % 128 != 0 || bias != nullptr)) return -2;
+  if (ldy < (silu_gu ? N / 2 : N)) return -3;
+  const int nwg = ((M + kT - 1) / kT) * ((N + kT - 1) / kT);
+#define OAMD_TILE(PH)                                                                                   \
+  if (silu_gu) gemm_tile256_kernel<kEpiSilu, PH><<<nwg, 512, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);  \
+  else if (bias) gemm_tile256_kernel<kEpiBias, PH><<<nwg, 512, 0, stream>>>(X, W, Y, bias, M, N, K, ldy); \
+  else gemm_tile256_kernel<kEpiStore, PH><<<nwg, 512, 0, stream>>>(X, W, Y, bias, M, N, K, ldy)
+  if (variant == 2) { OAMD_TILE(2); } else { OAMD_TILE(4); }
+#undef OAMD_TILE
+  OAMD_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace oamd

@@ -20,9 +20,9 @@ Tensor parallelism is Megatron-style: QKV and gate|up column-parallel (whole
 heads / whole FFN columns per rank), O and down row-parallel followed by one
 all-reduce each (2 per layer), embeddings replicated (2.1 GB at 70B, fits the
 288 GB HBM trivially), lm_head vocab-parallel.
-Decode-bucket GEMMs go to the gfx950 gemm_decode kernel where it wins (ops.linear),
-prefill GEMMs to hipBLASLt through torch; everything else is a
-hand-written HIP kernel (operator_amd.ops).
+Decode-bucket GEMMs go to the gfx950 gemm_skinny / gemm_decode kernels, prefill GEMMs
+and the lm_head to the 256x256-tile gemm_tile kernel (fused bias / SwiGLU epilogues);
+everything else is a hand-written HIP kernel too (operator_amd.ops).
 """
 from __future__ import annotations
 
@@ -33,7 +33,6 @@ import os
 from dataclasses import dataclass, field
 
 import torch
-import torch.nn.functional as F
 
 from operator_amd import ops
 from operator_amd.ops import reference as ref
@@ -248,10 +247,10 @@ class LlamaModel:
             kc, vc = kv.layer(i)
             # a split-K decode QKV projection hands its fp32 slabs to rope_kv, which sums
             # them per element (no separate reduce kernel) and adds a Qwen2 bias before
-            # rounding; a prefill bias rides hipBLASLt's epilogue
+            # rounding; a prefill bias rides the tile GEMM's epilogue
             bias = lw.bqkv
             if bias is not None and fb.is_prefill and lw.sqkv is None:
-                qkv, bias = F.linear(x, lw.wqkv, bias), None
+                qkv, bias = ops.linear(x, lw.wqkv, bias=bias), None
             else:
                 qkv = self._lin(x, lw.wqkv, lw.sqkv, defer=True)
             q, k, v = ops.rope_kv(qkv, fb.positions, self.cos, self.sin, self.hq, self.hkv, kc, vc, fb.slots,

@@ -19,7 +19,7 @@ __all__ = [
     "rmsnorm", "silu_mul", "embedding", "rope_kv", "attn_prefill", "attn_decode", "sample",
     "kernels", "patterns", "native_available", "reference", "prefill_work_list", "prefill_block_q", "prefill_variant", "decode_splits",
     "decode_workspace", "linear", "gemm_splits", "gemm_plan", "gate_up_silu", "interleave_gate_up",
-    "quantize_fp8", "linear_fp8", "fp8_plan", "SplitK",
+    "quantize_fp8", "linear_fp8", "fp8_plan", "SplitK", "linear_tile", "tile_ok", "BLAS_CALLS",
 ]
 
 DECODE_MIN_SPLIT_TOKENS = 256  # never split a sequence into pieces shorter than this
@@ -108,6 +108,8 @@ def gate_up_silu(x: torch.Tensor, wgu: torch.Tensor, block: int | None) -> torch
             y = torch.empty(M, N // 2, dtype=x.dtype, device=x.device)
             kernels().gemm_decode(x, wgu, y, None, 1, 128, bm, True, False, ns)
             return y
+    if block == 64 and tile_ok(x, wgu) and N % 128 == 0:
+        return linear_tile(x, wgu, silu_gu=True)   # prefill: SwiGLU fused into the tile epilogue
     return silu_mul(linear(x, wgu), block=block)
 
 
@@ -246,6 +248,13 @@ def row_tile(M: int) -> int:
     return next(b for b in (256, 128, 64) if M % b == 0)
 
 
+def _measured_blas(M: int, N: int, K: int) -> bool:
+    """The tuned table measured hipBLASLt fastest for this decode-bucket shape (small-M
+    GEMMs that neither the decode kernels nor the 256-row tile kernel win)."""
+    t = _gemm_table_get()
+    return t.get(("skinny", M, N, K) if M <= SKINNY_MAX_M else (M, N, K)) == "blas"
+
+
 def gemm_splits(M: int, N: int, K: int) -> int:
     """Heuristic split-K ways for gemm_decode (shapes not in the tuned table): the
     smallest S | 8 whose (N/64) x S blocks reach one block per CU (256)."""
@@ -265,7 +274,7 @@ def gemm_plan(M: int, N: int, K: int):
     if M % 64 or N % 64 or K % 64 or M > 256:
         return None
     t = _gemm_table_get().get((M, N, K))
-    if t == "blas":
+    if t in ("blas", "tile"):   # hipBLASLt / the 256x256-tile kernel (linear decides which)
         return None
     if t is not None:
         return tuple(t)
@@ -292,16 +301,55 @@ def skinny_plan(M: int, N: int, K: int) -> int | None:
     return S
 
 
+BLAS_CALLS = {"n": 0}   # GPU GEMMs that fell back to hipBLASLt (tests assert it stays 0 on model shapes)
+
+
+def _blas(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None, bias: torch.Tensor | None):
+    if x.is_cuda:
+        BLAS_CALLS["n"] += 1
+        if os.environ.get("OAMD_FORBID_BLAS") == "1":
+            raise RuntimeError(f"hipBLASLt fallback for x {tuple(x.shape)} {x.dtype}, w {tuple(w.shape)} "
+                               "(OAMD_FORBID_BLAS=1)")
+    if out is not None:
+        return F.linear(x, w, bias, out=out) if bias is None else out.copy_(F.linear(x, w, bias))
+    return F.linear(x, w, bias)
+
+
+def tile_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+    """Shapes the 256x256-tile gfx950 GEMM (gemm_tile) takes: bf16, K % 64, N % 16."""
+    return (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.dim() == 2
+            and x.is_contiguous() and w.is_contiguous() and x.shape[1] % 64 == 0 and w.shape[0] % 16 == 0
+            and x.shape[0] >= 1)
+
+
+def linear_tile(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None,
+                bias: torch.Tensor | None = None, silu_gu: bool = False) -> torch.Tensor:
+    """Prefill / lm_head GEMM on the compute-bound gfx950 tile kernel (256 x 256 tiles,
+    LDS-DMA ping-pong pipeline; fused bias or SwiGLU epilogue)."""
+    M = x.shape[0]
+    N = w.shape[0]
+    y = out if out is not None else torch.empty(M, N // 2 if silu_gu else N, dtype=x.dtype, device=x.device)
+    kernels().gemm_tile(x, w, y, bias, silu_gu)
+    return y
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None, splits: int | None = None,
            partial: torch.Tensor | None = None, bn: int | None = None, bm: int | None = None,
-           defer_reduce: bool = False, stages: int | None = None):
-    """y = x @ w^T (bf16). Decode-bucket shapes run on gfx950 kernels where they beat
-    hipBLASLt: M <= 32 on the weight-streaming gemm_skinny, M in {64, 128, 256} on the
-    LDS-staged gemm_decode (tuned tables); everything else (prefill, odd shapes, CPU)
-    on hipBLASLt / torch."""
+           defer_reduce: bool = False, stages: int | None = None, bias: torch.Tensor | None = None):
+    """y = x @ w^T (+ bias) in bf16 on the gfx950 kernels: M <= 32 decode buckets on the
+    weight-streaming gemm_skinny, M in {64, 128, 256} on the LDS-staged split-K
+    gemm_decode (tuned tables), everything else (prefill, the lm_head, biased
+    projections) on the 256x256-tile gemm_tile. hipBLASLt only for shapes none of them
+    takes (K % 64 != 0, N % 16 != 0, non-bf16); CPU tensors on torch."""
     M, K = x.shape
     N = w.shape[0]
     plan = None
+    if bias is not None:
+        if tile_ok(x, w) and (out is None or out.stride(1) == 1):
+            return linear_tile(x, w, out, bias)
+        return _blas(x, w, out, bias)
+    if x.is_cuda and bm is None and bn is None and splits is None and _measured_blas(M, N, K):
+        return _blas(x, w, out, None)
     if (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous() and M <= SKINNY_MAX_M
             and bm is None and bn is None):
         S = splits or skinny_plan(M, N, K)
@@ -319,7 +367,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None, sp
         if plan is None and (splits or bn or bm) and M % 64 == 0 and M <= 256 and N % 64 == 0 and K % 64 == 0:
             plan = (row_tile(M), 64, 1)  # explicit request (tests / tuning)
     if plan is None:
-        return F.linear(x, w, out=out) if out is not None else F.linear(x, w)
+        if tile_ok(x, w) and (out is None or out.stride(1) == 1):
+            return linear_tile(x, w, out)
+        return _blas(x, w, out, None)
     bm, bn, S = bm or plan[0], bn or plan[1], splits or plan[2]
     ns = stages or (plan[3] if len(plan) > 3 else 3)
     if S > 1 and (partial is None or partial.numel() < S * M * N):

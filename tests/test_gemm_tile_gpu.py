@@ -1,0 +1,90 @@
+"""gfx950 256x256-tile GEMM (csrc/kernels/gemm_tile.hip: prefill projections and the
+lm_head) against the plain-PyTorch fp32 reference: M / N tails, every epilogue
+(store, bias, fused SwiGLU over the 64-row interleaved gate|up weight), strided
+outputs, and an asymmetric-operand layout check (cdna_hip_programming.md §3)."""
+import pytest
+import torch
+
+from operator_amd import ops
+from operator_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+VARIANTS = (4, 2)   # gemm_tile schedules: 4 or 2 phases per K-tile
+
+
+def _rand(*shape, scale=1.0):
+    return (torch.randn(*shape, device=DEV) * scale).to(torch.bfloat16)
+
+
+def _close(y, r, tol=2e-2):
+    torch.testing.assert_close(y.float(), r.float(), atol=tol, rtol=tol)
+
+
+@pytest.mark.parametrize("M", [1, 77, 256, 300, 1024])
+@pytest.mark.parametrize("N,K", [(16, 64), (272, 192), (512, 1024), (6144, 4096), (4096, 14336)])
+def test_gemm_tile_store_and_bias(M, N, K):
+    if M * N * K > 1024 * 6144 * 4096:
+        pytest.skip("covered by the smaller shapes")
+    torch.manual_seed(M * 7 + N + K)
+    x = _rand(M, K)
+    w = _rand(N, K, scale=0.05)
+    r = x.float() @ w.float().t()
+    b = _rand(N, scale=0.5)
+    for v in VARIANTS:
+        y = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        ops.kernels().gemm_tile(x, w, y, None, False, v)
+        _close(y, r)
+        yb = torch.empty_like(y)
+        ops.kernels().gemm_tile(x, w, yb, b, False, v)
+        _close(yb, r + b.float())
+
+
+def test_gemm_tile_layout_exact():
+    """Small-integer operands (exact in bf16 and fp32): every output element must be
+    bit-exact, which catches a transposed or shifted fragment / store map."""
+    M, N, K = 300, 528, 256
+    g = torch.Generator(device="cpu").manual_seed(3)
+    x = torch.randint(-3, 4, (M, K), generator=g).to(DEV, torch.bfloat16)
+    w = torch.randint(-3, 4, (N, K), generator=g).to(DEV, torch.bfloat16)
+    w[5, :] = 0
+    w[5, 17] = 1   # column 5 of y = x[:, 17]
+    r = x.float() @ w.float().t()     # exact in fp32; y is that rounded once to bf16
+    for v in VARIANTS:
+        y = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        ops.kernels().gemm_tile(x, w, y, None, False, v)
+        assert torch.equal(y, r.to(torch.bfloat16))
+        assert torch.equal(y[:, 5].float(), x[:, 17].float())
+
+
+@pytest.mark.parametrize("M", [5, 256, 513])
+@pytest.mark.parametrize("inter,K", [(64, 128), (192, 256), (1536, 1024)])
+def test_gemm_tile_silu(M, inter, K):
+    torch.manual_seed(inter + M)
+    x = _rand(M, K)
+    g = _rand(inter, K, scale=0.05)
+    u = _rand(inter, K, scale=0.05)
+    wgu = ops.interleave_gate_up(g, u)
+    gg = (x.float() @ g.float().t()).to(torch.bfloat16)
+    uu = (x.float() @ u.float().t()).to(torch.bfloat16)
+    r = ref.silu_mul(torch.cat([gg, uu], 1), None)
+    for v in VARIANTS:
+        y = torch.empty(M, inter, dtype=torch.bfloat16, device=DEV)
+        ops.kernels().gemm_tile(x, wgu, y, None, True, v)
+        _close(y, r, 3e-2)
+
+
+def test_gemm_tile_strided_output():
+    """Writing into a column slice of a wider buffer (ldy > N) leaves the rest alone."""
+    M, N, K = 130, 256, 128
+    x, w = _rand(M, K), _rand(N, K, scale=0.1)
+    buf = torch.full((M, N + 64), 7.0, dtype=torch.bfloat16, device=DEV)
+    ops.kernels().gemm_tile(x, w, buf[:, 32:32 + N])
+    _close(buf[:, 32:32 + N], x.float() @ w.float().t())
+    assert (buf[:, :32] == 7).all() and (buf[:, 32 + N:] == 7).all()
+
+
+def test_gemm_tile_rejects_bad_shapes():
+    x, w = _rand(8, 100), _rand(32, 100)
+    with pytest.raises(RuntimeError):
+        ops.kernels().gemm_tile(x, w, torch.empty(8, 32, dtype=torch.bfloat16, device=DEV))

@@ -307,3 +307,33 @@ def test_fp8_kv_cache_engine_tracks_bf16_cache():
     cos = torch.nn.functional.cosine_similarity(outs[torch.bfloat16].flatten(), outs[torch.float8_e4m3fn].flatten(),
                                                 dim=0)
     assert cos > 0.99, float(cos)
+
+
+def test_llama3_8b_prefill_and_lm_head_never_use_hipblaslt(monkeypatch):
+    """Every prefill projection (QKV, O, gate|up + SwiGLU, down) and the lm_head of the
+    Llama-3-8B shapes run on the hand-written gfx950 kernels: with OAMD_FORBID_BLAS=1 any
+    hipBLASLt fallback raises. Two layers of the real architecture, prefill batches of
+    1k and 4k packed tokens (tails included) and the M = 64 / 256 decode buckets."""
+    from dataclasses import replace
+
+    from operator_amd import ops
+
+    monkeypatch.setenv("OAMD_FORBID_BLAS", "1")
+    cfg = replace(get_config("llama3-8b"), layers=2)
+    m = LlamaModel(cfg, device="cuda").init_random(seed=3)
+    kv = PagedKVCache(cfg.layers, 128, cfg.kv_heads, 128, 64, device="cuda")
+    n0 = ops.BLAS_CALLS["n"]
+    for lens in ([1024], [700, 1300, 2096]):
+        T = sum(lens)
+        ids = torch.randint(0, cfg.vocab_size, (T,), device="cuda")
+        pos = torch.cat([torch.arange(n) for n in lens]).cuda()
+        last = torch.tensor(lens).cumsum(0).cuda() - 1
+        fb = ForwardBatch(ids, pos, torch.full((T,), -1, dtype=torch.long, device="cuda"), True, last, seq_lens=lens)
+        lg = m.forward(fb, kv)
+        assert lg.shape == (len(lens), cfg.vocab_size) and torch.isfinite(lg.float()).all()
+    eng = LLMEngine(m, kv, max_batch=256, max_context=512, use_graphs=False)
+    for B in (64, 256):
+        reqs = [GenRequest(list(range(1, 17)), max_tokens=2, temperature=0.0, ignore_eos=True) for _ in range(B)]
+        eng.generate(reqs)
+        assert all(len(r.output) == 2 for r in reqs)
+    assert ops.BLAS_CALLS["n"] == n0
