@@ -64,6 +64,28 @@ class CustomAllReduce {
     TORCH_CHECK(rc == 0, "one-shot all-reduce launch failed rc=", rc);
   }
 
+  // residual += all_reduce(in) (bf16-rounded); y = rmsnorm(residual) * w — one launch.
+  void all_reduce_rmsnorm(const at::Tensor& in, at::Tensor& residual, const at::Tensor& w, at::Tensor& y, double eps) {
+    TORCH_CHECK(opened_ || world_ == 1, "CustomAllReduce: open() the peer handles first");
+    for (const at::Tensor* t : {&in, const_cast<const at::Tensor*>(&residual), &w, const_cast<const at::Tensor*>(&y)}) {
+      TORCH_CHECK(t->is_cuda() && t->device().index() == device_, "tensors must be on this device");
+      TORCH_CHECK(t->is_contiguous() && t->scalar_type() == at::kBFloat16, "bf16 contiguous tensors");
+    }
+    TORCH_CHECK(in.dim() == 2 && residual.sizes() == in.sizes() && y.sizes() == in.sizes(), "[rows, hidden] shapes");
+    TORCH_CHECK(w.numel() == in.size(1), "w [hidden]");
+    const int64_t rows = in.size(0), hidden = in.size(1);
+    TORCH_CHECK(hidden % 8 == 0 && hidden <= 16384, "hidden % 8 == 0 and <= 16384");
+    TORCH_CHECK(rows * hidden * 2 <= cap_, "size must be <= capacity");
+    const c10::hip::HIPGuardMasqueradingAsCUDA g(in.device());
+    const int rc = oamd::car_all_reduce_rmsnorm(in.data_ptr(), reinterpret_cast<oamd::bf16_t*>(residual.data_ptr()),
+                                                reinterpret_cast<const oamd::bf16_t*>(w.data_ptr()),
+                                                reinterpret_cast<oamd::bf16_t*>(y.data_ptr()), (int)rows, (int)hidden,
+                                                (float)eps, (int)rank_, (int)world_, bases_.data(), (size_t)cap_,
+                                                (int)blocks_, herr_dev_, timeout_s_,
+                                                c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream());
+    TORCH_CHECK(rc == 0, "one-shot all-reduce + rmsnorm launch failed rc=", rc);
+  }
+
   // Host read of the mapped error word: no device synchronisation, so the engine
   // can poll it after every decode window without draining its pipelined windows.
   int64_t error() const { return herr_ != nullptr ? oamd::car_error(herr_) : 0; }
@@ -113,6 +135,7 @@ void register_comm_bindings(pybind11::module_& m) {
       .def("handle", &CustomAllReduce::handle)
       .def("open", &CustomAllReduce::open)
       .def("all_reduce", &CustomAllReduce::all_reduce)
+      .def("all_reduce_rmsnorm", &CustomAllReduce::all_reduce_rmsnorm)
       .def("error", &CustomAllReduce::error)
       .def("reset", &CustomAllReduce::reset)
       .def("close", &CustomAllReduce::close)

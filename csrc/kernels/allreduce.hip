@@ -166,6 +166,122 @@ __global__ void __launch_bounds__(car::kThreads) oneshot_allreduce_kernel(const 
   if (tid == 0) rounds[b] = round;
 }
 
+// Fused TP block epilogue: h = h + bf16(sum over ranks of in); y = RMSNorm(h) * w.
+// Row-partitioned (block b owns rows [r0, r1)), so after the one-hop push and the
+// per-block flag wait each block holds whole rows and normalises them in place:
+// the all-reduce's output never round-trips through HBM before the norm, and one
+// launch replaces two (the fusion that makes TP=8 pay).
+// Numerics are those of all-reduce + rmsnorm_kernel: the sum is rounded to bf16,
+// the residual add is rounded to bf16, the normalised value is rounded before w.
+template <int W, int MAXV>
+__global__ void __launch_bounds__(car::kThreads) oneshot_ar_rmsnorm_kernel(
+    const uint4* __restrict__ in, bf16_t* __restrict__ residual, const bf16_t* __restrict__ w,
+    bf16_t* __restrict__ y, int rows, int hidden, float eps, int64_t capvec, int rank, CarPeers peers,
+    uint32_t* herr, uint64_t timeout_ticks) {
+  __shared__ uint32_t s_round;
+  __shared__ uint32_t s_err;
+  __shared__ float scratch[car::kThreads / 64];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  char* mine = peers.base[rank];
+  uint32_t* rounds = reinterpret_cast<uint32_t*>(mine + car::kRoundsOff);
+  uint32_t* err = reinterpret_cast<uint32_t*>(mine + car::kErrOff);
+  if (tid == 0) {
+    s_round = rounds[b] + 1;
+    s_err = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __syncthreads();
+  const uint32_t round = s_round;
+  const int par = round & 1;
+  const int nvr = hidden >> 3;
+  const int per = (rows + gridDim.x - 1) / gridDim.x;
+  const int r0 = min(rows, per * b), r1 = min(rows, r0 + per);
+  const int64_t v0 = (int64_t)r0 * nvr, v1 = (int64_t)r1 * nvr;
+  uint4* y4 = reinterpret_cast<uint4*>(y);
+  if (s_err) {
+    poison<true>(y4, v0, v1, tid);
+    return;
+  }
+  for (int64_t v = v0 + tid; v < v1; v += car::kThreads) {
+    const uint4 x = in[v];
+#pragma unroll
+    for (int p = 0; p < W; ++p) {
+      uint4* dst = reinterpret_cast<uint4*>(peers.base[p] + car::kDataOff) + ((int64_t)par * W + rank) * capvec;
+      dst[v] = x;
+    }
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (tid < W) {
+    uint32_t* f = reinterpret_cast<uint32_t*>(peers.base[tid] + car::kFlagsOff) + b * car::kMaxRanks + rank;
+    __hip_atomic_store(f, round, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (tid < W) {
+    uint32_t* f = reinterpret_cast<uint32_t*>(mine + car::kFlagsOff) + b * car::kMaxRanks + tid;
+    const uint64_t t0 = (uint64_t)wall_clock64();
+    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < round) {
+      __builtin_amdgcn_s_sleep(2);
+      if ((uint64_t)wall_clock64() - t0 > timeout_ticks) {
+        s_err = 1;
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  if (s_err) {
+    if (tid == 0) {
+      __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (herr != nullptr) __hip_atomic_store(herr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      rounds[b] = round;
+    }
+    poison<true>(y4, v0, v1, tid);
+    return;
+  }
+  const uint4* slots = reinterpret_cast<const uint4*>(mine + car::kDataOff) + (int64_t)par * W * capvec;
+  const u16x8* w8 = reinterpret_cast<const u16x8*>(w);
+  for (int r = r0; r < r1; ++r) {
+    u16x8* hr = reinterpret_cast<u16x8*>(residual + (int64_t)r * hidden);
+    u16x8* yr = reinterpret_cast<u16x8*>(y + (int64_t)r * hidden);
+    float v[MAXV][8];
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      const int vi = tid + i * car::kThreads;
+      if (vi < nvr) {
+        const int64_t g = (int64_t)r * nvr + vi;
+        float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        uint4 x[W];
+#pragma unroll
+        for (int p = 0; p < W; ++p) x[p] = slots[(int64_t)p * capvec + g];
+#pragma unroll
+        for (int p = 0; p < W; ++p) acc8(a, x[p], true);
+        const u16x8 hv = hr[vi];
+        u16x8 s;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          s[j] = f2bf(bf2f(f2bf(a[j])) + bf2f(hv[j]));
+          v[i][j] = bf2f(s[j]);
+          ss += v[i][j] * v[i][j];
+        }
+        hr[vi] = s;
+      }
+    }
+    const float tot = block_sum<car::kThreads>(ss, scratch);
+    const float rs = rsqrtf(tot / static_cast<float>(hidden) + eps);
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      const int vi = tid + i * car::kThreads;
+      if (vi < nvr) {
+        const u16x8 wv = w8[vi];
+        u16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = f2bf(bf2f(f2bf(v[i][j] * rs)) * bf2f(wv[j]));
+        yr[vi] = o;
+      }
+    }
+  }
+  if (tid == 0) rounds[b] = round;
+}
+
 // ------------------------------------------------------------------ host side
 
 size_t car_buffer_bytes(size_t cap_bytes, int world) { return car::kDataOff + 2 * (size_t)world * cap_bytes; }
@@ -252,6 +368,51 @@ int car_all_reduce(const void* in, void* out, int64_t bytes, bool bf16, int rank
     default: return -1;
   }
 #undef OAMD_CAR
+  OAMD_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace oamd
+
+namespace oamd {
+
+int car_all_reduce_rmsnorm(const void* in, bf16_t* residual, const bf16_t* w, bf16_t* y, int rows, int hidden,
+                           float eps, int rank, int world, void* const* bases, size_t cap_bytes, int blocks,
+                           uint32_t* herr_dev, double timeout_s, hipStream_t stream) {
+  if (world < 1 || world > car::kMaxRanks || rank < 0 || rank >= world) return -1;
+  if (rows < 1 || hidden < 8 || hidden % 8 != 0 || hidden > car::kThreads * 8 * 4) return -2;
+  if ((size_t)rows * hidden * 2 > cap_bytes || cap_bytes % 16 != 0) return -2;
+  if (blocks < 1 || blocks > car::kMaxBlocks) return -3;
+  if ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(residual) | reinterpret_cast<uintptr_t>(w) |
+       reinterpret_cast<uintptr_t>(y)) & 15)
+    return -4;
+  CarPeers peers{};
+  for (int p = 0; p < world; ++p) peers.base[p] = static_cast<char*>(bases[p]);
+  const int64_t capvec = cap_bytes / 16;
+  const uint4* i4 = static_cast<const uint4*>(in);
+  const uint64_t ticks = timeout_s > 0 ? (uint64_t)(timeout_s * 1e8) : car::kDefaultTimeoutTicks;
+  const bool big = hidden > car::kThreads * 8 * 2;
+#define OAMD_CARN(W)                                                                                          \
+  case W:                                                                                                     \
+    if (big)                                                                                                  \
+      oneshot_ar_rmsnorm_kernel<W, 4><<<blocks, car::kThreads, 0, stream>>>(                                  \
+          i4, residual, w, y, rows, hidden, eps, capvec, rank, peers, herr_dev, ticks);                       \
+    else                                                                                                      \
+      oneshot_ar_rmsnorm_kernel<W, 2><<<blocks, car::kThreads, 0, stream>>>(                                  \
+          i4, residual, w, y, rows, hidden, eps, capvec, rank, peers, herr_dev, ticks);                       \
+    break;
+  switch (world) {
+    OAMD_CARN(1)
+    OAMD_CARN(2)
+    OAMD_CARN(3)
+    OAMD_CARN(4)
+    OAMD_CARN(5)
+    OAMD_CARN(6)
+    OAMD_CARN(7)
+    OAMD_CARN(8)
+    default: return -1;
+  }
+#undef OAMD_CARN
   OAMD_LAUNCH_CHECK();
   return 0;
 }

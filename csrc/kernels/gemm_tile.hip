@@ -160,6 +160,7 @@ __global__ void __launch_bounds__(512) gemm_tile256_kernel(const bf16_t* __restr
   for (int r = 0; r < 4; ++r) issue(r, 0, 0);
   if constexpr (PH == 2) vm_wait<2>(); else vm_wait<4>();
   seg_barrier();
+  if constexpr (PH == 3) read_w(lds + 1 * kRegion, wf0);
   if (g == 1) seg_barrier();   // ping-pong: waves 4-7 one segment behind
 
   if constexpr (PH == 2) {
@@ -186,6 +187,47 @@ __global__ void __launch_bounds__(512) gemm_tile256_kernel(const bf16_t* __restr
       mfma_q(acc[1][0], wf0);
       mfma_q(acc[1][1], wf1);
       if (g == 0 && more) vm_wait<2>();
+      seg_barrier();
+    }
+  } else if constexpr (PH == 3) {
+    // balanced four-phase schedule: LDS fragment reads 8 / 4 / 8 / 4 per phase; the
+    // W0 fragments of tile t+1 are read in phase 4 of tile t (its registers are free
+    // there), so X0 / W0 of tile t+1 are retired at the end of phase 3
+    for (int t = 0; t < T; ++t) {
+      const char* cur = lds + (t & 1) * kBuf;
+      const int nb = (t + 1) & 1;
+      const bool more = t + 1 < T;
+      // -- phase 1: (X0, W0); issue X0 of tile t+1; retire W1 of tile t
+      read_x(cur + 0 * kRegion);
+      if (more) issue(0, nb, t + 1);
+      if (g == 1) { if (more) vm_wait<4>(); else vm_wait<2>(); }
+      seg_barrier();
+      mfma_q(acc[0][0], wf0);
+      if (g == 0) { if (more) vm_wait<4>(); else vm_wait<2>(); }
+      seg_barrier();
+      // -- phase 2: (X0, W1); issue W0 of tile t+1; retire X1 of tile t
+      read_w(cur + 2 * kRegion, wf1);
+      if (more) issue(1, nb, t + 1);
+      if (g == 1) { if (more) vm_wait<4>(); else vm_wait<0>(); }
+      seg_barrier();
+      mfma_q(acc[0][1], wf1);
+      if (g == 0) { if (more) vm_wait<4>(); else vm_wait<0>(); }
+      seg_barrier();
+      // -- phase 3: (X1, W0); issue W1 of tile t+1; retire X0 / W0 of tile t+1
+      read_x(cur + 3 * kRegion);
+      if (more) issue(2, nb, t + 1);
+      if (g == 1 && more) vm_wait<2>();
+      seg_barrier();
+      mfma_q(acc[1][0], wf0);
+      if (g == 0 && more) vm_wait<2>();
+      seg_barrier();
+      // -- phase 4: (X1, W1); issue X1 of tile t+1, read W0 fragments of tile t+1
+      if (more) {
+        read_w(lds + nb * kBuf + 1 * kRegion, wf0);
+        issue(3, nb, t + 1);
+      }
+      seg_barrier();
+      mfma_q(acc[1][1], wf1);
       seg_barrier();
     }
   } else
@@ -271,6 +313,192 @@ __global__ void __launch_bounds__(512) gemm_tile256_kernel(const bf16_t* __restr
     }
 }
 
+// Variant 1: four waves (one per SIMD), each owning a 128 x 128 output block: 64
+// accumulator fragments = all 256 AGPRs, so the LDS fragment traffic per MFMA is
+// 2/3 of the 8-wave layout (16 ds_read_b128 per 64 MFMAs) and far fewer waves wait
+// at barriers (rocprofv3: the 8-wave schedule spends 31 % of wave-cycles in waits).
+// The MFMAs are inline asm with the accumulator TIED in an AGPR ("+a"): with the
+// builtin, hipcc's register allocator shuffles the 256 accumulators through
+// v_accvgpr copies (hundreds per K-tile). Fragments are double-buffered in VGPRs
+// (substep s+1 is read while substep s computes) and ONE raw barrier per K-tile
+// separates "tile t+1 landed, every wave done reading tile t" from the DMA of tile
+// t+2 into tile t's buffer, which then has a whole K-tile to land.
+__device__ __forceinline__ void mfma_tied(f32x4& acc, const u16x8& a, const u16x8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+
+template <int EPI>
+__global__ void __launch_bounds__(256) gemm_tile256_w4_kernel(const bf16_t* __restrict__ X,
+                                                              const bf16_t* __restrict__ W, bf16_t* __restrict__ Y,
+                                                              const bf16_t* __restrict__ bias, int M, int N, int K,
+                                                              int ldy) {
+  __shared__ __attribute__((aligned(1024))) char lds[2 * kBuf];   // per buffer: X rows 0-255, then W rows 0-255
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 1, wn = w & 1;
+
+  const int mt = (M + kT - 1) / kT, nt = (N + kT - 1) / kT;
+  const int nwg = mt * nt;
+  const int lid = xcd_remap(blockIdx.x, nwg);
+  const int gsz = kGroupM * nt;
+  const int first_m = (lid / gsz) * kGroupM;
+  const int gm = min(mt - first_m, kGroupM);
+  const int tm = first_m + (lid % gsz) % gm;
+  const int tn = (lid % gsz) / gm;
+  const int m0 = tm * kT, n0 = tn * kT;
+
+  // DMA: wave w issues image rows 8w + 32i + lane/8 (i < 8: X, i >= 8: W); the
+  // swizzle term ((row >> 1) & 7) is the same for every i
+  const int lrow = lane >> 3;
+  const int chunk = (lane & 7) ^ ((4 * w + (lrow >> 1)) & 7);
+  const bf16_t* xs[8];
+  const bf16_t* ws[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    xs[i] = X + (int64_t)min(m0 + 8 * w + 32 * i + lrow, M - 1) * K + chunk * 8;
+    ws[i] = W + (int64_t)min(n0 + 8 * w + 32 * i + lrow, N - 1) * K + chunk * 8;
+  }
+  auto issue = [&](int buf, int kt) {
+    char* dst = lds + buf * kBuf + w * 1024;
+    const int k0 = kt * kBK;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      __builtin_amdgcn_global_load_lds(xs[i] + k0, (__attribute__((address_space(3))) void*)(dst + i * 4096), 16, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      __builtin_amdgcn_global_load_lds(ws[i] + k0, (__attribute__((address_space(3))) void*)(dst + 32768 + i * 4096),
+                                       16, 0, 0);
+  };
+
+  const int l15 = lane & 15, lq = lane >> 4, sw = (l15 >> 1) & 7;
+  const int c0 = (lq ^ sw) << 4, c1 = ((4 + lq) ^ sw) << 4;
+  const int xrow = (wm * 128 + l15) * 128;            // + bt * 2048
+  const int wrow = 32768 + (wn * 32 + l15) * 128;     // + f * 16384 + type * 8192 + j * 2048
+
+  f32x4 acc[8][8];   // [token block][feature block fe = f*4 + type*2 + j]
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  u16x8 xa[8], wa[8], xb[8], wb[8];
+  // fragment q of a substep's 16 reads, in the order the next substep consumes them
+  // (all W fragments feed its first MFMA row, X fragment i its row i)
+  auto rd1 = [&](const char* buf, int c, u16x8 (&xf)[8], u16x8 (&wf)[8], int q) {
+    constexpr int kOrd[16] = {8, 9, 0, 10, 11, 1, 12, 13, 2, 14, 15, 3, 4, 5, 6, 7};   // >= 8: W fragment
+    const int o = kOrd[q];
+    if (o >= 8) {
+      const int i = o - 8;
+      wf[i] = *reinterpret_cast<const u16x8*>(buf + wrow + (i >> 2) * 16384 + ((i >> 1) & 1) * 8192 + (i & 1) * 2048 + c);
+    } else {
+      xf[o] = *reinterpret_cast<const u16x8*>(buf + xrow + o * 2048 + c);
+    }
+  };
+  auto issue1 = [&](int buf, int kt, int q) {   // DMA instruction q (of 16) of K-tile kt
+    char* dst = lds + buf * kBuf + w * 1024;
+    const int k0 = kt * kBK;
+    if (q < 8)
+      __builtin_amdgcn_global_load_lds(xs[q] + k0, (__attribute__((address_space(3))) void*)(dst + q * 4096), 16, 0, 0);
+    else
+      __builtin_amdgcn_global_load_lds(ws[q - 8] + k0,
+                                       (__attribute__((address_space(3))) void*)(dst + 32768 + (q - 8) * 4096), 16, 0, 0);
+  };
+  // 64 MFMAs of one substep; after each 8-MFMA row, two fragment reads of the next
+  // substep (from `nbuf`) and, if `dma`, two DMA instructions of K-tile `kt`
+  auto mm = [&](u16x8 (&xf)[8], u16x8 (&wf)[8], const char* nbuf, int c, u16x8 (&nx)[8], u16x8 (&nw)[8],
+                bool rd_next, bool dma, int dbuf, int kt) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) mfma_tied(acc[i][j], wf[j], xf[i]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (rd_next) {
+        rd1(nbuf, c, nx, nw, 2 * i);
+        rd1(nbuf, c, nx, nw, 2 * i + 1);
+      }
+      if (dma) {
+        issue1(dbuf, kt, 2 * i);
+        issue1(dbuf, kt, 2 * i + 1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  // the zero-initialised accumulators are read as SrcC by asm MFMAs, whose hazards
+  // hipcc does not pad: pin the writes above an explicit nop
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
+  asm volatile("s_nop 4");
+
+  const int T = K / kBK;
+  issue(0, 0);
+  vm_wait<0>();
+  seg_barrier();
+#pragma unroll
+  for (int q = 0; q < 16; ++q) rd1(lds, c0, xa, wa, q);
+  if (T > 1) issue(1, 1);
+  // one loop, no peeled copy: a second code path makes hipcc move accumulators with
+  // v_accvgpr_write right before an asm MFMA reads them (an unpadded hazard)
+  for (int t = 0; t < T; ++t) {
+    const char* cur = lds + (t & 1) * kBuf;
+    const bool more = t + 1 < T;
+    // S0: substep 0 of tile t, reading substep 1's fragments of tile t
+    mm(xa, wa, cur, c1, xb, wb, true, false, 0, 0);
+    // tile t+1 landed (this wave's DMA); every wave done reading tile t
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    vm_wait<0>();
+    if (more) seg_barrier();
+    // S1: substep 1 of tile t, reading substep 0 of tile t+1; tile t+2's DMA goes
+    // into tile t's buffer
+    mm(xb, wb, lds + ((t + 1) & 1) * kBuf, c0, xa, wa, more, t + 2 < T, t & 1, t + 2);
+  }
+  // the accumulators were written by asm MFMAs the hazard recognizer cannot see:
+  // cover the MFMA-write -> accvgpr-read latency before the epilogue reads them
+  asm volatile("s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
+
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int tok = m0 + wm * 128 + i * 16 + l15;
+    if (tok >= M) continue;
+    bf16_t* yrow = Y + (int64_t)tok * ldy;
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        if constexpr (EPI == kEpiSilu) {
+          const int col = (n0 >> 1) + f * 64 + wn * 32 + j * 16 + 4 * lq;
+          if (2 * col >= N) continue;
+          const f32x4 gt = acc[i][f * 4 + j], up = acc[i][f * 4 + 2 + j];
+          f32x4 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float gg = bf2f(f2bf(gt[r]));
+            const float uu = bf2f(f2bf(up[r]));
+            const float sg = bf2f(f2bf(gg / (1.f + __expf(-gg))));
+            o[r] = sg * uu;
+          }
+          *reinterpret_cast<uint2*>(yrow + col) = pack4(o);
+        } else {
+#pragma unroll
+          for (int ty = 0; ty < 2; ++ty) {
+            const int col = n0 + f * 128 + ty * 64 + wn * 32 + j * 16 + 4 * lq;
+            if (col >= N) continue;
+            f32x4 v = acc[i][f * 4 + ty * 2 + j];
+            if constexpr (EPI == kEpiBias) {
+              const uint2 bb = *reinterpret_cast<const uint2*>(bias + col);
+              v[0] += __uint_as_float(bb.x << 16);
+              v[1] += __uint_as_float(bb.x & 0xffff0000u);
+              v[2] += __uint_as_float(bb.y << 16);
+              v[3] += __uint_as_float(bb.y & 0xffff0000u);
+            }
+            *reinterpret_cast<uint2*>(yrow + col) = pack4(v);
+          }
+        }
+      }
+  }
+}
+
 int gemm_tile(const bf16_t* X, const bf16_t* W, bf16_t* Y, const bf16_t* bias, int M, int N, int K, int ldy,
               bool silu_gu, int variant, hipStream_t stream) {
   if (M < 1 || N < 16 || N % 16 != 0 || K < kBK || K % kBK != 0) return -1;
@@ -281,7 +509,17 @@ int gemm_tile(const bf16_t* X, const bf16_t* W, bf16_t* Y, const bf16_t* bias, i
   if (silu_gu) gemm_tile256_kernel<kEpiSilu, PH><<<nwg, 512, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);  \
   else if (bias) gemm_tile256_kernel<kEpiBias, PH><<<nwg, 512, 0, stream>>>(X, W, Y, bias, M, N, K, ldy); \
   else gemm_tile256_kernel<kEpiStore, PH><<<nwg, 512, 0, stream>>>(X, W, Y, bias, M, N, K, ldy)
-  if (variant == 2) { OAMD_TILE(2); } else { OAMD_TILE(4); }
+  if (variant == 1) {
+    if (silu_gu) gemm_tile256_w4_kernel<kEpiSilu><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+    else if (bias) gemm_tile256_w4_kernel<kEpiBias><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+    else gemm_tile256_w4_kernel<kEpiStore><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+  } else if (variant == 2) {
+    OAMD_TILE(2);
+  } else if (variant == 3) {
+    OAMD_TILE(3);
+  } else {
+    OAMD_TILE(4);
+  }
 #undef OAMD_TILE
   OAMD_LAUNCH_CHECK();
   return 0;

@@ -79,6 +79,11 @@ int car_host_flag(uint32_t** host, uint32_t** dev);   // host-mapped error word 
 void car_free_host_flag(uint32_t* host);
 int car_error(const uint32_t* host);
 int car_reset(void* base, uint32_t* host);
+// Fused one-shot all-reduce + residual add + RMSNorm (bf16 rows of `hidden`, hidden % 8 == 0, <= 16384):
+// residual += bf16(sum over ranks of in); y = rmsnorm(residual) * w.
+int car_all_reduce_rmsnorm(const void* in, bf16_t* residual, const bf16_t* w, bf16_t* y, int rows, int hidden,
+                           float eps, int rank, int world, void* const* bases, size_t cap_bytes, int blocks,
+                           uint32_t* herr_dev, double timeout_s, hipStream_t stream);
 int car_all_reduce(const void* in, void* out, int64_t bytes, bool bf16, int rank, int world, void* const* bases,
                    size_t cap_bytes, int blocks, uint32_t* herr_dev, double timeout_s, hipStream_t stream);
 

@@ -90,6 +90,10 @@ PRESETS: dict[str, LlamaConfig] = {
                         max_position=4096, bos_id=1000, eos_ids=(1001,)),
     "tiny-gqa4": LlamaConfig(name="tiny-gqa4", vocab_size=2048, hidden=1024, intermediate=1024, layers=2, heads=8,
                              kv_heads=2, max_position=4096, bos_id=2000, eos_ids=(2001,)),
+    # 70B-shaped head layout (GQA 8: 64/8 heads at 70B) that every TP degree up to 8 divides:
+    # heads, kv heads, FFN width (64-feature SwiGLU blocks per rank) and vocab
+    "tiny-tp8": LlamaConfig(name="tiny-tp8", vocab_size=2048, hidden=512, intermediate=1024, layers=2, heads=16,
+                            kv_heads=8, max_position=4096, bos_id=2000, eos_ids=(2001,)),
     # qwen2-shaped: q/k/v bias and a GQA group of 7 (Qwen2.5-7B's 28/4)
     "tiny-qwen": LlamaConfig(name="tiny-qwen", arch="qwen2", vocab_size=2048, hidden=896, intermediate=1024, layers=2,
                              heads=7, kv_heads=1, rope_theta=1e6, rms_eps=1e-6, max_position=4096, qkv_bias=True,

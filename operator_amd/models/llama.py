@@ -8,11 +8,11 @@ AIInterfaceRestClient.java:37-39). Per layer:
     qkv = x @ Wqkv^T                          GEMM (fused QKV projection)
     q,k,v = rope_kv(qkv) -> paged KV write    HIP  (fused RoPE + cache scatter)
     o   = attn(q, K, V)                       HIP  (MFMA flash prefill | split-KV paged decode)
-    a   = o @ Wo^T        [TP: all-reduce]    GEMM
-    x   = rmsnorm(a + h)                      HIP
+    a   = o @ Wo^T                            GEMM
+    x   = rmsnorm(allreduce(a) + h)           HIP  (TP: one fused one-shot AR + norm kernel)
     gu  = x @ Wgu^T                           GEMM (fused gate|up)
     m   = silu(g) * u                         HIP (fused into the gate|up GEMM at decode)
-    d   = m @ Wd^T        [TP: all-reduce]    GEMM
+    d   = m @ Wd^T        [TP: fused AR+norm] GEMM
 logits = rmsnorm(h) @ Wlm^T (vocab-parallel under TP); tokens = Gumbel-max
 sampler on each vocab shard + a max over shards.
 
@@ -261,16 +261,14 @@ class LlamaModel:
                 o = ops.attn_decode(q, kc, vc, fb.block_tables, fb.context_lens, self.scale, fb.num_splits,
                                     workspace=ws, k_scale=kv.k_scale, v_scale=kv.v_scale)
             a = self._lin(o.view(T, self.hq * c.head_dim), lw.wo, lw.so, defer=True)
-            self.tp.all_reduce_(a)
-            x = ops.rmsnorm(a, lw.mlp_norm, c.rms_eps, residual=h)
+            x = self.tp.all_reduce_rmsnorm(a, lw.mlp_norm, c.rms_eps, residual=h)   # fused under TP
             if lw.sgu is None:
                 m = ops.gate_up_silu(x, lw.wgu, self.gu_block)
             else:
                 m = ops.silu_mul(ops.linear_fp8(x, lw.wgu, lw.sgu), block=self.gu_block)
             d = self._lin(m, lw.wd, lw.sd, defer=True)
-            self.tp.all_reduce_(d)
             nw = self.layers[i + 1].attn_norm if i + 1 < len(self.layers) else self.final_norm
-            x = ops.rmsnorm(d, nw, c.rms_eps, residual=h)
+            x = self.tp.all_reduce_rmsnorm(d, nw, c.rms_eps, residual=h)
         if fb.logits_index is not None:
             x = x.index_select(0, fb.logits_index)
         return ops.linear(x, self.lm_head)

@@ -90,6 +90,21 @@ class Group:
             dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.pg)
         return t
 
+    def all_reduce_rmsnorm(self, t, w: torch.Tensor, eps: float, residual: torch.Tensor) -> torch.Tensor:
+        """The TP block epilogue: residual += all_reduce(t); return rmsnorm(residual) * w.
+        With the one-shot IPC all-reduce enabled this is ONE fused gfx950 kernel (the
+        reduced rows are normalised by the block that summed them); otherwise the
+        all-reduce (RCCL / gloo) then the rmsnorm kernel. World 1: just the rmsnorm
+        (``t`` may then be split-K slabs, summed inside the norm)."""
+        from operator_amd import ops
+
+        if self.world > 1:
+            car = getattr(self, "oneshot", None)
+            if car is not None and isinstance(t, torch.Tensor) and car.fits_rows(t) and residual.is_contiguous():
+                return car.all_reduce_rmsnorm_(t, residual, w, eps)
+            self.all_reduce_(t)
+        return ops.rmsnorm(t, w, eps, residual=residual)
+
     def all_gather(self, t: torch.Tensor, dim: int = 0) -> torch.Tensor:
         if self.world == 1:
             return t

@@ -67,6 +67,21 @@ class OneShotAllReduce:
         self.calls += 1
         return out
 
+    def fits_rows(self, t: torch.Tensor) -> bool:
+        """The fused all-reduce + RMSNorm takes bf16 [rows, hidden] within capacity."""
+        return (self.fits(t) and t.dtype == torch.bfloat16 and t.dim() == 2 and t.shape[1] % 8 == 0
+                and t.shape[1] <= 16384)
+
+    def all_reduce_rmsnorm_(self, t: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float,
+                            out: torch.Tensor | None = None) -> torch.Tensor:
+        """residual += sum over ranks of t (bf16-rounded); returns rmsnorm(residual) * w.
+        One launch: the row-partitioned one-shot push, then each block normalises whole
+        rows straight from its receive slots."""
+        y = out if out is not None else torch.empty_like(t)
+        self.ext.all_reduce_rmsnorm(t, residual, w, y, float(eps))
+        self.calls += 1
+        return y
+
     @property
     def failed(self) -> bool:
         """A call timed out waiting for a peer. Sticky: every later call returns NaN

@@ -54,6 +54,28 @@ def _worker(rank: int, world: int, port: int, q) -> None:
                     assert torch.equal(t.cpu(), want), (dtype, n, (t.cpu().float() - want.float()).abs().max())
                     call += 1
                     checked += 1
+        # fused all-reduce + residual + RMSNorm (the TP block epilogue), interleaved with
+        # plain calls on the same per-block round counters
+        from operator_amd import ops
+
+        for rows, hidden in ((1, 4096), (7, 8192), (64, 8192), (256, 8192), (100, 16384)):
+            xs = [_inputs(r, rows * hidden, torch.bfloat16, call).view(rows, hidden) for r in range(world)]
+            h0 = _inputs(99, rows * hidden, torch.bfloat16, call).view(rows, hidden).to(dev)
+            wv = (1 + 0.1 * _inputs(98, hidden, torch.float32, call)).to(torch.bfloat16).to(dev)
+            ssum = sum(x.float() for x in xs).to(torch.bfloat16).to(dev)
+            h_ref = h0.clone()
+            y_ref = ops.rmsnorm(ssum.clone(), wv, 1e-5, residual=h_ref)
+            h = h0.clone()
+            y = grp.all_reduce_rmsnorm(xs[rank].to(dev), wv, 1e-5, residual=h)
+            torch.cuda.synchronize()
+            assert torch.equal(h, h_ref), (rows, hidden, (h.float() - h_ref.float()).abs().max())
+            torch.testing.assert_close(y.float(), y_ref.float(), atol=1e-2, rtol=1e-2)
+            t = xs[rank].reshape(-1).to(dev)
+            grp.all_reduce_(t)                      # a plain call in between
+            torch.cuda.synchronize()
+            assert torch.equal(t.cpu(), sum(x.float() for x in xs).to(torch.bfloat16).reshape(-1))
+            call += 1
+            checked += 1
         # hipGraph capture: the round counter lives on the device, so replays stay in step
         n = 16384
         buf = torch.zeros(n, dtype=torch.bfloat16, device=dev)
@@ -108,7 +130,7 @@ def test_oneshot_allreduce_two_ranks_one_gpu():
                 p.kill()
     errs = [r for r in res if r[1] != "ok"]
     assert not errs, errs[0][2]
-    assert all(r[2] >= 25 for r in res), res
+    assert all(r[2] >= 30 for r in res), res
 
 
 def _missing_peer_worker(rank: int, world: int, port: int, q) -> None:

@@ -10,7 +10,7 @@ from operator_amd.ops import reference as ref
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-VARIANTS = (4, 2)   # gemm_tile schedules: 4 or 2 phases per K-tile
+VARIANTS = (1, 3, 4, 2)   # gemm_tile schedules: 4-wave 128x128, balanced 4-phase, 4-phase, 2-phase
 
 
 def _rand(*shape, scale=1.0):
