@@ -61,7 +61,7 @@ __device__ __forceinline__ uint2 pack4(f32x4 v) {
 
 }  // namespace
 
-template <int EPI, int PH>
+template <int EPI>
 __global__ void __launch_bounds__(512) gemm_tile256_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
                                                            bf16_t* __restrict__ Y, const bf16_t* __restrict__ bias,
                                                            int M, int N, int K, int ldy) {
@@ -158,79 +158,10 @@ __global__ void __launch_bounds__(512) gemm_tile256_kernel(const bf16_t* __restr
   // prologue: all four regions of K-tile 0; X0 and W0 retired before the first reads
 #pragma unroll
   for (int r = 0; r < 4; ++r) issue(r, 0, 0);
-  if constexpr (PH == 2) vm_wait<2>(); else vm_wait<4>();
+  vm_wait<4>();
   seg_barrier();
-  if constexpr (PH == 3) read_w(lds + 1 * kRegion, wf0);
   if (g == 1) seg_barrier();   // ping-pong: waves 4-7 one segment behind
 
-  if constexpr (PH == 2) {
-    // two phases per K-tile (32 MFMAs each): A = X0 x {W0, W1}, B = X1 x {W0, W1};
-    // A issues X0 / W0 of tile t+1, B issues W1 / X1; half the barriers of PH = 4
-    for (int t = 0; t < T; ++t) {
-      const char* cur = lds + (t & 1) * kBuf;
-      const int nb = (t + 1) & 1;
-      const bool more = t + 1 < T;
-      read_x(cur + 0 * kRegion);
-      read_w(cur + 1 * kRegion, wf0);
-      read_w(cur + 2 * kRegion, wf1);
-      if (more) { issue(0, nb, t + 1); issue(1, nb, t + 1); }
-      if (g == 1) { if (more) vm_wait<4>(); else vm_wait<0>(); }
-      seg_barrier();
-      mfma_q(acc[0][0], wf0);
-      mfma_q(acc[0][1], wf1);
-      if (g == 0) { if (more) vm_wait<4>(); else vm_wait<0>(); }
-      seg_barrier();
-      read_x(cur + 3 * kRegion);
-      if (more) { issue(2, nb, t + 1); issue(3, nb, t + 1); }
-      if (g == 1 && more) vm_wait<2>();
-      seg_barrier();
-      mfma_q(acc[1][0], wf0);
-      mfma_q(acc[1][1], wf1);
-      if (g == 0 && more) vm_wait<2>();
-      seg_barrier();
-    }
-  } else if constexpr (PH == 3) {
-    // balanced four-phase schedule: LDS fragment reads 8 / 4 / 8 / 4 per phase; the
-    // W0 fragments of tile t+1 are read in phase 4 of tile t (its registers are free
-    // there), so X0 / W0 of tile t+1 are retired at the end of phase 3
-    for (int t = 0; t < T; ++t) {
-      const char* cur = lds + (t & 1) * kBuf;
-      const int nb = (t + 1) & 1;
-      const bool more = t + 1 < T;
-      // -- phase 1: (X0, W0); issue X0 of tile t+1; retire W1 of tile t
-      read_x(cur + 0 * kRegion);
-      if (more) issue(0, nb, t + 1);
-      if (g == 1) { if (more) vm_wait<4>(); else vm_wait<2>(); }
-      seg_barrier();
-      mfma_q(acc[0][0], wf0);
-      if (g == 0) { if (more) vm_wait<4>(); else vm_wait<2>(); }
-      seg_barrier();
-      // -- phase 2: (X0, W1); issue W0 of tile t+1; retire X1 of tile t
-      read_w(cur + 2 * kRegion, wf1);
-      if (more) issue(1, nb, t + 1);
-      if (g == 1) { if (more) vm_wait<4>(); else vm_wait<0>(); }
-      seg_barrier();
-      mfma_q(acc[0][1], wf1);
-      if (g == 0) { if (more) vm_wait<4>(); else vm_wait<0>(); }
-      seg_barrier();
-      // -- phase 3: (X1, W0); issue W1 of tile t+1; retire X0 / W0 of tile t+1
-      read_x(cur + 3 * kRegion);
-      if (more) issue(2, nb, t + 1);
-      if (g == 1 && more) vm_wait<2>();
-      seg_barrier();
-      mfma_q(acc[1][0], wf0);
-      if (g == 0 && more) vm_wait<2>();
-      seg_barrier();
-      // -- phase 4: (X1, W1); issue X1 of tile t+1, read W0 fragments of tile t+1
-      if (more) {
-        read_w(lds + nb * kBuf + 1 * kRegion, wf0);
-        issue(3, nb, t + 1);
-      }
-      seg_barrier();
-      mfma_q(acc[1][1], wf1);
-      seg_barrier();
-    }
-  } else
   for (int t = 0; t < T; ++t) {
     const char* cur = lds + (t & 1) * kBuf;
     const int nb = (t + 1) & 1;
@@ -351,23 +282,28 @@ __global__ void __launch_bounds__(256) gemm_tile256_w4_kernel(const bf16_t* __re
   // swizzle term ((row >> 1) & 7) is the same for every i
   const int lrow = lane >> 3;
   const int chunk = (lane & 7) ^ ((4 * w + (lrow >> 1)) & 7);
-  const bf16_t* xs[8];
-  const bf16_t* ws[8];
+  // 32-bit byte offsets of this lane's source rows (the launcher guarantees M*K*2 and
+  // N*K*2 < 4 GiB): half the VGPRs of 64-bit pointers, and the loads take the
+  // scalar-base + vector-offset form
+  uint32_t xs[8], ws[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    xs[i] = X + (int64_t)min(m0 + 8 * w + 32 * i + lrow, M - 1) * K + chunk * 8;
-    ws[i] = W + (int64_t)min(n0 + 8 * w + 32 * i + lrow, N - 1) * K + chunk * 8;
+    xs[i] = ((uint32_t)min(m0 + 8 * w + 32 * i + lrow, M - 1) * (uint32_t)K + chunk * 8) * 2u;
+    ws[i] = ((uint32_t)min(n0 + 8 * w + 32 * i + lrow, N - 1) * (uint32_t)K + chunk * 8) * 2u;
   }
+  const char* Xb = reinterpret_cast<const char*>(X);
+  const char* Wb = reinterpret_cast<const char*>(W);
   auto issue = [&](int buf, int kt) {
     char* dst = lds + buf * kBuf + w * 1024;
     const int k0 = kt * kBK;
 #pragma unroll
     for (int i = 0; i < 8; ++i)
-      __builtin_amdgcn_global_load_lds(xs[i] + k0, (__attribute__((address_space(3))) void*)(dst + i * 4096), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(Xb + xs[i] + 2 * k0, (__attribute__((address_space(3))) void*)(dst + i * 4096),
+                                       16, 0, 0);
 #pragma unroll
     for (int i = 0; i < 8; ++i)
-      __builtin_amdgcn_global_load_lds(ws[i] + k0, (__attribute__((address_space(3))) void*)(dst + 32768 + i * 4096),
-                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds(Wb + ws[i] + 2 * k0,
+                                       (__attribute__((address_space(3))) void*)(dst + 32768 + i * 4096), 16, 0, 0);
   };
 
   const int l15 = lane & 15, lq = lane >> 4, sw = (l15 >> 1) & 7;
@@ -397,15 +333,17 @@ __global__ void __launch_bounds__(256) gemm_tile256_w4_kernel(const bf16_t* __re
     char* dst = lds + buf * kBuf + w * 1024;
     const int k0 = kt * kBK;
     if (q < 8)
-      __builtin_amdgcn_global_load_lds(xs[q] + k0, (__attribute__((address_space(3))) void*)(dst + q * 4096), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(Xb + xs[q] + 2 * k0, (__attribute__((address_space(3))) void*)(dst + q * 4096),
+                                       16, 0, 0);
     else
-      __builtin_amdgcn_global_load_lds(ws[q - 8] + k0,
+      __builtin_amdgcn_global_load_lds(Wb + ws[q - 8] + 2 * k0,
                                        (__attribute__((address_space(3))) void*)(dst + 32768 + (q - 8) * 4096), 16, 0, 0);
   };
   // 64 MFMAs of one substep; after each 8-MFMA row, two fragment reads of the next
   // substep (from `nbuf`) and, if `dma`, two DMA instructions of K-tile `kt`
+  // stage == 2: this substep also issues K-tile kt's LDS-DMA into buffer dbuf
   auto mm = [&](u16x8 (&xf)[8], u16x8 (&wf)[8], const char* nbuf, int c, u16x8 (&nx)[8], u16x8 (&nw)[8],
-                bool rd_next, bool dma, int dbuf, int kt) {
+                bool rd_next, int stage, int dbuf, int kt) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
 #pragma unroll
@@ -415,7 +353,7 @@ __global__ void __launch_bounds__(256) gemm_tile256_w4_kernel(const bf16_t* __re
         rd1(nbuf, c, nx, nw, 2 * i);
         rd1(nbuf, c, nx, nw, 2 * i + 1);
       }
-      if (dma) {
+      if (stage == 2) {
         issue1(dbuf, kt, 2 * i);
         issue1(dbuf, kt, 2 * i + 1);
       }
@@ -444,14 +382,14 @@ __global__ void __launch_bounds__(256) gemm_tile256_w4_kernel(const bf16_t* __re
     const char* cur = lds + (t & 1) * kBuf;
     const bool more = t + 1 < T;
     // S0: substep 0 of tile t, reading substep 1's fragments of tile t
-    mm(xa, wa, cur, c1, xb, wb, true, false, 0, 0);
+    mm(xa, wa, cur, c1, xb, wb, true, 0, 0, t + 2);
     // tile t+1 landed (this wave's DMA); every wave done reading tile t
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     vm_wait<0>();
     if (more) seg_barrier();
-    // S1: substep 1 of tile t, reading substep 0 of tile t+1; tile t+2's DMA goes
-    // into tile t's buffer
-    mm(xb, wb, lds + ((t + 1) & 1) * kBuf, c0, xa, wa, more, t + 2 < T, t & 1, t + 2);
+    // S1: substep 1 of tile t, reading substep 0 of tile t+1; tile t+2 goes into
+    // tile t's buffer
+    mm(xb, wb, lds + ((t + 1) & 1) * kBuf, c0, xa, wa, more, t + 2 < T ? 2 : 0, t & 1, t + 2);
   }
   // the accumulators were written by asm MFMAs the hazard recognizer cannot see:
   // cover the MFMA-write -> accvgpr-read latency before the epilogue reads them
@@ -505,22 +443,16 @@ int gemm_tile(const bf16_t* X, const bf16_t* W, bf16_t* Y, const bf16_t* bias, i
   if (silu_gu && (N % 128 != 0 || bias != nullptr)) return -2;
   if (ldy < (silu_gu ? N / 2 : N)) return -3;
   const int nwg = ((M + kT - 1) / kT) * ((N + kT - 1) / kT);
-#define OAMD_TILE(PH)                                                                                   \
-  if (silu_gu) gemm_tile256_kernel<kEpiSilu, PH><<<nwg, 512, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);  \
-  else if (bias) gemm_tile256_kernel<kEpiBias, PH><<<nwg, 512, 0, stream>>>(X, W, Y, bias, M, N, K, ldy); \
-  else gemm_tile256_kernel<kEpiStore, PH><<<nwg, 512, 0, stream>>>(X, W, Y, bias, M, N, K, ldy)
-  if (variant == 1) {
+  const bool off32 = (int64_t)M * K * 2 < (1LL << 32) && (int64_t)N * K * 2 < (1LL << 32);
+  if (variant == 1 && off32) {   // 4-wave 128x128 per wave (32-bit source offsets)
     if (silu_gu) gemm_tile256_w4_kernel<kEpiSilu><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
     else if (bias) gemm_tile256_w4_kernel<kEpiBias><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
     else gemm_tile256_w4_kernel<kEpiStore><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-  } else if (variant == 2) {
-    OAMD_TILE(2);
-  } else if (variant == 3) {
-    OAMD_TILE(3);
-  } else {
-    OAMD_TILE(4);
+  } else {   // default: 8-wave ping-pong
+    if (silu_gu) gemm_tile256_kernel<kEpiSilu><<<nwg, 512, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+    else if (bias) gemm_tile256_kernel<kEpiBias><<<nwg, 512, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+    else gemm_tile256_kernel<kEpiStore><<<nwg, 512, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
   }
-#undef OAMD_TILE
   OAMD_LAUNCH_CHECK();
   return 0;
 }

@@ -351,6 +351,8 @@ py::list score_events(const std::vector<int64_t>& hit_doc, const std::vector<int
 
 }  // namespace
 
+void register_verify(py::module_& m);   // verify.cpp (N3 / N4)
+
 PYBIND11_MODULE(_patterns, m) {
   m.doc() = "operator_amd host pattern compiler / packer / scorer";
   m.def("compile_dfa", &compile_dfa, py::arg("factors"));
@@ -362,4 +364,5 @@ PYBIND11_MODULE(_patterns, m) {
   m.def("score_events", &score_events);
   m.attr("MAX_FACTOR_LEN") = kMaxFactorLen;
   m.attr("MAX_STATES") = kMaxStates;
+  register_verify(m);
 }

@@ -128,6 +128,8 @@ class MatchEngine:
         self._fm_ptr = np.asarray(fm_ptr, dtype=np.int64)
         self._fm_ids = np.asarray(fm_ids if fm_ids else [0], dtype=np.int64)
         self._verify = np.asarray(self.cp.matcher_verify + [False], dtype=bool)
+        self._init_verifier()
+        self._mp_cache: dict[int, MatchedPattern] = {}
         if self.device.type == "cuda" and self.cp.factors:
             self._upload_dfa()
         # Scans run on a stream of their own: the LLM engine keeps the default stream
@@ -136,6 +138,29 @@ class MatchEngine:
         self._stream = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
         if self._stream is not None:
             torch.cuda.synchronize(self.device)   # DFA tables uploaded before the first scan
+
+    def _init_verifier(self) -> None:
+        """Per-matcher verification mode for the native post-processing (N4):
+        0 = the factor hit is exact, 1 = native Pike-VM regex on the candidate line
+        (patterns/nfa.py), 2 = Python ``re`` (outside the exactly-simulated subset)."""
+        from operator_amd.ops import patterns
+        from operator_amd.patterns.nfa import compile_nfa
+
+        import re as _re
+
+        progs, mode = [], []
+        for i, m in enumerate(self.cp.matchers):
+            if not self.cp.matcher_verify[i]:
+                progs.append(None)
+                mode.append(0)
+                continue
+            prog = compile_nfa(m.regex_source(), _re.IGNORECASE if m.ignore_case else 0)
+            progs.append(prog)
+            mode.append(1 if prog is not None else 2)
+        self._mode = np.asarray(mode + [2], dtype=np.int8)
+        self._rx = patterns().RegexSet(progs)
+        self.native_verify = int(sum(1 for x in mode if x == 1))
+        self.python_verify = int(sum(1 for x in mode if x == 2))
 
     def _on_stream(self):
         return torch.cuda.stream(self._stream) if self._stream is not None else contextlib.nullcontext()
@@ -296,49 +321,44 @@ class MatchEngine:
         raw = self.scan_gpu(docs) if (self.device.type == "cuda" and self.cp.factors) else (
             self.scan_cpu(docs) if self.cp.factors else np.zeros((0, 4), np.int64))
         t1 = time.perf_counter()
-        offs: dict[tuple[int, int, int], int] = {}
-        out: set[tuple[int, int, int]] = set()
-        if raw.shape[0]:
-            f = raw[:, 1]
-            cnt = self._fm_ptr[f + 1] - self._fm_ptr[f]
-            rep = np.repeat(np.arange(raw.shape[0]), cnt)
-            starts = np.repeat(self._fm_ptr[f], cnt)
-            within = np.arange(rep.shape[0]) - np.repeat(np.cumsum(cnt) - cnt, cnt)
-            mat = self._fm_ids[starts + within]
-            doc, line, off = raw[rep, 0], raw[rep, 2], raw[rep, 3]
-            need = self._verify[mat]
-            # fast path: exact factors
-            for d_, m_, l_, o_ in zip(doc[~need].tolist(), mat[~need].tolist(), line[~need].tolist(),
-                                      off[~need].tolist()):
-                k = (d_, m_, l_)
-                if k not in out:
-                    out.add(k)
-                    offs[k] = o_
-            # verify path: regex / case-sensitive on the candidate line only
-            checked: dict[tuple[int, int, int], bool] = {}
-            for d_, m_, l_, o_ in zip(doc[need].tolist(), mat[need].tolist(), line[need].tolist(),
-                                      off[need].tolist()):
-                k = (d_, m_, l_)
-                if k in checked:
-                    continue
-                s, e = _line_bounds(docs[d_], o_)
-                ok = self.cp.regexes[m_].search(docs[d_][s:e]) is not None
-                checked[k] = ok
-                if ok:
-                    out.add(k)
-                    offs[k] = o_
+        from operator_amd.ops import patterns
+
+        P = patterns()
+        # native: factor -> matcher expansion, candidate-line verification (Pike VM),
+        # (doc, matcher, line) de-duplication; Python `re` only for matchers outside
+        # the NFA subset (`pending`)
+        done, pending = P.postprocess_hits(raw.reshape(-1, 4), self._fm_ptr, self._fm_ids, self._mode, docs, self._rx)
+        parts = [done]
+        if pending.shape[0]:
+            keep = []
+            for d_, m_, l_, o_ in pending.tolist():
+                s_, e_ = _line_bounds(docs[d_], o_)
+                if self.cp.regexes[m_].search(docs[d_][s_:e_]) is not None:
+                    keep.append((d_, m_, l_, o_))
+            parts.append(np.asarray(keep, dtype=np.int64).reshape(-1, 4))
         # matchers with no usable factor: evaluated on every line on the CPU
         for m_ in self.cp.unfiltered:
+            if self._rx.has(m_):
+                parts.append(P.line_scan(docs, self._rx, m_))
+                continue
             rx = self.cp.regexes[m_]
+            rows = []
             for d_, doc_b in enumerate(docs):
                 lo = _line_offsets(doc_b)
                 for li, ls in enumerate(lo):
                     le = lo[li + 1] - 1 if li + 1 < len(lo) else len(doc_b)
                     if rx.search(doc_b[ls:le]):
-                        k = (d_, m_, li)
-                        out.add(k)
-                        offs[k] = max(ls, le - 1) if le > ls else ls
-        arr = np.asarray(sorted(out), dtype=np.int64).reshape(-1, 3)
+                        rows.append((d_, m_, li, max(ls, le - 1) if le > ls else ls))
+            parts.append(np.asarray(rows, dtype=np.int64).reshape(-1, 4))
+        allh = np.concatenate(parts, 0) if len(parts) > 1 else done
+        if len(parts) > 1 and allh.shape[0]:
+            order = np.lexsort((allh[:, 2], allh[:, 1], allh[:, 0]))
+            allh = allh[order]
+            keep = np.ones(allh.shape[0], dtype=bool)
+            keep[1:] = np.any(allh[1:, :3] != allh[:-1, :3], axis=1)
+            allh = allh[keep]
+        offs = dict(zip(map(tuple, allh[:, :3].tolist()), allh[:, 3].tolist()))
+        arr = np.ascontiguousarray(allh[:, :3])
         self.stats.verified_hits += arr.shape[0]
         self.stats.scan_ms += (t1 - t0) * 1e3
         self.stats.host_ms += (time.perf_counter() - t1) * 1e3
@@ -430,23 +450,52 @@ class MatchEngine:
 
     def analyze(self, docs: list[bytes], pods: list[tuple[str, str]] | None = None) -> list[AnalysisResult]:
         """Full AnalysisResult per doc (pods = [(name, namespace)] for labelling)."""
+        from operator_amd.ops import patterns
+
         with self._lock:
             t0 = time.perf_counter()
             self._doc_newlines = None
             evs, offs = self.events(docs)
             nls = self._doc_newlines[1] if self._doc_newlines and self._doc_newlines[0] is docs else None
-            out = []
+            # the +-k context windows of every reported event, extracted natively in one
+            # call over the whole batch (N3)
+            cp = self.cp
+            pats = cp.patset.patterns
+            q_doc, q_off, q_k = [], [], []
             for di, (doc, ev) in enumerate(zip(docs, evs)):
-                out.append(self._result(di, doc, ev, offs, pods[di] if pods else (None, None),
+                lo = None
+                for e in ev[: self.max_events]:
+                    off = offs.get((di, cp.pattern_primary[e.pattern], e.line))
+                    if off is None:
+                        if lo is None:
+                            lo = _line_offsets(doc)
+                        off = lo[e.line] if e.line < len(lo) else 0
+                    q_doc.append(di)
+                    q_off.append(off)
+                    q_k.append(pats[e.pattern].context_lines)
+            ctxs = patterns().contexts(docs, q_doc, q_off, q_k) if q_doc else []
+            out = []
+            j = 0
+            for di, (doc, ev) in enumerate(zip(docs, evs)):
+                n = min(len(ev), self.max_events)
+                out.append(self._result(doc, ev, ctxs[j:j + n], pods[di] if pods else (None, None),
                                         (time.perf_counter() - t0) * 1e3, None if nls is None else nls[di]))
+                j += n
             self._doc_newlines = None
             self.stats.docs += len(docs)
             return out
 
-    def _result(self, di: int, doc: bytes, ev: list[oracle.Event], offs: dict, pod, ms: float,
+    def _matched(self, pi: int) -> MatchedPattern:
+        mp = self._mp_cache.get(pi)
+        if mp is None:   # immutable per pattern: built once, shared by every event
+            p = self.cp.patset.patterns[pi]
+            mp = self._mp_cache[pi] = MatchedPattern.model_construct(
+                id=p.id, name=p.name, severity=p.severity, category=p.category or None, library=p.library or None)
+        return mp
+
+    def _result(self, doc: bytes, ev: list[oracle.Event], ctxs: list, pod, ms: float,
                 newlines: int | None = None) -> AnalysisResult:
-        cp = self.cp
-        pats = cp.patset.patterns
+        pats = self.cp.patset.patterns
         dist = {s: 0 for s in SEVERITIES}
         sig = 0
         hi = -1
@@ -457,20 +506,12 @@ class MatchEngine:
             if e.score >= self.significance:
                 sig += 1
         events = []
-        for e in ev[: self.max_events]:
+        for e, (ctx, line) in zip(ev[: self.max_events], ctxs):
             p = pats[e.pattern]
-            off = offs.get((di, cp.pattern_primary[e.pattern], e.line))
-            if off is None:
-                lo = _line_offsets(doc)
-                off = lo[e.line] if e.line < len(lo) else 0
-            ctx, line = _context(doc, off, p.context_lines)
             # model_construct: these are the engine's own, already-typed values (validation
             # was ~2/3 of the host time per result with a few thousand results per scan)
             events.append(AnalysisEvent.model_construct(
-                line_number=e.line + 1,
-                matched_pattern=MatchedPattern.model_construct(id=p.id, name=p.name, severity=p.severity,
-                                                               category=p.category or None,
-                                                               library=p.library or None),
+                line_number=e.line + 1, matched_pattern=self._matched(e.pattern),
                 score=round(e.score, 6), context=ctx, matched_line=line,
                 remediation=p.remediation or None))
         summary = AnalysisSummary.model_construct(highest_severity=SEVERITIES[hi] if hi >= 0 else None,

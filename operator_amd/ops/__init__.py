@@ -248,9 +248,14 @@ def row_tile(M: int) -> int:
     return next(b for b in (256, 128, 64) if M % b == 0)
 
 
+LM_HEAD_MIN_N = 32768
+
+
 def _measured_blas(M: int, N: int, K: int) -> bool:
     """The tuned table measured hipBLASLt fastest for this decode-bucket shape (small-M
     GEMMs that neither the decode kernels nor the 256-row tile kernel win)."""
+    if N >= LM_HEAD_MIN_N:   # vocab projections always run on gemm_tile (weight-streaming bound there)
+        return False
     t = _gemm_table_get()
     return t.get(("skinny", M, N, K) if M <= SKINNY_MAX_M else (M, N, K)) == "blas"
 

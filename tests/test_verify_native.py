@@ -1,0 +1,105 @@
+"""Native N3/N4 (csrc/patterns/verify.cpp + operator_amd/patterns/nfa.py) against
+Python: the Pike-VM verifier must give exactly `re.search(line) is not None` for
+every regex it accepts (anything else is left to `re`), and the native context
+windows must equal the Python reference `_context`."""
+import random
+import re
+
+import pytest
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+from operator_amd.engine.match import _context
+from operator_amd.ops import patterns
+from operator_amd.patterns.nfa import compile_nfa
+
+FIXED = [
+    rb"OutOfMemoryError", rb"exit code \d+", rb"(?i)connection (refused|reset)", rb"^FATAL\b", rb"timeout$",
+    rb"[A-Z][a-z]+Exception: .*", rb"\bpanic: ", rb"fail(ed|ure)?", rb"a{2,4}b", rb"x*?y+?", rb"\d{3}-\d{4}",
+    rb"[^\s]+@[^\s]+", rb"\Berror", rb"(ab|cd)*ef", rb"(?i:disk)\s+full", rb"\Aerror\Z", rb"[.]\w+", rb"colou?r",
+    rb"(a|b|)c", rb"", rb"(?s)a.b", rb"[\d\-_]+", rb"\W+", rb"caf\xc3\xa9",
+]
+UNSUPPORTED = [rb"(a)\1", rb"foo(?=bar)", rb"(?<!x)y", rb"(?(1)a|b)"]
+
+
+def _lines(rng: random.Random, n: int):
+    alphabet = b"abcdefxyzABEF0123456789 _-.:@\t\xc3\xa9"
+    out = [b"", b"OutOfMemoryError", b"FATAL boot", b"connection REFUSED", b"exit code 137", b"aaab", b"aab",
+           b"xxyy", b"555-1234", b"user@host", b"abef", b"cdabef", b"disk   FULL", b"error", b"a\nb", b"color"]
+    for _ in range(n):
+        out.append(bytes(rng.choice(alphabet) for _ in range(rng.randint(0, 40))))
+    return out
+
+
+def _check(rx: bytes, flags: int, lines) -> None:
+    prog = compile_nfa(rx, flags)
+    assert prog is not None, rx
+    rs = patterns().RegexSet([prog])
+    py = re.compile(rx, flags)
+    for ln in lines:
+        assert rs.search(0, ln) == (py.search(ln) is not None), (rx, flags, ln)
+
+
+@pytest.mark.parametrize("rx", FIXED)
+@pytest.mark.parametrize("flags", [0, re.IGNORECASE])
+def test_nfa_matches_python_re(rx, flags):
+    _check(rx, flags, _lines(random.Random(hash(rx) & 0xffff), 200))
+
+
+@pytest.mark.parametrize("rx", UNSUPPORTED)
+def test_unsupported_constructs_fall_back_to_re(rx):
+    assert compile_nfa(rx) is None
+
+
+_atoms = st.sampled_from([b"a", b"b", b"x", b"0", b".", b"\\d", b"\\w", b"\\s", b"[a-c]", b"[^ab]", b"[0-9x]",
+                          b"\\b", b"^", b"$", b"A", b"-"])
+
+
+@st.composite
+def _regex(draw, depth=0):
+    parts = []
+    for _ in range(draw(st.integers(1, 4))):
+        kind = draw(st.integers(0, 6 if depth < 2 else 2))
+        if kind <= 2:
+            a = draw(_atoms)
+        elif kind == 3:
+            a = b"(" + draw(_regex(depth + 1)) + b"|" + draw(_regex(depth + 1)) + b")"
+        else:
+            a = b"(" + draw(_regex(depth + 1)) + b")"
+        if a not in (b"\\b", b"^", b"$"):
+            a += draw(st.sampled_from([b"", b"*", b"+", b"?", b"{1,3}", b"*?", b"{2}"]))
+        parts.append(a)
+    return b"".join(parts)
+
+
+@settings(max_examples=300, deadline=None)
+@given(_regex(), st.lists(st.binary(min_size=0, max_size=24).map(lambda b: bytes(x % 128 for x in b if x != 10)),
+                          min_size=1, max_size=12), st.booleans())
+def test_nfa_property_random_regexes(rx, lines, icase):
+    flags = re.IGNORECASE if icase else 0
+    try:
+        re.compile(rx, flags)
+    except re.error:
+        return
+    prog = compile_nfa(rx, flags)
+    if prog is None:
+        return
+    _check(rx, flags, lines + [b"ab0 x-A", b"", b"bbb", b"A0A"])
+
+
+def test_native_contexts_equal_python():
+    rng = random.Random(5)
+    docs = [b"", b"one line no newline", b"a\nb\nc\n", b"\n\n\nx\n", b"first\nsecond\nthird\nfourth\nfifth",
+            "café\nnaïve\n\xff\xfe bad utf8\n".encode("utf-8") + b"\xff\xfe\n"]
+    for _ in range(20):
+        docs.append(b"\n".join(bytes(rng.choice(b"abc xyz") for _ in range(rng.randint(0, 12)))
+                               for _ in range(rng.randint(1, 9))))
+    q = []
+    for di, d in enumerate(docs):
+        for off in sorted({0, len(d) // 2, max(0, len(d) - 1), len(d)} | {rng.randint(0, len(d)) for _ in range(3)}):
+            for k in (0, 1, 2, 5):
+                q.append((di, off, k))
+    got = patterns().contexts(docs, [x[0] for x in q], [x[1] for x in q], [x[2] for x in q])
+    for (di, off, k), (ctx, line) in zip(q, got):
+        ref_ctx, ref_line = _context(docs[di], off, k)
+        assert (list(ctx), line) == (ref_ctx, ref_line), (docs[di], off, k)

@@ -13,7 +13,7 @@ agg = collections.defaultdict(lambda: collections.defaultdict(list))
 dur = collections.defaultdict(dict)
 for r in csv.DictReader(open(a.csv)):
     name = r["Kernel_Name"]
-    if a.match not in name:
+    if not re.search(a.match, name):
         continue
     short = re.sub(r"\(.*", "", name)[:80]
     agg[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
