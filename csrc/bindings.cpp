@@ -175,25 +175,47 @@ void gemm_decode(const at::Tensor& x, const at::Tensor& w, const c10::optional<a
                        (int)bn, (int)bm, silu_gu, w_tiled, (int)stages, cur_stream()));
 }
 
-void gemm_tile(const at::Tensor& x, const at::Tensor& w, at::Tensor& y, const c10::optional<at::Tensor>& bias,
-               bool silu_gu, int64_t variant) {
-  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(y); CHECK_CONTIG(x); CHECK_CONTIG(w);
-  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 2, "x [M,K], w [N,K], y [M,N]");
+void gemm_tile(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& y_opt,
+               const c10::optional<at::Tensor>& bias, bool silu_gu, int64_t variant, int64_t splits,
+               const c10::optional<at::Tensor>& partial) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2, "x [M,K], w [N,K]");
   const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
   TORCH_CHECK(w.size(1) == K, "gemm_tile: w [N, K] must match x [M, K]");
   TORCH_CHECK(M >= 1 && K >= 64 && K % 64 == 0 && N % 16 == 0, "gemm_tile: K % 64 == 0, N % 16 == 0");
-  TORCH_CHECK(y.size(0) == M && y.size(1) == (silu_gu ? N / 2 : N) && y.stride(1) == 1 && y.stride(0) % 4 == 0,
-              "gemm_tile: y [M, N] (N/2 with silu_gu), unit column stride, 8-B aligned rows");
-  TORCH_CHECK(reinterpret_cast<uintptr_t>(y.data_ptr()) % 8 == 0, "gemm_tile: y must be 8-B aligned");
+  TORCH_CHECK(splits >= 1 && splits <= 64 && K % (64 * splits) == 0, "gemm_tile: K % (64 * splits) == 0");
+  bf16_t* yp = nullptr;
+  int64_t ldy = silu_gu ? N / 2 : N;
+  if (y_opt.has_value()) {
+    const at::Tensor& y = *y_opt;
+    CHECK_BF16(y);
+    TORCH_CHECK(y.dim() == 2 && y.size(0) == M && y.size(1) == (silu_gu ? N / 2 : N) && y.stride(1) == 1 &&
+                    y.stride(0) % 4 == 0,
+                "gemm_tile: y [M, N] (N/2 with silu_gu), unit column stride, 8-B aligned rows");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(y.data_ptr()) % 8 == 0, "gemm_tile: y must be 8-B aligned");
+    TORCH_CHECK(splits == 1 || silu_gu || y.stride(0) == N, "gemm_tile: split-K reduce needs a contiguous y");
+    yp = ptr<bf16_t>(y);
+    ldy = y.stride(0);
+  } else {
+    TORCH_CHECK(splits > 1 && !silu_gu, "y may be omitted only for split-K slabs summed by the consumer");
+  }
   TORCH_CHECK(!silu_gu || (N % 128 == 0 && !bias.has_value()), "gemm_tile: SwiGLU needs N % 128, no bias");
+  TORCH_CHECK(splits == 1 || !bias.has_value(), "gemm_tile: no bias with split-K");
   if (bias.has_value()) {
     CHECK_BF16(*bias); CHECK_CONTIG(*bias);
     TORCH_CHECK(bias->numel() == N, "gemm_tile: bias [N]");
   }
+  float* pp = nullptr;
+  if (splits > 1) {
+    TORCH_CHECK(partial.has_value(), "gemm_tile: split-K needs a partial buffer");
+    CHECK_DT(*partial, at::kFloat); CHECK_CONTIG(*partial);
+    TORCH_CHECK(partial->numel() >= splits * M * N, "gemm_tile: partial buffer too small");
+    pp = partial->data_ptr<float>();
+  }
   TORCH_CHECK(M * K < (1LL << 40) && N * K < (1LL << 40) && M < (1LL << 31) && N < (1LL << 31), "gemm too large");
   const c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
-  RC(oamd::gemm_tile(ptr<bf16_t>(x), ptr<bf16_t>(w), ptr<bf16_t>(y), optr<bf16_t>(bias), (int)M, (int)N, (int)K,
-                     (int)y.stride(0), silu_gu, (int)variant, cur_stream()));
+  RC(oamd::gemm_tile(ptr<bf16_t>(x), ptr<bf16_t>(w), yp, optr<bf16_t>(bias), (int)M, (int)N, (int)K, (int)ldy,
+                     silu_gu, (int)variant, (int)splits, pp, cur_stream()));
 }
 
 void gemm_skinny(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& y_opt,
@@ -408,7 +430,8 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("bm") = 0, pybind11::arg("silu_gu") = false, pybind11::arg("w_tiled") = false,
         pybind11::arg("stages") = 3);
   m.def("gemm_tile", &gemm_tile, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"),
-        pybind11::arg("bias") = pybind11::none(), pybind11::arg("silu_gu") = false, pybind11::arg("variant") = 0);
+        pybind11::arg("bias") = pybind11::none(), pybind11::arg("silu_gu") = false, pybind11::arg("variant") = 0,
+        pybind11::arg("splits") = 1, pybind11::arg("partial") = pybind11::none());
   m.def("gemm_skinny", &gemm_skinny, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"),
         pybind11::arg("p") = pybind11::none(), pybind11::arg("splits") = 1, pybind11::arg("silu_gu") = false);
   m.def("attn_prefill", &attn_prefill, pybind11::arg("q"), pybind11::arg("k"), pybind11::arg("v"),

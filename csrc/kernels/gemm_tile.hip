@@ -42,7 +42,7 @@ constexpr int kRegion = 16384;   // 128 rows x 128 B
 constexpr int kBuf = 4 * kRegion;
 constexpr int kGroupM = 8;
 
-enum { kEpiStore = 0, kEpiBias = 1, kEpiSilu = 2 };
+enum { kEpiStore = 0, kEpiBias = 1, kEpiSilu = 2, kEpiPartial = 3 };   // partial: fp32 split-K slab
 
 template <int N>
 __device__ __forceinline__ void vm_wait() {
@@ -64,7 +64,7 @@ __device__ __forceinline__ uint2 pack4(f32x4 v) {
 template <int EPI>
 __global__ void __launch_bounds__(512) gemm_tile256_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
                                                            bf16_t* __restrict__ Y, const bf16_t* __restrict__ bias,
-                                                           int M, int N, int K, int ldy) {
+                                                           int M, int N, int K, int ldy, float* __restrict__ P) {
   __shared__ __attribute__((aligned(1024))) char lds[2 * kBuf];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -95,7 +95,7 @@ __global__ void __launch_bounds__(512) gemm_tile256_kernel(const bf16_t* __restr
       const bool isx = (r == 0 || r == 3);
       const int half = (r == 2 || r == 3) ? 128 : 0;
       const int64_t grow = isx ? min(m0 + half + row, M - 1) : min(n0 + half + row, N - 1);
-      src[r][i] = (isx ? X : W) + grow * K + chunk * 8;
+      src[r][i] = (isx ? X : W) + grow * K + chunk * 8 + (int64_t)blockIdx.y * (K / gridDim.y);
     }
   auto issue = [&](int r, int buf, int kt) {
     char* dst = lds + buf * kBuf + r * kRegion;
@@ -154,7 +154,7 @@ __global__ void __launch_bounds__(512) gemm_tile256_kernel(const bf16_t* __restr
     __builtin_amdgcn_sched_barrier(0);
   };
 
-  const int T = K / kBK;
+  const int T = K / gridDim.y / kBK;   // K-tiles of this block's split-K slice (blockIdx.y)
   // prologue: all four regions of K-tile 0; X0 and W0 retired before the first reads
 #pragma unroll
   for (int r = 0; r < 4; ++r) issue(r, 0, 0);
@@ -210,7 +210,14 @@ __global__ void __launch_bounds__(512) gemm_tile256_kernel(const bf16_t* __restr
       bf16_t* yrow = Y + (int64_t)tok * ldy;
 #pragma unroll
       for (int f = 0; f < 2; ++f) {
-        if constexpr (EPI == kEpiSilu) {
+        if constexpr (EPI == kEpiPartial) {   // fp32 slab [blockIdx.y][M][N], 16-B stores
+          float* prow = P + ((int64_t)blockIdx.y * M + tok) * N;
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int col = n0 + f * 128 + e * 64 + wc * 16 + 4 * lq;
+            if (col < N) *reinterpret_cast<f32x4*>(prow + col) = acc[h][f][b][e];
+          }
+        } else if constexpr (EPI == kEpiSilu) {
           // interleaved gate|up: 128-row block f = 64 gate rows then their 64 up rows
           const int col = (n0 >> 1) + f * 64 + wc * 16 + 4 * lq;
           if (2 * col >= N) continue;
@@ -437,21 +444,63 @@ __global__ void __launch_bounds__(256) gemm_tile256_w4_kernel(const bf16_t* __re
   }
 }
 
+// y[m, f] = SwiGLU of the split-K sums of the interleaved gate|up slabs (64-feature
+// blocks): g = bf16(sum_s P[s][m][128 b + j]), u = bf16(sum_s P[s][m][128 b + 64 + j]),
+// y = bf16(bf16(silu(g)) * u) — the numerics of the fused epilogue. 4 features per thread.
+__global__ void splitk_silu_reduce_kernel(const float* __restrict__ P, bf16_t* __restrict__ Y, int M, int N, int S,
+                                          int ldy) {
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  const int NO = N / 2;
+  if (i >= (int64_t)M * NO) return;
+  const int m = (int)(i / NO), f = (int)(i % NO);
+  const int col = (f >> 6) * 128 + (f & 63);
+  const int64_t MN = (int64_t)M * N;
+  const float* pr = P + (int64_t)m * N + col;
+  f32x4 g = *reinterpret_cast<const f32x4*>(pr), u = *reinterpret_cast<const f32x4*>(pr + 64);
+  for (int s = 1; s < S; ++s) {
+    g += *reinterpret_cast<const f32x4*>(pr + s * MN);
+    u += *reinterpret_cast<const f32x4*>(pr + s * MN + 64);
+  }
+  f32x4 o;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float gg = bf2f(f2bf(g[r]));
+    const float uu = bf2f(f2bf(u[r]));
+    o[r] = bf2f(f2bf(gg / (1.f + __expf(-gg)))) * uu;
+  }
+  *reinterpret_cast<uint2*>(Y + (int64_t)m * ldy + f) = pack4(o);
+}
+
 int gemm_tile(const bf16_t* X, const bf16_t* W, bf16_t* Y, const bf16_t* bias, int M, int N, int K, int ldy,
-              bool silu_gu, int variant, hipStream_t stream) {
+              bool silu_gu, int variant, int S, float* P, hipStream_t stream) {
   if (M < 1 || N < 16 || N % 16 != 0 || K < kBK || K % kBK != 0) return -1;
   if (silu_gu && (N % 128 != 0 || bias != nullptr)) return -2;
-  if (ldy < (silu_gu ? N / 2 : N)) return -3;
+  if (Y != nullptr && ldy < (silu_gu ? N / 2 : N)) return -3;
+  if (S < 1 || S > 64 || K % (kBK * S) != 0 || (S > 1 && (P == nullptr || bias != nullptr))) return -5;
+  if (Y == nullptr && (S == 1 || silu_gu)) return -6;
   const int nwg = ((M + kT - 1) / kT) * ((N + kT - 1) / kT);
+  if (S > 1) {   // fp32 slabs, then (unless the consumer sums them) one reduce pass
+    gemm_tile256_kernel<kEpiPartial><<<dim3(nwg, S), 512, 0, stream>>>(X, W, Y, bias, M, N, K, ldy, P);
+    OAMD_LAUNCH_CHECK();
+    if (Y == nullptr) return 0;
+    if (silu_gu) {
+      const int64_t threads = (int64_t)M * (N / 2) / 4;
+      splitk_silu_reduce_kernel<<<(threads + 255) / 256, 256, 0, stream>>>(P, Y, M, N, S, ldy);
+      OAMD_LAUNCH_CHECK();
+      return 0;
+    }
+    if (ldy != N) return -7;
+    return splitk_reduce(P, Y, (int64_t)M * N, S, stream);
+  }
   const bool off32 = (int64_t)M * K * 2 < (1LL << 32) && (int64_t)N * K * 2 < (1LL << 32);
   if (variant == 1 && off32) {   // 4-wave 128x128 per wave (32-bit source offsets)
     if (silu_gu) gemm_tile256_w4_kernel<kEpiSilu><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
     else if (bias) gemm_tile256_w4_kernel<kEpiBias><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
     else gemm_tile256_w4_kernel<kEpiStore><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
   } else {   // default: 8-wave ping-pong
-    if (silu_gu) gemm_tile256_kernel<kEpiSilu><<<nwg, 512, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-    else if (bias) gemm_tile256_kernel<kEpiBias><<<nwg, 512, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-    else gemm_tile256_kernel<kEpiStore><<<nwg, 512, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+    if (silu_gu) gemm_tile256_kernel<kEpiSilu><<<nwg, 512, 0, stream>>>(X, W, Y, bias, M, N, K, ldy, nullptr);
+    else if (bias) gemm_tile256_kernel<kEpiBias><<<nwg, 512, 0, stream>>>(X, W, Y, bias, M, N, K, ldy, nullptr);
+    else gemm_tile256_kernel<kEpiStore><<<nwg, 512, 0, stream>>>(X, W, Y, bias, M, N, K, ldy, nullptr);
   }
   OAMD_LAUNCH_CHECK();
   return 0;

@@ -30,8 +30,10 @@ int gemm_decode(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, in
 // Compute-bound 256x256-tile GEMM (prefill projections, lm_head; gemm_tile.hip): Y[M, N] = X[M,K] W[N,K]^T
 // (+ bias[N]) for any M >= 1, N % 16 == 0, K % 64 == 0; silu_gu: fused SwiGLU over the 64-row interleaved
 // gate|up weight (N % 128 == 0), Y [M, N/2]. ldy = Y's row stride in elements.
+// S > 1: S-way split-K into fp32 slabs P[S][M][N], then reduced into Y (SwiGLU applied when silu_gu);
+// Y == nullptr leaves the slabs to the consumer (rmsnorm / rope_kv sum them).
 int gemm_tile(const bf16_t* X, const bf16_t* W, bf16_t* Y, const bf16_t* bias, int M, int N, int K, int ldy,
-              bool silu_gu, int variant, hipStream_t stream);
+              bool silu_gu, int variant, int S, float* P, hipStream_t stream);
 // Y[M, N] = bf16(sum_s P[s][M][N]) (fp32 split-K slabs).
 int splitk_reduce(const float* P, bf16_t* Y, int64_t MN, int S, hipStream_t stream);
 // Skinny-M decode GEMM (M <= 32, gemm_skinny.hip): N % 16 == 0, K % (128 S) == 0; S-way split-K slabs P

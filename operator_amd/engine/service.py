@@ -100,11 +100,11 @@ class LocalMatchService:
         try:
             with self._lock:
                 eng = self.engine
+            t0 = time.perf_counter()
             res = eng.analyze(docs, pods)
             self.batches += 1
             if self.metrics:
-                self.metrics.scan_batches.inc()
-                self.metrics.scan_bytes.inc(sum(map(len, docs)))
+                self.metrics.observe_scan(sum(map(len, docs)), time.perf_counter() - t0)
             for (_, f), r in zip(batch, res):
                 f.set_result(r)
         except Exception as e:  # noqa: BLE001

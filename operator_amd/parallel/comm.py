@@ -17,6 +17,8 @@ collective on the hot path (per-rank engines, host-side result gathering).
 from __future__ import annotations
 
 import datetime
+import threading
+import time
 import os
 from dataclasses import dataclass
 
@@ -54,6 +56,35 @@ def init_from_env(backend: str | None = None, timeout_s: int = 600) -> DistInfo:
     return DistInfo(rank, world, local, backend)
 
 
+class _CollectiveStats:
+    """Process-wide collective counters for the metrics endpoint (SURVEY.md §5.5 "RCCL
+    time"): calls and bytes per (op, impl); wall time only where the host waits on
+    the call (an RCCL / gloo collective issued eagerly: the launch-to-return time as
+    seen by the host; calls recorded into a hipGraph are counted at capture only)."""
+
+    def __init__(self):
+        self._d: dict[tuple[str, str], list[float]] = {}
+        self._lock = threading.Lock()
+
+    def add(self, op: str, impl: str, nbytes: int, seconds: float = 0.0) -> None:
+        with self._lock:
+            st = self._d.setdefault((op, impl), [0, 0, 0.0])
+            st[0] += 1
+            st[1] += nbytes
+            st[2] += seconds
+
+    def snapshot(self) -> dict:
+        with self._lock:
+            return {k: tuple(v) for k, v in self._d.items()}
+
+
+COLLECTIVES = _CollectiveStats()
+
+
+def _nbytes(t) -> int:
+    return t.numel() * t.element_size() if isinstance(t, torch.Tensor) else 0
+
+
 class Group:
     """Process-group handle; world==1 makes every collective a no-op."""
 
@@ -86,8 +117,11 @@ class Group:
         if self.world > 1:
             car = getattr(self, "oneshot", None)
             if car is not None and car.fits(t):
+                COLLECTIVES.add("all_reduce", "oneshot", _nbytes(t))
                 return car.all_reduce_(t)
+            t0 = time.perf_counter()
             dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.pg)
+            COLLECTIVES.add("all_reduce", dist.get_backend(self.pg), _nbytes(t), time.perf_counter() - t0)
         return t
 
     def all_reduce_rmsnorm(self, t, w: torch.Tensor, eps: float, residual: torch.Tensor) -> torch.Tensor:
@@ -101,6 +135,7 @@ class Group:
         if self.world > 1:
             car = getattr(self, "oneshot", None)
             if car is not None and isinstance(t, torch.Tensor) and car.fits_rows(t) and residual.is_contiguous():
+                COLLECTIVES.add("all_reduce_rmsnorm", "oneshot", _nbytes(t))
                 return car.all_reduce_rmsnorm_(t, residual, w, eps)
             self.all_reduce_(t)
         return ops.rmsnorm(t, w, eps, residual=residual)
@@ -109,7 +144,9 @@ class Group:
         if self.world == 1:
             return t
         out = [torch.empty_like(t) for _ in range(self.world)]
+        t0 = time.perf_counter()
         dist.all_gather(out, t.contiguous(), group=self.pg)
+        COLLECTIVES.add("all_gather", dist.get_backend(self.pg), _nbytes(t) * self.world, time.perf_counter() - t0)
         return torch.cat(out, dim=dim)
 
     def all_gather_into(self, t: torch.Tensor) -> torch.Tensor:
@@ -118,7 +155,9 @@ class Group:
             return t.unsqueeze(0)
         t = t.contiguous()
         out = torch.empty((self.world * t.shape[0], *t.shape[1:]), dtype=t.dtype, device=t.device)
+        t0 = time.perf_counter()
         dist.all_gather_into_tensor(out, t, group=self.pg)
+        COLLECTIVES.add("all_gather", dist.get_backend(self.pg), _nbytes(out), time.perf_counter() - t0)
         return out.view(self.world, *t.shape)
 
     def broadcast_(self, t: torch.Tensor, src_local: int = 0) -> torch.Tensor:

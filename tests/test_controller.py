@@ -585,3 +585,25 @@ def test_sink_concurrency_bounds_result_writers(monkeypatch):
     for t in ts:
         t.join()
     assert state["stored"] == 12 and 1 <= state["max"] <= 3
+
+
+def test_metrics_rates_and_collectives():
+    """SURVEY.md §5.5 gauges: scan GB/s of the last batch, tokens/s and analyses/s over
+    a window, and the process-wide collective counters."""
+    from operator_amd.parallel.comm import COLLECTIVES
+    from operator_amd.utils.metrics import Metrics
+
+    m = Metrics()
+    m.observe_scan(2 * 10**9, 0.5)
+    COLLECTIVES.add("all_reduce", "gloo", 4096, 0.002)
+    m.tokens_generated.inc(10)
+    m.render()
+    m.tokens_generated.inc(500)
+    import time as _t
+
+    _t.sleep(0.05)
+    txt = m.render().decode()
+    vals = {ln.split(" ")[0]: float(ln.split(" ")[-1]) for ln in txt.splitlines() if ln and not ln.startswith("#")}
+    assert vals["podmortem_scan_gigabytes_per_second"] == 4.0
+    assert vals["podmortem_tokens_per_second"] > 0
+    assert vals['podmortem_collective_calls_total{impl="gloo",op="all_reduce"}'] >= 1

@@ -1,0 +1,88 @@
+#!/usr/bin/env python3
+"""Decode-bucket GEMMs (M = 64 / 128 / 256, Llama-3-8B projections): the LDS-DMA
+split-K gemm_decode (tuned table, what ops.linear / gate_up_silu pick) vs the
+256x256-tile gemm_tile at split-K S in {1, 2, 4, 8, 16}, interleaved rounds in one
+process, random operands. One JSON line per (M, shape)."""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from operator_amd import ops  # noqa: E402
+
+SHAPES = [("gate_up+silu", 28672, 4096, True), ("qkv", 6144, 4096, False), ("o", 4096, 4096, False),
+          ("down", 4096, 14336, False)]
+
+
+def timeit(fn, iters):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--m", default="64,128,256")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=50)
+    a = ap.parse_args()
+    C = ops.kernels()
+    for M in [int(x) for x in a.m.split(",")]:
+        for name, N, K, silu in SHAPES:
+            torch.manual_seed(0)
+            x = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)
+            ws = [((torch.rand(N, K, device="cuda") * 2 - 1) * 0.05).to(torch.bfloat16) for _ in range(4)]
+            y = torch.empty(M, N // 2 if silu else N, dtype=torch.bfloat16, device="cuda")
+            P = torch.empty(16 * M * N, dtype=torch.float32, device="cuda")
+            it = {"i": 0}
+
+            def cur():
+                w = ws[it["i"] % 4]
+                it["i"] += 1
+                return ops.gate_up_silu(x, w, 64) if silu else ops.linear(x, w)
+
+            def tile(S):
+                def f():
+                    w = ws[it["i"] % 4]
+                    it["i"] += 1
+                    C.gemm_tile(x, w, y, None, silu, 0, S, P if S > 1 else None)
+                return f
+
+            cands = {"decode": cur}
+            for S in (1, 2, 4, 8, 16):
+                if K % (64 * S) == 0:
+                    cands[f"tile_s{S}"] = tile(S)
+            t = {k: [] for k in cands}
+            for _ in range(a.rounds):
+                for k, f in cands.items():
+                    t[k].append(timeit(f, a.iters))
+            med = {k: round(statistics.median(v), 2) for k, v in t.items()}
+            # numerics: tile vs the current path
+            ref = cur()
+            errs = {}
+            for S in (1, 2, 4):
+                if K % (64 * S) == 0:
+                    C.gemm_tile(x, ws[(it["i"] - 1) % 4], y, None, silu, 0, S, P if S > 1 else None)
+                    errs[S] = round((y.float() - ref.float()).abs().max().item(), 4)
+            best = min(med, key=med.get)
+            wb = N * K * 2
+            print(json.dumps({"M": M, "shape": name, "N": N, "K": K, "us": med, "best": best,
+                              "best_weight_tb_s": round(wb / med[best] / 1e6, 2), "max_diff_vs_decode": errs}),
+                  flush=True)
+
+
+if __name__ == "__main__":
+    main()
