@@ -88,3 +88,44 @@ def test_gemm_tile_rejects_bad_shapes():
     x, w = _rand(8, 100), _rand(32, 100)
     with pytest.raises(RuntimeError):
         ops.kernels().gemm_tile(x, w, torch.empty(8, 32, dtype=torch.bfloat16, device=DEV))
+
+
+@pytest.mark.parametrize("M", [1, 64, 130, 256])
+@pytest.mark.parametrize("N,K", [(128, 64), (384, 192), (1024, 1024), (4096, 4096)])
+def test_gemm_pp_decode(M, N, K):
+    """Ping-pong decode GEMM (gemm_pp.hip): both row tiles, every split count, nt and
+    default weight policy, reduced and deferred (slab) outputs."""
+    torch.manual_seed(M + N + K)
+    x = _rand(M, K)
+    w = _rand(N, K, scale=0.05)
+    r = x.float() @ w.float().t()
+    P = torch.empty(8 * M * N, dtype=torch.float32, device=DEV)
+    for bm in (128, 256):
+        for S in (1, 2, 4, 8):
+            if K % (64 * S):
+                continue
+            for nt in (True, False):
+                y = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+                ops.kernels().gemm_pp(x, w, y, P if S > 1 else None, S, bm, False, nt)
+                _close(y, r)
+            if S > 1:
+                ops.kernels().gemm_pp(x, w, None, P, S, bm, False, True)
+                torch.cuda.synchronize()
+                _close(P[:S * M * N].view(S, M, N).sum(0), r)
+
+
+@pytest.mark.parametrize("M", [3, 128, 256])
+def test_gemm_pp_silu(M):
+    inter, K = 1024, 2048
+    torch.manual_seed(M)
+    x = _rand(M, K)
+    g = _rand(inter, K, scale=0.05)
+    u = _rand(inter, K, scale=0.05)
+    wgu = ops.interleave_gate_up(g, u)
+    gg = (x.float() @ g.float().t()).to(torch.bfloat16)
+    uu = (x.float() @ u.float().t()).to(torch.bfloat16)
+    r = ref.silu_mul(torch.cat([gg, uu], 1), None)
+    for bm in (128, 256):
+        y = torch.empty(M, inter, dtype=torch.bfloat16, device=DEV)
+        ops.kernels().gemm_pp(x, wgu, y, None, 1, bm, True, True)
+        _close(y, r, 3e-2)

@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--m", default="64,128,256")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--tile", action="store_true", help="also time gemm_tile split-K")
     a = ap.parse_args()
     C = ops.kernels()
     for M in [int(x) for x in a.m.split(",")]:
@@ -61,10 +62,23 @@ def main():
                     C.gemm_tile(x, w, y, None, silu, 0, S, P if S > 1 else None)
                 return f
 
+            def pp(S, bm, nt):
+                def f():
+                    w = ws[it["i"] % 4]
+                    it["i"] += 1
+                    C.gemm_pp(x, w, y, P if S > 1 else None, S, bm, silu, nt)
+                return f
+
             cands = {"decode": cur}
-            for S in (1, 2, 4, 8, 16):
-                if K % (64 * S) == 0:
-                    cands[f"tile_s{S}"] = tile(S)
+            if a.tile:
+                for S in (1, 2, 4, 8, 16):
+                    if K % (64 * S) == 0:
+                        cands[f"tile_s{S}"] = tile(S)
+            for bm in ((128, 256) if M > 128 else (128,)):
+                for S in ((1,) if silu else (1, 2, 4, 8)):
+                    if K % (64 * S) == 0:
+                        for nt in (True, False):
+                            cands[f"pp_bm{bm}_s{S}{'_nt' if nt else ''}"] = pp(S, bm, nt)
             t = {k: [] for k in cands}
             for _ in range(a.rounds):
                 for k, f in cands.items():
@@ -73,10 +87,9 @@ def main():
             # numerics: tile vs the current path
             ref = cur()
             errs = {}
-            for S in (1, 2, 4):
-                if K % (64 * S) == 0:
-                    C.gemm_tile(x, ws[(it["i"] - 1) % 4], y, None, silu, 0, S, P if S > 1 else None)
-                    errs[S] = round((y.float() - ref.float()).abs().max().item(), 4)
+            for S in ((1,) if silu else (1, 4)):
+                C.gemm_pp(x, ws[(it["i"] - 1) % 4], y, P if S > 1 else None, S, 128, silu, True)
+                errs[f"pp_s{S}"] = round((y.float() - ref.float()).abs().max().item(), 4)
             best = min(med, key=med.get)
             wb = N * K * 2
             print(json.dumps({"M": M, "shape": name, "N": N, "K": K, "us": med, "best": best,

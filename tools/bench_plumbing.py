@@ -62,14 +62,29 @@ def main():
     ap.add_argument("--crs", type=int, default=20)
     ap.add_argument("--workers", type=int, default=64)
     ap.add_argument("--match", choices=["stub", "cpu"], default="stub")
+    ap.add_argument("--pool", type=int, default=0,
+                    help="engines in N worker processes behind the EnginePool (the `run --gpus N` topology: "
+                         "CPU matcher + echo explainer per worker) instead of in this process")
+    ap.add_argument("--log-kb", type=int, default=0, help="pad every pod log to this size (KiB)")
     a = ap.parse_args()
     s = load_settings(env={}, overrides={"patterns.cache_dir": "/tmp/oamd-plumbing", "health.enabled": False,
                                          "operator.workers": a.workers})
     fk = FakeKube()
     done = {}
-    match = StubMatch() if a.match == "stub" else LocalMatchService(MatchEngine(catalog_library(), device="cpu"),
-                                                                   max_wait_ms=2.0)
-    op = Operator(fk, s, match_service=match, explain_service=EchoExplainService())
+    pool = None
+    if a.pool:
+        from operator_amd.engine.pool import EnginePool, PoolExplainService, PoolMatchService
+
+        s.services.explain = "echo"
+        s.services.match = "cpu"
+        pool = EnginePool(s, catalog_library(), ["cpu"] * a.pool)
+        assert pool.wait_ready(300) == a.pool, pool.health()
+        match, explain = PoolMatchService(pool), PoolExplainService(pool)
+    else:
+        match = StubMatch() if a.match == "stub" else LocalMatchService(MatchEngine(catalog_library(), device="cpu"),
+                                                                       max_wait_ms=2.0)
+        explain = EchoExplainService()
+    op = Operator(fk, s, match_service=match, explain_service=explain)
     op.pipeline.listeners.append(lambda monitor, pod, outcome: done.setdefault(pod["metadata"]["name"],
                                                                                  time.perf_counter()))
     op.start(http=False)
@@ -86,9 +101,13 @@ def main():
         assert ok, "reconcile timed out"
         rec.append(time.perf_counter() - t0)
     names = [f"p{i}" for i in range(a.failures)]
+    log = LOG
+    if a.log_kb:
+        filler = b"INFO request served in 3 ms from cache shard 7\n"
+        log = filler * max(0, (a.log_kb * 1024 - len(LOG)) // len(filler)) + LOG
     for n in names:
         fk.create(PODS, running_pod(n, labels={"app": "demo"}))
-        fk.set_log("default", n, LOG)
+        fk.set_log("default", n, log)
     t_fail = {}
     t0 = time.perf_counter()
     for n in names:
@@ -101,12 +120,16 @@ def main():
     elapsed = time.perf_counter() - t0
     lat = sorted(done[n] - t_fail[n] for n in names)
     op.stop()
+    if pool is not None:
+        pool.close()
     print(json.dumps({"bench": "plumbing (BASELINE config 1)", "failures": a.failures,
+                      "topology": f"EnginePool x{a.pool} (CPU matcher + echo)" if a.pool else "in-process",
+                      "log_bytes": len(log),
                       "analyses_per_s": round(a.failures / elapsed, 1),
                       "p50_ms": round(statistics.median(lat) * 1e3, 1), "p99_ms": round(lat[int(0.99 * len(lat))] * 1e3, 1),
                       "reconcile_p50_ms": round(statistics.median(rec) * 1e3, 2),
                       "reconcile_max_ms": round(max(rec) * 1e3, 2), "crs": a.crs,
-                      "engines": ("stub log-parser" if a.match == "stub" else "CPU matcher (catalog)") +
+                      "engines": ("stub log-parser" if a.match == "stub" and not a.pool else "CPU matcher (catalog)") +
                       " + echo explainer", "pipeline_workers": a.workers}))
 
 
