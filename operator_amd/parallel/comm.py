@@ -170,6 +170,52 @@ class Group:
             dist.barrier(group=self.pg)
 
 
+class SimulatedTPGroup(Group):
+    """Rank 0's shard of a TP=``world`` replica on ONE device, for per-rank performance
+    (tools/bench_tp.py --simulate-tp): the model is sharded exactly as at TP=world and
+    every collective launches the world-1 one-shot kernels (the same push / flag /
+    reduce code path and fused RMSNorm, with no peer to wait for), so a step costs what
+    one rank's step costs minus the xGMI transfer time. Gathers replicate the local
+    shard. Without a GPU the collectives are no-ops."""
+
+    def __init__(self, world: int, device):
+        self.pg, self.rank, self.world, self.ranks = None, 0, int(world), list(range(int(world)))
+        self.car = None
+        if torch.device(device).type == "cuda":
+            from .custom_ar import DEFAULT_MAX_BYTES, OneShotAllReduce
+
+            self.car = OneShotAllReduce(Group.single(), device, DEFAULT_MAX_BYTES)
+
+    def enable_oneshot(self, device, max_bytes: int | None = None) -> bool:
+        return self.car is not None
+
+    def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
+        if self.car is not None and self.car.fits(t):
+            COLLECTIVES.add("all_reduce", "oneshot-sim", _nbytes(t))
+            return self.car.all_reduce_(t)
+        return t
+
+    def all_reduce_rmsnorm(self, t, w: torch.Tensor, eps: float, residual: torch.Tensor) -> torch.Tensor:
+        from operator_amd import ops
+
+        if self.car is not None and isinstance(t, torch.Tensor) and self.car.fits_rows(t) and residual.is_contiguous():
+            COLLECTIVES.add("all_reduce_rmsnorm", "oneshot-sim", _nbytes(t))
+            return self.car.all_reduce_rmsnorm_(t, residual, w, eps)
+        return ops.rmsnorm(t, w, eps, residual=residual)
+
+    def all_gather(self, t: torch.Tensor, dim: int = 0) -> torch.Tensor:
+        return torch.cat([t] * self.world, dim=dim)
+
+    def all_gather_into(self, t: torch.Tensor) -> torch.Tensor:
+        return t.unsqueeze(0).expand(self.world, *t.shape).contiguous()
+
+    def broadcast_(self, t: torch.Tensor, src_local: int = 0) -> torch.Tensor:
+        return t
+
+    def barrier(self) -> None:
+        pass
+
+
 def split_groups(tp: int) -> tuple[Group, Group]:
     """Return (tp_group, dp_group) for this rank. World must be a multiple of tp."""
     if not (dist.is_available() and dist.is_initialized()):

@@ -145,3 +145,20 @@ def test_tp_leader_failure_is_fatal(tmp_path):
                        start_method="spawn")
     res = torch.load(tmp_path / "fail.pt", weights_only=True)
     assert res["fatal"] and not res["alive"] and "out of memory" in res["error"]
+
+
+def test_bench_tp_simulate_runs_one_rank_shard():
+    """tools/bench_tp.py --simulate-tp 8: one process drives rank 0's TP=8 shard (per-rank
+    shapes, simulated collectives) and reports the shard's weight floor."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "bench_tp.py"), "--simulate-tp", "8", "--model",
+                        "tiny-tp8", "--dtype", "float32", "--batch", "3", "--prompt", "24", "--gen", "6", "--kv-gb",
+                        "0.05"], capture_output=True, text=True, timeout=300, cwd=root, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][0])
+    assert out["simulated_tp"] == 8 and out["tp"] == 8 and out["decode_tok_s"] > 0 and out["weight_floor_ms"] > 0
