@@ -290,6 +290,18 @@ void quantize_fp8(const at::Tensor& x, at::Tensor& q, at::Tensor& sx) {
                              x.stride(0), cur_stream()));
 }
 
+void silu_quantize_fp8(const at::Tensor& gu, at::Tensor& q, at::Tensor& sx) {
+  CHECK_DEV(gu); CHECK_BF16(gu); CHECK_CONTIG(q); CHECK_CONTIG(sx); CHECK_DT(sx, at::kFloat);
+  TORCH_CHECK(gu.dim() == 2 && gu.stride(1) == 1, "gu must be [M, 2I] row-major");
+  TORCH_CHECK(q.scalar_type() == at::kByte || q.scalar_type() == at::kFloat8_e4m3fn, "q must be uint8 / e4m3fn");
+  const int64_t M = gu.size(0), I = gu.size(1) / 2;
+  TORCH_CHECK(gu.size(1) % 128 == 0 && I <= 16384, "silu_quantize_fp8: 2I % 128 == 0, I <= 16384");
+  TORCH_CHECK(q.numel() == M * I && sx.numel() == M, "silu_quantize_fp8 shapes");
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(gu.device());
+  RC(oamd::silu_quantize_fp8(ptr<bf16_t>(gu), static_cast<uint8_t*>(q.data_ptr()), ptr<float>(sx), (int)M, (int)I,
+                             gu.stride(0), cur_stream()));
+}
+
 void gemm_fp8(const at::Tensor& x8, const at::Tensor& w8, const at::Tensor& sx, const at::Tensor& sw, at::Tensor& y,
               const c10::optional<at::Tensor>& p, int64_t splits, int64_t bn, int64_t bm) {
   CHECK_DEV(x8); CHECK_CONTIG(x8); CHECK_CONTIG(w8); CHECK_CONTIG(sx); CHECK_CONTIG(sw); CHECK_BF16(y);
@@ -451,6 +463,7 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("ml_part"), pybind11::arg("num_splits"), pybind11::arg("scale"), pybind11::arg("variant") = 0,
         pybind11::arg("k_scale") = 1.0, pybind11::arg("v_scale") = 1.0);
   m.def("quantize_fp8", &quantize_fp8);
+  m.def("silu_quantize_fp8", &silu_quantize_fp8);
   m.def("score_events", &score_events);
   m.def("gemm_fp8", &gemm_fp8, pybind11::arg("x8"), pybind11::arg("w8"), pybind11::arg("sx"), pybind11::arg("sw"),
         pybind11::arg("y"), pybind11::arg("p") = pybind11::none(), pybind11::arg("splits") = 1,

@@ -52,6 +52,9 @@ int gemm_fp8(const uint8_t* X, const uint8_t* W, const float* sx, const float* s
              int N, int K, int S, int BN, int BM, hipStream_t stream);
 // Per-row dynamic quantization to e4m3fn: sx[m] = max|x[m]| / 448.
 int quantize_fp8_rows(const bf16_t* x, uint8_t* q, float* sx, int M, int K, int64_t ld, hipStream_t stream);
+// Fused SwiGLU + per-row e4m3fn quantization of the 64-feature-interleaved gate|up rows [M, 2 inter]
+// (inter % 64 == 0, <= 16384): q [M, inter], sx [M].
+int silu_quantize_fp8(const bf16_t* gu, uint8_t* q, float* sx, int M, int inter, int64_t ld, hipStream_t stream);
 
 // Pattern-event scoring + per-doc ranking / summary (N5), see score.hip.
 int score_events(const int64_t* keys, const int* hit_doc, const int* doc_ptr, int n_hits, int n_docs,

@@ -134,14 +134,15 @@ def _worker_main(idx: int, device: str, settings_obj: dict, patterns, roles: tup
     pool = ThreadPoolExecutor(max_workers=max(4, s.operator.workers or 2 * s.engine.max_batch + 16))
 
     def run(rid, kind, payload):
+        # requests and results cross the process boundary as the pydantic objects
+        # themselves (pickled by the queue): no dict round trip, no re-validation of a
+        # whole AnalysisResult on the controller's GIL per failure
         try:
             if kind == "match":
-                res = matcher.analyze(PodFailureData.model_validate(payload))
-                outq.put(("ok", idx, rid, res.to_obj()))
+                res = matcher.analyze(payload)
             else:
-                res = explainer.explain(AnalysisResult.model_validate(payload[0]),
-                                        AIProviderConfig.model_validate(payload[1]))
-                outq.put(("ok", idx, rid, res.to_obj()))
+                res = explainer.explain(payload[0], payload[1])
+            outq.put(("ok", idx, rid, res))
         except Exception as e:  # noqa: BLE001 - per-request failure, worker stays up
             outq.put(("err", idx, rid, f"{type(e).__name__}: {e}"))
 
@@ -309,12 +310,12 @@ class EnginePool:
 
     def submit_match(self, data: PodFailureData) -> Future:
         fut: Future = Future()
-        self._dispatch("match", data.model_dump(by_alias=True, exclude_none=True), fut)
+        self._dispatch("match", data, fut)
         return fut
 
     def submit_explain(self, result: AnalysisResult, cfg: AIProviderConfig) -> Future:
         fut: Future = Future()
-        self._dispatch("explain", (result.to_obj(), cfg.model_dump(by_alias=True, exclude_none=True)), fut)
+        self._dispatch("explain", (result, cfg), fut)
         return fut
 
     def worker_stats(self, timeout: float = 30.0) -> list[dict]:
@@ -370,11 +371,8 @@ class EnginePool:
                 elif kind in ("ok", "err"):
                     item = w.inflight.pop(msg[2], None)
                     if item is not None and not item[2].done():
-                        if kind == "ok" and item[0] == "stats":
+                        if kind == "ok":
                             item[2].set_result(msg[3])
-                        elif kind == "ok":
-                            cls = AnalysisResult if item[0] == "match" else AIResponse
-                            item[2].set_result(cls.model_validate(msg[3]))
                         else:
                             item[2].set_exception(RuntimeError(msg[3]))
 

@@ -265,7 +265,8 @@ class LlamaModel:
             if lw.sgu is None:
                 m = ops.gate_up_silu(x, lw.wgu, self.gu_block)
             else:
-                m = ops.silu_mul(ops.linear_fp8(x, lw.wgu, lw.sgu), block=self.gu_block)
+                gu = ops.linear_fp8(x, lw.wgu, lw.sgu)   # SwiGLU fused into the down GEMM's input quantization
+                m = ops.silu_quantize_fp8(gu, self.gu_block) if gu.is_cuda else ops.silu_mul(gu, block=self.gu_block)
             d = self._lin(m, lw.wd, lw.sd, defer=True)
             nw = self.layers[i + 1].attn_norm if i + 1 < len(self.layers) else self.final_norm
             x = self.tp.all_reduce_rmsnorm(d, nw, c.rms_eps, residual=h)

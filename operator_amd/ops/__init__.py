@@ -19,7 +19,7 @@ __all__ = [
     "rmsnorm", "silu_mul", "embedding", "rope_kv", "attn_prefill", "attn_decode", "sample",
     "kernels", "patterns", "native_available", "reference", "prefill_work_list", "prefill_block_q", "prefill_variant", "decode_splits",
     "decode_workspace", "linear", "gemm_splits", "gemm_plan", "gate_up_silu", "interleave_gate_up",
-    "quantize_fp8", "linear_fp8", "fp8_plan", "SplitK", "linear_tile", "tile_ok", "BLAS_CALLS",
+    "quantize_fp8", "silu_quantize_fp8", "linear_fp8", "fp8_plan", "SplitK", "linear_tile", "tile_ok", "BLAS_CALLS",
 ]
 
 DECODE_MIN_SPLIT_TOKENS = 256  # never split a sequence into pieces shorter than this
@@ -404,6 +404,18 @@ def quantize_fp8(x: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
     return (xf / sx[:, None]).to(torch.float8_e4m3fn), sx
 
 
+def silu_quantize_fp8(gu: torch.Tensor, block: int | None = GU_BLOCK) -> tuple[torch.Tensor, torch.Tensor]:
+    """quantize_fp8(silu_mul(gu, block)) — on the GPU one kernel for 64-feature
+    interleaved gate|up rows (the SwiGLU never round-trips HBM as bf16)."""
+    inter = gu.shape[1] // 2
+    if gu.is_cuda and block == GU_BLOCK and inter <= 16384 and gu.stride(1) == 1:
+        q = torch.empty(gu.shape[0], inter, dtype=torch.float8_e4m3fn, device=gu.device)
+        sx = torch.empty(gu.shape[0], dtype=torch.float32, device=gu.device)
+        kernels().silu_quantize_fp8(gu, q, sx)
+        return q, sx
+    return quantize_fp8(silu_mul(gu, block=block))
+
+
 def fp8_plan(M: int, N: int, K: int) -> tuple[int, int, int]:
     """(bm, bn, splits) for gemm_fp8: row tile by M, 128-column tiles for wide N, and
     split-K until the blocks reach one per CU (K permitting)."""
@@ -420,18 +432,19 @@ def fp8_plan(M: int, N: int, K: int) -> tuple[int, int, int]:
     return bm, bn, S
 
 
-def linear_fp8(x: torch.Tensor, w8: torch.Tensor, sw: torch.Tensor, out: torch.Tensor | None = None,
-               plan: tuple[int, int, int] | None = None) -> torch.Tensor:
-    """y = x @ (w8 * sw)^T with x quantized per token to e4m3fn (W8A8, fp32 accumulate)."""
-    M, K = x.shape
+def linear_fp8(x: torch.Tensor | tuple[torch.Tensor, torch.Tensor], w8: torch.Tensor, sw: torch.Tensor,
+               out: torch.Tensor | None = None, plan: tuple[int, int, int] | None = None) -> torch.Tensor:
+    """y = x @ (w8 * sw)^T with x quantized per token to e4m3fn (W8A8, fp32 accumulate).
+    ``x`` may already be quantized: a (q, sx) pair from quantize_fp8 / silu_quantize_fp8."""
+    q, sx = x if isinstance(x, tuple) else quantize_fp8(x)
+    M, K = q.shape
     N = w8.shape[0]
-    q, sx = quantize_fp8(x)
-    if not x.is_cuda:
+    if not q.is_cuda:
         y = (q.float() * sx[:, None]) @ (w8.float() * sw[:, None]).t()
-        return out.copy_(y) if out is not None else y.to(x.dtype)
+        return out.copy_(y) if out is not None else y.to(torch.bfloat16 if isinstance(x, tuple) else x.dtype)
     bm, bn, S = plan or fp8_plan(M, N, K)
-    y = out if out is not None else torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
-    part = torch.empty(S * M * N, dtype=torch.float32, device=x.device) if S > 1 else None
+    y = out if out is not None else torch.empty(M, N, dtype=torch.bfloat16, device=q.device)
+    part = torch.empty(S * M * N, dtype=torch.float32, device=q.device) if S > 1 else None
     kernels().gemm_fp8(q, w8, sx, sw, y, part, S, bn, bm)
     return y
 

@@ -218,9 +218,10 @@ def test_gate_up_silu_fused(M):
                 torch.testing.assert_close(y.float(), ref_.float(), atol=2e-2, rtol=2e-2, msg=f"bm={bm} ns={ns}")
 
 
-def test_quantize_fp8_matches_torch():
+@pytest.mark.parametrize("K", [1024, 3584, 8192, 14336, 20480])  # reg paths 2/4/8 vectors + streaming
+def test_quantize_fp8_matches_torch(K):
     torch.manual_seed(9)
-    x = _rand(37, 1024) * 3
+    x = _rand(37, K) * 3
     x[5] = 0  # all-zero row: scale 1, zeros
     q, sx = ops.quantize_fp8(x)
     amax = x.float().abs().amax(1)
@@ -232,6 +233,21 @@ def test_quantize_fp8_matches_torch():
     ulp = torch.clamp(want_q.abs(), min=2 ** -6) * 2 ** -3
     assert ((got - want_q).abs() <= ulp + 1e-12).all()
     assert (q[5].float() == 0).all()
+
+
+@pytest.mark.parametrize("inter", [1024, 3584, 14336])
+def test_silu_quantize_fp8_matches_unfused(inter):
+    """Fused SwiGLU + per-row quantization == quantize_fp8(silu_mul(gu)) (64-interleaved)."""
+    torch.manual_seed(10)
+    gu = _rand(19, 2 * inter) * 2
+    q, sx = ops.silu_quantize_fp8(gu, block=64)
+    m = ops.silu_mul(gu, block=64)
+    q0, s0 = ops.quantize_fp8(m)
+    torch.testing.assert_close(sx, s0, rtol=1e-6, atol=0)
+    got, want = q.float(), q0.float()
+    ulp = torch.clamp(want.abs(), min=2 ** -6) * 2 ** -3
+    assert ((got - want).abs() <= ulp + 1e-12).all()
+    assert (got == want).float().mean() > 0.99
 
 
 @pytest.mark.parametrize("M", [1, 37, 64, 200, 256])
