@@ -290,20 +290,32 @@ void quantize_fp8(const at::Tensor& x, at::Tensor& q, at::Tensor& sx) {
                              x.stride(0), cur_stream()));
 }
 
-void silu_quantize_fp8(const at::Tensor& gu, at::Tensor& q, at::Tensor& sx) {
-  CHECK_DEV(gu); CHECK_BF16(gu); CHECK_CONTIG(q); CHECK_CONTIG(sx); CHECK_DT(sx, at::kFloat);
+// gu: bf16 [M, 2I] gate|up rows, or (slabs given) a shape carrier [M, 2I] whose values are the
+// S fp32 split-K slabs [S, M, 2I] of the producing GEMM.
+void silu_quantize_fp8(const at::Tensor& gu, at::Tensor& q, at::Tensor& sx, const c10::optional<at::Tensor>& slabs,
+                       int64_t splits) {
+  CHECK_DEV(gu); CHECK_CONTIG(q); CHECK_CONTIG(sx); CHECK_DT(sx, at::kFloat);
   TORCH_CHECK(gu.dim() == 2 && gu.stride(1) == 1, "gu must be [M, 2I] row-major");
   TORCH_CHECK(q.scalar_type() == at::kByte || q.scalar_type() == at::kFloat8_e4m3fn, "q must be uint8 / e4m3fn");
   const int64_t M = gu.size(0), I = gu.size(1) / 2;
   TORCH_CHECK(gu.size(1) % 128 == 0 && I <= 16384, "silu_quantize_fp8: 2I % 128 == 0, I <= 16384");
   TORCH_CHECK(q.numel() == M * I && sx.numel() == M, "silu_quantize_fp8 shapes");
+  const float* pp = nullptr;
+  if (slabs.has_value()) {
+    CHECK_DT(*slabs, at::kFloat); CHECK_CONTIG(*slabs);
+    TORCH_CHECK(splits >= 1 && slabs->numel() >= splits * M * 2 * I, "slabs: fp32 [splits, M, 2I]");
+    pp = slabs->data_ptr<float>();
+  } else {
+    CHECK_BF16(gu);
+  }
   const c10::hip::HIPGuardMasqueradingAsCUDA g(gu.device());
-  RC(oamd::silu_quantize_fp8(ptr<bf16_t>(gu), static_cast<uint8_t*>(q.data_ptr()), ptr<float>(sx), (int)M, (int)I,
-                             gu.stride(0), cur_stream()));
+  RC(oamd::silu_quantize_fp8(pp != nullptr ? nullptr : ptr<bf16_t>(gu), pp, (int)splits,
+                             static_cast<uint8_t*>(q.data_ptr()), ptr<float>(sx), (int)M, (int)I,
+                             pp != nullptr ? 2 * I : gu.stride(0), cur_stream()));
 }
 
 void gemm_fp8(const at::Tensor& x8, const at::Tensor& w8, const at::Tensor& sx, const at::Tensor& sw, at::Tensor& y,
-              const c10::optional<at::Tensor>& p, int64_t splits, int64_t bn, int64_t bm) {
+              const c10::optional<at::Tensor>& p, int64_t splits, int64_t bn, int64_t bm, bool reduce) {
   CHECK_DEV(x8); CHECK_CONTIG(x8); CHECK_CONTIG(w8); CHECK_CONTIG(sx); CHECK_CONTIG(sw); CHECK_BF16(y);
   CHECK_CONTIG(y); CHECK_DT(sx, at::kFloat); CHECK_DT(sw, at::kFloat);
   for (auto* t : {&x8, &w8})
@@ -323,7 +335,7 @@ void gemm_fp8(const at::Tensor& x8, const at::Tensor& w8, const at::Tensor& sx, 
   }
   const c10::hip::HIPGuardMasqueradingAsCUDA g(x8.device());
   RC(oamd::gemm_fp8(static_cast<const uint8_t*>(x8.data_ptr()), static_cast<const uint8_t*>(w8.data_ptr()),
-                    ptr<float>(sx), ptr<float>(sw), ptr<bf16_t>(y), pp, (int)M, (int)N, (int)K, (int)splits, (int)bn,
+                    ptr<float>(sx), ptr<float>(sw), (reduce || splits == 1) ? ptr<bf16_t>(y) : nullptr, pp, (int)M, (int)N, (int)K, (int)splits, (int)bn,
                     (int)bm, cur_stream()));
 }
 
@@ -463,11 +475,12 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("ml_part"), pybind11::arg("num_splits"), pybind11::arg("scale"), pybind11::arg("variant") = 0,
         pybind11::arg("k_scale") = 1.0, pybind11::arg("v_scale") = 1.0);
   m.def("quantize_fp8", &quantize_fp8);
-  m.def("silu_quantize_fp8", &silu_quantize_fp8);
+  m.def("silu_quantize_fp8", &silu_quantize_fp8, pybind11::arg("gu"), pybind11::arg("q"), pybind11::arg("sx"),
+        pybind11::arg("slabs") = pybind11::none(), pybind11::arg("splits") = 1);
   m.def("score_events", &score_events);
   m.def("gemm_fp8", &gemm_fp8, pybind11::arg("x8"), pybind11::arg("w8"), pybind11::arg("sx"), pybind11::arg("sw"),
         pybind11::arg("y"), pybind11::arg("p") = pybind11::none(), pybind11::arg("splits") = 1,
-        pybind11::arg("bn") = 64, pybind11::arg("bm") = 64);
+        pybind11::arg("bn") = 64, pybind11::arg("bm") = 64, pybind11::arg("reduce") = true);
   m.def("gemm_decode", &gemm_decode, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"),
         pybind11::arg("p") = pybind11::none(), pybind11::arg("splits") = 1, pybind11::arg("bn") = 64,
         pybind11::arg("bm") = 0, pybind11::arg("silu_gu") = false, pybind11::arg("w_tiled") = false,

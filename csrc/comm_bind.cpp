@@ -65,24 +65,55 @@ class CustomAllReduce {
   }
 
   // residual += all_reduce(in) (bf16-rounded); y = rmsnorm(residual) * w — one launch.
-  void all_reduce_rmsnorm(const at::Tensor& in, at::Tensor& residual, const at::Tensor& w, at::Tensor& y, double eps) {
+  // `in` = None with `slabs` = S fp32 split-K slabs of the producing GEMM (summed in the kernel);
+  // q8/sx given: y is also emitted as per-row e4m3fn for the next fp8 GEMM.
+  void all_reduce_rmsnorm(const c10::optional<at::Tensor>& in, at::Tensor& residual, const at::Tensor& w,
+                          at::Tensor& y, double eps, const c10::optional<at::Tensor>& slabs, int64_t splits,
+                          const c10::optional<at::Tensor>& q8, const c10::optional<at::Tensor>& sx) {
     TORCH_CHECK(opened_ || world_ == 1, "CustomAllReduce: open() the peer handles first");
-    for (const at::Tensor* t : {&in, const_cast<const at::Tensor*>(&residual), &w, const_cast<const at::Tensor*>(&y)}) {
-      TORCH_CHECK(t->is_cuda() && t->device().index() == device_, "tensors must be on this device");
-      TORCH_CHECK(t->is_contiguous() && t->scalar_type() == at::kBFloat16, "bf16 contiguous tensors");
+    TORCH_CHECK(in.has_value() != slabs.has_value(), "exactly one of in / slabs");
+    TORCH_CHECK(q8.has_value() == sx.has_value(), "q8 and sx together");
+    auto on_dev = [&](const at::Tensor& t) {
+      TORCH_CHECK(t.is_cuda() && t.device().index() == device_ && t.is_contiguous(), "contiguous tensors on this device");
+    };
+    for (const at::Tensor* t : {const_cast<const at::Tensor*>(&residual), &w, const_cast<const at::Tensor*>(&y)}) {
+      on_dev(*t);
+      TORCH_CHECK(t->scalar_type() == at::kBFloat16, "bf16 residual / w / y");
     }
-    TORCH_CHECK(in.dim() == 2 && residual.sizes() == in.sizes() && y.sizes() == in.sizes(), "[rows, hidden] shapes");
-    TORCH_CHECK(w.numel() == in.size(1), "w [hidden]");
-    const int64_t rows = in.size(0), hidden = in.size(1);
+    TORCH_CHECK(residual.dim() == 2 && y.sizes() == residual.sizes(), "[rows, hidden] shapes");
+    const int64_t rows = residual.size(0), hidden = residual.size(1);
+    TORCH_CHECK(w.numel() == hidden, "w [hidden]");
     TORCH_CHECK(hidden % 8 == 0 && hidden <= 16384, "hidden % 8 == 0 and <= 16384");
     TORCH_CHECK(rows * hidden * 2 <= cap_, "size must be <= capacity");
-    const c10::hip::HIPGuardMasqueradingAsCUDA g(in.device());
-    const int rc = oamd::car_all_reduce_rmsnorm(in.data_ptr(), reinterpret_cast<oamd::bf16_t*>(residual.data_ptr()),
-                                                reinterpret_cast<const oamd::bf16_t*>(w.data_ptr()),
-                                                reinterpret_cast<oamd::bf16_t*>(y.data_ptr()), (int)rows, (int)hidden,
-                                                (float)eps, (int)rank_, (int)world_, bases_.data(), (size_t)cap_,
-                                                (int)blocks_, herr_dev_, timeout_s_,
-                                                c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream());
+    const void* ip = nullptr;
+    const float* sp = nullptr;
+    if (in.has_value()) {
+      on_dev(*in);
+      TORCH_CHECK(in->scalar_type() == at::kBFloat16 && in->sizes() == residual.sizes(), "in: bf16 [rows, hidden]");
+      ip = in->data_ptr();
+    } else {
+      on_dev(*slabs);
+      TORCH_CHECK(slabs->scalar_type() == at::kFloat && splits >= 1 && slabs->numel() >= splits * rows * hidden,
+                  "slabs: fp32 [splits, rows, hidden]");
+      sp = slabs->data_ptr<float>();
+    }
+    uint8_t* qp = nullptr;
+    float* xp = nullptr;
+    if (q8.has_value()) {
+      on_dev(*q8);
+      on_dev(*sx);
+      TORCH_CHECK((q8->scalar_type() == at::kByte || q8->scalar_type() == at::kFloat8_e4m3fn) &&
+                      q8->numel() == rows * hidden && sx->scalar_type() == at::kFloat && sx->numel() == rows,
+                  "q8 e4m3fn [rows, hidden], sx fp32 [rows]");
+      qp = static_cast<uint8_t*>(q8->data_ptr());
+      xp = sx->data_ptr<float>();
+    }
+    const c10::hip::HIPGuardMasqueradingAsCUDA g(residual.device());
+    const int rc = oamd::car_all_reduce_rmsnorm(
+        ip, sp, (int)splits, reinterpret_cast<oamd::bf16_t*>(residual.data_ptr()),
+        reinterpret_cast<const oamd::bf16_t*>(w.data_ptr()), reinterpret_cast<oamd::bf16_t*>(y.data_ptr()), qp, xp,
+        (int)rows, (int)hidden, (float)eps, (int)rank_, (int)world_, bases_.data(), (size_t)cap_, (int)blocks_,
+        herr_dev_, timeout_s_, c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream());
     TORCH_CHECK(rc == 0, "one-shot all-reduce + rmsnorm launch failed rc=", rc);
   }
 
@@ -135,7 +166,9 @@ void register_comm_bindings(pybind11::module_& m) {
       .def("handle", &CustomAllReduce::handle)
       .def("open", &CustomAllReduce::open)
       .def("all_reduce", &CustomAllReduce::all_reduce)
-      .def("all_reduce_rmsnorm", &CustomAllReduce::all_reduce_rmsnorm)
+      .def("all_reduce_rmsnorm", &CustomAllReduce::all_reduce_rmsnorm, pybind11::arg("in"), pybind11::arg("residual"),
+           pybind11::arg("w"), pybind11::arg("y"), pybind11::arg("eps"), pybind11::arg("slabs") = pybind11::none(),
+           pybind11::arg("splits") = 1, pybind11::arg("q8") = pybind11::none(), pybind11::arg("sx") = pybind11::none())
       .def("error", &CustomAllReduce::error)
       .def("reset", &CustomAllReduce::reset)
       .def("close", &CustomAllReduce::close)

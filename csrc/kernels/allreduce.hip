@@ -173,14 +173,21 @@ __global__ void __launch_bounds__(car::kThreads) oneshot_allreduce_kernel(const 
 // launch replaces two (the fusion that makes TP=8 pay).
 // Numerics are those of all-reduce + rmsnorm_kernel: the sum is rounded to bf16,
 // the residual add is rounded to bf16, the normalised value is rounded before w.
-template <int W, int MAXV>
+// SLABS: the input is S fp32 split-K slabs [S, rows, hidden] of the producing GEMM,
+// summed in slab order and rounded to bf16 on the way into the peers' receive slots
+// (bit-identical to splitk_reduce_fp32 + the bf16 path, one kernel fewer).
+// Q8: also emit the normalised rows as per-row e4m3fn (q8, sx) for the next fp8 GEMM,
+// bit-identical to quantize_fp8(y) — the activation quantization kernel disappears.
+template <int W, int MAXV, bool SLABS, bool Q8>
 __global__ void __launch_bounds__(car::kThreads) oneshot_ar_rmsnorm_kernel(
-    const uint4* __restrict__ in, bf16_t* __restrict__ residual, const bf16_t* __restrict__ w,
-    bf16_t* __restrict__ y, int rows, int hidden, float eps, int64_t capvec, int rank, CarPeers peers,
-    uint32_t* herr, uint64_t timeout_ticks) {
+    const uint4* __restrict__ in, const float* __restrict__ slabs, int S, bf16_t* __restrict__ residual,
+    const bf16_t* __restrict__ w, bf16_t* __restrict__ y, uint8_t* __restrict__ q8, float* __restrict__ sx,
+    int rows, int hidden, float eps, int64_t capvec, int rank, CarPeers peers, uint32_t* herr,
+    uint64_t timeout_ticks) {
   __shared__ uint32_t s_round;
   __shared__ uint32_t s_err;
   __shared__ float scratch[car::kThreads / 64];
+  __shared__ float mscratch[car::kThreads / 64];
   const int b = blockIdx.x, tid = threadIdx.x;
   char* mine = peers.base[rank];
   uint32_t* rounds = reinterpret_cast<uint32_t*>(mine + car::kRoundsOff);
@@ -199,10 +206,24 @@ __global__ void __launch_bounds__(car::kThreads) oneshot_ar_rmsnorm_kernel(
   uint4* y4 = reinterpret_cast<uint4*>(y);
   if (s_err) {
     poison<true>(y4, v0, v1, tid);
+    if constexpr (Q8)
+      for (int r = r0 + tid; r < r1; r += car::kThreads) sx[r] = __builtin_nanf("");
     return;
   }
+  const int64_t MN = (int64_t)rows * hidden;
   for (int64_t v = v0 + tid; v < v1; v += car::kThreads) {
-    const uint4 x = in[v];
+    uint4 x;
+    if constexpr (SLABS) {
+      const float* pv = slabs + v * 8;
+      f32x4 a0 = *reinterpret_cast<const f32x4*>(pv), a1 = *reinterpret_cast<const f32x4*>(pv + 4);
+      for (int s = 1; s < S; ++s) {
+        a0 += *reinterpret_cast<const f32x4*>(pv + s * MN);
+        a1 += *reinterpret_cast<const f32x4*>(pv + s * MN + 4);
+      }
+      x = make_uint4(pack_bf2(a0[0], a0[1]), pack_bf2(a0[2], a0[3]), pack_bf2(a1[0], a1[1]), pack_bf2(a1[2], a1[3]));
+    } else {
+      x = in[v];
+    }
 #pragma unroll
     for (int p = 0; p < W; ++p) {
       uint4* dst = reinterpret_cast<uint4*>(peers.base[p] + car::kDataOff) + ((int64_t)par * W + rank) * capvec;
@@ -234,6 +255,8 @@ __global__ void __launch_bounds__(car::kThreads) oneshot_ar_rmsnorm_kernel(
       rounds[b] = round;
     }
     poison<true>(y4, v0, v1, tid);
+    if constexpr (Q8)
+      for (int r = r0 + tid; r < r1; r += car::kThreads) sx[r] = __builtin_nanf("");
     return;
   }
   const uint4* slots = reinterpret_cast<const uint4*>(mine + car::kDataOff) + (int64_t)par * W * capvec;
@@ -276,6 +299,41 @@ __global__ void __launch_bounds__(car::kThreads) oneshot_ar_rmsnorm_kernel(
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = f2bf(bf2f(f2bf(v[i][j] * rs)) * bf2f(wv[j]));
         yr[vi] = o;
+        if constexpr (Q8) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[i][j] = bf2f(o[j]);
+        }
+      }
+    }
+    if constexpr (Q8) {
+      float am = 0.f;
+#pragma unroll
+      for (int i = 0; i < MAXV; ++i)
+        if (tid + i * car::kThreads < nvr)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) am = fmaxf(am, fabsf(v[i][j]));
+      am = wave_max(am);
+      if ((tid & 63) == 0) mscratch[tid >> 6] = am;
+      __syncthreads();
+      am = 0.f;
+#pragma unroll
+      for (int k = 0; k < car::kThreads / 64; ++k) am = fmaxf(am, mscratch[k]);
+      __syncthreads();   // mscratch is reused by the next row
+      const float sc = am > 0.f ? am / 448.f : 1.f;
+      const float inv = 1.f / sc;
+      if (tid == 0) sx[r] = sc;
+      uint8_t* qr = q8 + (int64_t)r * hidden;
+#pragma unroll
+      for (int i = 0; i < MAXV; ++i) {
+        const int vi = tid + i * car::kThreads;
+        if (vi < nvr) {
+          int lo = 0, hi = 0;
+          lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][0] * inv, v[i][1] * inv, lo, false);
+          lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][2] * inv, v[i][3] * inv, lo, true);
+          hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][4] * inv, v[i][5] * inv, hi, false);
+          hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][6] * inv, v[i][7] * inv, hi, true);
+          *reinterpret_cast<uint2*>(qr + vi * 8) = make_uint2(static_cast<uint32_t>(lo), static_cast<uint32_t>(hi));
+        }
       }
     }
   }
@@ -376,15 +434,18 @@ int car_all_reduce(const void* in, void* out, int64_t bytes, bool bf16, int rank
 
 namespace oamd {
 
-int car_all_reduce_rmsnorm(const void* in, bf16_t* residual, const bf16_t* w, bf16_t* y, int rows, int hidden,
-                           float eps, int rank, int world, void* const* bases, size_t cap_bytes, int blocks,
-                           uint32_t* herr_dev, double timeout_s, hipStream_t stream) {
+int car_all_reduce_rmsnorm(const void* in, const float* slabs, int S, bf16_t* residual, const bf16_t* w, bf16_t* y,
+                           uint8_t* q8, float* sx, int rows, int hidden, float eps, int rank, int world,
+                           void* const* bases, size_t cap_bytes, int blocks, uint32_t* herr_dev, double timeout_s,
+                           hipStream_t stream) {
+  if ((slabs == nullptr) == (in == nullptr) || (slabs != nullptr && S < 1)) return -5;
+  if ((q8 == nullptr) != (sx == nullptr)) return -5;
   if (world < 1 || world > car::kMaxRanks || rank < 0 || rank >= world) return -1;
   if (rows < 1 || hidden < 8 || hidden % 8 != 0 || hidden > car::kThreads * 8 * 4) return -2;
   if ((size_t)rows * hidden * 2 > cap_bytes || cap_bytes % 16 != 0) return -2;
   if (blocks < 1 || blocks > car::kMaxBlocks) return -3;
-  if ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(residual) | reinterpret_cast<uintptr_t>(w) |
-       reinterpret_cast<uintptr_t>(y)) & 15)
+  if ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(slabs) | reinterpret_cast<uintptr_t>(residual) |
+       reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(y) | reinterpret_cast<uintptr_t>(q8)) & 15)
     return -4;
   CarPeers peers{};
   for (int p = 0; p < world; ++p) peers.base[p] = static_cast<char*>(bases[p]);
@@ -392,14 +453,24 @@ int car_all_reduce_rmsnorm(const void* in, bf16_t* residual, const bf16_t* w, bf
   const uint4* i4 = static_cast<const uint4*>(in);
   const uint64_t ticks = timeout_s > 0 ? (uint64_t)(timeout_s * 1e8) : car::kDefaultTimeoutTicks;
   const bool big = hidden > car::kThreads * 8 * 2;
+  const int mode = (slabs != nullptr ? 1 : 0) | (q8 != nullptr ? 2 : 0);
+#define OAMD_CARK(W, MV, SL, Q)                                                                               \
+  oneshot_ar_rmsnorm_kernel<W, MV, SL, Q><<<blocks, car::kThreads, 0, stream>>>(                              \
+      i4, slabs, S, residual, w, y, q8, sx, rows, hidden, eps, capvec, rank, peers, herr_dev, ticks)
+#define OAMD_CARM(W, MV)                                                                                      \
+  switch (mode) {                                                                                             \
+    case 0: OAMD_CARK(W, MV, false, false); break;                                                            \
+    case 1: OAMD_CARK(W, MV, true, false); break;                                                             \
+    case 2: OAMD_CARK(W, MV, false, true); break;                                                             \
+    default: OAMD_CARK(W, MV, true, true); break;                                                             \
+  }
 #define OAMD_CARN(W)                                                                                          \
   case W:                                                                                                     \
-    if (big)                                                                                                  \
-      oneshot_ar_rmsnorm_kernel<W, 4><<<blocks, car::kThreads, 0, stream>>>(                                  \
-          i4, residual, w, y, rows, hidden, eps, capvec, rank, peers, herr_dev, ticks);                       \
-    else                                                                                                      \
-      oneshot_ar_rmsnorm_kernel<W, 2><<<blocks, car::kThreads, 0, stream>>>(                                  \
-          i4, residual, w, y, rows, hidden, eps, capvec, rank, peers, herr_dev, ticks);                       \
+    if (big) {                                                                                                \
+      OAMD_CARM(W, 4)                                                                                         \
+    } else {                                                                                                  \
+      OAMD_CARM(W, 2)                                                                                         \
+    }                                                                                                         \
     break;
   switch (world) {
     OAMD_CARN(1)
@@ -412,6 +483,8 @@ int car_all_reduce_rmsnorm(const void* in, bf16_t* residual, const bf16_t* w, bf
     OAMD_CARN(8)
     default: return -1;
   }
+#undef OAMD_CARM
+#undef OAMD_CARK
 #undef OAMD_CARN
   OAMD_LAUNCH_CHECK();
   return 0;

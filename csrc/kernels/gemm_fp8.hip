@@ -145,9 +145,12 @@ __global__ void __launch_bounds__(f8::kWaves * 64, 1)
 // SILU: the input is the 64-feature-interleaved gate|up projection [M, 2K] and the
 // row quantized is bf16(bf16(silu(bf16 g)) * bf16 u) — the SwiGLU and the down
 // projection's input quantization in one kernel.
+// P (SILU only): the gate|up rows are S fp32 split-K slabs [S, M, 2K] instead of bf16 `x`;
+// they are summed in slab order and bf16-rounded first (== splitk_reduce_fp32 then SILU).
 template <int MAXV, bool SILU>
 __global__ void __launch_bounds__(256) quantize_rows_reg_kernel(const bf16_t* __restrict__ x, uint8_t* __restrict__ q,
-                                                                float* __restrict__ sx, int K, int64_t ld) {
+                                                                float* __restrict__ sx, int K, int64_t ld,
+                                                                const float* __restrict__ P, int S) {
   __shared__ float red[4];
   const int64_t m = blockIdx.x;
   const bf16_t* xr = x + m * ld;
@@ -160,8 +163,30 @@ __global__ void __launch_bounds__(256) quantize_rows_reg_kernel(const bf16_t* __
     if (vi < nv) {
       if constexpr (SILU) {
         const int c = (vi >> 3) * 128 + (vi & 7) * 8;   // 64-feature blocks: gate then up
-        const u16x8 gv = *reinterpret_cast<const u16x8*>(xr + c);
-        const u16x8 uv = *reinterpret_cast<const u16x8*>(xr + c + 64);
+        u16x8 gv, uv;
+        if (P != nullptr) {
+          const int64_t MN = (int64_t)gridDim.x * 2 * K;
+          const float* pr = P + m * 2 * K + c;
+          f32x4 g0 = *reinterpret_cast<const f32x4*>(pr), g1 = *reinterpret_cast<const f32x4*>(pr + 4);
+          f32x4 u0 = *reinterpret_cast<const f32x4*>(pr + 64), u1 = *reinterpret_cast<const f32x4*>(pr + 68);
+          for (int s = 1; s < S; ++s) {
+            const float* ps = pr + s * MN;
+            g0 += *reinterpret_cast<const f32x4*>(ps);
+            g1 += *reinterpret_cast<const f32x4*>(ps + 4);
+            u0 += *reinterpret_cast<const f32x4*>(ps + 64);
+            u1 += *reinterpret_cast<const f32x4*>(ps + 68);
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            gv[j] = f2bf(g0[j]);
+            gv[j + 4] = f2bf(g1[j]);
+            uv[j] = f2bf(u0[j]);
+            uv[j + 4] = f2bf(u1[j]);
+          }
+        } else {
+          gv = *reinterpret_cast<const u16x8*>(xr + c);
+          uv = *reinterpret_cast<const u16x8*>(xr + c + 64);
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float g = bf2f(gv[j]);
@@ -236,21 +261,22 @@ int quantize_fp8_rows(const bf16_t* x, uint8_t* q, float* sx, int M, int K, int6
   if (M == 0) return 0;
   if (K % 8 != 0) return -1;
   const int nv = K / 8;
-  if (nv <= 256 * 2) quantize_rows_reg_kernel<2, false><<<M, 256, 0, stream>>>(x, q, sx, K, ld);
-  else if (nv <= 256 * 4) quantize_rows_reg_kernel<4, false><<<M, 256, 0, stream>>>(x, q, sx, K, ld);
-  else if (nv <= 256 * 8) quantize_rows_reg_kernel<8, false><<<M, 256, 0, stream>>>(x, q, sx, K, ld);
+  if (nv <= 256 * 2) quantize_rows_reg_kernel<2, false><<<M, 256, 0, stream>>>(x, q, sx, K, ld, nullptr, 1);
+  else if (nv <= 256 * 4) quantize_rows_reg_kernel<4, false><<<M, 256, 0, stream>>>(x, q, sx, K, ld, nullptr, 1);
+  else if (nv <= 256 * 8) quantize_rows_reg_kernel<8, false><<<M, 256, 0, stream>>>(x, q, sx, K, ld, nullptr, 1);
   else quantize_fp8_rows_kernel<<<M, 256, 0, stream>>>(x, q, sx, K, ld);
   OAMD_LAUNCH_CHECK();
   return 0;
 }
 
-int silu_quantize_fp8(const bf16_t* gu, uint8_t* q, float* sx, int M, int inter, int64_t ld, hipStream_t stream) {
+int silu_quantize_fp8(const bf16_t* gu, const float* P, int S, uint8_t* q, float* sx, int M, int inter, int64_t ld,
+                      hipStream_t stream) {
   if (M == 0) return 0;
-  if (inter % 64 != 0) return -1;
+  if (inter % 64 != 0 || (gu == nullptr) == (P == nullptr) || S < 1) return -1;
   const int nv = inter / 8;
-  if (nv <= 256 * 2) quantize_rows_reg_kernel<2, true><<<M, 256, 0, stream>>>(gu, q, sx, inter, ld);
-  else if (nv <= 256 * 4) quantize_rows_reg_kernel<4, true><<<M, 256, 0, stream>>>(gu, q, sx, inter, ld);
-  else if (nv <= 256 * 8) quantize_rows_reg_kernel<8, true><<<M, 256, 0, stream>>>(gu, q, sx, inter, ld);
+  if (nv <= 256 * 2) quantize_rows_reg_kernel<2, true><<<M, 256, 0, stream>>>(gu, q, sx, inter, ld, P, S);
+  else if (nv <= 256 * 4) quantize_rows_reg_kernel<4, true><<<M, 256, 0, stream>>>(gu, q, sx, inter, ld, P, S);
+  else if (nv <= 256 * 8) quantize_rows_reg_kernel<8, true><<<M, 256, 0, stream>>>(gu, q, sx, inter, ld, P, S);
   else return -2;
   OAMD_LAUNCH_CHECK();
   return 0;
@@ -288,7 +314,7 @@ int gemm_fp8(const uint8_t* X, const uint8_t* W, const float* sx, const float* s
 #undef OAMD_G8M
 #undef OAMD_G8
   OAMD_LAUNCH_CHECK();
-  if (S > 1) {
+  if (S > 1 && Y != nullptr) {   // Y == nullptr: the consumer sums the slabs
     const int64_t MN = (int64_t)M * N;
     splitk_reduce_fp32_kernel<<<(MN / 4 + 255) / 256, 256, 0, stream>>>(P, Y, MN, S);
     OAMD_LAUNCH_CHECK();

@@ -54,7 +54,9 @@ int gemm_fp8(const uint8_t* X, const uint8_t* W, const float* sx, const float* s
 int quantize_fp8_rows(const bf16_t* x, uint8_t* q, float* sx, int M, int K, int64_t ld, hipStream_t stream);
 // Fused SwiGLU + per-row e4m3fn quantization of the 64-feature-interleaved gate|up rows [M, 2 inter]
 // (inter % 64 == 0, <= 16384): q [M, inter], sx [M].
-int silu_quantize_fp8(const bf16_t* gu, uint8_t* q, float* sx, int M, int inter, int64_t ld, hipStream_t stream);
+// gu == nullptr: the gate|up rows are the S fp32 split-K slabs P [S, M, 2 inter] (summed, bf16-rounded).
+int silu_quantize_fp8(const bf16_t* gu, const float* P, int S, uint8_t* q, float* sx, int M, int inter, int64_t ld,
+                      hipStream_t stream);
 
 // Pattern-event scoring + per-doc ranking / summary (N5), see score.hip.
 int score_events(const int64_t* keys, const int* hit_doc, const int* doc_ptr, int n_hits, int n_docs,
@@ -90,10 +92,13 @@ void car_free_host_flag(uint32_t* host);
 int car_error(const uint32_t* host);
 int car_reset(void* base, uint32_t* host);
 // Fused one-shot all-reduce + residual add + RMSNorm (bf16 rows of `hidden`, hidden % 8 == 0, <= 16384):
-// residual += bf16(sum over ranks of in); y = rmsnorm(residual) * w.
-int car_all_reduce_rmsnorm(const void* in, bf16_t* residual, const bf16_t* w, bf16_t* y, int rows, int hidden,
-                           float eps, int rank, int world, void* const* bases, size_t cap_bytes, int blocks,
-                           uint32_t* herr_dev, double timeout_s, hipStream_t stream);
+// residual += bf16(sum over ranks of in); y = rmsnorm(residual) * w. Exactly one of `in` (bf16 rows) and
+// `slabs` (S fp32 split-K slabs [S, rows, hidden], summed then bf16-rounded) is non-null; q8/sx non-null
+// also emit per-row e4m3fn of y (== quantize_fp8_rows(y)).
+int car_all_reduce_rmsnorm(const void* in, const float* slabs, int S, bf16_t* residual, const bf16_t* w, bf16_t* y,
+                           uint8_t* q8, float* sx, int rows, int hidden, float eps, int rank, int world,
+                           void* const* bases, size_t cap_bytes, int blocks, uint32_t* herr_dev, double timeout_s,
+                           hipStream_t stream);
 int car_all_reduce(const void* in, void* out, int64_t bytes, bool bf16, int rank, int world, void* const* bases,
                    size_t cap_bytes, int blocks, uint32_t* herr_dev, double timeout_s, hipStream_t stream);
 

@@ -157,8 +157,8 @@ class LlamaModel:
     def _lin(self, x: torch.Tensor, w: torch.Tensor, sc: torch.Tensor | None, defer: bool = False):
         """Projection; ``defer`` lets a split-K decode GEMM hand its fp32 slabs to the
         following rmsnorm (only when no TP all-reduce sits in between)."""
-        if sc is not None:
-            return ops.linear_fp8(x, w, sc)
+        if sc is not None:   # every fp8 consumer (rope_kv, the AR + norm, SwiGLU) sums slabs
+            return ops.linear_fp8(x, w, sc, defer_reduce=defer)
         return ops.linear(x, w, defer_reduce=defer and self.tp.world == 1)
 
     def _shard_layer(self, wq, wk, wv, wo, wg, wu, wd, an, mn, bias=None) -> LayerWeights:
@@ -240,6 +240,7 @@ class LlamaModel:
         h = ops.embedding(fb.input_ids, self.embed)          # residual stream [T, H]
         x = ops.rmsnorm(h, self.layers[0].attn_norm, c.rms_eps)
         T = h.shape[0]
+        q8 = self.fp8 and h.is_cuda   # block epilogues emit e4m3fn rows for the next fp8 GEMM
         ws = None
         if not fb.is_prefill and h.is_cuda:  # split-KV partials, shared by every layer
             ws = ops.decode_workspace(T, self.hq, fb.num_splits, h.device)
@@ -261,15 +262,17 @@ class LlamaModel:
                 o = ops.attn_decode(q, kc, vc, fb.block_tables, fb.context_lens, self.scale, fb.num_splits,
                                     workspace=ws, k_scale=kv.k_scale, v_scale=kv.v_scale)
             a = self._lin(o.view(T, self.hq * c.head_dim), lw.wo, lw.so, defer=True)
-            x = self.tp.all_reduce_rmsnorm(a, lw.mlp_norm, c.rms_eps, residual=h)   # fused under TP
+            x = self.tp.all_reduce_rmsnorm(a, lw.mlp_norm, c.rms_eps, residual=h, quant=q8)   # fused under TP
             if lw.sgu is None:
                 m = ops.gate_up_silu(x, lw.wgu, self.gu_block)
+            elif q8:   # SwiGLU (+ the split-K sum) fused into the down GEMM's input quantization
+                m = ops.silu_quantize_fp8(ops.linear_fp8(x, lw.wgu, lw.sgu, defer_reduce=True), self.gu_block)
             else:
-                gu = ops.linear_fp8(x, lw.wgu, lw.sgu)   # SwiGLU fused into the down GEMM's input quantization
-                m = ops.silu_quantize_fp8(gu, self.gu_block) if gu.is_cuda else ops.silu_mul(gu, block=self.gu_block)
+                m = ops.silu_mul(ops.linear_fp8(x, lw.wgu, lw.sgu), block=self.gu_block)
             d = self._lin(m, lw.wd, lw.sd, defer=True)
-            nw = self.layers[i + 1].attn_norm if i + 1 < len(self.layers) else self.final_norm
-            x = self.tp.all_reduce_rmsnorm(d, nw, c.rms_eps, residual=h)
+            last = i + 1 == len(self.layers)
+            nw = self.final_norm if last else self.layers[i + 1].attn_norm
+            x = self.tp.all_reduce_rmsnorm(d, nw, c.rms_eps, residual=h, quant=q8 and not last)
         if fb.logits_index is not None:
             x = x.index_select(0, fb.logits_index)
         return ops.linear(x, self.lm_head)

@@ -102,6 +102,10 @@ def gate_up_silu(x: torch.Tensor, wgu: torch.Tensor, block: int | None) -> torch
     if (x.is_cuda and block == 64 and x.dtype == torch.bfloat16 and M % 64 == 0 and M <= 256 and N % 128 == 0
             and K % 64 == 0 and x.is_contiguous() and wgu.is_contiguous()):
         t = _gemm_table_get().get(("silu", M, N, K))
+        if isinstance(t, str) and t.startswith("pp"):   # ping-pong kernel, nt weight loads (bm 128 / 256)
+            y = torch.empty(M, N // 2, dtype=x.dtype, device=x.device)
+            kernels().gemm_pp(x, wgu, y, None, 1, int(t[2:]), True, True)
+            return y
         if t != "blas":
             bm = t[0] if t else row_tile(M)
             ns = t[1] if t and len(t) > 1 else 3
@@ -404,15 +408,24 @@ def quantize_fp8(x: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
     return (xf / sx[:, None]).to(torch.float8_e4m3fn), sx
 
 
-def silu_quantize_fp8(gu: torch.Tensor, block: int | None = GU_BLOCK) -> tuple[torch.Tensor, torch.Tensor]:
+def silu_quantize_fp8(gu, block: int | None = GU_BLOCK) -> tuple[torch.Tensor, torch.Tensor]:
     """quantize_fp8(silu_mul(gu, block)) — on the GPU one kernel for 64-feature
-    interleaved gate|up rows (the SwiGLU never round-trips HBM as bf16)."""
-    inter = gu.shape[1] // 2
-    if gu.is_cuda and block == GU_BLOCK and inter <= 16384 and gu.stride(1) == 1:
-        q = torch.empty(gu.shape[0], inter, dtype=torch.float8_e4m3fn, device=gu.device)
-        sx = torch.empty(gu.shape[0], dtype=torch.float32, device=gu.device)
-        kernels().silu_quantize_fp8(gu, q, sx)
-        return q, sx
+    interleaved gate|up rows (the SwiGLU never round-trips HBM as bf16). ``gu`` may be
+    the gate|up GEMM's split-K slabs (:class:`SplitK`), summed inside the kernel."""
+    M, N2 = gu.shape
+    inter = N2 // 2
+    if gu.is_cuda and block == GU_BLOCK and inter <= 16384 and N2 % 128 == 0:
+        q = torch.empty(M, inter, dtype=torch.float8_e4m3fn, device=gu.device)
+        sx = torch.empty(M, dtype=torch.float32, device=gu.device)
+        if isinstance(gu, SplitK):
+            kernels().silu_quantize_fp8(torch.empty(M, N2, dtype=torch.bfloat16, device=gu.device), q, sx,
+                                        gu.p, gu.S)
+            return q, sx
+        if gu.stride(1) == 1:
+            kernels().silu_quantize_fp8(gu, q, sx)
+            return q, sx
+    if isinstance(gu, SplitK):
+        gu = gu.materialize()
     return quantize_fp8(silu_mul(gu, block=block))
 
 
@@ -433,9 +446,12 @@ def fp8_plan(M: int, N: int, K: int) -> tuple[int, int, int]:
 
 
 def linear_fp8(x: torch.Tensor | tuple[torch.Tensor, torch.Tensor], w8: torch.Tensor, sw: torch.Tensor,
-               out: torch.Tensor | None = None, plan: tuple[int, int, int] | None = None) -> torch.Tensor:
+               out: torch.Tensor | None = None, plan: tuple[int, int, int] | None = None,
+               defer_reduce: bool = False):
     """y = x @ (w8 * sw)^T with x quantized per token to e4m3fn (W8A8, fp32 accumulate).
-    ``x`` may already be quantized: a (q, sx) pair from quantize_fp8 / silu_quantize_fp8."""
+    ``x`` may already be quantized: a (q, sx) pair from quantize_fp8 / silu_quantize_fp8.
+    ``defer_reduce``: a split-K plan returns its fp32 slabs (:class:`SplitK`) for a
+    consumer that sums them (rope_kv, rmsnorm, the fused all-reduce + norm, SwiGLU)."""
     q, sx = x if isinstance(x, tuple) else quantize_fp8(x)
     M, K = q.shape
     N = w8.shape[0]
@@ -445,6 +461,9 @@ def linear_fp8(x: torch.Tensor | tuple[torch.Tensor, torch.Tensor], w8: torch.Te
     bm, bn, S = plan or fp8_plan(M, N, K)
     y = out if out is not None else torch.empty(M, N, dtype=torch.bfloat16, device=q.device)
     part = torch.empty(S * M * N, dtype=torch.float32, device=q.device) if S > 1 else None
+    if defer_reduce and S > 1 and out is None:
+        kernels().gemm_fp8(q, w8, sx, sw, y, part, S, bn, bm, False)
+        return SplitK(part, S, M, N)
     kernels().gemm_fp8(q, w8, sx, sw, y, part, S, bn, bm)
     return y
 

@@ -124,21 +124,26 @@ class Group:
             COLLECTIVES.add("all_reduce", dist.get_backend(self.pg), _nbytes(t), time.perf_counter() - t0)
         return t
 
-    def all_reduce_rmsnorm(self, t, w: torch.Tensor, eps: float, residual: torch.Tensor) -> torch.Tensor:
+    def all_reduce_rmsnorm(self, t, w: torch.Tensor, eps: float, residual: torch.Tensor, quant: bool = False):
         """The TP block epilogue: residual += all_reduce(t); return rmsnorm(residual) * w.
         With the one-shot IPC all-reduce enabled this is ONE fused gfx950 kernel (the
-        reduced rows are normalised by the block that summed them); otherwise the
-        all-reduce (RCCL / gloo) then the rmsnorm kernel. World 1: just the rmsnorm
-        (``t`` may then be split-K slabs, summed inside the norm)."""
+        reduced rows are normalised by the block that summed them; ``t`` may be the
+        producing GEMM's split-K slabs, summed on the way in); otherwise the all-reduce
+        (RCCL / gloo) then the rmsnorm kernel. World 1: just the rmsnorm (which also sums
+        slabs). ``quant``: return per-row e4m3fn ``(q, sx)`` of the result (fused into the
+        one-shot kernel) for an fp8 GEMM."""
         from operator_amd import ops
 
         if self.world > 1:
             car = getattr(self, "oneshot", None)
-            if car is not None and isinstance(t, torch.Tensor) and car.fits_rows(t) and residual.is_contiguous():
-                COLLECTIVES.add("all_reduce_rmsnorm", "oneshot", _nbytes(t))
-                return car.all_reduce_rmsnorm_(t, residual, w, eps)
+            if car is not None and car.fits_rows(t) and residual.is_contiguous():
+                COLLECTIVES.add("all_reduce_rmsnorm", "oneshot", 2 * t.shape[0] * t.shape[1])
+                return car.all_reduce_rmsnorm_(t, residual, w, eps, quant=quant)
+            if isinstance(t, ops.SplitK):
+                t = t.materialize()
             self.all_reduce_(t)
-        return ops.rmsnorm(t, w, eps, residual=residual)
+        y = ops.rmsnorm(t, w, eps, residual=residual)
+        return ops.quantize_fp8(y) if quant else y
 
     def all_gather(self, t: torch.Tensor, dim: int = 0) -> torch.Tensor:
         if self.world == 1:
@@ -195,13 +200,14 @@ class SimulatedTPGroup(Group):
             return self.car.all_reduce_(t)
         return t
 
-    def all_reduce_rmsnorm(self, t, w: torch.Tensor, eps: float, residual: torch.Tensor) -> torch.Tensor:
+    def all_reduce_rmsnorm(self, t, w: torch.Tensor, eps: float, residual: torch.Tensor, quant: bool = False):
         from operator_amd import ops
 
-        if self.car is not None and isinstance(t, torch.Tensor) and self.car.fits_rows(t) and residual.is_contiguous():
-            COLLECTIVES.add("all_reduce_rmsnorm", "oneshot-sim", _nbytes(t))
-            return self.car.all_reduce_rmsnorm_(t, residual, w, eps)
-        return ops.rmsnorm(t, w, eps, residual=residual)
+        if self.car is not None and self.car.fits_rows(t) and residual.is_contiguous():
+            COLLECTIVES.add("all_reduce_rmsnorm", "oneshot-sim", 2 * t.shape[0] * t.shape[1])
+            return self.car.all_reduce_rmsnorm_(t, residual, w, eps, quant=quant)
+        y = ops.rmsnorm(t, w, eps, residual=residual)
+        return ops.quantize_fp8(y) if quant else y
 
     def all_gather(self, t: torch.Tensor, dim: int = 0) -> torch.Tensor:
         return torch.cat([t] * self.world, dim=dim)

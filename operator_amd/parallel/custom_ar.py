@@ -67,20 +67,35 @@ class OneShotAllReduce:
         self.calls += 1
         return out
 
-    def fits_rows(self, t: torch.Tensor) -> bool:
-        """The fused all-reduce + RMSNorm takes bf16 [rows, hidden] within capacity."""
+    def fits_rows(self, t) -> bool:
+        """The fused all-reduce + RMSNorm takes bf16 [rows, hidden] (or the fp32 split-K
+        slabs of such rows, ``ops.SplitK``) within capacity."""
+        if isinstance(t, ops.SplitK):
+            rows, hidden = t.shape
+            return (t.p.is_cuda and t.p.is_contiguous() and hidden % 8 == 0 and hidden <= 16384
+                    and rows * hidden * 2 <= self.max_bytes)
         return (self.fits(t) and t.dtype == torch.bfloat16 and t.dim() == 2 and t.shape[1] % 8 == 0
                 and t.shape[1] <= 16384)
 
-    def all_reduce_rmsnorm_(self, t: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float,
-                            out: torch.Tensor | None = None) -> torch.Tensor:
+    def all_reduce_rmsnorm_(self, t, residual: torch.Tensor, w: torch.Tensor, eps: float,
+                            out: torch.Tensor | None = None, quant: bool = False):
         """residual += sum over ranks of t (bf16-rounded); returns rmsnorm(residual) * w.
         One launch: the row-partitioned one-shot push, then each block normalises whole
-        rows straight from its receive slots."""
-        y = out if out is not None else torch.empty_like(t)
-        self.ext.all_reduce_rmsnorm(t, residual, w, y, float(eps))
+        rows straight from its receive slots. ``t`` may be split-K slabs (summed in the
+        kernel); ``quant`` returns the rows as per-row e4m3fn ``(q, sx)`` instead, for
+        the next fp8 GEMM (== ``ops.quantize_fp8(y)``)."""
+        rows, hidden = residual.shape
+        y = out if out is not None else torch.empty_like(residual)
+        q8 = sx = None
+        if quant:
+            q8 = torch.empty(rows, hidden, dtype=torch.float8_e4m3fn, device=residual.device)
+            sx = torch.empty(rows, dtype=torch.float32, device=residual.device)
+        if isinstance(t, ops.SplitK):
+            self.ext.all_reduce_rmsnorm(None, residual, w, y, float(eps), t.p, t.S, q8, sx)
+        else:
+            self.ext.all_reduce_rmsnorm(t, residual, w, y, float(eps), None, 1, q8, sx)
         self.calls += 1
-        return y
+        return (q8, sx) if quant else y
 
     @property
     def failed(self) -> bool:

@@ -70,6 +70,29 @@ def _worker(rank: int, world: int, port: int, q) -> None:
             torch.cuda.synchronize()
             assert torch.equal(h, h_ref), (rows, hidden, (h.float() - h_ref.float()).abs().max())
             torch.testing.assert_close(y.float(), y_ref.float(), atol=1e-2, rtol=1e-2)
+            # split-K slabs in (summed in slab order, bf16-rounded) and e4m3fn rows out
+            S = 4
+            ps = [(_inputs(50 + r, S * rows * hidden, torch.float32, call) / S).view(S, rows, hidden)
+                  for r in range(world)]
+            ts = []
+            for pr in ps:
+                a = pr[0].clone()
+                for k in range(1, S):
+                    a += pr[k]
+                ts.append(a.to(torch.bfloat16))
+            ssum = sum(x.float() for x in ts).to(torch.bfloat16).to(dev)
+            h_ref = h0.clone()
+            y_ref = ops.rmsnorm(ssum.clone(), wv, 1e-5, residual=h_ref)
+            h = h0.clone()
+            slabs = ops.SplitK(ps[rank].reshape(-1).to(dev), S, rows, hidden)
+            q8, sx = grp.all_reduce_rmsnorm(slabs, wv, 1e-5, residual=h, quant=True)
+            torch.cuda.synchronize()
+            assert torch.equal(h, h_ref), ("slabs", rows, hidden, (h.float() - h_ref.float()).abs().max())
+            y_k = ops.rmsnorm(ssum.clone(), wv, 1e-5, residual=h0.clone())   # same op as the kernel's y
+            q_ref, s_ref = ops.quantize_fp8(y_k)
+            torch.testing.assert_close(sx, s_ref, rtol=2e-2, atol=0)
+            deq, deq_ref = q8.float() * sx[:, None], q_ref.float() * s_ref[:, None]
+            torch.testing.assert_close(deq, deq_ref, atol=3e-2 * float(deq_ref.abs().max()), rtol=0.07)
             t = xs[rank].reshape(-1).to(dev)
             grp.all_reduce_(t)                      # a plain call in between
             torch.cuda.synchronize()

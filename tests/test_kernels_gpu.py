@@ -250,6 +250,32 @@ def test_silu_quantize_fp8_matches_unfused(inter):
     assert (got == want).float().mean() > 0.99
 
 
+def test_silu_quantize_fp8_from_splitk_slabs():
+    """SplitK gate|up slabs -> summed + bf16-rounded in-kernel == reduce then fused kernel."""
+    torch.manual_seed(11)
+    S, M, inter = 4, 23, 3584
+    P = torch.randn(S, M, 2 * inter, device="cuda") / 2
+    a = P[0].clone()
+    for k in range(1, S):
+        a += P[k]
+    q0, s0 = ops.silu_quantize_fp8(a.to(torch.bfloat16), block=64)
+    q, sx = ops.silu_quantize_fp8(ops.SplitK(P.reshape(-1), S, M, 2 * inter), block=64)
+    assert torch.equal(sx, s0)
+    assert torch.equal(q.view(torch.uint8), q0.view(torch.uint8))
+
+
+def test_linear_fp8_deferred_slabs_match_reduced():
+    torch.manual_seed(12)
+    M, N, K = 64, 1280, 8192
+    x = _rand(M, K)
+    w8, sw = ops.quantize_fp8(_rand(N, K) * 0.05)
+    plan = (64, 64, 8)
+    y = ops.linear_fp8(x, w8, sw, plan=plan)
+    sk = ops.linear_fp8(x, w8, sw, plan=plan, defer_reduce=True)
+    assert isinstance(sk, ops.SplitK) and sk.S == 8
+    assert torch.equal(sk.materialize(), y) or torch.allclose(sk.materialize().float(), y.float(), atol=1e-2)
+
+
 @pytest.mark.parametrize("M", [1, 37, 64, 200, 256])
 @pytest.mark.parametrize("N,K", [(256, 512), (640, 2048), (128, 4096)])
 def test_gemm_fp8(M, N, K):
