@@ -20,11 +20,37 @@ VERSION = "v1alpha1"
 API_VERSION = f"{GROUP}/{VERSION}"
 
 
+_FAST_SPECS: dict[type, list] = {}
+
+
 class KModel(BaseModel):
     model_config = ConfigDict(alias_generator=to_camel, populate_by_name=True, extra="allow")
 
     def to_obj(self) -> dict:
         return self.model_dump(by_alias=True, exclude_none=True, mode="json")
+
+    @classmethod
+    def fast(cls, **values):
+        """``model_construct`` for a producer's own, already-typed values given by field
+        name: the same object (defaults and default factories filled in field order,
+        ``model_fields_set`` = the names given, empty extras), without model_construct's
+        per-call walk over every field's aliases — the match engine builds thousands of
+        results per scan batch and that walk was ~70 % of their host time."""
+        spec = _FAST_SPECS.get(cls)
+        if spec is None:   # every field in definition order (merging keeps that order), factories
+            fields = cls.model_fields
+            spec = _FAST_SPECS[cls] = ({n: f.default for n, f in fields.items()},
+                                       [(n, f.default_factory) for n, f in fields.items() if f.default_factory])
+        d = {**spec[0], **values}
+        for name, fac in spec[1]:
+            if name not in values:
+                d[name] = fac()
+        m = cls.__new__(cls)
+        object.__setattr__(m, "__dict__", d)
+        object.__setattr__(m, "__pydantic_fields_set__", set(values))
+        object.__setattr__(m, "__pydantic_extra__", {})
+        object.__setattr__(m, "__pydantic_private__", None)
+        return m
 
 
 # ---------------------------------------------------------------- kube basics

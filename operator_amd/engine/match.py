@@ -40,6 +40,17 @@ class ScanStats:
     host_ms: float = 0.0
 
 
+def uuid4_strs(n: int) -> list[str]:
+    """n random (version 4) UUID strings from one urandom call (uuid.uuid4() per result
+    was a quarter of the host time of a 4096-result batch)."""
+    raw = bytearray(os.urandom(16 * n))
+    raw[6::16] = bytes((b & 0x0F) | 0x40 for b in raw[6::16])
+    raw[8::16] = bytes((b & 0x3F) | 0x80 for b in raw[8::16])
+    h = raw.hex()
+    return [f"{h[i:i + 8]}-{h[i + 8:i + 12]}-{h[i + 12:i + 16]}-{h[i + 16:i + 20]}-{h[i + 20:i + 32]}"
+            for i in range(0, 32 * n, 32)]
+
+
 def _line_bounds(doc: bytes, off: int) -> tuple[int, int]:
     s = doc.rfind(b"\n", 0, off) + 1
     e = doc.find(b"\n", off)
@@ -476,10 +487,11 @@ class MatchEngine:
             ctxs = patterns().contexts(docs, q_doc, q_off, q_k) if q_doc else []
             out = []
             j = 0
+            ids = uuid4_strs(len(docs))
             for di, (doc, ev) in enumerate(zip(docs, evs)):
                 n = min(len(ev), self.max_events)
                 out.append(self._result(doc, ev, ctxs[j:j + n], pods[di] if pods else (None, None),
-                                        (time.perf_counter() - t0) * 1e3, None if nls is None else nls[di]))
+                                        (time.perf_counter() - t0) * 1e3, None if nls is None else nls[di], ids[di]))
                 j += n
             self._doc_newlines = None
             self.stats.docs += len(docs)
@@ -489,12 +501,12 @@ class MatchEngine:
         mp = self._mp_cache.get(pi)
         if mp is None:   # immutable per pattern: built once, shared by every event
             p = self.cp.patset.patterns[pi]
-            mp = self._mp_cache[pi] = MatchedPattern.model_construct(
+            mp = self._mp_cache[pi] = MatchedPattern.fast(
                 id=p.id, name=p.name, severity=p.severity, category=p.category or None, library=p.library or None)
         return mp
 
     def _result(self, doc: bytes, ev: list[oracle.Event], ctxs: list, pod, ms: float,
-                newlines: int | None = None) -> AnalysisResult:
+                newlines: int | None = None, analysis_id: str | None = None) -> AnalysisResult:
         pats = self.cp.patset.patterns
         dist = {s: 0 for s in SEVERITIES}
         sig = 0
@@ -508,17 +520,17 @@ class MatchEngine:
         events = []
         for e, (ctx, line) in zip(ev[: self.max_events], ctxs):
             p = pats[e.pattern]
-            # model_construct: these are the engine's own, already-typed values (validation
-            # was ~2/3 of the host time per result with a few thousand results per scan)
-            events.append(AnalysisEvent.model_construct(
+            # KModel.fast: these are the engine's own, already-typed values (validation was
+            # ~2/3 of the host time per result, model_construct's field walk most of the rest)
+            events.append(AnalysisEvent.fast(
                 line_number=e.line + 1, matched_pattern=self._matched(e.pattern),
                 score=round(e.score, 6), context=ctx, matched_line=line,
                 remediation=p.remediation or None))
-        summary = AnalysisSummary.model_construct(highest_severity=SEVERITIES[hi] if hi >= 0 else None,
+        summary = AnalysisSummary.fast(highest_severity=SEVERITIES[hi] if hi >= 0 else None,
                                                   significant_events=sig, total_events=len(ev),
                                                   severity_distribution={k: v for k, v in dist.items() if v})
-        return AnalysisResult.model_construct(
-            analysis_id=str(uuid.uuid4()), pod_name=pod[0], pod_namespace=pod[1], events=events, summary=summary,
+        return AnalysisResult.fast(
+            analysis_id=analysis_id or str(uuid.uuid4()), pod_name=pod[0], pod_namespace=pod[1], events=events, summary=summary,
             metadata={"engine": "gpu-ac" if self.device.type == "cuda" else "cpu-oracle",
                       "patternsChecked": len(pats),
                       "totalLines": (doc.count(b"\n") if newlines is None else newlines) + 1,

@@ -397,7 +397,7 @@ FP8_MAX = 448.0  # OCP e4m3fn
 def quantize_fp8(x: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
     """Per-row e4m3fn quantization: (q [M, K] float8_e4m3fn, s [M] fp32), x ~= q * s."""
     M, K = x.shape
-    if x.is_cuda:
+    if x.is_cuda and x.dtype == torch.bfloat16 and K % 8 == 0:
         q = torch.empty(M, K, dtype=torch.float8_e4m3fn, device=x.device)
         sx = torch.empty(M, dtype=torch.float32, device=x.device)
         kernels().quantize_fp8(x.contiguous(), q, sx)

@@ -157,7 +157,7 @@ def test_bench_tp_simulate_runs_one_rank_shard():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     r = subprocess.run([sys.executable, os.path.join(root, "tools", "bench_tp.py"), "--simulate-tp", "8", "--model",
-                        "tiny-tp8", "--dtype", "float32", "--batch", "3", "--prompt", "24", "--gen", "6", "--kv-gb",
+                        "tiny-tp8", "--dtype", "float32", "--weights", "bfloat16", "--cpu", "--batch", "3", "--prompt", "24", "--gen", "6", "--kv-gb",
                         "0.05"], capture_output=True, text=True, timeout=300, cwd=root, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][0])

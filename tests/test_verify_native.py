@@ -103,3 +103,35 @@ def test_native_contexts_equal_python():
     for (di, off, k), (ctx, line) in zip(q, got):
         ref_ctx, ref_line = _context(docs[di], off, k)
         assert (list(ctx), line) == (ref_ctx, ref_line), (docs[di], off, k)
+
+
+def test_fast_construct_equals_model_construct():
+    """KModel.fast (the match engine's result builder) builds what model_construct builds."""
+    from operator_amd.api.models import AnalysisEvent, AnalysisResult, AnalysisSummary, MatchedPattern
+
+    mp = MatchedPattern.fast(id="oom", name="OOM", severity="HIGH")
+    assert mp == MatchedPattern.model_construct(id="oom", name="OOM", severity="HIGH")
+    assert mp.model_fields_set == {"id", "name", "severity"}
+    ev = AnalysisEvent.fast(line_number=3, matched_pattern=mp, score=0.5, matched_line="x")
+    want = AnalysisEvent.model_construct(line_number=3, matched_pattern=mp, score=0.5, matched_line="x")
+    assert ev == want and ev.context == [] and ev.to_obj() == want.to_obj()
+    e2 = AnalysisEvent.fast()
+    assert e2.context is not ev.context            # default factories are per instance
+    sm = AnalysisSummary.fast(total_events=2)
+    r = AnalysisResult.fast(analysis_id="a", events=[ev], summary=sm)
+    r0 = AnalysisResult.model_construct(analysis_id="a", events=[ev], summary=sm)
+    assert r == r0 and r.to_obj() == r0.to_obj() and list(r.__dict__) == list(r0.__dict__)
+    assert r.model_dump_json() == r0.model_dump_json()
+
+
+def test_uuid4_strs_are_version4_uuids():
+    import uuid
+
+    from operator_amd.engine.match import uuid4_strs
+
+    ids = uuid4_strs(500)
+    assert len(set(ids)) == 500
+    for s in ids:
+        u = uuid.UUID(s)
+        assert u.version == 4 and u.variant == uuid.RFC_4122 and str(u) == s
+    assert uuid4_strs(0) == []

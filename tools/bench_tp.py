@@ -38,6 +38,7 @@ from operator_amd.parallel.comm import init_from_env, split_groups  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--model", default="llama3-70b")
 ap.add_argument("--weights", default="fp8", choices=["fp8", "bfloat16"])
+ap.add_argument("--cpu", action="store_true", help="run on the CPU (gloo) even where a GPU is visible")
 ap.add_argument("--dtype", default="bfloat16")
 ap.add_argument("--batch", type=int, default=64)
 ap.add_argument("--prompt", type=int, default=1024)
@@ -50,7 +51,7 @@ ap.add_argument("--simulate-tp", type=int, default=0,
 a = ap.parse_args()
 
 info = init_from_env()
-gpu = torch.cuda.is_available()
+gpu = torch.cuda.is_available() and not a.cpu
 dev = torch.device("cuda", info.local_rank) if gpu else torch.device("cpu")
 if gpu:
     torch.cuda.set_device(dev)
