@@ -137,5 +137,7 @@ def build(verbose: bool = False, force: bool = False) -> list[Path]:
 if __name__ == "__main__":
     v = "-v" in sys.argv
     f = "-f" in sys.argv or "--force" in sys.argv
-    for p in build(verbose=v, force=f):
+    # --host-only: just the host C++ pattern module (no ROCm needed): the multi-arch
+    # controller image (docker/Dockerfile.controller), whose engines are remote or CPU
+    for p in ([build_patterns(v, f)] if "--host-only" in sys.argv else build(verbose=v, force=f)):
         print(p)

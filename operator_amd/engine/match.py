@@ -15,6 +15,7 @@ CPU path: the same post-processing fed by the pure-Python oracle.
 from __future__ import annotations
 
 import contextlib
+import gc
 import os
 import threading
 import time
@@ -38,6 +39,20 @@ class ScanStats:
     verified_hits: int = 0
     scan_ms: float = 0.0
     host_ms: float = 0.0
+
+
+@contextlib.contextmanager
+def _gc_paused():
+    """No cyclic-GC passes while a batch's results are allocated: each of the ~10^5 new
+    objects of a 4096-log batch counts toward a collection, and the generation-2 passes
+    they trigger re-scan every live object of the process (none of them a cycle)."""
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
 
 
 def uuid4_strs(n: int) -> list[str]:
@@ -141,6 +156,7 @@ class MatchEngine:
         self._verify = np.asarray(self.cp.matcher_verify + [False], dtype=bool)
         self._init_verifier()
         self._mp_cache: dict[int, MatchedPattern] = {}
+        self.last_timing: dict[str, float] = {}   # stage split of the last analyze() (host seconds)
         if self.device.type == "cuda" and self.cp.factors:
             self._upload_dfa()
         # Scans run on a stream of their own: the LLM engine keeps the default stream
@@ -463,10 +479,11 @@ class MatchEngine:
         """Full AnalysisResult per doc (pods = [(name, namespace)] for labelling)."""
         from operator_amd.ops import patterns
 
-        with self._lock:
+        with self._lock, _gc_paused():
             t0 = time.perf_counter()
             self._doc_newlines = None
             evs, offs = self.events(docs)
+            t_ev = time.perf_counter()
             nls = self._doc_newlines[1] if self._doc_newlines and self._doc_newlines[0] is docs else None
             # the +-k context windows of every reported event, extracted natively in one
             # call over the whole batch (N3)
@@ -485,6 +502,7 @@ class MatchEngine:
                     q_off.append(off)
                     q_k.append(pats[e.pattern].context_lines)
             ctxs = patterns().contexts(docs, q_doc, q_off, q_k) if q_doc else []
+            t_ctx = time.perf_counter()
             out = []
             j = 0
             ids = uuid4_strs(len(docs))
@@ -495,6 +513,8 @@ class MatchEngine:
                 j += n
             self._doc_newlines = None
             self.stats.docs += len(docs)
+            t_end = time.perf_counter()
+            self.last_timing = {"events_s": t_ev - t0, "contexts_s": t_ctx - t_ev, "results_s": t_end - t_ctx}
             return out
 
     def _matched(self, pi: int) -> MatchedPattern:

@@ -27,7 +27,7 @@ class CollectiveTimeout(RuntimeError):
 
 
 DEFAULT_MAX_BYTES = 8 << 20   # 256 tokens x 8192 x 2 B (70B hidden) = 4 MB, with room
-DEFAULT_BLOCKS = 64   # one block per decode row at B=64: the fused AR + norm is per-row latency bound
+DEFAULT_BLOCKS = 32
 
 
 class OneShotAllReduce:

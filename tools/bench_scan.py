@@ -78,7 +78,7 @@ def main():
             res = eng.analyze(docs)
             warm.append(time.perf_counter() - u1)
         t1, t2 = 0.0, min(warm)
-        stage = {}
+        stage = {"analyze_" + k: round(v, 4) for k, v in eng.last_timing.items()}
         for name, fn in (("scan_gpu", lambda: eng.scan_gpu(docs)), ("events", lambda: eng.events(docs))):
             best = 1e9
             for _ in range(3):

@@ -11,7 +11,8 @@ ap.add_argument("trace")
 ap.add_argument("--window-json", required=True)
 a = ap.parse_args()
 rows = list(csv.DictReader(gzip.open(a.trace, "rt") if a.trace.endswith(".gz") else open(a.trace)))
-t0, t1 = json.load(open(a.window_json))["detail"]["timed_monotonic_ns"]
+line = [x for x in open(a.window_json) if x.startswith("{") and '"metric"' in x][-1]   # bench.py's JSON line
+t0, t1 = json.loads(line)["detail"]["timed_monotonic_ns"]
 S = lambda r: int(r["Start_Timestamp"])  # noqa: E731
 E = lambda r: int(r["End_Timestamp"])  # noqa: E731
 ks = sorted([r for r in rows if t0 <= S(r) <= t1], key=S)
