@@ -20,6 +20,7 @@ import os
 import threading
 import time
 import uuid
+from collections.abc import Sequence
 from dataclasses import dataclass
 
 import numpy as np
@@ -39,6 +40,29 @@ class ScanStats:
     verified_hits: int = 0
     scan_ms: float = 0.0
     host_ms: float = 0.0
+
+
+class LazyResults(Sequence):
+    """``MatchEngine.analyze(lazy=True)``: a batch's results, each built on first
+    access and cached (a race builds one twice; the first stored copy wins)."""
+
+    def __init__(self, build, n: int):
+        self._build, self._items, self._lock = build, [None] * n, threading.Lock()
+
+    def __len__(self) -> int:
+        return len(self._items)
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[j] for j in range(*i.indices(len(self._items)))]
+        r = self._items[i]
+        if r is None:
+            r = self._build(i if i >= 0 else len(self._items) + i)
+            with self._lock:
+                if self._items[i] is None:
+                    self._items[i] = r
+                r = self._items[i]
+        return r
 
 
 @contextlib.contextmanager
@@ -475,8 +499,14 @@ class MatchEngine:
             evs = [oracle.score_doc(cp, h) for h in per]
         return evs, offs
 
-    def analyze(self, docs: list[bytes], pods: list[tuple[str, str]] | None = None) -> list[AnalysisResult]:
-        """Full AnalysisResult per doc (pods = [(name, namespace)] for labelling)."""
+    def analyze(self, docs: list[bytes], pods: list[tuple[str, str]] | None = None,
+                lazy: bool = False) -> "list[AnalysisResult] | LazyResults":
+        """Full AnalysisResult per doc (pods = [(name, namespace)] for labelling).
+
+        ``lazy``: return once the batch's compact per-doc event lists exist (scan,
+        verify, score); each doc's context windows and pydantic objects are built on
+        first access (``LazyResults``) — the consumer that reads result i pays for it,
+        and the scan engine is free for the next batch that much sooner."""
         from operator_amd.ops import patterns
 
         with self._lock, _gc_paused():
@@ -485,37 +515,58 @@ class MatchEngine:
             evs, offs = self.events(docs)
             t_ev = time.perf_counter()
             nls = self._doc_newlines[1] if self._doc_newlines and self._doc_newlines[0] is docs else None
+            self._doc_newlines = None
+            self.stats.docs += len(docs)
+            ids = uuid4_strs(len(docs))
+            if lazy:
+                ms = (t_ev - t0) * 1e3
+                self.last_timing = {"events_s": t_ev - t0}
+
+                def build(di: int) -> AnalysisResult:
+                    doc, ev = docs[di], evs[di]
+                    q_off, q_k = self._context_queries(di, doc, ev, offs)
+                    ctxs = patterns().contexts([doc], [0] * len(q_off), q_off, q_k) if q_off else []
+                    return self._result(doc, ev, ctxs, pods[di] if pods else (None, None), ms,
+                                        None if nls is None else nls[di], ids[di])
+
+                return LazyResults(build, len(docs))
             # the +-k context windows of every reported event, extracted natively in one
             # call over the whole batch (N3)
-            cp = self.cp
-            pats = cp.patset.patterns
             q_doc, q_off, q_k = [], [], []
             for di, (doc, ev) in enumerate(zip(docs, evs)):
-                lo = None
-                for e in ev[: self.max_events]:
-                    off = offs.get((di, cp.pattern_primary[e.pattern], e.line))
-                    if off is None:
-                        if lo is None:
-                            lo = _line_offsets(doc)
-                        off = lo[e.line] if e.line < len(lo) else 0
-                    q_doc.append(di)
-                    q_off.append(off)
-                    q_k.append(pats[e.pattern].context_lines)
+                o_, k_ = self._context_queries(di, doc, ev, offs)
+                q_doc.extend([di] * len(o_))
+                q_off.extend(o_)
+                q_k.extend(k_)
             ctxs = patterns().contexts(docs, q_doc, q_off, q_k) if q_doc else []
             t_ctx = time.perf_counter()
             out = []
             j = 0
-            ids = uuid4_strs(len(docs))
             for di, (doc, ev) in enumerate(zip(docs, evs)):
                 n = min(len(ev), self.max_events)
                 out.append(self._result(doc, ev, ctxs[j:j + n], pods[di] if pods else (None, None),
                                         (time.perf_counter() - t0) * 1e3, None if nls is None else nls[di], ids[di]))
                 j += n
-            self._doc_newlines = None
-            self.stats.docs += len(docs)
             t_end = time.perf_counter()
             self.last_timing = {"events_s": t_ev - t0, "contexts_s": t_ctx - t_ev, "results_s": t_end - t_ctx}
             return out
+
+    def _context_queries(self, di: int, doc: bytes, ev: list[oracle.Event], offs: dict) -> tuple[list, list]:
+        """(byte offset, context lines) of each reported event of doc ``di``: the offset
+        of its primary matcher's hit on that line (the line start if none is known)."""
+        cp = self.cp
+        pats = cp.patset.patterns
+        q_off, q_k = [], []
+        lo = None
+        for e in ev[: self.max_events]:
+            off = offs.get((di, cp.pattern_primary[e.pattern], e.line))
+            if off is None:
+                if lo is None:
+                    lo = _line_offsets(doc)
+                off = lo[e.line] if e.line < len(lo) else 0
+            q_off.append(off)
+            q_k.append(pats[e.pattern].context_lines)
+        return q_off, q_k
 
     def _matched(self, pi: int) -> MatchedPattern:
         mp = self._mp_cache.get(pi)

@@ -101,12 +101,12 @@ class LocalMatchService:
             with self._lock:
                 eng = self.engine
             t0 = time.perf_counter()
-            res = eng.analyze(docs, pods)
+            res = eng.analyze(docs, pods, lazy=True)
             self.batches += 1
             if self.metrics:
                 self.metrics.observe_scan(sum(map(len, docs)), time.perf_counter() - t0)
-            for (_, f), r in zip(batch, res):
-                f.set_result(r)
+            for i, (_, f) in enumerate(batch):   # each waiter wakes as soon as ITS result is built
+                f.set_result(res[i])
         except Exception as e:  # noqa: BLE001
             log.error("match batch of %d failed: %s", len(batch), e)
             for _, f in batch:

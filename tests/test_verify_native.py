@@ -135,3 +135,23 @@ def test_uuid4_strs_are_version4_uuids():
         u = uuid.UUID(s)
         assert u.version == 4 and u.variant == uuid.RFC_4122 and str(u) == s
     assert uuid4_strs(0) == []
+
+
+def test_lazy_analyze_equals_eager():
+    """analyze(lazy=True) builds, per doc on first access, what the eager batch builds."""
+    from operator_amd.engine.match import LazyResults, MatchEngine
+    from operator_amd.patterns.synth import LogFactory, synthetic_library
+
+    docs, _ = LogFactory(n_patterns=120, seed=3).batch(12, 6 * 1024, n_failures=2)
+    eng = MatchEngine(synthetic_library(120, seed=0), device="cpu")
+    pods = [(f"p{i}", "ns") for i in range(len(docs))]
+    eager = eng.analyze(docs, pods)
+    lazy = eng.analyze(docs, pods, lazy=True)
+    assert isinstance(lazy, LazyResults) and len(lazy) == len(eager)
+    strip = lambda r: {k: v for k, v in r.to_obj().items() if k not in ("analysisId", "metadata")}  # noqa: E731
+    assert sum(len(r.events or []) for r in eager) > 0
+    for i in (3, 0, len(docs) - 1):            # any order
+        assert strip(lazy[i]) == strip(eager[i])
+    assert [strip(r) for r in lazy] == [strip(r) for r in eager]
+    assert lazy[2] is lazy[2] and lazy[-1] is lazy[len(docs) - 1]
+    assert len({r.analysis_id for r in lazy}) == len(docs)

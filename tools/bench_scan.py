@@ -79,6 +79,16 @@ def main():
             warm.append(time.perf_counter() - u1)
         t1, t2 = 0.0, min(warm)
         stage = {"analyze_" + k: round(v, 4) for k, v in eng.last_timing.items()}
+        lz, mat = [], []
+        for _ in range(3):   # lazy: compact per-doc events only; then materialize every result
+            u1 = time.perf_counter()
+            lres = eng.analyze(docs, lazy=True)
+            u2 = time.perf_counter()
+            list(lres)
+            lz.append(u2 - u1)
+            mat.append(time.perf_counter() - u2)
+        stage["analyze_lazy_s"] = round(min(lz), 4)
+        stage["lazy_materialize_all_s"] = round(min(mat), 4)
         for name, fn in (("scan_gpu", lambda: eng.scan_gpu(docs)), ("events", lambda: eng.events(docs))):
             best = 1e9
             for _ in range(3):
