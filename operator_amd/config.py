@@ -109,6 +109,7 @@ class EngineCfg(BaseModel):
     extra_models: list[str] = []      # more local models on the same GPU(s): "preset" or "name=/hf/dir"; an
                                       # AIProvider whose modelId names one is served by it (KV budget split)
     seed: int = 0
+    weight_cache_dir: str = ""        # ready-to-run weight shards as safetensors, mmapped at start
     dtype: str = "bfloat16"
     weight_dtype: str = "bfloat16"   # bfloat16 | fp8 (W8A8 e4m3fn projections, e.g. Llama-3-70B)
     device: str = "cuda"

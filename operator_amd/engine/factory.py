@@ -24,6 +24,7 @@ def build_llm(s: Settings, device: str | torch.device | None = None, tp=None):
     from operator_amd.engine.tokenizer import Tokenizer, load_chat_template
     from operator_amd.models.config import config_from_hf, get_config
     from operator_amd.models.kv_cache import PagedKVCache
+    from operator_amd.models import weight_cache
     from operator_amd.models.llama import LlamaModel
 
     e = s.engine
@@ -38,10 +39,7 @@ def build_llm(s: Settings, device: str | torch.device | None = None, tp=None):
             and getattr(tp, "oneshot", None) is None:
         tp.enable_oneshot(dev, int(e.oneshot_allreduce_mb * (1 << 20)))
     model = LlamaModel(cfg, device=dev, tp=tp, dtype=dtype, weight_dtype=e.weight_dtype)
-    if e.model_path:
-        model.load_hf(e.model_path)
-    else:
-        model.init_random(e.seed)
+    weight_cache.load_or_build(model, e.weight_cache_dir, e.model_path, e.seed)
     # KV cache: the compute dtype, or OCP fp8 (e4m3fn, per-tensor scales) with engine.kv_dtype=fp8
     if e.kv_dtype not in ("auto", "fp8"):
         raise ValueError(f"engine.kv_dtype must be auto or fp8, not {e.kv_dtype!r}")

@@ -189,3 +189,40 @@ def test_engine_step_failure_releases_pages_and_keeps_serving():
     finally:
         loop.stop()
         loop.join(10)
+
+
+@pytest.mark.parametrize("wd", ["bfloat16", "fp8"])
+def test_weight_cache_roundtrip(tmp_path, wd):
+    """engine.weight_cache_dir: the first start builds and writes the shard, the next maps
+    it back (identical tensors); another seed / dtype is a different key, never a hit."""
+    import os
+
+    from operator_amd.models import weight_cache
+
+    cfg = get_config("tiny-gqa4")
+    a = LlamaModel(cfg, device="cpu", dtype=torch.float32, weight_dtype=wd)
+    assert weight_cache.load_or_build(a, str(tmp_path), None, 7) == "miss"
+    files = os.listdir(tmp_path)
+    assert len(files) == 1 and files[0].endswith("-r0of1.safetensors")
+    b = LlamaModel(cfg, device="cpu", dtype=torch.float32, weight_dtype=wd)
+    assert weight_cache.load_or_build(b, str(tmp_path), None, 7) == "hit"
+    assert len(b.layers) == len(a.layers)
+    for t0, t1 in [(a.embed, b.embed), (a.lm_head, b.lm_head), (a.final_norm, b.final_norm)]:
+        assert torch.equal(t0, t1)
+    for la, lb in zip(a.layers, b.layers):
+        for f in weight_cache.LAYER_FIELDS:
+            x, y = getattr(la, f), getattr(lb, f)
+            assert (x is None) == (y is None)
+            if x is not None:
+                assert x.dtype == y.dtype and torch.equal(x.view(torch.uint8), y.view(torch.uint8)), f
+    c = LlamaModel(cfg, device="cpu", dtype=torch.float32, weight_dtype=wd)
+    assert weight_cache.load_or_build(c, str(tmp_path), None, 8) == "miss"   # another seed: new key
+    assert len(os.listdir(tmp_path)) == 2
+    assert weight_cache.load_or_build(LlamaModel(cfg, device="cpu", dtype=torch.float32), None, None, 7) == "off"
+    # a damaged file is rebuilt, not trusted
+    p = os.path.join(tmp_path, files[0])
+    with open(p, "r+b") as fh:
+        fh.truncate(100)
+    d = LlamaModel(cfg, device="cpu", dtype=torch.float32, weight_dtype=wd)
+    assert weight_cache.load_or_build(d, str(tmp_path), None, 7) == "miss"
+    assert torch.equal(d.embed, a.embed)

@@ -215,6 +215,27 @@ def test_fp8_weights_model_runs_and_tracks_bf16():
     assert cos > 0.98, float(cos)
 
 
+@pytest.mark.parametrize("wd", ["bfloat16", "fp8"])
+def test_weight_cache_maps_shard_onto_the_gpu(tmp_path, wd):
+    """A model started from the weight cache (safetensors mmapped straight to the device)
+    computes exactly what the freshly built one does."""
+    from operator_amd.models import weight_cache
+
+    cfg = get_config("tiny-gqa4")
+    outs = []
+    for expect in ("miss", "hit"):
+        m = LlamaModel(cfg, device="cuda", weight_dtype=wd)
+        assert weight_cache.load_or_build(m, str(tmp_path), None, 11) == expect
+        assert m.embed.is_cuda and m.layers[0].wqkv.is_cuda
+        kv = PagedKVCache(cfg.layers, 64, cfg.kv_heads, 128, 16, device="cuda")
+        T = 40
+        fb = ForwardBatch(torch.arange(T, device="cuda"), torch.arange(T, device="cuda"),
+                          torch.full((T,), -1, dtype=torch.long, device="cuda"), True, None, seq_lens=[T],
+                          prefill_work=None)
+        outs.append(m.forward(fb, kv))
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_graph_prefill_equals_eager_prefill():
     """A prefill replayed from a captured bucket graph (tokens padded to the bucket,
     padding slots -1, padding attention items -1) writes the same KV cache and samples
