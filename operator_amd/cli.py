@@ -97,7 +97,7 @@ def _build_pool(s, patterns):
 
         n = torch.cuda.device_count()  # counts devices without initialising the GPU
         devices = [f"cuda:{i}" for i in range(min(max(1, s.engine.gpus), max(1, n)))]
-    roles = tuple(r for r, on in (("match", s.services.match in ("local", "cpu")),
+    roles = tuple(r for r, on in (("match", s.services.match in ("local", "cpu", "stub")),
                                   ("explain", s.services.explain == "local")) if on)
     pool = EnginePool(s, patterns, devices, roles=roles)
     return pool, PoolMatchService(pool), PoolExplainService(pool)
@@ -105,12 +105,14 @@ def _build_pool(s, patterns):
 
 def _build_services(s, metrics):
     from operator_amd.engine.factory import build_explain_service, build_match_engine
-    from operator_amd.engine.service import LocalMatchService, RemoteLogParser
+    from operator_amd.engine.service import LocalMatchService, RemoteLogParser, StubMatchService
 
     if s.services.match == "remote":
         matcher = RemoteLogParser(s.services.log_parser_url, s.services.log_parser_read_timeout_s,
                                   s.services.log_parser_connect_timeout_s)
         factory = None
+    elif s.services.match == "stub":
+        matcher, factory = StubMatchService(), None
     else:
         factory = lambda ps: build_match_engine(s, ps)  # noqa: E731
         matcher = None

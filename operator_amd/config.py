@@ -87,7 +87,7 @@ class PatternsCfg(BaseModel):
 
 
 class ServicesCfg(BaseModel):
-    match: str = "local"              # local | remote | cpu
+    match: str = "local"              # local | remote | cpu | stub (fixed result: plumbing benchmarks)
     explain: str = "local"            # local | remote | echo | none
     log_parser_url: str = "http://podmortem-log-parser-service.podmortem-system.svc.cluster.local:8080"
     log_parser_read_timeout_s: float = 30.0
@@ -103,6 +103,7 @@ class ServicesCfg(BaseModel):
 class EngineCfg(BaseModel):
     gpus: int = 1                     # engine processes (one per GPU) behind the controller
     pool: bool = False                # run the engines out of process even with one GPU
+    pool_log_arena_mb: float = 64     # per engine worker: shared-memory ring the pod logs travel through
     model: str = "llama3-8b"
     model_path: Optional[str] = None  # HF safetensors dir (its config.json wins over `model`); random init when absent
     chat_template: str = "auto"       # auto = the checkpoint's tokenizer_config.json template; none; a file; Jinja

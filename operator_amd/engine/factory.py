@@ -124,5 +124,7 @@ def build_match_service(s: Settings, patterns: PatternSet, metrics=None):
     if s.services.match == "remote":
         return service.RemoteLogParser(s.services.log_parser_url, s.services.log_parser_read_timeout_s,
                                        s.services.log_parser_connect_timeout_s)
+    if s.services.match == "stub":
+        return service.StubMatchService()
     return service.LocalMatchService(build_match_engine(s, patterns), s.services.match_max_batch,
                                      s.services.match_batch_wait_ms, metrics)

@@ -19,6 +19,11 @@ local pipes instead of HTTP.
 * Fault injection: ``inject_crash(i)`` makes worker i exit abruptly, for the
   recovery tests (the engine-side half of the §5.3 fault matrix).
 * Pattern updates (PatternLibrary sync) are broadcast to every worker.
+* Pod logs travel through a per-worker shared-memory arena (``_LogArena``): the
+  controller copies the log's bytes into the worker's ring once and sends only
+  (offset, length) with the log-less request; the worker hands those bytes to its
+  scan batcher without a str round trip. Logs that do not fit the free ring space
+  fall back to the pickled request.
 
 Workers are started with the ``spawn`` method before the controller touches
 any GPU, so no process ever forks a GPU-initialised parent.
@@ -70,6 +75,74 @@ def _tp_init(tp_rank: int, tp_world: int, tp_port: int, device: str):
     return Group()
 
 
+class _LogArena:
+    """Ring allocator over one worker's shared-memory log buffer (controller side).
+    Allocations are released when their request's reply (or the worker's death)
+    arrives; space is reclaimed in allocation order, so one slow request holds back
+    at most the ring behind it, and a full ring only means the pickled path."""
+
+    def __init__(self, size: int):
+        from multiprocessing import shared_memory
+
+        self.shm = shared_memory.SharedMemory(create=True, size=size)
+        self.size = size
+        self._live: dict[int, list] = {}       # rid -> [start, end, released]
+        self._order: list[int] = []            # rids in allocation order
+        self.head = self.tail = 0              # next free byte / oldest live byte
+        self.copied = self.fallbacks = 0
+
+    def reset(self) -> None:   # the worker died: nothing it read is in flight any more
+        self._live.clear()
+        self._order.clear()
+        self.head = self.tail = 0
+
+    def put(self, rid: int, data: bytes) -> int | None:
+        n = len(data)
+        if n == 0 or n > self.size // 4:
+            self.fallbacks += 1
+            return None
+        if not self._live:
+            self.head = self.tail = 0
+        if self.head >= self.tail:                       # free: [head, size) and [0, tail)
+            if self.head + n <= self.size:
+                off = self.head
+            elif n < self.tail:
+                off = 0
+            else:
+                self.fallbacks += 1
+                return None
+        elif self.head + n < self.tail:                  # free: [head, tail)
+            off = self.head
+        else:
+            self.fallbacks += 1
+            return None
+        self.shm.buf[off:off + n] = data
+        self.head = off + n
+        self._live[rid] = [off, off + n, False]
+        self._order.append(rid)
+        self.copied += 1
+        return off
+
+    def release(self, rid: int) -> None:
+        a = self._live.get(rid)
+        if a is None:
+            return
+        a[2] = True
+        while self._order and self._live[self._order[0]][2]:
+            del self._live[self._order.pop(0)]
+        if self._order:
+            self.tail = self._live[self._order[0]][0]
+        else:
+            self.head = self.tail = 0
+
+    def close(self) -> None:
+        try:
+            self.shm.close()
+            self.shm.unlink()
+        except (FileNotFoundError, OSError):
+            pass
+
+
 def _follower_main(idx: int, device: str, settings_obj: dict, tp_rank: int, tp_world: int, tp_port: int,
                    outq) -> None:
     """Non-leader rank of a TP replica: holds its model shard and mirrors the leader's steps."""
@@ -89,7 +162,7 @@ def _follower_main(idx: int, device: str, settings_obj: dict, tp_rank: int, tp_w
 
 
 def _worker_main(idx: int, device: str, settings_obj: dict, patterns, roles: tuple[str, ...], inq, outq,
-                 heartbeat_s: float, tp_world: int = 1, tp_port: int = 0) -> None:
+                 heartbeat_s: float, tp_world: int = 1, tp_port: int = 0, arena_name: str | None = None) -> None:
     logging.basicConfig(level=os.environ.get("PODMORTEM_LOG_LEVEL", "WARNING"))
     from concurrent.futures import ThreadPoolExecutor
 
@@ -98,12 +171,14 @@ def _worker_main(idx: int, device: str, settings_obj: dict, patterns, roles: tup
 
     s = Settings.model_validate(settings_obj)
     s.engine.device = device
-    if device == "cpu":
+    if device == "cpu" and s.services.match != "stub":
         s.services.match = "cpu"
     matcher = explainer = None
     try:
         tp = _tp_init(0, tp_world, tp_port, device) if tp_world > 1 else None
-        if "match" in roles:
+        if "match" in roles and s.services.match == "stub":
+            matcher = service.StubMatchService()
+        elif "match" in roles:
             matcher = service.LocalMatchService(factory.build_match_engine(s, patterns, device=device),
                                                 s.services.match_max_batch, s.services.match_batch_wait_ms)
         if "explain" in roles:
@@ -132,6 +207,22 @@ def _worker_main(idx: int, device: str, settings_obj: dict, patterns, roles: tup
     # one thread per in-flight request (an explain blocks its thread until generated):
     # as many as the engine can batch, twice, like the controller's own pipeline pool
     pool = ThreadPoolExecutor(max_workers=max(4, s.operator.workers or 2 * s.engine.max_batch + 16))
+
+    arena = None
+    if arena_name:
+        from multiprocessing import shared_memory
+
+        # the controller owns and unlinks the segment (spawned workers share its
+        # resource tracker, which already holds the one registration of this name)
+        arena = shared_memory.SharedMemory(name=arena_name)
+
+    def run_shm(rid, payload, off, n):
+        log_bytes = bytes(arena.buf[off:off + n])   # copied out before the reply frees the slot
+        try:
+            fut = matcher.submit(payload, log_bytes)
+            outq.put(("ok", idx, rid, fut.result()))
+        except Exception as e:  # noqa: BLE001
+            outq.put(("err", idx, rid, f"{type(e).__name__}: {e}"))
 
     def run(rid, kind, payload):
         # requests and results cross the process boundary as the pydantic objects
@@ -165,6 +256,8 @@ def _worker_main(idx: int, device: str, settings_obj: dict, patterns, roles: tup
             continue
         if kind in ("match", "explain"):
             pool.submit(run, msg[1], kind, msg[2])
+        elif kind == "match_shm":
+            pool.submit(run_shm, msg[1], msg[2], msg[3], msg[4])
     stop.set()
     pool.shutdown(wait=True)
     if matcher is not None:
@@ -205,12 +298,16 @@ class _Worker:
         self.restarts = 0
         self.inflight: dict[int, tuple] = {}
         self.info: dict = {}
+        self.arena: _LogArena | None = None
 
 
 class EnginePool:
     def __init__(self, settings, patterns, devices: list[str], roles: tuple[str, ...] = ("match", "explain"),
-                 heartbeat_s: float = 2.0, heartbeat_timeout_s: float = 30.0, max_restarts: int = 3):
+                 heartbeat_s: float = 2.0, heartbeat_timeout_s: float = 30.0, max_restarts: int = 3,
+                 log_arena_mb: float | None = None):
         self.settings, self.patterns, self.roles = settings, patterns, roles
+        mb = getattr(settings.engine, "pool_log_arena_mb", 64) if log_arena_mb is None else log_arena_mb
+        self.log_arena_bytes = int(mb * (1 << 20)) if "match" in roles else 0
         self.heartbeat_s, self.heartbeat_timeout_s = heartbeat_s, heartbeat_timeout_s
         self.max_restarts = max_restarts
         self._ctx = mp.get_context("spawn")
@@ -234,6 +331,10 @@ class EnginePool:
 
     # ---------------------------------------------------------------- lifecycle
     def _spawn(self, w: _Worker) -> None:
+        if self.log_arena_bytes and w.arena is None:
+            w.arena = _LogArena(self.log_arena_bytes)
+        if w.arena is not None:
+            w.arena.reset()
         w.inq = self._ctx.Queue()
         w.ready, w.alive, w.last_beat = False, True, time.time()
         world = 1 + len(w.follower_devices)
@@ -242,7 +343,7 @@ class EnginePool:
         w.proc = self._ctx.Process(
             target=_worker_main, name=f"engine-{w.idx}",
             args=(w.idx, w.device, settings, self.patterns, self.roles, w.inq, self._outq,
-                  self.heartbeat_s, world, port), daemon=True)
+                  self.heartbeat_s, world, port, w.arena.shm.name if w.arena is not None else None), daemon=True)
         w.followers = [self._ctx.Process(target=_follower_main, name=f"engine-{w.idx}-tp{r}",
                                          args=(w.idx, d, settings, r, world, port, self._outq), daemon=True)
                        for r, d in enumerate(w.follower_devices, start=1)]
@@ -286,6 +387,9 @@ class EnginePool:
                     if not fut.done():
                         fut.set_exception(WorkerDied("engine pool closed"))
                 w.inflight.clear()
+                if w.arena is not None:
+                    w.arena.close()
+                    w.arena = None
 
     # ---------------------------------------------------------------- requests
     def _pick(self) -> _Worker | None:
@@ -306,6 +410,12 @@ class EnginePool:
                     return
             rid = next(self._ids) if rid is None else rid
             w.inflight[rid] = (kind, payload, fut)
+            if kind == "match" and w.arena is not None and payload.logs:
+                off = w.arena.put(rid, payload.logs.encode("utf-8", "replace"))
+                if off is not None:   # the log rides the shared-memory ring; the request carries none
+                    w.inq.put(("match_shm", rid, payload.model_copy(update={"logs": None}), off,
+                               w.arena._live[rid][1] - off))   # noqa: SLF001
+                    return
             w.inq.put((kind, rid, payload))
 
     def submit_match(self, data: PodFailureData) -> Future:
@@ -356,25 +466,35 @@ class EnginePool:
                 continue
             except (EOFError, OSError):
                 return
-            kind, idx = msg[0], msg[1]
-            w = self.workers[idx]
-            with self._lock:
-                if kind == "hb":
-                    w.last_beat = time.time()
-                elif kind == "ready":
-                    w.ready, w.info, w.last_beat = True, msg[2], time.time()
-                    self._ready_cv.notify_all()
-                elif kind == "fatal":
-                    log.error("engine worker %d failed to start: %s", idx, msg[2])
-                    w.info["fatal"] = msg[2]
-                    w.restarts = self.max_restarts  # a start-up failure is not transient
-                elif kind in ("ok", "err"):
-                    item = w.inflight.pop(msg[2], None)
-                    if item is not None and not item[2].done():
-                        if kind == "ok":
-                            item[2].set_result(msg[3])
-                        else:
-                            item[2].set_exception(RuntimeError(msg[3]))
+            if msg[0] == "batch":
+                for m in msg[2]:
+                    self._handle(m)
+            else:
+                self._handle(msg)
+
+    def _handle(self, msg) -> None:
+        kind, idx = msg[0], msg[1]
+        w = self.workers[idx]
+        item = None
+        with self._lock:
+            if kind == "hb":
+                w.last_beat = time.time()
+            elif kind == "ready":
+                w.ready, w.info, w.last_beat = True, msg[2], time.time()
+                self._ready_cv.notify_all()
+            elif kind == "fatal":
+                log.error("engine worker %d failed to start: %s", idx, msg[2])
+                w.info["fatal"] = msg[2]
+                w.restarts = self.max_restarts  # a start-up failure is not transient
+            elif kind in ("ok", "err"):
+                if w.arena is not None:
+                    w.arena.release(msg[2])
+                item = w.inflight.pop(msg[2], None)
+        if item is not None and not item[2].done():   # waiters wake outside the pool lock
+            if kind == "ok":
+                item[2].set_result(msg[3])
+            else:
+                item[2].set_exception(RuntimeError(msg[3]))
 
     def _monitor_loop(self) -> None:
         while not self._closing:
@@ -414,7 +534,9 @@ class EnginePool:
         with self._lock:
             return {"workers": [{"idx": w.idx, "device": w.device, "tp_devices": [w.device, *w.follower_devices],
                                  "alive": w.alive, "ready": w.ready,
-                                 "inflight": len(w.inflight), "restarts": w.restarts} for w in self.workers],
+                                 "inflight": len(w.inflight), "restarts": w.restarts,
+                                 "shm_logs": w.arena.copied if w.arena else 0,
+                                 "shm_fallbacks": w.arena.fallbacks if w.arena else 0} for w in self.workers],
                     **self.stats}
 
 

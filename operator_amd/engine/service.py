@@ -53,9 +53,11 @@ class LocalMatchService:
     def analyze(self, data: PodFailureData) -> AnalysisResult:
         return self.submit(data).result()
 
-    def submit(self, data: PodFailureData) -> Future:
+    def submit(self, data: PodFailureData, log_bytes: bytes | None = None) -> Future:
+        """``log_bytes``: the pod log already as bytes (the engine pool's shared-memory
+        transfer), used instead of ``data.logs``."""
         f: Future = Future()
-        self._q.put((data, f))
+        self._q.put((data, f, log_bytes))
         return f
 
     def analyze_many(self, datas: list[PodFailureData]) -> list[AnalysisResult]:
@@ -95,8 +97,8 @@ class LocalMatchService:
             self._run_batch(batch)
 
     def _run_batch(self, batch) -> None:
-        docs = [(d.logs or "").encode("utf-8", "replace") for d, _ in batch]
-        pods = [_pod_id(d.pod) for d, _ in batch]
+        docs = [raw if raw is not None else (d.logs or "").encode("utf-8", "replace") for d, _, raw in batch]
+        pods = [_pod_id(d.pod) for d, _, _ in batch]
         try:
             with self._lock:
                 eng = self.engine
@@ -105,13 +107,42 @@ class LocalMatchService:
             self.batches += 1
             if self.metrics:
                 self.metrics.observe_scan(sum(map(len, docs)), time.perf_counter() - t0)
-            for i, (_, f) in enumerate(batch):   # each waiter wakes as soon as ITS result is built
+            for i, (_, f, _) in enumerate(batch):   # each waiter wakes as soon as ITS result is built
                 f.set_result(res[i])
         except Exception as e:  # noqa: BLE001
             log.error("match batch of %d failed: %s", len(batch), e)
-            for _, f in batch:
+            for _, f, _ in batch:
                 if not f.done():
                     f.set_exception(e)
+
+
+class StubMatchService:
+    """The stub log-parser of BASELINE config 1 (``services.match=stub``): one fixed
+    CRITICAL out-of-memory event per pod, no scan — for benchmarking the operator's and
+    the engine pool's plumbing on its own."""
+
+    def analyze(self, data: PodFailureData) -> AnalysisResult:
+        return self.submit(data).result()
+
+    def submit(self, data: PodFailureData, log_bytes: bytes | None = None) -> Future:
+        from operator_amd.api.models import AnalysisEvent, AnalysisSummary, MatchedPattern
+
+        name, ns = _pod_id(data.pod)
+        ev = AnalysisEvent(line_number=91, score=0.9, matched_line="java.lang.OutOfMemoryError: Java heap space",
+                           matched_pattern=MatchedPattern(id="oom", name="Java heap exhausted", severity="CRITICAL"))
+        f: Future = Future()
+        f.set_result(AnalysisResult(pod_name=name, pod_namespace=ns, events=[ev],
+                                    summary=AnalysisSummary(highest_severity="CRITICAL", significant_events=1,
+                                                            total_events=1),
+                                    metadata={"bytes": len(log_bytes) if log_bytes is not None
+                                              else len((data.logs or "").encode())}))
+        return f
+
+    def swap_engine(self, engine) -> None:
+        pass
+
+    def close(self) -> None:
+        pass
 
 
 class LocalExplainService:

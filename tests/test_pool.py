@@ -53,6 +53,35 @@ def test_pool_match_matches_in_process_engine(pool):
         assert got.to_obj()["summary"] == want.to_obj()["summary"]
         assert [e["matchedPattern"]["id"] for e in got.to_obj()["events"]] == \
                [e["matchedPattern"]["id"] for e in want.to_obj()["events"]]
+        assert [e["context"] for e in got.to_obj()["events"]] == [e["context"] for e in want.to_obj()["events"]]
+    # the logs travelled through the workers' shared-memory rings, not the pickled queue
+    assert sum(w["shm_logs"] for w in pool.health()["workers"]) >= len(docs)
+
+
+def test_log_arena_ring_allocation():
+    """The controller-side ring: in-order reclaim, wrap-around, fallback when full."""
+    from operator_amd.engine.pool import _LogArena
+
+    a = _LogArena(1000)
+    try:
+        assert a.put(1, b"a" * 250) == 0 and a.put(2, b"b" * 200) == 250
+        assert a.put(3, b"c" * 260) is None                 # > size // 4: pickled instead
+        assert a.put(3, b"c" * 250) == 450 and a.put(4, b"d" * 250) == 700
+        assert a.put(5, b"e" * 100) is None                 # 950 + 100 > 1000 and the tail is 0
+        a.release(2)                                        # out of order: 1 still holds the tail
+        assert a.tail == 0 and a.put(5, b"e" * 100) is None
+        a.release(1)                                        # reclaims 1 and 2: tail -> 450
+        assert a.tail == 450
+        assert a.put(5, b"e" * 100) == 0                    # wraps
+        assert bytes(a.shm.buf[0:100]) == b"e" * 100 and bytes(a.shm.buf[450:700]) == b"c" * 250
+        assert a.put(6, b"f" * 250) == 100                  # [100, 350) < tail 450
+        assert a.put(7, b"g" * 100) is None                 # would reach the tail
+        for r in (3, 4, 5, 6):
+            a.release(r)
+        assert a.head == a.tail == 0 and a.put(8, b"h" * 250) == 0
+        assert a.copied == 7 and a.fallbacks == 4
+    finally:
+        a.close()
 
 
 def test_pool_explain_and_routing(pool):

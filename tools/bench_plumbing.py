@@ -76,7 +76,7 @@ def main():
         from operator_amd.engine.pool import EnginePool, PoolExplainService, PoolMatchService
 
         s.services.explain = "echo"
-        s.services.match = "cpu"
+        s.services.match = "stub" if a.match == "stub" else "cpu"
         pool = EnginePool(s, catalog_library(), ["cpu"] * a.pool)
         assert pool.wait_ready(300) == a.pool, pool.health()
         match, explain = PoolMatchService(pool), PoolExplainService(pool)
@@ -120,16 +120,20 @@ def main():
     elapsed = time.perf_counter() - t0
     lat = sorted(done[n] - t_fail[n] for n in names)
     op.stop()
+    shm = None
     if pool is not None:
+        h = pool.health()["workers"]
+        shm = {"shm_logs": sum(w["shm_logs"] for w in h), "shm_fallbacks": sum(w["shm_fallbacks"] for w in h)}
         pool.close()
-    print(json.dumps({"bench": "plumbing (BASELINE config 1)", "failures": a.failures,
-                      "topology": f"EnginePool x{a.pool} (CPU matcher + echo)" if a.pool else "in-process",
+    print(json.dumps({"pool_log_transfer": shm, "bench": "plumbing (BASELINE config 1)", "failures": a.failures,
+                      "topology": (f"EnginePool x{a.pool} ({'stub' if a.match == 'stub' else 'CPU'} matcher + echo)"
+                                   if a.pool else "in-process"),
                       "log_bytes": len(log),
                       "analyses_per_s": round(a.failures / elapsed, 1),
                       "p50_ms": round(statistics.median(lat) * 1e3, 1), "p99_ms": round(lat[int(0.99 * len(lat))] * 1e3, 1),
                       "reconcile_p50_ms": round(statistics.median(rec) * 1e3, 2),
                       "reconcile_max_ms": round(max(rec) * 1e3, 2), "crs": a.crs,
-                      "engines": ("stub log-parser" if a.match == "stub" and not a.pool else "CPU matcher (catalog)") +
+                      "engines": ("stub log-parser" if a.match == "stub" else "CPU matcher (catalog)") +
                       " + echo explainer", "pipeline_workers": a.workers}))
 
 
