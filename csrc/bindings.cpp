@@ -373,7 +373,8 @@ void score_events(const at::Tensor& keys, const at::Tensor& hit_doc, const at::T
 void attn_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                  const at::Tensor& block_tables, const at::Tensor& seq_lens, at::Tensor& out,
                  at::Tensor& o_part, at::Tensor& ml_part, int64_t num_splits, double scale, int64_t variant,
-                 double k_scale, double v_scale) {
+                 double k_scale, double v_scale, const c10::optional<at::Tensor>& q8,
+                 const c10::optional<at::Tensor>& sx) {
   CHECK_DEV(q); CHECK_BF16(q); CHECK_CONTIG(q); CHECK_BF16(out); CHECK_CONTIG(out);
   const bool fp8 = kv_is_fp8(k_cache);
   TORCH_CHECK(fp8 ? kv_is_fp8(v_cache) : (k_cache.scalar_type() == at::kBFloat16 &&
@@ -396,11 +397,22 @@ void attn_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tenso
               "partial buffers too small");
   TORCH_CHECK(B * num_splits < (1LL << 31), "grid too large");
   TORCH_CHECK(k_scale > 0 && v_scale > 0, "KV scales must be positive");
+  TORCH_CHECK(q8.has_value() == sx.has_value(), "q8 and sx together");
+  uint8_t* q8p = nullptr;
+  float* sxp = nullptr;
+  if (q8.has_value()) {
+    CHECK_CONTIG(*q8); CHECK_CONTIG(*sx); CHECK_DT(*sx, at::kFloat);
+    TORCH_CHECK((q8->scalar_type() == at::kByte || q8->scalar_type() == at::kFloat8_e4m3fn) &&
+                    q8->numel() == B * Hq * D && sx->numel() == B && Hq * D <= 8192,
+                "q8 e4m3fn [B, Hq*D], sx fp32 [B], Hq*D <= 8192");
+    q8p = static_cast<uint8_t*>(q8->data_ptr());
+    sxp = sx->data_ptr<float>();
+  }
   const c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
   RC(oamd::attn_decode(ptr<bf16_t>(q), k_cache.data_ptr(), v_cache.data_ptr(), fp8, (float)k_scale, (float)v_scale,
                        ptr<int>(block_tables), ptr<int>(seq_lens), ptr<bf16_t>(out), ptr<float>(o_part),
                        ptr<float>(ml_part), (int)B, (int)Hq, (int)Hkv, (int)D, (int)page, (int)block_tables.size(1),
-                       (int)num_splits, (float)scale, (int)variant, cur_stream()));
+                       (int)num_splits, (float)scale, (int)variant, cur_stream(), q8p, sxp));
 }
 
 void attn_prefill(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor& o,
@@ -473,7 +485,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("attn_decode", &attn_decode, pybind11::arg("q"), pybind11::arg("k_cache"), pybind11::arg("v_cache"),
         pybind11::arg("block_tables"), pybind11::arg("seq_lens"), pybind11::arg("out"), pybind11::arg("o_part"),
         pybind11::arg("ml_part"), pybind11::arg("num_splits"), pybind11::arg("scale"), pybind11::arg("variant") = 0,
-        pybind11::arg("k_scale") = 1.0, pybind11::arg("v_scale") = 1.0);
+        pybind11::arg("k_scale") = 1.0, pybind11::arg("v_scale") = 1.0, pybind11::arg("q8") = pybind11::none(),
+        pybind11::arg("sx") = pybind11::none());
   m.def("quantize_fp8", &quantize_fp8);
   m.def("silu_quantize_fp8", &silu_quantize_fp8, pybind11::arg("gu"), pybind11::arg("q"), pybind11::arg("sx"),
         pybind11::arg("slabs") = pybind11::none(), pybind11::arg("splits") = 1);

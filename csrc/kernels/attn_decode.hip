@@ -354,10 +354,72 @@ __global__ void attn_decode_combine_kernel(const float* __restrict__ o_part, con
   out[(int64_t)bh * D + d] = f2bf(L > 0.f ? o / L : 0.f);
 }
 
+// Split combine fused with the o-projection's input quantization (fp8 W8A8 models): one
+// 256-thread block per token row of Hq x 128 outputs. Each element is the bf16 of the
+// split-KV combine (or the attention kernel's own bf16 output for a row of one split),
+// exactly as attn_decode_combine_kernel writes it; the row is then quantized per token
+// to e4m3fn exactly as quantize_fp8_rows does (amax of the bf16 values / 448), so the
+// separate quantization pass over `out` disappears.
+template <int MAXV>
+__global__ void __launch_bounds__(256) attn_decode_combine_q8_kernel(
+    const float* __restrict__ o_part, const float* __restrict__ ml_part, const int* __restrict__ seq_lens,
+    const bf16_t* __restrict__ out, uint8_t* __restrict__ q8, float* __restrict__ sx, int Hq, int num_splits,
+    int max_tokens, int chunk) {
+  constexpr int D = 128;
+  __shared__ float red[4];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int len = min(seq_lens[b], max_tokens);
+  const int per = len > 0 ? split_len(len, num_splits, chunk) : 1;
+  const int ns = len > 0 ? (len + per - 1) / per : 1;
+  const int n = Hq * D;
+  float v[MAXV];
+  float amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int e = tid + i * 256;
+    v[i] = 0.f;
+    if (e < n) {
+      const int h = e / D, d = e % D;
+      const int64_t bh = (int64_t)b * Hq + h;
+      if (len <= 0 || ns == 1 || num_splits == 1) {
+        v[i] = bf2f(out[bh * D + d]);
+      } else {
+        const float* ml = ml_part + bh * num_splits * 2;
+        float M = -INFINITY;
+        for (int s = 0; s < ns; ++s) M = fmaxf(M, ml[2 * s]);
+        float L = 0.f, o = 0.f;
+        for (int s = 0; s < ns; ++s) {
+          const float wgt = exp2f(ml[2 * s] - M);
+          L += wgt * ml[2 * s + 1];
+          o += wgt * o_part[(bh * num_splits + s) * D + d];
+        }
+        v[i] = bf2f(f2bf(L > 0.f ? o / L : 0.f));
+      }
+      amax = fmaxf(amax, fabsf(v[i]));
+    }
+  }
+  amax = wave_max(amax);
+  if ((tid & 63) == 0) red[tid >> 6] = amax;
+  __syncthreads();
+  amax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const float sc = amax > 0.f ? amax / 448.f : 1.f;
+  const float inv = 1.f / sc;
+  if (tid == 0) sx[b] = sc;
+  uint8_t* qr = q8 + (int64_t)b * n;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int e = tid + i * 256;
+    if (e < n) {
+      const int pk = __builtin_amdgcn_cvt_pk_fp8_f32(v[i] * inv, 0.f, 0, false);
+      qr[e] = static_cast<uint8_t>(pk & 0xff);
+    }
+  }
+}
+
 int attn_decode(const bf16_t* q, const void* k_cache, const void* v_cache, bool fp8, float k_scale, float v_scale,
                 const int* block_tables, const int* seq_lens, bf16_t* out, float* o_part, float* ml_part, int B,
                 int Hq, int Hkv, int head_dim, int page_size, int max_pages, int num_splits, float scale, int variant,
-                hipStream_t stream) {
+                hipStream_t stream, uint8_t* q8, float* sx) {
   if (B == 0) return 0;
   if (head_dim != 128) return -1;
   if (page_size < 16 || (page_size & (page_size - 1)) != 0) return -2;
@@ -408,6 +470,22 @@ int attn_decode(const bf16_t* q, const void* k_cache, const void* v_cache, bool 
   }
 #undef OAMD_DEC
   OAMD_LAUNCH_CHECK();
+  if (q8 != nullptr) {   // combine (if split) + per-token e4m3fn rows for the fp8 o-projection
+    const int n = Hq * 128;
+    if (n <= 256 * 4)
+      attn_decode_combine_q8_kernel<4><<<B, 256, 0, stream>>>(o_part, ml_part, seq_lens, out, q8, sx, Hq, num_splits,
+                                                               max_pages * page_size, chunk);
+    else if (n <= 256 * 16)
+      attn_decode_combine_q8_kernel<16><<<B, 256, 0, stream>>>(o_part, ml_part, seq_lens, out, q8, sx, Hq,
+                                                                num_splits, max_pages * page_size, chunk);
+    else if (n <= 256 * 32)
+      attn_decode_combine_q8_kernel<32><<<B, 256, 0, stream>>>(o_part, ml_part, seq_lens, out, q8, sx, Hq,
+                                                                num_splits, max_pages * page_size, chunk);
+    else
+      return -6;
+    OAMD_LAUNCH_CHECK();
+    return 0;
+  }
   if (num_splits > 1) {
     attn_decode_combine_kernel<<<B * Hq, 128, 0, stream>>>(o_part, ml_part, seq_lens, out, Hq, num_splits,
                                                            max_pages * page_size, chunk);

@@ -69,7 +69,9 @@ int score_events(const int64_t* keys, const int* hit_doc, const int* doc_ptr, in
 int attn_decode(const bf16_t* q, const void* k_cache, const void* v_cache, bool fp8, float k_scale, float v_scale,
                 const int* block_tables, const int* seq_lens, bf16_t* out, float* o_part, float* ml_part, int B,
                 int Hq, int Hkv, int head_dim, int page_size, int max_pages, int num_splits, float scale, int variant,
-                hipStream_t stream);
+                hipStream_t stream, uint8_t* q8 = nullptr, float* sx = nullptr);
+// (q8, sx non-null: the output rows are also emitted as per-token e4m3fn [B, Hq*128] + fp32 scales,
+// == quantize_fp8_rows(out); `out` then holds valid bf16 only for rows of a single split.)
 // Causal prefill attention; the work list holds one item per attn_prefill_block_q(Hq, Hkv, variant)
 // query rows of a sequence. variant 1 = per-query-head kernel (64 rows), 2 = GQA-grouped 16-row
 // waves, 3 = GQA-grouped swapped-operand 32x32 MFMA waves (2 and 3 need Hq / Hkv in {1, 2, 4, 8}).

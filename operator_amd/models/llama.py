@@ -258,10 +258,10 @@ class LlamaModel:
                                   want_kv=fb.is_prefill, bias=bias, k_scale=kv.k_scale, v_scale=kv.v_scale)
             if fb.is_prefill:
                 o = ops.attn_prefill(q, k, v, fb.seq_lens, self.scale, work=fb.prefill_work)
-            else:
+            else:   # fp8: the split-combine kernel also emits the o-projection's e4m3fn rows
                 o = ops.attn_decode(q, kc, vc, fb.block_tables, fb.context_lens, self.scale, fb.num_splits,
-                                    workspace=ws, k_scale=kv.k_scale, v_scale=kv.v_scale)
-            a = self._lin(o.view(T, self.hq * c.head_dim), lw.wo, lw.so, defer=True)
+                                    workspace=ws, k_scale=kv.k_scale, v_scale=kv.v_scale, quant=q8)
+            a = self._lin(o if isinstance(o, tuple) else o.view(T, self.hq * c.head_dim), lw.wo, lw.so, defer=True)
             x = self.tp.all_reduce_rmsnorm(a, lw.mlp_norm, c.rms_eps, residual=h, quant=q8)   # fused under TP
             if lw.sgu is None:
                 m = ops.gate_up_silu(x, lw.wgu, self.gu_block)

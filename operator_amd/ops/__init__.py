@@ -22,8 +22,10 @@ __all__ = [
     "quantize_fp8", "silu_quantize_fp8", "linear_fp8", "fp8_plan", "SplitK", "linear_tile", "tile_ok", "BLAS_CALLS",
 ]
 
-DECODE_MIN_SPLIT_TOKENS = 256  # never split a sequence into pieces shorter than this
-DECODE_TARGET_BLOCKS = 512     # split only while B x Hkv decode-attention workgroups < this
+# never split a sequence into pieces shorter than this / split only while B x Hkv
+# decode-attention workgroups < this (env overrides for tuning runs)
+DECODE_MIN_SPLIT_TOKENS = int(os.environ.get("OAMD_DECODE_MIN_SPLIT", "256"))
+DECODE_TARGET_BLOCKS = int(os.environ.get("OAMD_DECODE_TARGET_BLOCKS", "512"))
 
 
 class SplitK:
@@ -490,23 +492,29 @@ def decode_workspace(B: int, Hq: int, num_splits: int, device, D: int = 128):
 def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
                 seq_lens: torch.Tensor, scale: float, num_splits: int, out: torch.Tensor | None = None,
                 workspace: tuple[torch.Tensor, torch.Tensor] | None = None, variant: int = 0,
-                k_scale: float = 1.0, v_scale: float = 1.0) -> torch.Tensor:
+                k_scale: float = 1.0, v_scale: float = 1.0, quant: bool = False):
     """Paged decode attention; ``num_splits`` workgroups per (sequence, kv-head)
     (``decode_splits``). Any value >= 1 is correct; it only changes the schedule.
-    The cache is bf16, or e4m3fn holding x / k_scale and x / v_scale."""
+    The cache is bf16, or e4m3fn holding x / k_scale and x / v_scale.
+    ``quant``: return the [B, Hq*D] output rows as per-token e4m3fn ``(q, sx)`` for an
+    fp8 o-projection, produced by the split-combine kernel itself (== quantize_fp8)."""
     if not q.is_cuda:
         r = reference.attn_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, k_scale, v_scale)
         if out is not None:
             out.copy_(r)
-            return out
-        return r
+            r = out
+        return quantize_fp8(r.reshape(r.shape[0], -1)) if quant else r
     B, Hq, D = q.shape
     o = out if out is not None else torch.empty_like(q)
     if workspace is None:
         workspace = decode_workspace(B, Hq, num_splits, q.device)
+    q8 = sx = None
+    if quant:
+        q8 = torch.empty(B, Hq * D, dtype=torch.float8_e4m3fn, device=q.device)
+        sx = torch.empty(B, dtype=torch.float32, device=q.device)
     kernels().attn_decode(q, k_cache, v_cache, block_tables, seq_lens, o, workspace[0], workspace[1],
-                          num_splits, scale, variant, k_scale, v_scale)
-    return o
+                          num_splits, scale, variant, k_scale, v_scale, q8, sx)
+    return (q8, sx) if quant else o
 
 
 def sample(logits: torch.Tensor, temperature: torch.Tensor, seeds: torch.Tensor, positions: torch.Tensor,

@@ -426,3 +426,23 @@ def test_rope_kv_writes_fp8_cache():
     torch.testing.assert_close(vd, vb.cpu().float(), atol=0.07 * v_scale, rtol=0.07)
     exact = ref.kv_store(vb.cpu().float(), torch.float8_e4m3fn, v_scale)
     assert torch.equal(vc.cpu().view(torch.uint8), exact.view(torch.uint8))
+
+
+@pytest.mark.parametrize("Hq,Hkv,splits,variant", [(8, 1, 8, 0), (8, 1, 1, 0), (32, 8, 4, 0), (64, 8, 2, 2)])
+def test_attn_decode_fused_quant_matches_quantized_output(Hq, Hkv, splits, variant):
+    """quant=True: the split-combine kernel's e4m3fn rows == quantize_fp8 of the bf16 output."""
+    torch.manual_seed(21)
+    B, D, page = 6, 128, 16
+    lens = torch.tensor([1, 17, 300, 64, 129, 511], dtype=torch.int32)
+    pages = (int(lens.max()) + page - 1) // page
+    kc = _rand(B * pages, Hkv, page, D)
+    vc = _rand(B * pages, Hkv, page, D)
+    bt = torch.arange(B * pages, dtype=torch.int32).view(B, pages)
+    q = _rand(B, Hq, D)
+    dev = "cuda"
+    args = (q.to(dev), kc.to(dev), vc.to(dev), bt.to(dev), lens.to(dev), D ** -0.5, splits)
+    o = ops.attn_decode(*args, variant=variant)
+    q8, sx = ops.attn_decode(*args, variant=variant, quant=True)
+    q0, s0 = ops.quantize_fp8(o.view(B, Hq * D))
+    torch.testing.assert_close(sx, s0, rtol=0, atol=0)
+    assert torch.equal(q8.view(torch.uint8), q0.view(torch.uint8))
