@@ -136,3 +136,25 @@ def test_profiled_state_order_gives_identical_scan():
     assert b.hot_coverage is not None and b.hot_coverage[1] >= b.hot_coverage[0]
     assert len(ra) > 0 and _rows(ra) == _rows(rb)
     assert _rows(b.scan_gpu(docs[::-1])) == _rows(a.scan_gpu(docs[::-1]))
+
+
+def test_scan_graph_replays_equal_eager_scans():
+    """The captured scan tail (scan_graphs=True) returns what the eager launches return,
+    across batches that share a graph bucket and batches that need a new one, and it
+    falls back to the eager rescan on match overflow."""
+    ps = synthetic_library(400, seed=1)
+    fac = LogFactory(n_patterns=400, seed=6)
+    batches = [fac.batch(n, kb * 1024, n_failures=3, seed=s)[0]
+               for n, kb, s in ((32, 16, 1), (32, 16, 2), (30, 17, 3), (64, 64, 4), (5, 3, 5))]
+    eager = MatchEngine(ps, device="cuda", seg_bytes=1024, scan_graphs=False, profile_bytes=0)
+    graph = MatchEngine(ps, device="cuda", seg_bytes=1024, scan_graphs=True, profile_bytes=0)
+    for docs in batches + batches[:2]:
+        assert _rows(graph.scan_gpu(docs)) == _rows(eager.scan_gpu(docs))
+        ra = [r.metadata["totalLines"] for r in graph.analyze(docs)]
+        assert ra == [d.count(b"\n") + 1 for d in docs]
+    assert graph.graph_replays >= 10 and eager.graph_replays == 0
+    assert len(graph._graphs) < 2 * len(batches)
+    small = MatchEngine(PatternSet.from_dicts([{"id": "e", "primary_pattern": {"literal": "e"}}]), device="cuda",
+                        seg_bytes=256, match_cap=64, profile_bytes=0)
+    assert small.scan_gpu([b"eee\n" * 500]).shape[0] == 1500 and small.match_cap >= 1500
+    assert small.scan_gpu([b"eee\n" * 500]).shape[0] == 1500   # the grown cap: a graph again
