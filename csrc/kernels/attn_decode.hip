@@ -355,18 +355,19 @@ __global__ void attn_decode_combine_kernel(const float* __restrict__ o_part, con
 }
 
 // Split combine fused with the o-projection's input quantization (fp8 W8A8 models): one
-// 256-thread block per token row of Hq x 128 outputs. Each element is the bf16 of the
+// 1024-thread block per token row of Hq x 128 outputs. Each element is the bf16 of the
 // split-KV combine (or the attention kernel's own bf16 output for a row of one split),
 // exactly as attn_decode_combine_kernel writes it; the row is then quantized per token
 // to e4m3fn exactly as quantize_fp8_rows does (amax of the bf16 values / 448), so the
 // separate quantization pass over `out` disappears.
 template <int MAXV>
-__global__ void __launch_bounds__(256) attn_decode_combine_q8_kernel(
+__global__ void __launch_bounds__(1024) attn_decode_combine_q8_kernel(
     const float* __restrict__ o_part, const float* __restrict__ ml_part, const int* __restrict__ seq_lens,
     const bf16_t* __restrict__ out, uint8_t* __restrict__ q8, float* __restrict__ sx, int Hq, int num_splits,
     int max_tokens, int chunk) {
   constexpr int D = 128;
-  __shared__ float red[4];
+  constexpr int NT = 1024;
+  __shared__ float red[NT / 64];
   const int b = blockIdx.x, tid = threadIdx.x;
   const int len = min(seq_lens[b], max_tokens);
   const int per = len > 0 ? split_len(len, num_splits, chunk) : 1;
@@ -376,7 +377,7 @@ __global__ void __launch_bounds__(256) attn_decode_combine_q8_kernel(
   float amax = 0.f;
 #pragma unroll
   for (int i = 0; i < MAXV; ++i) {
-    const int e = tid + i * 256;
+    const int e = tid + i * NT;
     v[i] = 0.f;
     if (e < n) {
       const int h = e / D, d = e % D;
@@ -401,14 +402,16 @@ __global__ void __launch_bounds__(256) attn_decode_combine_q8_kernel(
   amax = wave_max(amax);
   if ((tid & 63) == 0) red[tid >> 6] = amax;
   __syncthreads();
-  amax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  amax = 0.f;
+#pragma unroll
+  for (int k = 0; k < NT / 64; ++k) amax = fmaxf(amax, red[k]);
   const float sc = amax > 0.f ? amax / 448.f : 1.f;
   const float inv = 1.f / sc;
   if (tid == 0) sx[b] = sc;
   uint8_t* qr = q8 + (int64_t)b * n;
 #pragma unroll
   for (int i = 0; i < MAXV; ++i) {
-    const int e = tid + i * 256;
+    const int e = tid + i * NT;
     if (e < n) {
       const int pk = __builtin_amdgcn_cvt_pk_fp8_f32(v[i] * inv, 0.f, 0, false);
       qr[e] = static_cast<uint8_t>(pk & 0xff);
@@ -472,15 +475,15 @@ int attn_decode(const bf16_t* q, const void* k_cache, const void* v_cache, bool 
   OAMD_LAUNCH_CHECK();
   if (q8 != nullptr) {   // combine (if split) + per-token e4m3fn rows for the fp8 o-projection
     const int n = Hq * 128;
-    if (n <= 256 * 4)
-      attn_decode_combine_q8_kernel<4><<<B, 256, 0, stream>>>(o_part, ml_part, seq_lens, out, q8, sx, Hq, num_splits,
+    if (n <= 1024)
+      attn_decode_combine_q8_kernel<1><<<B, 1024, 0, stream>>>(o_part, ml_part, seq_lens, out, q8, sx, Hq, num_splits,
                                                                max_pages * page_size, chunk);
-    else if (n <= 256 * 16)
-      attn_decode_combine_q8_kernel<16><<<B, 256, 0, stream>>>(o_part, ml_part, seq_lens, out, q8, sx, Hq,
-                                                                num_splits, max_pages * page_size, chunk);
-    else if (n <= 256 * 32)
-      attn_decode_combine_q8_kernel<32><<<B, 256, 0, stream>>>(o_part, ml_part, seq_lens, out, q8, sx, Hq,
-                                                                num_splits, max_pages * page_size, chunk);
+    else if (n <= 4096)
+      attn_decode_combine_q8_kernel<4><<<B, 1024, 0, stream>>>(o_part, ml_part, seq_lens, out, q8, sx, Hq,
+                                                               num_splits, max_pages * page_size, chunk);
+    else if (n <= 8192)
+      attn_decode_combine_q8_kernel<8><<<B, 1024, 0, stream>>>(o_part, ml_part, seq_lens, out, q8, sx, Hq,
+                                                               num_splits, max_pages * page_size, chunk);
     else
       return -6;
     OAMD_LAUNCH_CHECK();

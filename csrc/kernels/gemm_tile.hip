@@ -61,7 +61,12 @@ __device__ __forceinline__ uint2 pack4(f32x4 v) {
 
 }  // namespace
 
-template <int EPI>
+// PH2: the K-tile in TWO barrier segments per wave group instead of four — segment A
+// computes quadrants (X0, W0) and (X0, W1) (32 MFMAs) and issues X0 / W0 / W1 of the next
+// K-tile (all three were last read in segment A of the previous tile), segment B computes
+// (X1, W0) and (X1, W1) from the W fragments still in registers and issues X1. Half the
+// barriers per K-tile; every region still has a whole K-tile of DMA flight.
+template <int EPI, bool PH2 = false>
 __global__ void __launch_bounds__(512) gemm_tile256_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
                                                            bf16_t* __restrict__ Y, const bf16_t* __restrict__ bias,
                                                            int M, int N, int K, int ldy, float* __restrict__ P) {
@@ -155,6 +160,43 @@ __global__ void __launch_bounds__(512) gemm_tile256_kernel(const bf16_t* __restr
   };
 
   const int T = K / gridDim.y / kBK;   // K-tiles of this block's split-K slice (blockIdx.y)
+  if constexpr (PH2) {
+    // prologue: all four regions of K-tile 0; X0, W0 and W1 retired before the first reads
+#pragma unroll
+    for (int r = 0; r < 4; ++r) issue(r, 0, 0);
+    vm_wait<2>();
+    seg_barrier();
+    if (g == 1) seg_barrier();   // ping-pong: waves 4-7 one segment behind
+    for (int t = 0; t < T; ++t) {
+      const char* cur = lds + (t & 1) * kBuf;
+      const int nb = (t + 1) & 1;
+      const bool more = t + 1 < T;
+      // -- segment A: (X0, W0), (X0, W1); issue X0, W0, W1 of tile t+1; retire X1 of tile t
+      read_x(cur + 0 * kRegion);
+      read_w(cur + 1 * kRegion, wf0);
+      read_w(cur + 2 * kRegion, wf1);
+      if (more) {
+        issue(0, nb, t + 1);
+        issue(1, nb, t + 1);
+        issue(2, nb, t + 1);
+      }
+      if (g == 1) { if (more) vm_wait<6>(); else vm_wait<0>(); }
+      seg_barrier();
+      mfma_q(acc[0][0], wf0);
+      mfma_q(acc[0][1], wf1);
+      if (g == 0) { if (more) vm_wait<6>(); else vm_wait<0>(); }
+      seg_barrier();
+      // -- segment B: (X1, W0), (X1, W1); issue X1 of tile t+1; retire X0 / W0 / W1 of t+1
+      read_x(cur + 3 * kRegion);
+      if (more) issue(3, nb, t + 1);
+      if (g == 1 && more) vm_wait<2>();
+      seg_barrier();
+      mfma_q(acc[1][0], wf0);
+      mfma_q(acc[1][1], wf1);
+      if (g == 0 && more) vm_wait<2>();
+      seg_barrier();
+    }
+  } else {
   // prologue: all four regions of K-tile 0; X0 and W0 retired before the first reads
 #pragma unroll
   for (int r = 0; r < 4; ++r) issue(r, 0, 0);
@@ -197,6 +239,7 @@ __global__ void __launch_bounds__(512) gemm_tile256_kernel(const bf16_t* __restr
     mfma_q(acc[1][1], wf1);
     if (g == 0 && more) vm_wait<4>();
     seg_barrier();
+  }
   }
   if (g == 0) seg_barrier();   // pairs with the waves 4-7 stagger barrier
 
@@ -497,7 +540,14 @@ int gemm_tile(const bf16_t* X, const bf16_t* W, bf16_t* Y, const bf16_t* bias, i
     if (silu_gu) gemm_tile256_w4_kernel<kEpiSilu><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
     else if (bias) gemm_tile256_w4_kernel<kEpiBias><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
     else gemm_tile256_w4_kernel<kEpiStore><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-  } else {   // default: 8-wave ping-pong
+  } else if (variant == 2 || (variant == 0 && M > 256)) {
+    // 8-wave ping-pong, two barrier segments per K-tile: 1.8-2.7 % over four segments on
+    // the prefill shapes (M = 32k, profiles/gemm_tile_ph2_vs_ph4.jsonl); the lm_head at
+    // M <= 256 keeps four (weight-streaming bound there, 1 % the other way)
+    if (silu_gu) gemm_tile256_kernel<kEpiSilu, true><<<nwg, 512, 0, stream>>>(X, W, Y, bias, M, N, K, ldy, nullptr);
+    else if (bias) gemm_tile256_kernel<kEpiBias, true><<<nwg, 512, 0, stream>>>(X, W, Y, bias, M, N, K, ldy, nullptr);
+    else gemm_tile256_kernel<kEpiStore, true><<<nwg, 512, 0, stream>>>(X, W, Y, bias, M, N, K, ldy, nullptr);
+  } else {   // 8-wave ping-pong, four segments per K-tile (variant 3, or 0 at M <= 256)
     if (silu_gu) gemm_tile256_kernel<kEpiSilu><<<nwg, 512, 0, stream>>>(X, W, Y, bias, M, N, K, ldy, nullptr);
     else if (bias) gemm_tile256_kernel<kEpiBias><<<nwg, 512, 0, stream>>>(X, W, Y, bias, M, N, K, ldy, nullptr);
     else gemm_tile256_kernel<kEpiStore><<<nwg, 512, 0, stream>>>(X, W, Y, bias, M, N, K, ldy, nullptr);

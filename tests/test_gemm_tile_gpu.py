@@ -10,7 +10,7 @@ from operator_amd.ops import reference as ref
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-VARIANTS = (0, 1)   # gemm_tile schedules: 8-wave ping-pong (default), 4-wave 128x128 per wave
+VARIANTS = (0, 1, 2, 3)   # gemm_tile schedules: auto (default), 4-wave 128x128 per wave, 8-wave 2-segment, 8-wave 4-segment
 
 
 def _rand(*shape, scale=1.0):
