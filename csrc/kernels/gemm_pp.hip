@@ -54,7 +54,10 @@ __device__ __forceinline__ uint2 pack4(f32x4 v) { return make_uint2(pack_bf2(v[0
 }  // namespace
 
 // XH: 128-token halves per tile (1 or 2). Regions per buffer: [X half 0][W][X half 1].
-template <int XH, int EPI, bool NT>
+// ONE (XH == 2): the K-tile in ONE barrier segment per wave group (both X halves' 32
+// MFMAs behind one pair of barriers, all three regions of tile t+2 issued together) —
+// the XH == 1 schedule with a second X fragment set, half the barriers of two phases.
+template <int XH, int EPI, bool NT, bool ONE = false>
 __global__ void __launch_bounds__(512) gemm_pp_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
                                                       bf16_t* __restrict__ Y, float* __restrict__ P, int M, int N,
                                                       int K) {
@@ -111,12 +114,19 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const bf16_t* __restrict__
   for (int h = 0; h < XH; ++h)
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[h][b][0] = acc[h][b][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  u16x8 xf[4][2], wf[2][2];
+  u16x8 xf[4][2], xf2[4][2], wf[2][2];
   auto read_x = [&](const char* reg) {
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       xf[b][0] = *reinterpret_cast<const u16x8*>(reg + xo0 + b * 2048);
       xf[b][1] = *reinterpret_cast<const u16x8*>(reg + xo1 + b * 2048);
+    }
+  };
+  auto read_x2 = [&](const char* reg) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      xf2[b][0] = *reinterpret_cast<const u16x8*>(reg + xo0 + b * 2048);
+      xf2[b][1] = *reinterpret_cast<const u16x8*>(reg + xo1 + b * 2048);
     }
   };
   auto read_w = [&](const char* reg) {
@@ -141,6 +151,24 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const bf16_t* __restrict__
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
   };
+  auto mfma_q2 = [&](f32x4 (&a0)[4][2], f32x4 (&a1)[4][2]) {   // both X halves, one cluster
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          a0[b][e] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, wf[e][s]),
+                                                             __builtin_bit_cast(bf16x8_t, xf[b][s]), a0[b][e], 0, 0, 0);
+          a1[b][e] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, wf[e][s]),
+                                                             __builtin_bit_cast(bf16x8_t, xf2[b][s]), a1[b][e], 0, 0, 0);
+        }
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+  };
 
   // prologue: K-tiles 0 and 1 in flight; tile 0's first phase regions (X0, W) retired
 #pragma unroll
@@ -148,9 +176,9 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const bf16_t* __restrict__
   if (T > 1) {
 #pragma unroll
     for (int r = 0; r < NR; ++r) issue(r, 1, 1);
-    if constexpr (XH == 2) vmw<GL * 4>(); else vmw<GL * 2>();   // leave X1(0) [XH 2] + tile 1 in flight
+    if constexpr (XH == 2 && !ONE) vmw<GL * 4>(); else vmw<GL * NR>();   // leave X1(0) [XH 2] + tile 1 in flight
   } else {
-    if constexpr (XH == 2) vmw<GL>(); else vmw<0>();
+    if constexpr (XH == 2 && !ONE) vmw<GL>(); else vmw<0>();
   }
   seg();
   if (g == 1) seg();   // ping-pong: waves 4-7 one segment behind
@@ -165,7 +193,7 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const bf16_t* __restrict__
     const int nb = (t + 2) % kNBuf;
     const bool m2 = t + 2 < T;
     const bool m1 = t + 1 < T;
-    if constexpr (XH == 2) {
+    if constexpr (XH == 2 && !ONE) {
       // phase 1 (X0, W): issue X0 and W of tile t+2
       read_x(cur);
       read_w(cur + kRegion);
@@ -193,12 +221,19 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const bf16_t* __restrict__
       // their read segment already.
       read_x(cur);
       read_w(cur + kRegion);
-      if (m2 && g == 1) { issue(0, nb, t + 2); issue(1, nb, t + 2); }
-      if (g == 1) { if (m2) vmw<GL * 2>(); else vmw<0>(); }
+      if constexpr (XH == 2) read_x2(cur + 2 * kRegion);
+      if (m2 && g == 1) {
+#pragma unroll
+        for (int r = 0; r < NR; ++r) issue(r, nb, t + 2);
+      }
+      if (g == 1) { if (m2) vmw<GL * NR>(); else vmw<0>(); }
       seg();
-      mfma_q(acc[0]);
-      if (m2 && g == 0) { issue(0, nb, t + 2); issue(1, nb, t + 2); }
-      if (g == 0) { if (m2) vmw<GL * 2>(); else vmw<0>(); }
+      if constexpr (XH == 2) mfma_q2(acc[0], acc[XH - 1]); else mfma_q(acc[0]);
+      if (m2 && g == 0) {
+#pragma unroll
+        for (int r = 0; r < NR; ++r) issue(r, nb, t + 2);
+      }
+      if (g == 0) { if (m2) vmw<GL * NR>(); else vmw<0>(); }
       seg();
     }
   }
@@ -235,7 +270,7 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const bf16_t* __restrict__
 }
 
 int gemm_pp(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, int N, int K, int S, int bm, bool silu_gu,
-            bool nt, hipStream_t stream) {
+            bool nt, hipStream_t stream, bool one_seg) {
   if (M < 1 || N % 128 != 0 || S < 1 || S > 32 || K % (kBK * S) != 0) return -1;
   if (bm != 128 && bm != 256) return -2;
   if (silu_gu && S != 1) return -3;
@@ -248,11 +283,17 @@ int gemm_pp(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, int N,
   if (epi == kSilu) OAMD_PP(XH, kSilu, NTB); \
   else if (epi == kPartial) OAMD_PP(XH, kPartial, NTB); \
   else OAMD_PP(XH, kStore, NTB)
-  if (bm == 256) {
+#define OAMD_PP1(E) gemm_pp_kernel<2, E, true, true><<<grid, 512, 0, stream>>>(X, W, Y, P, M, N, K)
+  if (bm == 256 && one_seg) {   // one barrier segment per K-tile (nt weights)
+    if (epi == kSilu) OAMD_PP1(kSilu);
+    else if (epi == kPartial) OAMD_PP1(kPartial);
+    else OAMD_PP1(kStore);
+  } else if (bm == 256) {
     if (nt) { OAMD_PP_E(2, true); } else { OAMD_PP_E(2, false); }
   } else {
     if (nt) { OAMD_PP_E(1, true); } else { OAMD_PP_E(1, false); }
   }
+#undef OAMD_PP1
 #undef OAMD_PP_E
 #undef OAMD_PP
   OAMD_LAUNCH_CHECK();

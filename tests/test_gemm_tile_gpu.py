@@ -112,6 +112,10 @@ def test_gemm_pp_decode(M, N, K):
                 ops.kernels().gemm_pp(x, w, None, P, S, bm, False, True)
                 torch.cuda.synchronize()
                 _close(P[:S * M * N].view(S, M, N).sum(0), r)
+            if bm == 256:   # one barrier segment per K-tile
+                y = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+                ops.kernels().gemm_pp(x, w, y, P if S > 1 else None, S, bm, False, True, True)
+                _close(y, r)
 
 
 @pytest.mark.parametrize("M", [3, 128, 256])
@@ -125,7 +129,7 @@ def test_gemm_pp_silu(M):
     gg = (x.float() @ g.float().t()).to(torch.bfloat16)
     uu = (x.float() @ u.float().t()).to(torch.bfloat16)
     r = ref.silu_mul(torch.cat([gg, uu], 1), None)
-    for bm in (128, 256):
+    for bm, one in ((128, False), (256, False), (256, True)):
         y = torch.empty(M, inter, dtype=torch.bfloat16, device=DEV)
-        ops.kernels().gemm_pp(x, wgu, y, None, 1, bm, True, True)
+        ops.kernels().gemm_pp(x, wgu, y, None, 1, bm, True, True, one)
         _close(y, r, 3e-2)

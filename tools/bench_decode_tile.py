@@ -62,11 +62,11 @@ def main():
                     C.gemm_tile(x, w, y, None, silu, 0, S, P if S > 1 else None)
                 return f
 
-            def pp(S, bm, nt):
+            def pp(S, bm, nt, one=False):
                 def f():
                     w = ws[it["i"] % 4]
                     it["i"] += 1
-                    C.gemm_pp(x, w, y, P if S > 1 else None, S, bm, silu, nt)
+                    C.gemm_pp(x, w, y, P if S > 1 else None, S, bm, silu, nt, one)
                 return f
 
             cands = {"decode": cur}
@@ -79,6 +79,8 @@ def main():
                     if K % (64 * S) == 0:
                         for nt in (True, False):
                             cands[f"pp_bm{bm}_s{S}{'_nt' if nt else ''}"] = pp(S, bm, nt)
+                        if bm == 256:
+                            cands[f"pp_bm256_s{S}_one"] = pp(S, bm, True, True)
             t = {k: [] for k in cands}
             for _ in range(a.rounds):
                 for k, f in cands.items():
