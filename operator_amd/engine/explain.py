@@ -120,6 +120,8 @@ class EngineLoop(threading.Thread):
                 self.llm.waiting.clear()
                 if hasattr(self.llm, "_prefilling"):
                     self.llm._prefilling = []
+                if hasattr(self.llm, "_pf"):
+                    self.llm._pf = None
                 self.fatal = e
                 return
 

@@ -121,25 +121,31 @@ class _BucketState:
         self.step = torch.zeros(1, dtype=torch.long, device=dev)
 
     def load(self, reqs: list[GenRequest], max_pages: int) -> None:
-        """Write the per-row state of ``reqs`` (rows beyond are padding)."""
+        """Write the per-row state of ``reqs`` (rows beyond are padding). Built in numpy
+        (one pass over the rows, no per-element tensor indexing: ~0.3 ms instead of
+        ~10 ms for 256 rows at every batch-composition change) and copied in once."""
         bp = self.bp
-        ids = torch.zeros(bp, dtype=torch.long)
-        pos = torch.zeros(bp, dtype=torch.long)
-        ctx = torch.zeros(bp, dtype=torch.int32)
-        bt = torch.zeros(bp, max_pages, dtype=torch.int32)
-        temp = torch.zeros(bp, dtype=torch.float32)
-        seeds = torch.zeros(bp, dtype=torch.long)
-        for i, r in enumerate(reqs):
-            ids[i] = r.output[-1]
-            pos[i] = r.length - 1
-            ctx[i] = r.length
-            bt[i, :len(r.pages)] = torch.as_tensor(r.pages, dtype=torch.int32)
-            temp[i] = r.temperature
-            seeds[i] = r.seed
+        n = len(reqs)
+        ids = np.zeros(bp, dtype=np.int64)
+        pos = np.zeros(bp, dtype=np.int64)
+        ctx = np.zeros(bp, dtype=np.int32)
+        bt = np.zeros((bp, max_pages), dtype=np.int32)
+        temp = np.zeros(bp, dtype=np.float32)
+        seeds = np.zeros(bp, dtype=np.int64)
+        if n:
+            lens = np.fromiter((r.length for r in reqs), dtype=np.int64, count=n)
+            ids[:n] = np.fromiter((r.output[-1] for r in reqs), dtype=np.int64, count=n)
+            pos[:n] = lens - 1
+            ctx[:n] = lens
+            temp[:n] = np.fromiter((r.temperature for r in reqs), dtype=np.float32, count=n)
+            seeds[:n] = np.fromiter((r.seed for r in reqs), dtype=np.int64, count=n)
+            for i, r in enumerate(reqs):
+                bt[i, :len(r.pages)] = r.pages
         nb = self.ids.is_cuda
         for dst, src in ((self.ids, ids), (self.pos, pos), (self.ctx, ctx), (self.bt, bt), (self.temp, temp),
                          (self.seeds, seeds)):
-            dst.copy_(src.pin_memory() if nb else src, non_blocking=nb)
+            t = torch.from_numpy(src)
+            dst.copy_(t.pin_memory() if nb else t, non_blocking=nb)
 
 
 @contextlib.contextmanager
@@ -215,8 +221,8 @@ class _DecodeGraph:
 
 class _PrefillGraph:
     """A prefill of up to ``T`` packed tokens / ``S`` sequences captured as one
-    hipGraph: embedding -> 32 layers (hipBLASLt GEMMs, norms, RoPE + KV write,
-    flash prefill attention) -> last-token lm_head -> sampler.
+    hipGraph: embedding -> 32 layers (gemm_tile GEMMs with fused SwiGLU, norms,
+    RoPE + KV write, flash prefill attention) -> last-token lm_head -> sampler.
 
     Why: an eager prefill is ~400 launches from the engine thread, each needing
     the GIL. At the start of a wave the operator's pipeline threads hold it for
@@ -235,7 +241,15 @@ class _PrefillGraph:
             ("ids", T, i64), ("pos", T, i64), ("slots", T, i64), ("last", S, i64), ("seeds", S, i64),
             ("spos", S, i64), ("cu", S + 1, i32), ("ws", self.W, i32), ("wq", self.W, i32),
             ("temp", S, torch.float32))}
-        self.host = {n: torch.zeros_like(t, device="cpu").pin_memory() for n, t in self.dev.items()}
+        # two pinned input sets + sampled-token buffers, used alternately: a launch
+        # returns without waiting for the GPU, so the engine can queue the next
+        # prefill batch before reading this one's tokens (LLMEngine._prefill); a set is
+        # rewritten only after the event of its previous launch (two launches ago)
+        self.hosts = [{n: torch.zeros_like(t, device="cpu").pin_memory() for n, t in self.dev.items()}
+                      for _ in range(2)]
+        self.outs = [torch.zeros(S, dtype=i64).pin_memory() for _ in range(2)]
+        self.events: list = [None, None]
+        self._i = 0
         self.graph: torch.cuda.CUDAGraph | None = None
         self.tok: torch.Tensor | None = None
 
@@ -261,9 +275,15 @@ class _PrefillGraph:
             self._run()
         self.graph = g
 
-    def run(self, ids, pos, slots, cu, ws, wq, last, temp, seeds, spos) -> list[int]:
-        """Inputs as numpy arrays of the real batch (<= T tokens, <= S sequences)."""
-        h = self.host
+    def launch(self, ids, pos, slots, cu, ws, wq, last, temp, seeds, spos):
+        """Queue one replay for the real batch (numpy inputs, <= T tokens, <= S
+        sequences); returns (pinned token buffer, event): ``event`` completes when the
+        batch's sampled first tokens are in the buffer."""
+        i = self._i
+        self._i ^= 1
+        if self.events[i] is not None:
+            self.events[i].synchronize()   # this set's copies (two launches ago) are done
+        h = self.hosts[i]
         b = len(last)
         for name, arr, fill in (("ids", ids, 0), ("pos", pos, 0), ("slots", slots, -1), ("last", last, 0),
                                 ("seeds", seeds, 0), ("spos", spos, 0), ("temp", temp, 0.0), ("ws", ws, -1),
@@ -274,7 +294,28 @@ class _PrefillGraph:
         for name in h:
             self.dev[name].copy_(h[name], non_blocking=True)
         _launch_graph(self.graph, 1, self.eng.device)
-        return self.tok[:b].tolist()   # synchronises: the pinned inputs are free again after this
+        out = self.outs[i]
+        out[:b].copy_(self.tok[:b], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.events[i] = ev
+        return out[:b], ev
+
+    def run(self, *args) -> list[int]:
+        """``launch`` and wait for the sampled tokens."""
+        out, ev = self.launch(*args)
+        ev.synchronize()
+        return out.tolist()
+
+
+@dataclass
+class _PendingPrefill:
+    """A launched prefill batch whose first tokens are still on the device."""
+    batch: list[GenRequest]
+    toks: object          # list[int] (known) or a pinned tensor filled when ``event`` completes
+    event: object
+    t0: float
+    tokens: int
 
 
 class LLMEngine:
@@ -308,6 +349,9 @@ class LLMEngine:
         # the batch between _admit (pages allocated, off `waiting`) and its append to
         # `running`: abort_all must release it too if the prefill raises
         self._prefilling: list[GenRequest] = []
+        # the last launched prefill batch, finished (first tokens read, rows joined to
+        # `running`) only after the next batch is queued behind it or when no batch follows
+        self._pf: _PendingPrefill | None = None
         self.stats = EngineStats()
         self._rid = itertools.count()
         self._graphs: dict[tuple[int, int], _DecodeGraph] = {}
@@ -378,6 +422,7 @@ class LLMEngine:
         with self._lock:
             reqs = list({id(r): r for r in (*self.running, *self._prefilling, *self.waiting)}.values())
             self.running, self.waiting, self._prefilling = [], deque(), []
+            self._pf = None
         for r in reqs:
             if r.pages:
                 self.kv.allocator.release(r.pages)
@@ -389,11 +434,11 @@ class LLMEngine:
         self._active = None
 
     def has_work(self) -> bool:
-        return bool(self.waiting or self.running)
+        return bool(self.waiting or self.running or self._pf is not None)
 
     def idle(self) -> bool:
         """Nothing running or in flight on the device (the next step would be a prefill)."""
-        return not self.running and self._inflight is None
+        return not self.running and self._inflight is None and self._pf is None
 
     def queued_prompt_tokens(self) -> int:
         """Prompt tokens waiting for admission (stops counting at one full prefill batch)."""
@@ -435,13 +480,22 @@ class LLMEngine:
             return self._reap()
         batch = self._admit() if self._inflight is None else []
         if batch:
+            # launch this batch, then finish the previous one: its first tokens are read
+            # while this batch is already queued on the GPU behind it (no host gap
+            # between prefill batches)
+            prev = self._pf
             if self._pstream is not None:
                 self._pstream.wait_stream(self._dstream)
                 with torch.cuda.stream(self._pstream):
-                    self._prefill(batch)
+                    self._pf = self._prefill(batch)
                 self._dstream.wait_stream(self._pstream)
             else:
-                self._prefill(batch)
+                self._pf = self._prefill(batch)
+            if prev is not None:
+                self._finish_prefill(prev)
+        elif self._pf is not None:
+            prev, self._pf = self._pf, None
+            self._finish_prefill(prev)
         elif self.running:
             if self._dstream is not None:
                 with torch.cuda.stream(self._dstream):
@@ -452,13 +506,18 @@ class LLMEngine:
             chk()
         return self._reap()
 
+    def _rows(self) -> int:
+        """Rows holding a decode slot: running + the launched, unfinished prefill batch."""
+        return len(self.running) + (len(self._pf.batch) if self._pf is not None else 0)
+
     def _admittable(self) -> bool:
-        return bool(self.waiting) and len(self.running) < self.max_batch
+        return bool(self.waiting) and self._rows() < self.max_batch
 
     def _admit(self) -> list[GenRequest]:
         out, toks = [], 0
+        rows = self._rows()
         with self._lock:
-            while self.waiting and len(self.running) + len(out) < self.max_batch:
+            while self.waiting and rows + len(out) < self.max_batch:
                 r = self.waiting[0]
                 if r.cancelled:
                     self.waiting.popleft()
@@ -467,7 +526,7 @@ class LLMEngine:
                     break
                 need = self.kv.pages_needed(len(r.prompt) + r.max_tokens)
                 if need > self.kv.allocator.free:
-                    if not self.running and not out:
+                    if not rows and not out:
                         r.error = "KV cache too small for request"
                         r.done = True
                         self.waiting.popleft()
@@ -477,17 +536,33 @@ class LLMEngine:
                 r.pages = self.kv.allocator.alloc(need)
                 self.waiting.popleft()
                 out.append(r)
-                self._prefilling = out
+                self._prefilling = (self._pf.batch if self._pf is not None else []) + out
                 toks += len(r.prompt)
         return out
 
-    def _prefill(self, batch: list[GenRequest]) -> None:
-        self._prefilling = batch
+    def _prefill(self, batch: list[GenRequest]) -> _PendingPrefill:
+        """Launch the prefill of ``batch``; ``_finish_prefill`` joins its rows."""
+        pend = self._pf.batch if self._pf is not None else []
+        self._prefilling = pend + batch
         with trace_range(f"prefill[{len(batch)}]"):
-            self._prefill_impl(batch)
-        self._prefilling = []
+            return self._prefill_impl(batch)
 
-    def _prefill_impl(self, batch: list[GenRequest]) -> None:
+    def _finish_prefill(self, pf: _PendingPrefill) -> None:
+        """Read a launched batch's first tokens and join its rows to ``running``."""
+        if pf.event is not None:
+            pf.event.synchronize()
+        toks = pf.toks.tolist() if isinstance(pf.toks, torch.Tensor) else pf.toks
+        now = time.perf_counter()
+        for r, tk in zip(pf.batch, toks):
+            r.output.append(int(tk))
+            r.t_first = now
+            self.running.append(r)
+        self._active = None  # new rows joined
+        self._prefilling = self._pf.batch if self._pf is not None else []
+        self.stats.prefill_tokens += pf.tokens
+        self.stats.prefill_s += now - pf.t0
+
+    def _prefill_impl(self, batch: list[GenRequest]) -> _PendingPrefill:
         t0 = time.perf_counter()
         dev = self.device
         # packed token ids / positions / cache slots built with numpy: this runs on the
@@ -507,23 +582,22 @@ class LLMEngine:
         seeds = [r.seed for r in batch]
         g = self._prefill_graph_for(len(ids), len(batch))
         if g is not None:
-            toks = g.run(ids, pos, slots, cu, ws, wq, last, temps, seeds, lens)
+            toks, ev = g.launch(ids, pos, slots, cu, ws, wq, last, temps, seeds, lens)
             self.stats.prefill_graph_replays += 1
         else:
             t = lambda x, dt=torch.long: torch.as_tensor(np.asarray(x)).to(dtype=dt).to(dev, non_blocking=True)  # noqa: E731
             work = (t(cu, torch.int32), t(ws, torch.int32), t(wq, torch.int32), var) if dev.type == "cuda" else None
             fb = ForwardBatch(t(ids), t(pos), t(slots), True, t(last), seq_lens=lens, prefill_work=work)
             logits = self.model.forward(fb, self.kv)
-            toks = self.model.sample(logits, t(temps, torch.float32), t(seeds), t(lens))
-            toks = toks.tolist()
-        now = time.perf_counter()
-        for r, tk in zip(batch, toks):
-            r.output.append(int(tk))
-            r.t_first = now
-            self.running.append(r)
-        self._active = None  # new rows joined
-        self.stats.prefill_tokens += len(ids)
-        self.stats.prefill_s += now - t0
+            tk = self.model.sample(logits, t(temps, torch.float32), t(seeds), t(lens))
+            if dev.type == "cuda":
+                toks = torch.empty(len(batch), dtype=torch.long, pin_memory=True)
+                toks.copy_(tk, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+            else:
+                toks, ev = tk.tolist(), None
+        return _PendingPrefill(batch, toks, ev, t0, len(ids))
 
     def _prefill_graph(self, T: int) -> _PrefillGraph:
         g = self._prefill_g.get(T)

@@ -191,6 +191,75 @@ def test_engine_step_failure_releases_pages_and_keeps_serving():
         loop.join(10)
 
 
+def test_pipelined_prefill_batches_match_one_at_a_time():
+    """Several prefill batches in a row (max_prefill_tokens forces one prompt per
+    batch): each batch is launched before the previous one's first tokens are read,
+    and every request still generates exactly what it generates alone."""
+    cfg, m, kv = _tiny("tiny-gqa4")
+    prompts = [list(range(3, 40)), list(range(50, 75)), list(range(9, 39)), list(range(100, 135))]
+    alone = []
+    for p in prompts:
+        e1 = LLMEngine(m, kv, max_batch=4, max_context=256, use_graphs=False)
+        alone.append(e1.generate([GenRequest(p, max_tokens=6, temperature=0.0, ignore_eos=True)])[0].output)
+    eng = LLMEngine(m, kv, max_batch=4, max_prefill_tokens=40, max_context=256, use_graphs=False)
+    reqs = [GenRequest(p, max_tokens=6, temperature=0.0, ignore_eos=True) for p in prompts]
+    for r in reqs:
+        eng.submit(r)
+    launched = []
+    real = eng._prefill
+
+    def spy(batch):
+        launched.append((len(batch), eng._pf is not None))   # a previous batch still pending?
+        return real(batch)
+
+    eng._prefill = spy
+    while any(not r.done for r in reqs):
+        eng.step()
+    assert [r.output for r in reqs] == alone
+    assert len(launched) == 4 and sum(p for _, p in launched) == 3   # batches 2-4 queued behind a pending one
+    assert kv.allocator.free == kv.num_pages
+
+
+def test_pipelined_prefill_failure_releases_both_batches():
+    """A launch that raises while the previous prefill batch is still pending fails
+    and releases both batches (pages allocated, rows not yet running)."""
+    from operator_amd.engine.explain import EngineLoop
+
+    cfg = get_config("tiny")
+    m = LlamaModel(cfg, device="cpu", dtype=torch.float32).init_random(seed=4)
+    kv = PagedKVCache(cfg.layers, 32, cfg.kv_heads, cfg.head_dim, 16, device="cpu", dtype=torch.float32)
+    eng = LLMEngine(m, kv, max_batch=4, max_prefill_tokens=32, max_context=256, use_graphs=False)
+    real, calls = m.forward, {"n": 0}
+
+    def flaky(fb, kv_):
+        calls["n"] += 1
+        if calls["n"] == 2:
+            assert fb.is_prefill and eng._pf is not None
+            raise RuntimeError("HIP out of memory (injected in the second prefill)")
+        return real(fb, kv_)
+
+    m.forward = flaky
+    reqs = [GenRequest(list(range(1, 30)), max_tokens=4, temperature=0.0, ignore_eos=True) for _ in range(2)]
+    for r in reqs:
+        eng.submit(r)
+    loop = EngineLoop(eng)
+    loop.start()
+    try:
+        loop.notify()
+        for r in reqs:
+            assert r.event.wait(60)
+        assert all(r.error and "out of memory" in r.error for r in reqs)
+        assert kv.allocator.free == kv.num_pages and loop.fatal is None and eng._pf is None
+        again = GenRequest(list(range(1, 30)), max_tokens=4, temperature=0.0, ignore_eos=True)
+        eng.submit(again)
+        loop.notify()
+        assert again.event.wait(60) and again.error is None and len(again.output) == 4
+        assert kv.allocator.free == kv.num_pages
+    finally:
+        loop.stop()
+        loop.join(10)
+
+
 @pytest.mark.parametrize("wd", ["bfloat16", "fp8"])
 def test_weight_cache_roundtrip(tmp_path, wd):
     """engine.weight_cache_dir: the first start builds and writes the shard, the next maps
