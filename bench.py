@@ -251,7 +251,7 @@ def main() -> int:
     from operator_amd.engine.service import LocalExplainService, LocalMatchService
     from operator_amd.kube.fake import FakeKube, failed_pod, running_pod
     from operator_amd.kube.resources import AIPROVIDERS, PODMORTEMS, PODS
-    from operator_amd.utils.tracing import trace_range
+    from operator_amd.utils.tracing import mark, trace_range
 
     s = settings(dev, a.max_batch, int(os.environ.get("OAMD_BENCH_WORLD", world)) if child else world)
 
@@ -289,10 +289,12 @@ def main() -> int:
             st = llm.stats
             return {"prefill_tokens": st.prefill_tokens, "decode_tokens": st.decode_tokens,
                     "prefill_graph_replays": st.prefill_graph_replays, "use_graphs": bool(llm.use_graphs),
+                    "prefill_padded_tokens": st.prefill_padded_tokens, "prefill_eager": st.prefill_eager,
                     "prefill_graph_buckets": sorted(getattr(llm, "_prefill_g", {})),
                     "dfa_states": getattr(meng, "dfa_states", None)}
         ws = pool.worker_stats()
-        out = {k: sum(w["llm"][k] for w in ws) for k in ("prefill_tokens", "decode_tokens", "prefill_graph_replays")}
+        out = {k: sum(w["llm"].get(k, 0) for w in ws) for k in ("prefill_tokens", "decode_tokens", "prefill_graph_replays",
+                                                                 "prefill_padded_tokens", "prefill_eager")}
         out.update(use_graphs=all(w.get("use_graphs") for w in ws),
                    prefill_graph_buckets=sorted({b for w in ws for b in w.get("prefill_graph_buckets", [])}),
                    dfa_states=ws[0].get("dfa_states") if ws else None)
@@ -412,6 +414,7 @@ def main() -> int:
                 if j + 1 < len(ws):
                     with exp_cv:
                         exp_cv.wait_for(lambda: explained["n"] >= base + (j + 1) * a.batch)
+                    mark(f"handoff[{w}]")
             done_ev.wait()
             op.drain(600)
     else:
@@ -543,6 +546,8 @@ def main() -> int:
                    "prompt_tokens_per_analysis": round(ptoks / max(1, a.batch * a.shards * a.steps), 1),
                    "prefill_graph_replays": replays,
                    "prefill_graph_buckets": stats1["prefill_graph_buckets"],
+                   "prefill_padded_tokens": stats1.get("prefill_padded_tokens", 0) - stats0.get("prefill_padded_tokens", 0),
+                   "prefill_eager_batches": stats1.get("prefill_eager", 0) - stats0.get("prefill_eager", 0),
                    "decode_tok_s_per_gpu": round(dtoks / elapsed, 1), "outcomes": counter["outcomes"],
                    "dfa_states": stats1["dfa_states"], "timed_monotonic_ns": [mono0, mono1],
                    "rccl_world": dist.get_world_size() if dist.is_initialized() else 1,

@@ -71,15 +71,33 @@ class EngineLoop(threading.Thread):
         arrival alone would run a 1-request prefill and queue everything behind it
         (measured at the start of a 256-failure wave: a 1-request prefill stretched to
         174 ms by the launch-side GIL contention of the burst, ahead of the first full
-        batch). So when idle, wait up to ``admit_wait_s`` for a full prefill batch."""
+        batch). So when idle, wait up to ``admit_wait_s`` for half a prefill batch; while
+        a prefill batch runs, queue the next one once a full batch waits or the running
+        one is done (prefill batches are pipelined: LLMEngine.step)."""
         llm = self.llm
         wait = getattr(llm, "admit_wait_s", 0.0)
-        if wait <= 0 or not llm.idle():
+        if wait <= 0:
             return
-        deadline = time.perf_counter() + wait
-        while (not self._stopping and time.perf_counter() < deadline
-               and llm.queued_prompt_tokens() < llm.max_prefill_tokens):
-            time.sleep(0.001)
+        full = llm.max_prefill_tokens
+        if llm.idle():
+            # half a batch starts the first prefill (LLMEngine._prefill_cap cuts it at a
+            # full graph bucket); the rest of the burst queues behind it
+            deadline = time.perf_counter() + wait
+            while (not self._stopping and time.perf_counter() < deadline
+                   and llm.queued_prompt_tokens() < full // 2):
+                time.sleep(0.001)
+            return
+        pf = getattr(llm, "_pf", None)
+        ev = getattr(pf, "event", None)
+        if ev is None or not llm.waiting:
+            return
+        # a prefill batch is still running on the GPU: queue the next one behind it only
+        # once a full batch waits, or when the GPU is about to need it (the running batch
+        # is done), instead of cutting the arrivals into small, padded batches
+        deadline = time.perf_counter() + 1.0
+        while (not self._stopping and time.perf_counter() < deadline and not ev.query()
+               and llm.queued_prompt_tokens() < full):
+            time.sleep(0.0002)
 
     def run(self) -> None:
         if self.llm.device.type == "cuda":

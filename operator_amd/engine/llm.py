@@ -77,6 +77,8 @@ class EngineStats:
     steps: int = 0
     graph_replays: int = 0
     prefill_graph_replays: int = 0
+    prefill_padded_tokens: int = 0   # bucket padding computed by prefill-graph replays
+    prefill_eager: int = 0           # prefill batches no graph bucket fit (<= 15 % padding)
 
 
 @dataclass
@@ -513,16 +515,30 @@ class LLMEngine:
     def _admittable(self) -> bool:
         return bool(self.waiting) and self._rows() < self.max_batch
 
+    def _prefill_cap(self) -> int:
+        """Token budget of the next prefill batch: a full batch (max_prefill_tokens)
+        when that many prompt tokens wait, else the largest graph bucket the queue
+        fills (>= 1024 tokens), so a partial batch replays a full bucket instead of
+        padding a larger one or running eagerly; the rest follows in the next batch."""
+        # the admitted queue only (never a TP leader's not-yet-broadcast submissions):
+        # every rank must cut the same batch
+        q = LLMEngine.queued_prompt_tokens(self)
+        if q >= self.max_prefill_tokens or not self.prefill_graphs:
+            return self.max_prefill_tokens
+        fit = [b for b in self.prefill_buckets if b <= q]
+        return fit[-1] if fit else self.max_prefill_tokens
+
     def _admit(self) -> list[GenRequest]:
         out, toks = [], 0
         rows = self._rows()
+        cap = self._prefill_cap()
         with self._lock:
             while self.waiting and rows + len(out) < self.max_batch:
                 r = self.waiting[0]
                 if r.cancelled:
                     self.waiting.popleft()
                     continue
-                if out and toks + len(r.prompt) > self.max_prefill_tokens:
+                if out and toks + len(r.prompt) > cap:
                     break
                 need = self.kv.pages_needed(len(r.prompt) + r.max_tokens)
                 if need > self.kv.allocator.free:
@@ -584,7 +600,9 @@ class LLMEngine:
         if g is not None:
             toks, ev = g.launch(ids, pos, slots, cu, ws, wq, last, temps, seeds, lens)
             self.stats.prefill_graph_replays += 1
+            self.stats.prefill_padded_tokens += g.T - len(ids)
         else:
+            self.stats.prefill_eager += 1
             t = lambda x, dt=torch.long: torch.as_tensor(np.asarray(x)).to(dtype=dt).to(dev, non_blocking=True)  # noqa: E731
             work = (t(cu, torch.int32), t(ws, torch.int32), t(wq, torch.int32), var) if dev.type == "cuda" else None
             fb = ForwardBatch(t(ids), t(pos), t(slots), True, t(last), seq_lens=lens, prefill_work=work)
@@ -733,12 +751,13 @@ class LLMEngine:
                 keep.append(r)
         if fin:
             self._active = None  # batch composition changed: reload device state next step
-            if self.finish_hook is not None:
-                try:
-                    self.finish_hook([r for r in fin if not r.cancelled])
-                except Exception:  # noqa: BLE001 - waiters fall back to their own detokenization
-                    pass
-            for r in fin:
-                r.event.set()
+            with trace_range(f"finish[{len(fin)}]"):
+                if self.finish_hook is not None:
+                    try:
+                        self.finish_hook([r for r in fin if not r.cancelled])
+                    except Exception:  # noqa: BLE001 - waiters fall back to their own detokenization
+                        pass
+                for r in fin:
+                    r.event.set()
         self.running = keep
         return fin
