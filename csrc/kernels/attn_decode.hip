@@ -7,8 +7,14 @@
 // bytes in flight for the WHOLE life of a workgroup:
 //   * a workgroup walks its token range in chunks of 4 x TW tokens (TW per
 //     wave), with the K/V registers double-buffered: the loads of chunk c+1
-//     are issued before chunk c is consumed (counted vmcnt, no drain), so
-//     there is no per-chunk load/compute bubble;
+//     are issued before chunk c is consumed (counted vmcnt, no drain), and the
+//     consume of chunk c requests chunk c+2 into the registers it frees (K right
+//     after the S MFMAs, V after P.V). tools/probe/kv_stream.hip measured why that
+//     matters: the same paged K/V stream with no compute reads at 6.3-6.6 TB/s,
+//     and a dependent per-chunk compute chain of the consume's length costs ~10 %;
+//   * the first two chunks are requested before the LDS page table / q are set
+//     up (page ids from scalar loads), and a sequence's kv-heads are dispatched
+//     back to back;
 //   * the per-call split count is chosen by the host so that only small
 //     batches are split (B x Hkv workgroups already fill 256 CUs at B >= 128):
 //     at serving batch sizes there is no partial output, no combine kernel and
@@ -120,7 +126,7 @@ __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2)
                        const int* __restrict__ block_tables, const int* __restrict__ seq_lens,
                        bf16_t* __restrict__ out, float* __restrict__ o_part, float* __restrict__ ml_part, int Hkv,
                        int page_size, int log2_page, int max_pages, int num_splits, float scale_log2,
-                       float v_scale) {
+                       float v_scale, int head_minor) {
   using T = KVT<KV>;
   constexpr int D = 128;
   constexpr int TW = 16 * NT;  // tokens per wave per chunk
@@ -130,11 +136,26 @@ __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2)
   __shared__ __attribute__((aligned(16))) float pw[4][TW * GP];  // per-wave P tile [token][head]
   __shared__ __attribute__((aligned(16))) float red[4][G][D];
   __shared__ float mls[4][G][2];
+  __shared__ u16x8 q_lds[4][64];
 
-  const int b = blockIdx.x / num_splits, s = blockIdx.x - b * num_splits, kvh = blockIdx.y;
+  // work item of this workgroup: (sequence, split, kv-head); head_minor dispatches the
+  // kv-heads of one sequence back to back (they read different head slices of the
+  // same pages), else one kv-head across all sequences first
+  int b, s, kvh;
+  if (head_minor) {
+    const int lin = blockIdx.x + gridDim.x * blockIdx.y;
+    kvh = lin % Hkv;
+    const int rest = lin / Hkv;
+    b = rest / num_splits;
+    s = rest - b * num_splits;
+  } else {
+    b = blockIdx.x / num_splits;
+    s = blockIdx.x - b * num_splits;
+    kvh = blockIdx.y;
+  }
   const int Hq = Hkv * G;
   const int len = min(seq_lens[b], max_pages * page_size);  // never index past the block table
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l15 = lane & 15, lg = lane >> 4;
   if (len <= 0) {  // padding row: zero output (written once, by split 0)
     if (s == 0)
@@ -148,47 +169,80 @@ __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2)
   const int ns_b = (len + per - 1) / per;
   const int nch = (end - start + CH - 1) / CH;
 
-  // Page ids of the split -> LDS: the data loads then depend only on LDS
-  // (lgkmcnt), never on a global load that would share vmcnt with them.
+  // Page ids of the split -> LDS: the steady-state data loads depend only on LDS
+  // (lgkmcnt), never on a global load that would share vmcnt with them. The first
+  // two chunks do not wait for that: their page ids come straight from the block
+  // table (wave-uniform scalar loads), so their K/V requests leave before the LDS
+  // page table and q are even written (one dependent latency less per workgroup).
   const int page0 = start >> log2_page;
   const int npg = ((end - 1) >> log2_page) - page0 + 1;
-  for (int i = tid; i < npg; i += 256) pg_lds[i] = block_tables[(int64_t)b * max_pages + page0 + i];
-
-  // q as the MFMA B operand: column = head (zero past G)
-  u16x8 qb[4];
-  {
+  const int* btb = block_tables + (int64_t)b * max_pages + page0;
+  const int pid0 = tid < npg ? btb[tid] : 0;   // issued before any K/V load (vmcnt is in order)
+  u16x8 qv[4];
+  if (w == 0) {
     const int hq = kvh * G + (l15 < G ? l15 : 0);
     const bf16_t* qp = q + ((int64_t)b * Hq + hq) * D + 32 * lg;
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) qb[ks] = *reinterpret_cast<const u16x8*>(qp + 8 * ks);
-    if (l15 >= G) {
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) qb[ks] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-    }
+    for (int ks = 0; ks < 4; ++ks) qv[ks] = *reinterpret_cast<const u16x8*>(qp + 8 * ks);
   }
-  __syncthreads();
 
   const int64_t head_off = (int64_t)kvh * page_size * D;
   const int64_t page_stride = (int64_t)Hkv * page_size * D;
-  auto row_off = [&](int tok) -> int64_t {  // tok in [start, end)
-    const int64_t page = pg_lds[(tok >> log2_page) - page0];
-    return page * page_stride + head_off + (int64_t)(tok & (page_size - 1)) * D;
+  // Every token a wave reads for one 16-token tile lies in ONE page (page_size >= 16,
+  // tiles 16-aligned; a tile wholly past `end` reads token end - 1 only), so each
+  // tile needs one page lookup and 32-bit in-page offsets.
+  auto tile_lds = [&](int base) -> int64_t {
+    const int t0 = min(base, end - 1);
+    return (int64_t)pg_lds[(t0 >> log2_page) - page0] * page_stride + head_off;
+  };
+  auto tile_bt = [&](int base) -> int64_t {
+    const int t0 = min(base, end - 1);
+    return (int64_t)btb[(t0 >> log2_page) - page0] * page_stride + head_off;
   };
   // Branch-free chunk load: rows past `end` are clamped duplicates (masked later).
-  auto load = [&](KVRegs<KV, NT>& r, int c) {
+  // K and V halves separately: a buffer's K registers are free as soon as the chunk's
+  // S = K Q^T MFMAs have read them, so the next-but-one chunk's K is requested there,
+  // a whole softmax + P.V earlier than its V.
+  auto load_k = [&](KVRegs<KV, NT>& r, int c, auto tile_base) {
     const int base = start + c * CH + w * TW;
 #pragma unroll
     for (int i = 0; i < NT; ++i) {
       const int tok = min(base + 16 * i + l15, end - 1);
       const int t16 = tok & 15;
       // tile of `tok`: its 16-token-aligned row, then (lg*16 + t16)*8 inside each ks block
-      const KV* p = kc + row_off(tok) - (int64_t)t16 * D + (lg * 16 + t16) * 8;
+      const KV* p = kc + tile_base(base + 16 * i) + ((tok & (page_size - 1)) - t16) * D + (lg * 16 + t16) * 8;
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) r.k[i][ks] = T::load(p + ks * 512);
     }
-#pragma unroll
-    for (int it = 0; it < 4 * NT; ++it) r.v[it] = T::load(vc + row_off(min(base + 4 * it + lg, end - 1)) + 8 * l15);
   };
+  auto load_v = [&](KVRegs<KV, NT>& r, int c, auto tile_base) {
+    const int base = start + c * CH + w * TW;
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+      const KV* pv = vc + tile_base(base + 16 * i) + 8 * l15;
+#pragma unroll
+      for (int it = 4 * i; it < 4 * i + 4; ++it)
+        r.v[it] = T::load(pv + (min(base + 4 * it + lg, end - 1) & (page_size - 1)) * D);
+    }
+  };
+  // Double-buffered stream over the chunks: the next chunk's loads are always in
+  // flight while the current one is consumed, and the consume of chunk c requests
+  // chunk c + 2 into the registers it frees. Loads past the last chunk re-read the
+  // last chunk (branch-free, L2 hits) so hipcc's wait counts stay exact.
+  KVRegs<KV, NT> ra, rb;
+  load_k(ra, 0, tile_bt);
+  load_v(ra, 0, tile_bt);
+  load_k(rb, min(1, nch - 1), tile_bt);
+  load_v(rb, min(1, nch - 1), tile_bt);
+  if (tid < npg) pg_lds[tid] = pid0;
+  for (int i = tid + 256; i < npg; i += 256) pg_lds[i] = btb[i];   // > 256 pages: rare
+  // q as the MFMA B operand (column = head, zero past G), staged once in LDS by wave 0
+  // and read per k-step (16 VGPRs fewer per lane than q in registers)
+  if (w == 0) {
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) q_lds[ks][lane] = l15 < G ? qv[ks] : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+  __syncthreads();
 
   float m_run = -1e30f, l_run = 0.f;  // per lane: head l15 (finite start: no inf - inf)
   float acc[G][8];
@@ -198,7 +252,8 @@ __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2)
     for (int j = 0; j < 8; ++j) acc[h][j] = 0.f;
   float* pwv = pw[w];
 
-  auto consume = [&](const KVRegs<KV, NT>& r, int c) {
+  // consume chunk c from r, refilling r with chunk `nc` (K after the MFMAs, V at the end)
+  auto consume = [&](KVRegs<KV, NT>& r, int c, int nc) {
     const int base = start + c * CH + w * TW;
     float sc[NT][4];
     float cmax = -INFINITY;
@@ -208,7 +263,7 @@ __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2)
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks)
         a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, T::to_bf16(r.k[i][ks])),
-                                                  __builtin_bit_cast(bf16x8_t, qb[ks]), a, 0, 0, 0);
+                                                  __builtin_bit_cast(bf16x8_t, q_lds[ks][lane]), a, 0, 0, 0);
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const int tok = base + 16 * i + 4 * lg + rr;
@@ -216,6 +271,7 @@ __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2)
         cmax = fmaxf(cmax, sc[i][rr]);
       }
     }
+    load_k(r, nc, tile_lds);
     cmax = fmaxf(cmax, __shfl_xor(cmax, 16, kWave));
     cmax = fmaxf(cmax, __shfl_xor(cmax, 32, kWave));
     const float m_new = fmaxf(m_run, cmax);
@@ -264,21 +320,15 @@ __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2)
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[h][j] += p[h] * vv[j];
     }
+    load_v(r, nc, tile_lds);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   };
 
-  // Double-buffered stream over the chunks: the next chunk's loads are always in
-  // flight while the current one is consumed. Loads past the last chunk re-read
-  // the last chunk (branch-free, L2 hits) so hipcc's wait counts stay exact.
-  KVRegs<KV, NT> ra, rb;
-  load(ra, 0);
   for (int c = 0; c < nch; c += 2) {
-    load(rb, min(c + 1, nch - 1));
-    consume(ra, c);
-    load(ra, min(c + 2, nch - 1));
-    if (c + 1 < nch) consume(rb, c + 1);
+    consume(ra, c, min(c + 2, nch - 1));
+    if (c + 1 < nch) consume(rb, c + 1, min(c + 3, nch - 1));
   }
 
   // ---- merge the 4 waves: reduce the 4 token sub-slots, then across waves ----
@@ -432,19 +482,23 @@ int attn_decode(const bf16_t* q, const void* k_cache, const void* v_cache, bool 
   while ((1 << log2p) < page_size) ++log2p;
   const int G = Hq / Hkv;
   const float scale_log2 = scale * k_scale * 1.4426950408889634f;
-  // variant: 0 = default (NT = 1: 16 tokens per wave per chunk, 164 VGPRs at
+  // variant bits 0-1: 0 = default (NT = 1: 16 tokens per wave per chunk, 162 VGPRs at
   // G = 4 -> 3 workgroups/CU); 2 = NT = 2 (32 tokens per wave, 2 workgroups/CU;
-  // bf16: 238 VGPRs, measured 4-10 % slower at B = 256). G > 4 stays NT = 1.
+  // bf16: 244 VGPRs, measured 3-5 % slower at B = 256). G > 4 stays NT = 1.
+  // Bit 2: the old dispatch order (below).
   int chunk = 0;
   dim3 grid(B * num_splits, Hkv, 1);
 #define OAMD_DEC(GG, NTT, KVT_)                                                                           \
   do {                                                                                                    \
     attn_decode_kernel<GG, NTT, KVT_><<<grid, 256, 0, stream>>>(                                         \
         q, static_cast<const KVT_*>(k_cache), static_cast<const KVT_*>(v_cache), block_tables, seq_lens, \
-        out, o_part, ml_part, Hkv, page_size, log2p, max_pages, num_splits, scale_log2, v_scale);        \
+        out, o_part, ml_part, Hkv, page_size, log2p, max_pages, num_splits, scale_log2, v_scale, hm);    \
     chunk = 64 * NTT;                                                                                     \
   } while (0)
-  const bool nt2 = variant == 2;
+  const bool nt2 = (variant & 3) == 2;
+  // kv-heads of one sequence dispatched back to back (default; tools/bench_attn.py at B = 256:
+  // -0.5..-1 % vs one kv-head across all sequences first, which variant bit 2 selects)
+  const int hm = (variant & 4) ? 0 : 1;
   if (fp8) {
     switch (G) {
       case 1: if (nt2) OAMD_DEC(1, 2, uint8_t); else OAMD_DEC(1, 1, uint8_t); break;
