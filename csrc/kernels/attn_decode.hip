@@ -133,7 +133,8 @@ __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2)
   constexpr int CH = 4 * TW;   // tokens per workgroup per chunk
   constexpr int GP = (G < 4) ? 4 : G;
   __shared__ int pg_lds[kMaxPagesLds];
-  __shared__ __attribute__((aligned(16))) float pw[4][TW * GP];  // per-wave P tile [token][head]
+  // per-wave P tile [token][head], then the per-(token group, head) rescale factors [lg][head]
+  __shared__ __attribute__((aligned(16))) float pw[4][TW * GP + 4 * GP];
   __shared__ __attribute__((aligned(16))) float red[4][G][D];
   __shared__ float mls[4][G][2];
   __shared__ u16x8 q_lds[4][64];
@@ -221,8 +222,8 @@ __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2)
     for (int i = 0; i < NT; ++i) {
       const KV* pv = vc + tile_base(base + 16 * i) + 8 * l15;
 #pragma unroll
-      for (int it = 4 * i; it < 4 * i + 4; ++it)
-        r.v[it] = T::load(pv + (min(base + 4 * it + lg, end - 1) & (page_size - 1)) * D);
+      for (int it = 4 * i; it < 4 * i + 4; ++it)   // token 16i + 4lg + (it - 4i): the S group lg
+        r.v[it] = T::load(pv + (min(base + 16 * i + 4 * lg + (it - 4 * i), end - 1) & (page_size - 1)) * D);
     }
   };
   // Double-buffered stream over the chunks: the next chunk's loads are always in
@@ -244,7 +245,12 @@ __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2)
   }
   __syncthreads();
 
-  float m_run = -1e30f, l_run = 0.f;  // per lane: head l15 (finite start: no inf - inf)
+  // Online softmax per (head, token group): lane (l15, lg) of the S = K Q^T tile holds head
+  // l15 of tokens 4lg..4lg+3 of every 16-token tile, and the P.V lanes (dims 8 l15.., lg)
+  // accumulate exactly those tokens, so each token group keeps its own running max / sum
+  // and a chunk needs no cross-lane reduction at all (the rescale factors ride the P tile
+  // through LDS); the 4 groups are merged once, after the stream.
+  float m_run = -1e30f, l_run = 0.f;  // finite start: no inf - inf
   float acc[G][8];
 #pragma unroll
   for (int h = 0; h < G; ++h)
@@ -256,7 +262,7 @@ __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2)
   auto consume = [&](KVRegs<KV, NT>& r, int c, int nc) {
     const int base = start + c * CH + w * TW;
     float sc[NT][4];
-    float cmax = -INFINITY;
+    float m_new = m_run;
 #pragma unroll
     for (int i = 0; i < NT; ++i) {
       f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -268,13 +274,10 @@ __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2)
       for (int rr = 0; rr < 4; ++rr) {
         const int tok = base + 16 * i + 4 * lg + rr;
         sc[i][rr] = (tok < end) ? a[rr] * scale_log2 : -INFINITY;
-        cmax = fmaxf(cmax, sc[i][rr]);
+        m_new = fmaxf(m_new, sc[i][rr]);
       }
     }
     load_k(r, nc, tile_lds);
-    cmax = fmaxf(cmax, __shfl_xor(cmax, 16, kWave));
-    cmax = fmaxf(cmax, __shfl_xor(cmax, 32, kWave));
-    const float m_new = fmaxf(m_run, cmax);
     const float alpha = exp2f(m_run - m_new);
     float psum = 0.f;
 #pragma unroll
@@ -285,34 +288,35 @@ __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2)
         psum += p;
         if (l15 < G) pwv[(16 * i + 4 * lg + rr) * GP + l15] = p;
       }
-    psum += __shfl_xor(psum, 16, kWave);
-    psum += __shfl_xor(psum, 32, kWave);
     l_run = l_run * alpha + psum;
     m_run = m_new;
-    float al[G];
-#pragma unroll
-    for (int h = 0; h < G; ++h) al[h] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(alpha), h));
+    if (l15 < G) pwv[TW * GP + lg * GP + l15] = alpha;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    auto row4 = [&](const float* src, float (&dst)[G]) {   // G floats of one LDS row
+      if constexpr (G % 4 == 0) {
+#pragma unroll
+        for (int h4 = 0; h4 < G; h4 += 4) {
+          const f32x4 v4 = *reinterpret_cast<const f32x4*>(src + h4);
+          dst[h4] = v4[0]; dst[h4 + 1] = v4[1]; dst[h4 + 2] = v4[2]; dst[h4 + 3] = v4[3];
+        }
+      } else {
+#pragma unroll
+        for (int h = 0; h < G; ++h) dst[h] = src[h];
+      }
+    };
+    float al[G];
+    row4(pwv + TW * GP + lg * GP, al);
 #pragma unroll
     for (int h = 0; h < G; ++h)
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[h][j] *= al[h];
 #pragma unroll
     for (int it = 0; it < 4 * NT; ++it) {
-      const int t = 4 * it + lg;
+      const int t = 16 * (it >> 2) + 4 * lg + (it & 3);
       float p[G];
-      if constexpr (G % 4 == 0) {
-#pragma unroll
-        for (int h4 = 0; h4 < G; h4 += 4) {
-          const f32x4 pv = *reinterpret_cast<const f32x4*>(&pwv[t * GP + h4]);
-          p[h4] = pv[0]; p[h4 + 1] = pv[1]; p[h4 + 2] = pv[2]; p[h4 + 3] = pv[3];
-        }
-      } else {
-#pragma unroll
-        for (int h = 0; h < G; ++h) p[h] = pwv[t * GP + h];
-      }
+      row4(pwv + t * GP, p);
       float vv[8];
       T::to_f32(r.v[it], vv);
 #pragma unroll
@@ -331,7 +335,28 @@ __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2)
     if (c + 1 < nch) consume(rb, c + 1, min(c + 3, nch - 1));
   }
 
-  // ---- merge the 4 waves: reduce the 4 token sub-slots, then across waves ----
+  // ---- merge the 4 token groups of each wave, then the 4 waves ----
+  {
+    float M = m_run;   // lane (head l15, group lg)
+    M = fmaxf(M, __shfl_xor(M, 16, kWave));
+    M = fmaxf(M, __shfl_xor(M, 32, kWave));
+    const float f = exp2f(m_run - M);
+    float L = l_run * f;
+    L += __shfl_xor(L, 16, kWave);
+    L += __shfl_xor(L, 32, kWave);
+    m_run = M;
+    l_run = L;
+    if (l15 < G) pwv[TW * GP + lg * GP + l15] = f;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+      const float fg = pwv[TW * GP + lg * GP + h];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[h][j] *= fg;
+    }
+  }
 #pragma unroll
   for (int h = 0; h < G; ++h)
 #pragma unroll

@@ -15,6 +15,8 @@ bandwidth, not hop latency, dominates — ``Group.all_reduce_`` keeps using RCCL
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -27,7 +29,9 @@ class CollectiveTimeout(RuntimeError):
 
 
 DEFAULT_MAX_BYTES = 8 << 20   # 256 tokens x 8192 x 2 B (70B hidden) = 4 MB, with room
-DEFAULT_BLOCKS = 32
+# workgroups of every one-shot call (fixed per group: each block keeps its own round
+# counter and data-slot parity, so every call of a group must use the same count)
+DEFAULT_BLOCKS = int(os.environ.get("OAMD_CAR_BLOCKS", "32"))
 
 
 class OneShotAllReduce:
