@@ -254,11 +254,19 @@ class LlamaModel:
                 qkv, bias = ops.linear(x, lw.wqkv, bias=bias), None
             else:
                 qkv = self._lin(x, lw.wqkv, lw.sqkv, defer=True)
-            q, k, v = ops.rope_kv(qkv, fb.positions, self.cos, self.sin, self.hq, self.hkv, kc, vc, fb.slots,
-                                  want_kv=fb.is_prefill, bias=bias, k_scale=kv.k_scale, v_scale=kv.v_scale)
             if fb.is_prefill:
+                q, k, v = ops.rope_kv(qkv, fb.positions, self.cos, self.sin, self.hq, self.hkv, kc, vc, fb.slots,
+                                      want_kv=True, bias=bias, k_scale=kv.k_scale, v_scale=kv.v_scale)
                 o = ops.attn_prefill(q, k, v, fb.seq_lens, self.scale, work=fb.prefill_work)
-            else:   # fp8: the split-combine kernel also emits the o-projection's e4m3fn rows
+            elif h.is_cuda and ops.decode_rope_fusable(qkv, self.hq, self.hkv, fb.num_splits):
+                # the new token's RoPE + KV write run inside the attention kernel; fp8: the
+                # split-combine kernel also emits the o-projection's e4m3fn rows
+                o = ops.attn_decode_rope(qkv, self.cos, self.sin, self.hq, self.hkv, kc, vc, fb.block_tables,
+                                         fb.context_lens, self.scale, fb.num_splits, bias=bias, workspace=ws,
+                                         k_scale=kv.k_scale, v_scale=kv.v_scale, quant=q8)
+            else:
+                q, _, _ = ops.rope_kv(qkv, fb.positions, self.cos, self.sin, self.hq, self.hkv, kc, vc, fb.slots,
+                                      want_kv=False, bias=bias, k_scale=kv.k_scale, v_scale=kv.v_scale)
                 o = ops.attn_decode(q, kc, vc, fb.block_tables, fb.context_lens, self.scale, fb.num_splits,
                                     workspace=ws, k_scale=kv.k_scale, v_scale=kv.v_scale, quant=q8)
             a = self._lin(o if isinstance(o, tuple) else o.view(T, self.hq * c.head_dim), lw.wo, lw.so, defer=True)

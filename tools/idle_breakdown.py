@@ -10,7 +10,8 @@ idle gap by the wave phase around it (the waves are cut as in tools/wave_gaps.py
   decode_internal   gaps inside the decode span (window hand-offs are the > 50 us ones)
   tail              last decode kernel -> end of the timed window
 
-Prints one JSON line per wave and one summary line (ms per wave per class, gap counts).
+Prints one JSON line per wave, one summary line (ms per wave per class) and the kernel
+pairs around the largest idle gaps (which hand-off they are).
 """
 import argparse
 import csv
@@ -23,6 +24,7 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--window-json", required=True)
     ap.add_argument("--big-us", type=float, default=50.0, help="gaps above this are host hand-offs")
+    ap.add_argument("--context", type=int, default=0, help="print the kernels around the N largest decode gaps")
     a = ap.parse_args()
     f = gzip.open(a.trace, "rt") if a.trace.endswith(".gz") else open(a.trace)
     line = [x for x in open(a.window_json) if x.startswith("{") and '"metric"' in x][-1]
@@ -34,11 +36,11 @@ def main():
             continue
         n = r["Kernel_Name"]
         kind = "p" if "attn_prefill" in n else "d" if "attn_decode" in n else ""
-        ks.append((s, e, kind))
+        ks.append((s, e, kind, n.split("(")[0][:60]))
     ks.sort()
     # waves: a wave starts at an attn_prefill kernel that follows an attn_decode kernel
     waves, cur, last = [], None, None
-    for s, e, kind in ks:
+    for s, e, kind, _ in ks:
         if kind == "p" and last != "p":
             cur = {"p0": s, "p1": e, "d0": None, "d1": None}
             waves.append(cur)
@@ -50,10 +52,18 @@ def main():
         if kind:
             last = kind
     # busy spans (union of kernel intervals) and the idle gaps between them
-    gaps, end = [], t0
-    for s, e, _ in ks:
+    gaps, end, prev = [], t0, "window start"
+    pairs = {}   # (kernel before, kernel after) of the big gaps -> [count, ms]
+    for s, e, _, name in ks:
         if s > end:
             gaps.append((end, s))
+            if (s - end) / 1e3 > a.big_us:
+                k = (prev, name)
+                pairs.setdefault(k, [0, 0.0])
+                pairs[k][0] += 1
+                pairs[k][1] += (s - end) / 1e6
+        if e >= end:
+            prev = name
         end = max(end, e)
     if t1 > end:
         gaps.append((end, t1))
@@ -97,6 +107,19 @@ def main():
                       "idle_ms_per_wave": {k: round(v / nw, 2) for k, v in sorted(tot.items())},
                       "idle_total_ms_per_wave": round(sum(tot.values()) / nw, 2),
                       "kernels": len(ks)}))
+    if a.context:   # the kernels around the largest idle gaps inside decode spans
+        big = []
+        for i in range(1, len(ks)):
+            g = ks[i][0] - max(x[1] for x in ks[max(0, i - 8):i])
+            if g > a.big_us * 1e3 and any(w["d0"] and w["d0"] <= ks[i][0] <= w["d1"] for w in waves):
+                big.append((g, i))
+        for g, i in sorted(big, reverse=True)[:a.context]:
+            t_ref = ks[i][0]
+            print(json.dumps({"gap_us": round(g / 1e3, 1), "around": [
+                [round((x[0] - t_ref) / 1e3, 1), round((x[1] - x[0]) / 1e3, 1), x[3][:48]] for x in ks[max(0, i - 4):i + 3]]}))
+    top = sorted(pairs.items(), key=lambda kv: -kv[1][1])[:8]
+    for (before, after), (n, ms) in top:
+        print(json.dumps({"kernel_before_gap": before, "kernel_after_gap": after, "count": n, "ms": round(ms, 2)}))
 
 
 if __name__ == "__main__":

@@ -11,6 +11,6 @@ args=${@:---steps 2 --warmup 1}
 timeout -k 10 600 rocprofv3 --kernel-trace -d gpurun_out/prof_fl -o run --output-format csv -- python3 bench.py $args > gpurun_out/fl.json 2> gpurun_out/fl.err
 python3 tools/trace_summary.py gpurun_out/prof_fl/run_kernel_trace.csv --out gpurun_out/fl_trace_summary.txt --top 80
 python3 tools/wave_gaps.py gpurun_out/prof_fl/run_kernel_trace.csv --window-json gpurun_out/fl.json > gpurun_out/fl_wave_gaps.jsonl
-python3 tools/idle_breakdown.py gpurun_out/prof_fl/run_kernel_trace.csv --window-json gpurun_out/fl.json > gpurun_out/fl_idle.jsonl
+python3 tools/idle_breakdown.py gpurun_out/prof_fl/run_kernel_trace.csv --window-json gpurun_out/fl.json --context 6 > gpurun_out/fl_idle.jsonl
 rm -f gpurun_out/prof_fl/run_kernel_trace.csv
 tail -c 400 gpurun_out/fl.json
