@@ -225,6 +225,7 @@ __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2)
   const int ncol = (Hq + 2 * Hkv) * D;
   const int nS = rp.xp ? rp.S : 1;
   f32x4 rv[2][4];
+  f32x4 csv[4];   // cos (g..g+7) | sin (g..g+7) of a rotation item's position, prefetched
   auto rp_col = [&](int item) -> int {   // first column of an item's x1
     if (item < (G + 1) * 8) {
       const int h = item >> 3, g = (item & 7) * 8;
@@ -233,6 +234,15 @@ __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2)
     return (Hq + Hkv + kvh) * D + (item - (G + 1) * 8) * 8;
   };
   if (fused) {
+    if (tid < (G + 1) * 8) {
+      const int pp = min(len - 1, rp.max_pos - 1), g = (tid & 7) * 8;
+      const float* cr = rp.cos_t + (int64_t)pp * (D / 2) + g;
+      const float* sr = rp.sin_t + (int64_t)pp * (D / 2) + g;
+      csv[0] = *reinterpret_cast<const f32x4*>(cr);
+      csv[1] = *reinterpret_cast<const f32x4*>(cr + 4);
+      csv[2] = *reinterpret_cast<const f32x4*>(sr);
+      csv[3] = *reinterpret_cast<const f32x4*>(sr + 4);
+    }
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int pr = tid + 256 * k;
@@ -352,11 +362,14 @@ __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2)
 #pragma unroll
       for (int j = 0; j < 8; ++j) x1[j] = x2[j] = 0.f;
       for (int sl = 0; sl < nS; ++sl) {
-        const float* src = rp_part + (item * kRopeMaxS + sl) * 16;
+        const f32x4* src = reinterpret_cast<const f32x4*>(rp_part + (item * kRopeMaxS + sl) * 16);
+        const f32x4 p0 = src[0], p1 = src[1], p2 = src[2], p3 = src[3];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          x1[j] += src[j];
-          x2[j] += src[8 + j];
+        for (int j = 0; j < 4; ++j) {
+          x1[j] += p0[j];
+          x1[4 + j] += p1[j];
+          x2[j] += p2[j];
+          x2[4 + j] += p3[j];
         }
       }
       if (rp.bias) {
@@ -370,15 +383,13 @@ __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2)
       }
       if (rot) {
         const int h = item >> 3, g = (item & 7) * 8;
-        const int pp = min(len - 1, rp.max_pos - 1);
-        const float* cr = rp.cos_t + (int64_t)pp * (D / 2) + g;
-        const float* sr = rp.sin_t + (int64_t)pp * (D / 2) + g;
         u16x8 o1, o2;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
+          const float c = csv[j >> 2][j & 3], sn = csv[2 + (j >> 2)][j & 3];
           const float a = bf2f(f2bf(x1[j])), bb = bf2f(f2bf(x2[j]));
-          o1[j] = f2bf(a * cr[j] - bb * sr[j]);
-          o2[j] = f2bf(bb * cr[j] + a * sr[j]);
+          o1[j] = f2bf(a * c - bb * sn);
+          o2[j] = f2bf(bb * c + a * sn);
         }
         if (h < G) {
           q_lds[(g & 31) >> 3][h + 16 * (g >> 5)] = o1;
@@ -395,6 +406,20 @@ __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2)
       }
     }
     __syncthreads();
+    if (writer && tid >= 64 && tid < 96) {   // the new token into the cache, for the next steps:
+      // issued here (wave 1; nothing in this kernel reads it) instead of delaying the end
+      const int ti = tid - 64, pos_new = len - 1;
+      const int64_t page = block_tables[(int64_t)b * max_pages + (pos_new >> log2_page)];
+      const int off = pos_new & (page_size - 1), t16 = off & 15;
+      const int64_t row = page * page_stride + head_off + (int64_t)off * D;
+      if (ti < 16) {   // tiled K: [16-token tile][ks][lg][token][8 dims], dim d = 32 lg + 8 ks + j
+        const int d = 8 * ti;
+        cache_put8(const_cast<KV*>(kc) + row - (int64_t)t16 * D + ((((d & 31) >> 3) * 4 + (d >> 5)) * 16 + t16) * 8,
+                   kv_new[0][ti], k_inv);
+      } else {
+        cache_put8(const_cast<KV*>(vc) + row + 8 * (ti - 16), kv_new[1][ti - 16], v_inv);
+      }
+    }
   }
 
   // Online softmax per (head, token group): lane (l15, lg) of the S = K Q^T tile holds head
@@ -576,19 +601,6 @@ __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2)
         ml[0] = M;
         ml[1] = L;
       }
-    }
-  }
-  if (writer && tid < 32) {   // the new token into the cache, for the next steps
-    const int pos_new = len - 1;
-    const int64_t page = block_tables[(int64_t)b * max_pages + (pos_new >> log2_page)];
-    const int off = pos_new & (page_size - 1), t16 = off & 15;
-    const int64_t row = page * page_stride + head_off + (int64_t)off * D;
-    if (tid < 16) {   // tiled K: [16-token tile][ks][lg][token][8 dims], dim d = 32 lg + 8 ks + j
-      const int d = 8 * tid;
-      cache_put8(const_cast<KV*>(kc) + row - (int64_t)t16 * D + ((((d & 31) >> 3) * 4 + (d >> 5)) * 16 + t16) * 8,
-                 kv_new[0][tid], k_inv);
-    } else {
-      cache_put8(const_cast<KV*>(vc) + row + 8 * (tid - 16), kv_new[1][tid - 16], v_inv);
     }
   }
 }

@@ -518,7 +518,12 @@ def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, b
 
 
 ROPE_MAX_SPLITS = 8   # kernels.h kRopeMaxS
-FUSED_DECODE_ROPE = os.environ.get("OAMD_FUSED_ROPE", "1") != "0"
+# Model routing only (decode_rope_fusable); attn_decode_rope itself always fuses when it can.
+# Off by default: measured on the flagship (rocprofv3 --stats, 2 waves each way) the fused
+# attention kernel took 199.9 us vs 191.7 us + 7 us of rope_kv unfused, i.e. the rotation in
+# every workgroup's prologue (slab loads -> LDS -> rotate -> barrier) costs what the separate
+# kernel did, and the whole step came out 0.4 % slower.
+FUSED_DECODE_ROPE = os.environ.get("OAMD_FUSED_ROPE", "0") == "1"
 
 
 def decode_rope_fusable(qkv, Hq: int, Hkv: int, num_splits: int) -> bool:
@@ -544,8 +549,7 @@ def attn_decode_rope(qkv, cos: torch.Tensor, sin: torch.Tensor, Hq: int, Hkv: in
     B = qkv.shape[0]
     D = cos.shape[1] * 2
     S = qkv.S if isinstance(qkv, SplitK) else 1
-    if (not seq_lens.is_cuda or not FUSED_DECODE_ROPE or S > ROPE_MAX_SPLITS
-            or ((Hq // Hkv + 1) * 8 + 16) * S > 512):
+    if not seq_lens.is_cuda or S > ROPE_MAX_SPLITS or ((Hq // Hkv + 1) * 8 + 16) * S > 512:
         P = k_cache.shape[2]
         pos = (seq_lens.to(torch.long) - 1).clamp_min(0)
         pg = torch.gather(block_tables, 1, (pos // P).clamp(max=block_tables.shape[1] - 1).unsqueeze(1)).squeeze(1)
