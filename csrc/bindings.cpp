@@ -80,6 +80,34 @@ void embedding(const at::Tensor& ids, const at::Tensor& table, at::Tensor& out) 
                      (int)table.size(1), table.size(0), cur_stream()));
 }
 
+void decode_slots(const at::Tensor& bt, const at::Tensor& pos, const at::Tensor& ctx, at::Tensor& slots,
+                  at::Tensor& spos, int64_t page_size) {
+  CHECK_DEV(bt); CHECK_DT(bt, at::kInt); CHECK_CONTIG(bt); CHECK_DT(pos, at::kLong); CHECK_CONTIG(pos);
+  CHECK_DT(ctx, at::kInt); CHECK_CONTIG(ctx); CHECK_DT(slots, at::kLong); CHECK_CONTIG(slots);
+  CHECK_DT(spos, at::kLong); CHECK_CONTIG(spos);
+  const int64_t B = pos.numel();
+  TORCH_CHECK(bt.dim() == 2 && bt.size(0) == B && ctx.numel() == B && slots.numel() == B && spos.numel() == B &&
+                  B <= 1024 && page_size > 0,
+              "decode_slots: bt [B, max_pages], pos/ctx/slots/spos [B], B <= 1024");
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(pos.device());
+  RC(oamd::decode_slots(ptr<int>(bt), ptr<int64_t>(pos), ptr<int>(ctx), ptr<int64_t>(slots), ptr<int64_t>(spos),
+                        (int)B, (int)bt.size(1), (int)page_size, cur_stream()));
+}
+
+void decode_advance(const at::Tensor& tok, at::Tensor& ids, at::Tensor& hist, at::Tensor& pos, at::Tensor& ctx,
+                    at::Tensor& step) {
+  CHECK_DEV(tok); CHECK_DT(tok, at::kLong); CHECK_CONTIG(tok); CHECK_DT(ids, at::kLong); CHECK_CONTIG(ids);
+  CHECK_DT(hist, at::kLong); CHECK_CONTIG(hist); CHECK_DT(pos, at::kLong); CHECK_CONTIG(pos);
+  CHECK_DT(ctx, at::kInt); CHECK_CONTIG(ctx); CHECK_DT(step, at::kLong);
+  const int64_t B = ids.numel();
+  TORCH_CHECK(tok.numel() == B && pos.numel() == B && ctx.numel() == B && hist.dim() == 2 && hist.size(0) == B &&
+                  step.numel() == 1 && B <= 1024,
+              "decode_advance: tok/ids/pos/ctx [B], hist [B, ms], step [1], B <= 1024");
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(ids.device());
+  RC(oamd::decode_advance(ptr<int64_t>(tok), ptr<int64_t>(ids), ptr<int64_t>(hist), ptr<int64_t>(pos),
+                          ptr<int>(ctx), ptr<int64_t>(step), (int)B, (int)hist.size(1), cur_stream()));
+}
+
 static bool kv_is_fp8(const at::Tensor& t) {
   return t.scalar_type() == at::kFloat8_e4m3fn || t.scalar_type() == at::kByte;
 }
@@ -564,6 +592,8 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("out"), pybind11::arg("o_part"), pybind11::arg("ml_part"), pybind11::arg("num_splits"),
         pybind11::arg("scale"), pybind11::arg("variant") = 0, pybind11::arg("k_scale") = 1.0,
         pybind11::arg("v_scale") = 1.0, pybind11::arg("q8") = pybind11::none(), pybind11::arg("sx") = pybind11::none());
+  m.def("decode_slots", &decode_slots);
+  m.def("decode_advance", &decode_advance);
   m.def("quantize_fp8", &quantize_fp8);
   m.def("silu_quantize_fp8", &silu_quantize_fp8, pybind11::arg("gu"), pybind11::arg("q"), pybind11::arg("sx"),
         pybind11::arg("slabs") = pybind11::none(), pybind11::arg("splits") = 1);

@@ -15,6 +15,12 @@ int rmsnorm(const bf16_t* x, bf16_t* residual, const bf16_t* w, bf16_t* y, int r
             hipStream_t stream);
 int silu_mul(const bf16_t* gu, bf16_t* out, int64_t rows, int inter, int block, int64_t in_stride,
              int64_t out_stride, hipStream_t stream);
+// Decode-step bookkeeping (norm_act.hip): cache slots + sampler positions of the step's tokens,
+// then the state advance after sampling (B <= 1024 rows, one workgroup each).
+int decode_slots(const int* bt, const int64_t* pos, const int* ctx, int64_t* slots, int64_t* spos, int B,
+                 int max_pages, int page_size, hipStream_t stream);
+int decode_advance(const int64_t* tok, int64_t* ids, int64_t* hist, int64_t* pos, int* ctx, int64_t* step, int B,
+                   int ms, hipStream_t stream);
 int embedding(const int64_t* ids, const bf16_t* table, bf16_t* out, int tokens, int hidden,
               int64_t vocab, hipStream_t stream);
 int rope_kv(const bf16_t* qkv, int64_t qkv_stride, const int64_t* pos, const float* cos_t,

@@ -194,4 +194,60 @@ int embedding(const int64_t* ids, const bf16_t* table, bf16_t* out, int tokens,
   return 0;
 }
 
+// Decode-step bookkeeping of a hipGraph-captured step (engine/llm.py _DecodeGraph), one
+// thread per batch row instead of ~15 one-op torch kernels:
+//   decode_slots:   slot = page(bt[row], pos / P) * P + pos % P for live rows (ctx > 0), else -1;
+//                   spos = pos + 1 (the sampler's stream position)
+//   decode_advance: ids = tok; hist[row, step % ms] = tok; live rows pos += 1, ctx += 1; then
+//                   (one thread) step += 1
+__global__ void decode_slots_kernel(const int* __restrict__ bt, const int64_t* __restrict__ pos,
+                                    const int* __restrict__ ctx, int64_t* __restrict__ slots,
+                                    int64_t* __restrict__ spos, int B, int max_pages, int page_size) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= B) return;
+  const int64_t p = pos[r];
+  int64_t pg = p / page_size;
+  pg = pg < max_pages - 1 ? pg : max_pages - 1;
+  slots[r] = ctx[r] > 0 ? (int64_t)bt[(int64_t)r * max_pages + pg] * page_size + p % page_size : -1;
+  spos[r] = p + 1;
+}
+
+__global__ void decode_advance_kernel(const int64_t* __restrict__ tok, int64_t* __restrict__ ids,
+                                      int64_t* __restrict__ hist, int64_t* __restrict__ pos, int* __restrict__ ctx,
+                                      int64_t* __restrict__ step, int B, int ms) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < B) {
+    const int64_t t = tok[r];
+    ids[r] = t;
+    hist[(int64_t)r * ms + (int)(step[0] % ms)] = t;
+    if (ctx[r] > 0) {
+      pos[r] += 1;
+      ctx[r] += 1;
+    }
+  }
+  __syncthreads();
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    // every block read step[0] before block 0's thread 0 bumps it: one block covers all rows
+    step[0] += 1;
+  }
+}
+
+int decode_slots(const int* bt, const int64_t* pos, const int* ctx, int64_t* slots, int64_t* spos, int B,
+                 int max_pages, int page_size, hipStream_t stream) {
+  if (B <= 0) return 0;
+  if (B > 1024) return -1;
+  decode_slots_kernel<<<1, 1024, 0, stream>>>(bt, pos, ctx, slots, spos, B, max_pages, page_size);
+  OAMD_LAUNCH_CHECK();
+  return 0;
+}
+
+int decode_advance(const int64_t* tok, int64_t* ids, int64_t* hist, int64_t* pos, int* ctx, int64_t* step, int B,
+                   int ms, hipStream_t stream) {
+  if (B <= 0) return 0;
+  if (B > 1024) return -1;   // one block: every row reads step before it is bumped
+  decode_advance_kernel<<<1, 1024, 0, stream>>>(tok, ids, hist, pos, ctx, step, B, ms);
+  OAMD_LAUNCH_CHECK();
+  return 0;
+}
+
 }  // namespace oamd

@@ -121,6 +121,8 @@ class _BucketState:
         self.seeds = torch.zeros(bp, dtype=torch.long, device=dev)
         self.hist = torch.zeros(bp, eng.multi_step, dtype=torch.long, device=dev)
         self.step = torch.zeros(1, dtype=torch.long, device=dev)
+        self.slots = torch.zeros(bp, dtype=torch.long, device=dev)   # per step: cache slot of each row's token
+        self.spos = torch.zeros(bp, dtype=torch.long, device=dev)    # per step: sampler stream position
 
     def load(self, reqs: list[GenRequest], max_pages: int) -> None:
         """Write the per-row state of ``reqs`` (rows beyond are padding). Built in numpy
@@ -179,18 +181,27 @@ class _DecodeGraph:
     def _run(self) -> None:
         e, st = self.eng, self.st
         P = e.kv.page_size
-        act = st.ctx > 0
-        pg = torch.gather(st.bt, 1, torch.clamp(st.pos // P, max=e.max_pages - 1).unsqueeze(1)).squeeze(1)
-        slots = torch.where(act, pg.to(torch.long) * P + st.pos % P, torch.full_like(st.pos, -1))
+        gpu = st.ids.is_cuda
+        if gpu:   # one bookkeeping kernel before and one after the forward (norm_act.hip)
+            ops.kernels().decode_slots(st.bt, st.pos, st.ctx, st.slots, st.spos, P)
+            slots, spos = st.slots, st.spos
+        else:
+            act = st.ctx > 0
+            pg = torch.gather(st.bt, 1, torch.clamp(st.pos // P, max=e.max_pages - 1).unsqueeze(1)).squeeze(1)
+            slots = torch.where(act, pg.to(torch.long) * P + st.pos % P, torch.full_like(st.pos, -1))
+            spos = st.pos + 1
         fb = ForwardBatch(st.ids, st.pos, slots, False, None, block_tables=st.bt, context_lens=st.ctx,
                           num_splits=self.splits)
         logits = e.model.forward(fb, e.kv)
-        tok = e.model.sample(logits, st.temp, st.seeds, st.pos + 1)
-        st.ids.copy_(tok)
-        st.hist.index_copy_(1, st.step % e.multi_step, tok.unsqueeze(1))   # wrap: a stray replay can never index past hist
-        st.pos.add_(act.to(torch.long))
-        st.ctx.add_(act.to(torch.int32))
-        st.step.add_(1)
+        tok = e.model.sample(logits, st.temp, st.seeds, spos)
+        if gpu:
+            ops.kernels().decode_advance(tok, st.ids, st.hist, st.pos, st.ctx, st.step)
+        else:
+            st.ids.copy_(tok)
+            st.hist.index_copy_(1, st.step % e.multi_step, tok.unsqueeze(1))   # wrap: a stray replay can never index past hist
+            st.pos.add_(act.to(torch.long))
+            st.ctx.add_(act.to(torch.int32))
+            st.step.add_(1)
 
     def capture(self, pool) -> None:
         # warm up on a side stream (allocator + hipBLASLt heuristics), then capture; the

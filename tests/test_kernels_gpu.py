@@ -497,3 +497,29 @@ def test_attn_decode_fused_rope_matches_rope_kv_then_attention(Hq, Hkv, src, fp8
         assert torch.equal(vc1.view(torch.uint8), vc2.view(torch.uint8)), ("V cache", ns)
         torch.testing.assert_close(o2.float(), o1.float(), atol=1e-2, rtol=1e-2)
         assert torch.equal(o2[sl == 0], torch.zeros_like(o2[sl == 0]))
+
+
+def test_decode_step_bookkeeping_kernels_match_torch():
+    """decode_slots / decode_advance (one thread per row) == the torch formulation of a
+    decode step's slot computation and state advance, padding rows (ctx 0) included."""
+    torch.manual_seed(31)
+    B, MP, P, ms = 200, 24, 64, 8
+    bt = torch.randint(0, 5000, (B, MP), dtype=torch.int32, device=DEV)
+    ctx = torch.randint(1, MP * P, (B,), dtype=torch.int32, device=DEV)
+    ctx[::7] = 0
+    pos = (ctx.long() - 1).clamp_min(0)
+    act = ctx > 0
+    pg = torch.gather(bt, 1, torch.clamp(pos // P, max=MP - 1).unsqueeze(1)).squeeze(1)
+    want_slots = torch.where(act, pg.long() * P + pos % P, torch.full_like(pos, -1))
+    slots, spos = torch.empty_like(pos), torch.empty_like(pos)
+    ops.kernels().decode_slots(bt, pos, ctx, slots, spos, P)
+    assert torch.equal(slots, want_slots) and torch.equal(spos, pos + 1)
+    tok = torch.randint(0, 128000, (B,), device=DEV)
+    for step0 in (0, 5, 7, 13):
+        ids, hist = torch.zeros(B, dtype=torch.long, device=DEV), torch.zeros(B, ms, dtype=torch.long, device=DEV)
+        p2, c2, st = pos.clone(), ctx.clone(), torch.tensor([step0], device=DEV)
+        ops.kernels().decode_advance(tok, ids, hist, p2, c2, st)
+        want_hist = torch.zeros_like(hist)
+        want_hist[:, step0 % ms] = tok
+        assert torch.equal(ids, tok) and torch.equal(hist, want_hist)
+        assert torch.equal(p2, pos + act.long()) and torch.equal(c2, ctx + act.int()) and st.item() == step0 + 1
