@@ -221,6 +221,11 @@ class ExplainEngine:
         self.loop = EngineLoop(llm)
         if hasattr(tokenizer, "decode_batch"):
             llm.finish_hook = self._detokenize
+        # byte-level BPE: stream each request's bytes per decode window (exact: checked by
+        # Tokenizer.byte_table), so finishing a wave only UTF-8-decodes 256 buffers
+        self._stream = hasattr(tokenizer, "byte_table") and tokenizer.byte_table() is not None
+        if self._stream:
+            llm.token_hook = self._feed
         self.prompts = PromptBatcher(self.build_prompts)
         self.prompts.start()
         if start_loop:
@@ -249,13 +254,30 @@ class ExplainEngine:
         h.update(bytes(str(ids), "ascii"))
         return h.hexdigest()
 
+    def _feed(self, reqs: list[GenRequest]) -> None:
+        """Engine-loop hook after each decode window: append the window's token bytes."""
+        feed = self.tok.feed
+        for r in reqs:
+            if r.detok is None:
+                r.detok = bytearray()
+            if r.detok_pos < len(r.output):
+                feed(r.detok, r.output[r.detok_pos:])
+                r.detok_pos = len(r.output)
+
     def _detokenize(self, reqs: list[GenRequest]) -> None:
-        """Engine-loop hook: the text of every request a step finished, in one call,
-        before their waiters wake (256 waiters each detokenizing 500 tokens under the
-        GIL held up the hand-off of a finished wave)."""
-        if reqs:
-            for r, t in zip(reqs, self.tok.decode_batch([r.output for r in reqs])):
-                r.text = t
+        """Engine-loop hook: the text of every request a step finished, before their
+        waiters wake (256 waiters each detokenizing 500 tokens under the GIL held up the
+        hand-off of a finished wave): the streamed bytes' UTF-8 text (byte-level BPE) or
+        one decode_batch call."""
+        if not reqs:
+            return
+        if self._stream:
+            self._feed(reqs)
+            for r in reqs:
+                r.text = self.tok.text_of(r.detok)
+            return
+        for r, t in zip(reqs, self.tok.decode_batch([r.output for r in reqs])):
+            r.text = t
 
     def _seed(self, ids: list[int]) -> int:
         return int(hashlib.sha1(bytes(str(ids), "ascii")).hexdigest()[:8], 16)

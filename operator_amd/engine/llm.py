@@ -62,6 +62,8 @@ class GenRequest:
     t_done: float = 0.0
     event: threading.Event = field(default_factory=threading.Event, repr=False)
     text: str | None = None        # detokenized output, filled by LLMEngine.finish_hook when set
+    detok: bytearray | None = None  # streaming detokenization (LLMEngine.token_hook): bytes so far
+    detok_pos: int = 0              # ... of output[:detok_pos]
 
     @property
     def length(self) -> int:
@@ -375,6 +377,10 @@ class LLMEngine:
         # called with the requests a step finished, before their waiters wake (ExplainEngine
         # detokenizes a whole finished batch in one GIL-free call there)
         self.finish_hook = None
+        # called with a decode window's requests once its tokens are appended, while the next
+        # window runs on the GPU (ExplainEngine streams their bytes, so a finished wave's text
+        # is ready without a detokenization pass on the critical path)
+        self.token_hook = None
         self._lock = threading.Lock()
         # Decode windows are pipelined on the GPU: window w+1 is launched before the
         # host reads window w's tokens, so the device never idles on the host's
@@ -727,6 +733,11 @@ class LLMEngine:
                 if (not r.ignore_eos) and int(tk) in self.eos:
                     r.done_pending = True
         self.stats.decode_tokens += win.B * win.k
+        if self.token_hook is not None:
+            try:
+                self.token_hook(win.reqs)
+            except Exception:  # noqa: BLE001 - the finish hook / waiters decode from scratch
+                self.token_hook = None
 
     def _decode(self) -> None:
         """Up to ``multi_step`` decode steps per window with no host round trip in

@@ -178,3 +178,51 @@ class Tokenizer:
         """``decode`` of many sequences in one call (the Rust core runs them in
         parallel without the GIL)."""
         return self.tk.decode_batch([self._keep(x) for x in seqs], skip_special_tokens=self.from_checkpoint)
+
+    # ------------------------------------------------------------------ incremental decoding
+    _bytes = None
+
+    def byte_table(self) -> list[bytes] | None:
+        """id -> the bytes it stands for, when decoding is a plain byte-level BPE (decode(ids)
+        == the UTF-8 ('replace') text of the concatenated bytes of the kept ids); None for any
+        other decoder. Checked once against ``decode`` on random sequences, so streaming
+        detokenization (``feed`` / ``text_of``) is used only where it is exact."""
+        if self._bytes is None:
+            self._bytes = self._build_byte_table() or False
+        return self._bytes or None
+
+    def _build_byte_table(self):
+        bs = list(range(ord("!"), ord("~") + 1)) + list(range(ord("\xa1"), ord("\xac") + 1)) + \
+            list(range(ord("\xae"), ord("\xff") + 1))
+        cs, n = bs[:], 0
+        for b in range(256):
+            if b not in bs:
+                bs.append(b)
+                cs.append(256 + n)
+                n += 1
+        u2b = {chr(c): b for b, c in zip(bs, cs)}
+        table = []
+        for i in range(self.n_vocab):
+            t = self.tk.id_to_token(i)
+            if t is None or any(c not in u2b for c in t):
+                return None
+            table.append(bytes(u2b[c] for c in t))
+        import random
+        rng = random.Random(7)
+        for k in range(64):
+            ids = [rng.randrange(0, self.n_vocab) for _ in range(rng.randrange(1, 300))]
+            if k % 2:   # also ids past the vocabulary, BOS/EOS
+                ids += [self.n_vocab + 5, self.eos_id, self.bos_id, 2 * self.n_vocab + 1]
+            kept = self._keep(ids)
+            if b"".join(table[j] for j in kept).decode("utf-8", "replace") != self.decode(ids):
+                return None
+        return table
+
+    def feed(self, buf: bytearray, ids: list[int]) -> None:
+        """Append the bytes of ``ids`` (the same ids ``decode`` keeps) to ``buf``."""
+        table, n, bos, eos = self._bytes, self.n_vocab, self.bos_id, self.eos_id
+        buf += b"".join([table[i % n] for i in ids if i != bos and i != eos])
+
+    @staticmethod
+    def text_of(buf: bytearray) -> str:
+        return buf.decode("utf-8", "replace")

@@ -214,3 +214,52 @@ def test_several_local_models_routed_by_model_id(tmp_path):
         assert msg.endswith("requested modelId other is mapped to tiny")
     finally:
         svc.close()
+
+
+def test_streaming_detokenization_is_exact_or_off(tmp_path):
+    """Tokenizer.byte_table: a byte-level BPE streams each request's bytes per decode window
+    (LLMEngine.token_hook) and its text equals decode() for any ids (ids past the vocabulary,
+    BOS/EOS, invalid UTF-8 included); a tokenizer whose decoding is not plain byte
+    concatenation (WordLevel joins with spaces) is detected and keeps decode_batch."""
+    import random
+
+    import torch
+
+    from operator_amd.engine.llm import GenRequest, LLMEngine
+    from operator_amd.engine.tokenizer import Tokenizer
+    from operator_amd.models.config import get_config
+    from operator_amd.models.kv_cache import PagedKVCache
+    from operator_amd.models.llama import LlamaModel
+
+    f = tmp_path / "tokenizer.json"
+    _checkpoint_tokenizer(f)
+    assert Tokenizer(100, 0, 1, path=str(f)).byte_table() is None
+    cfg = get_config("tiny")
+    tok = Tokenizer(cfg.vocab_size, cfg.bos_id, cfg.eos_ids[0])
+    assert tok.byte_table() is not None
+    rng = random.Random(3)
+    for _ in range(20):
+        ids = [rng.randrange(0, cfg.vocab_size + 50) for _ in range(rng.randrange(1, 200))]
+        buf = bytearray()
+        for w in range(0, len(ids), 8):
+            tok.feed(buf, ids[w:w + 8])
+        assert tok.text_of(buf) == tok.decode(ids)
+    # through the engine: the per-window hook sees every appended token exactly once
+    m = LlamaModel(cfg, device="cpu", dtype=torch.float32).init_random(seed=2)
+    kv = PagedKVCache(cfg.layers, 64, cfg.kv_heads, cfg.head_dim, 16, device="cpu", dtype=torch.float32)
+    eng = LLMEngine(m, kv, max_batch=4, max_context=256, use_graphs=False, multi_step=4)
+
+    def hook(reqs):
+        for r in reqs:
+            if r.detok is None:
+                r.detok = bytearray()
+            tok.feed(r.detok, r.output[r.detok_pos:])
+            r.detok_pos = len(r.output)
+
+    eng.token_hook = hook
+    reqs = [GenRequest(list(range(3, 20 + 7 * i)), max_tokens=13 + i, temperature=0.7, seed=i, ignore_eos=True)
+            for i in range(3)]
+    eng.generate(reqs)
+    for r in reqs:
+        hook([r])
+        assert tok.text_of(r.detok) == tok.decode(r.output)
