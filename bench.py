@@ -290,6 +290,9 @@ def main() -> int:
             return {"prefill_tokens": st.prefill_tokens, "decode_tokens": st.decode_tokens,
                     "prefill_graph_replays": st.prefill_graph_replays, "use_graphs": bool(llm.use_graphs),
                     "prefill_padded_tokens": st.prefill_padded_tokens, "prefill_eager": st.prefill_eager,
+                    "decode_launch_s": st.decode_launch_s, "decode_wait_s": st.decode_wait_s,
+                    "decode_windows": st.decode_windows, "decode_windows_ahead": st.decode_windows_ahead,
+                    "no_pipeline": dict(st.no_pipeline),
                     "prefill_graph_buckets": sorted(getattr(llm, "_prefill_g", {})),
                     "dfa_states": getattr(meng, "dfa_states", None)}
         ws = pool.worker_stats()
@@ -548,6 +551,12 @@ def main() -> int:
                    "prefill_graph_buckets": stats1["prefill_graph_buckets"],
                    "prefill_padded_tokens": stats1.get("prefill_padded_tokens", 0) - stats0.get("prefill_padded_tokens", 0),
                    "prefill_eager_batches": stats1.get("prefill_eager", 0) - stats0.get("prefill_eager", 0),
+                   # host seconds inside decode graph launches (blocked = GPU queue full) / waiting on windows
+                   "decode_launch_s": round(stats1.get("decode_launch_s", 0) - stats0.get("decode_launch_s", 0), 2),
+                   "decode_wait_s": round(stats1.get("decode_wait_s", 0) - stats0.get("decode_wait_s", 0), 2),
+                   "decode_windows": stats1.get("decode_windows", 0) - stats0.get("decode_windows", 0),
+                   "decode_windows_ahead": stats1.get("decode_windows_ahead", 0) - stats0.get("decode_windows_ahead", 0),
+                   "no_pipeline": stats1.get("no_pipeline", {}),
                    "decode_tok_s_per_gpu": round(dtoks / elapsed, 1), "outcomes": counter["outcomes"],
                    "dfa_states": stats1["dfa_states"], "timed_monotonic_ns": [mono0, mono1],
                    "rccl_world": dist.get_world_size() if dist.is_initialized() else 1,

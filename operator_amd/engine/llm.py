@@ -81,6 +81,11 @@ class EngineStats:
     prefill_graph_replays: int = 0
     prefill_padded_tokens: int = 0   # bucket padding computed by prefill-graph replays
     prefill_eager: int = 0           # prefill batches no graph bucket fit (<= 15 % padding)
+    decode_launch_s: float = 0.0     # host time inside decode-window graph launches (a launch that
+    decode_wait_s: float = 0.0       # ... blocks means the GPU queue is full) / waiting for windows
+    decode_windows: int = 0          # decode windows launched
+    decode_windows_ahead: int = 0    # ... of them queued behind the previous one (pipelined)
+    no_pipeline: dict = field(default_factory=dict)   # why a window was not queued ahead
 
 
 @dataclass
@@ -704,7 +709,9 @@ class LLMEngine:
                 # kernels from the launching thread, and Python-level replays beside
                 # GIL-holding operator threads measured 2.2x slower per step
                 # (tools/bench_graph_contention.py)
+                t_l = time.perf_counter()
                 _launch_graph(g.graph, k, self.device)
+                self.stats.decode_launch_s += time.perf_counter() - t_l
             else:
                 for _ in range(k):
                     g.run(False)
@@ -717,11 +724,14 @@ class LLMEngine:
         else:
             host, ev = st.hist, None
         self.stats.graph_replays += k if self.use_graphs else 0
+        self.stats.decode_windows += 1
         return _Window(st, reqs, B, k, host, ev)
 
     def _consume(self, win: _Window) -> None:
         if win.event is not None:
+            t_w = time.perf_counter()
             win.event.synchronize()
+            self.stats.decode_wait_s += time.perf_counter() - t_w
         toks = win.host[:win.B, :win.k].tolist()
         for r, row in zip(win.reqs, toks):
             if r.done:   # finished (EOS / cancel) in an earlier window: discard
@@ -748,10 +758,14 @@ class LLMEngine:
         self._inflight = None
         nxt = None
         same = len(prev.reqs) == len(self.running) and all(a is b for a, b in zip(prev.reqs, self.running))
-        if (self.pipeline and same and self._active is prev.st
-                and not self._admittable()
-                and all(r.max_tokens - len(r.output) - prev.k >= 1 for r in prev.reqs)):
+        why = ("off" if not self.pipeline else "composition" if not same else "state" if self._active is not prev.st
+               else "admit" if self._admittable()
+               else "tail" if not all(r.max_tokens - len(r.output) - prev.k >= 1 for r in prev.reqs) else None)
+        if why is None:
             nxt = self._launch(ahead=prev.k)
+            self.stats.decode_windows_ahead += 1
+        else:
+            self.stats.no_pipeline[why] = self.stats.no_pipeline.get(why, 0) + 1
         self._consume(prev)
         self._inflight = nxt
         self.stats.decode_s += time.perf_counter() - t0
