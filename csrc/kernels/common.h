@@ -84,18 +84,31 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return base + orig / nx;
 }
 
-// Counter-based RNG (squares-style mix of a 64-bit counter), used for Gumbel
-// sampling so a captured graph replays deterministic per (seed, step, row, col).
-__device__ __forceinline__ uint32_t hash_u32(uint64_t x) {
+// Counter-based RNG for Gumbel sampling, so a captured graph replays deterministic
+// per (seed, step, row, col). The 64-bit finalizer runs once per row and yields two
+// 32-bit keys; the per-column hash is a 32-bit two-round mix with the second key
+// injected between the rounds (8 VALU ops per column instead of the ~20 of a 64-bit
+// mix: the sampler's vocab loop is ALU-bound). Host mirror: ops/reference.py.
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
   x ^= x >> 33; x *= 0xff51afd7ed558ccdULL;
   x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL;
   x ^= x >> 33;
-  return static_cast<uint32_t>(x);
+  return x;
 }
 
-__device__ __forceinline__ float uniform01(uint64_t x) {
-  // (0,1): never exactly 0 so -log(-log(u)) stays finite.
-  return (static_cast<float>(hash_u32(x) >> 8) + 0.5f) * (1.0f / 16777216.0f);
+__device__ __forceinline__ uint32_t hash_col(uint32_t c, uint32_t k1, uint32_t k2) {
+  uint32_t h = c ^ k1;
+  h ^= h >> 16; h *= 0x7feb352du;
+  h ^= h >> 15; h ^= k2; h *= 0x846ca68bu;
+  h ^= h >> 16;
+  return h;
+}
+
+// Open (0,1) with 23 bits: both ends are exact floats (max 1 - 2^-24), so -log(-log(u))
+// stays finite. (24 bits + 0.5 rounded the top value to exactly 1.0f, whose Gumbel
+// noise is +inf: a column that won regardless of its logit.)
+__device__ __forceinline__ float uniform01(uint32_t h) {
+  return (static_cast<float>(h >> 9) + 0.5f) * (1.0f / 8388608.0f);
 }
 
 }  // namespace oamd

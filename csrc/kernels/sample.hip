@@ -34,15 +34,22 @@ __global__ void __launch_bounds__(1024) sample_kernel(const T* __restrict__ logi
   const T* lr = logits + row * stride;
   const float temp = temperature[row];
   const bool greedy = !(temp > 0.f);
-  const float inv_t = greedy ? 1.f : 1.f / temp;
-  const uint64_t key = (static_cast<uint64_t>(seeds[row]) * 0x9E3779B97F4A7C15ULL) ^
-                       (static_cast<uint64_t>(positions[row]) << 32);
+  // Perturbed values are compared in base 2: x/T - ln(-ln u) = ln2 * (x log2e / T -
+  // log2(-log2 u)) - ln(ln2), a monotone map, so the loop pays one FMA and two v_log_f32
+  // per column and the winner is mapped back once (out_val stays in natural units).
+  constexpr float kLog2e = 1.4426950408889634f, kLn2 = 0.6931471805599453f, kNegLnLn2 = 0.36651292058166435f;
+  const float inv_t = greedy ? 1.f : kLog2e / temp;
+  const uint64_t key = mix64((static_cast<uint64_t>(seeds[row]) * 0x9E3779B97F4A7C15ULL) ^
+                             (static_cast<uint64_t>(positions[row]) << 32));
+  const uint32_t k1 = static_cast<uint32_t>(key), k2 = static_cast<uint32_t>(key >> 32);
+  const uint32_t c0 = static_cast<uint32_t>(col_offset);
   float bv = -INFINITY;
   int bi = 0x7fffffff;
   auto visit = [&](float x, int i) {
     if (!greedy) {
-      const float u = uniform01(key + static_cast<uint64_t>(i + col_offset));
-      x = x * inv_t - __logf(-__logf(u));
+      const float u = uniform01(hash_col(c0 + static_cast<uint32_t>(i), k1, k2));
+      // -log2(u) >= 8.6e-8 exactly; the clamp only guards a hardware log rounding to 0
+      x = x * inv_t - __builtin_amdgcn_logf(fmaxf(-__builtin_amdgcn_logf(u), 5.9604645e-8f));
     }
     argmax_merge(bv, bi, x, i);
   };
@@ -51,8 +58,7 @@ __global__ void __launch_bounds__(1024) sample_kernel(const T* __restrict__ logi
   // does not change the result.
   constexpr int VEC = 16 / static_cast<int>(sizeof(T));
   const int nv = (reinterpret_cast<uintptr_t>(lr) & 15) == 0 ? vocab / VEC : 0;
-  for (int v = threadIdx.x; v < nv; v += blockDim.x) {
-    const uint4 raw = reinterpret_cast<const uint4*>(lr)[v];
+  auto visit16 = [&](const uint4& raw, int v) {
     const uint32_t wv[4] = {raw.x, raw.y, raw.z, raw.w};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -63,7 +69,22 @@ __global__ void __launch_bounds__(1024) sample_kernel(const T* __restrict__ logi
         visit(__uint_as_float(wv[k]), VEC * v + k);
       }
     }
+  };
+  // UNR row vectors per thread requested before any is consumed: one dependent HBM round
+  // trip per UNR vectors instead of per vector (the loop was latency-bound: ~16 trips
+  // of 16 B per thread for a 128k vocab row)
+  constexpr int UNR = 4;
+  const uint4* lv = reinterpret_cast<const uint4*>(lr);
+  const int step = blockDim.x;
+  int v0 = threadIdx.x;
+  for (; v0 + (UNR - 1) * step < nv; v0 += UNR * step) {
+    uint4 raw[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) raw[u] = lv[v0 + u * step];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) visit16(raw[u], v0 + u * step);
   }
+  for (int v = v0; v < nv; v += step) visit16(lv[v], v);
   for (int i = nv * VEC + threadIdx.x; i < vocab; i += blockDim.x) visit(load_logit<T>(lr, i), i);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -79,7 +100,7 @@ __global__ void __launch_bounds__(1024) sample_kernel(const T* __restrict__ logi
     int id = si[0];
     for (int j = 1; j < (int)(blockDim.x >> 6); ++j) argmax_merge(v, id, sv[j], si[j]);
     out_tokens[row] = ((id == 0x7fffffff) ? 0 : id) + col_offset;
-    if (out_val) out_val[row] = v;
+    if (out_val) out_val[row] = greedy ? v : v * kLn2 + kNegLnLn2;
   }
 }
 

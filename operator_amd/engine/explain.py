@@ -19,6 +19,7 @@ loop thread that owns the GPU (LLMEngine.step).
 from __future__ import annotations
 
 import hashlib
+import os
 import sys
 import threading
 import time
@@ -162,7 +163,10 @@ class PromptBatcher(threading.Thread):
     thread that launches the GPU work. Callers instead enqueue and wait; this
     thread takes everything queued (after ``wait_s`` for stragglers) and
     tokenizes it with ``render_bounded_batch`` (Rust ``encode_batch``, GIL
-    released, parallel)."""
+    released, parallel). ``build_many`` returns each caller's result, or an exception
+    for that caller alone; ExplainEngine's also submits the batch's requests to the
+    engine here, so a burst reaches the engine in whole batches instead of one
+    request per waiter thread as each wakes (~20 ms of a wave's start under the GIL)."""
 
     def __init__(self, build_many, wait_s: float = 0.002, max_batch: int = 32):
         super().__init__(name="prompt-batcher", daemon=True)
@@ -172,12 +176,15 @@ class PromptBatcher(threading.Thread):
         self.q: _queue.Queue = _queue.Queue()
         self._empty = _queue.Empty
 
-    def build(self, result: AnalysisResult, cfg: AIProviderConfig) -> list[int]:
+    def build(self, result: AnalysisResult, cfg: AIProviderConfig):
         from concurrent.futures import Future
 
         f: Future = Future()
         self.q.put((result, cfg, f))
-        return f.result()
+        r = f.result()
+        if isinstance(r, BaseException):
+            raise r
+        return r
 
     def stop(self) -> None:
         self.q.put(None)
@@ -226,7 +233,10 @@ class ExplainEngine:
         self._stream = hasattr(tokenizer, "byte_table") and tokenizer.byte_table() is not None
         if self._stream:
             llm.token_hook = self._feed
-        self.prompts = PromptBatcher(self.build_prompts)
+        # OAMD_BATCH_ADMIT=0: the batcher only tokenizes and each caller submits its own
+        # request (the previous hand-off, kept for A/B measurements)
+        self._batch_admit = os.environ.get("OAMD_BATCH_ADMIT", "1") != "0"
+        self.prompts = PromptBatcher(self._batch_build)
         self.prompts.start()
         if start_loop:
             self.loop.start()
@@ -282,34 +292,56 @@ class ExplainEngine:
     def _seed(self, ids: list[int]) -> int:
         return int(hashlib.sha1(bytes(str(ids), "ascii")).hexdigest()[:8], 16)
 
-    def _start(self, p: _Pending, ids: list[int]) -> None:
+    def _start(self, p: _Pending, ids: list[int], notify: bool = True) -> None:
         cfg = p.cfg
         p.req = GenRequest(ids, max_tokens=max(1, int(cfg.max_tokens)), temperature=float(cfg.temperature),
                            seed=self._seed(ids) + p.attempt, ignore_eos=self.ignore_eos)
         self.llm.submit(p.req)
+        if notify:
+            self.loop.notify()
+
+    def _batch_build(self, items: list[tuple[AnalysisResult, AIProviderConfig]]) -> list:
+        ids = self.build_prompts(items)
+        return self._admit_many(items, ids) if self._batch_admit else ids
+
+    def _admit_many(self, items: list[tuple[AnalysisResult, AIProviderConfig]],
+                    prompts: list[list[int]]) -> list[_Pending | AIResponse | BaseException]:
+        """Cache lookups and engine submission for a batch of built prompts, one engine
+        wake-up for the batch; an item's own failure (e.g. a prompt the engine cannot
+        hold) is returned in its slot."""
+        out: list[_Pending | AIResponse | BaseException] = []
+        for (res, cfg), ids in zip(items, prompts):
+            try:
+                key = self._key(ids, cfg) if cfg.caching_enabled else None
+                if key is not None:
+                    with self._lock:
+                        hit = self._cache.get(key)
+                        if hit is not None:
+                            self._cache.move_to_end(key)
+                            out.append(hit.model_copy(update={"cached": True}))
+                            continue
+                p = _Pending(None, key, cfg, time.perf_counter())  # type: ignore[arg-type]
+                p.ids = ids  # type: ignore[attr-defined]
+                self._start(p, ids, notify=False)
+                out.append(p)
+            except Exception as e:  # noqa: BLE001 - delivered to this item's caller
+                out.append(e)
         self.loop.notify()
+        return out
 
     # ------------------------------------------------------------------ API
     def explain_many(self, items: list[tuple[AnalysisResult, AIProviderConfig]]) -> list[AIResponse | ExplainError]:
-        """Explain a batch concurrently (continuous batching); per-item errors are returned, not raised."""
-        pend: list[_Pending | AIResponse | ExplainError] = []
+        """Explain a batch concurrently (continuous batching); per-item errors are returned, not raised
+        (except a failure to admit a single coalesced item, raised as before)."""
         if len(items) == 1 and self.prompts.is_alive():   # one caller of many: coalesced with the others
-            prompts = [self.prompts.build(*items[0])]
+            pend = [self.prompts.build(*items[0])]
+            if not self._batch_admit:
+                pend = self._admit_many(items, pend)
         else:
-            prompts = self.build_prompts(items)
-        for (res, cfg), ids in zip(items, prompts):
-            key = self._key(ids, cfg) if cfg.caching_enabled else None
-            if key is not None:
-                with self._lock:
-                    hit = self._cache.get(key)
-                    if hit is not None:
-                        self._cache.move_to_end(key)
-                        pend.append(hit.model_copy(update={"cached": True}))
-                        continue
-            p = _Pending(None, key, cfg, time.perf_counter())  # type: ignore[arg-type]
-            p.ids = ids  # type: ignore[attr-defined]
-            self._start(p, ids)
-            pend.append(p)
+            pend = self._admit_many(items, self.build_prompts(items))
+        for x in pend:
+            if isinstance(x, BaseException):
+                raise x
         out: list[AIResponse | ExplainError] = []
         for p in pend:
             if not isinstance(p, _Pending):

@@ -191,20 +191,27 @@ def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, b
 
 
 def gumbel_noise_ref(seed: int, position: int, vocab: int, col_offset: int = 0) -> torch.Tensor:
-    """Host mirror of the device counter hash (common.h hash_u32/uniform01), vectorised."""
+    """Host mirror of the device counter hash (common.h mix64 / hash_col / uniform01), vectorised."""
     import numpy as np
 
     M = (1 << 64) - 1
-    key = ((seed * 0x9E3779B97F4A7C15) & M) ^ ((position << 32) & M)
+    k = ((seed * 0x9E3779B97F4A7C15) & M) ^ ((position << 32) & M)
+    k ^= k >> 33
+    k = (k * 0xFF51AFD7ED558CCD) & M
+    k ^= k >> 33
+    k = (k * 0xC4CEB9FE1A85EC53) & M
+    k ^= k >> 33
+    k1, k2 = np.uint32(k & 0xFFFFFFFF), np.uint32(k >> 32)
     with np.errstate(over="ignore"):
-        x = (np.arange(vocab, dtype=np.uint64) + np.uint64((key + col_offset) & M))
-        x ^= x >> np.uint64(33)
-        x *= np.uint64(0xFF51AFD7ED558CCD)
-        x ^= x >> np.uint64(33)
-        x *= np.uint64(0xC4CEB9FE1A85EC53)
-        x ^= x >> np.uint64(33)
-    u = ((x & np.uint64(0xFFFFFFFF)) >> np.uint64(8)).astype(np.float64) + 0.5
-    u = torch.from_numpy(u / 16777216.0)
+        h = (np.arange(vocab, dtype=np.uint64) + np.uint64(col_offset & 0xFFFFFFFF)).astype(np.uint32) ^ k1
+        h ^= h >> np.uint32(16)
+        h *= np.uint32(0x7FEB352D)
+        h ^= h >> np.uint32(15)
+        h ^= k2
+        h *= np.uint32(0x846CA68B)
+        h ^= h >> np.uint32(16)
+    u = (h >> np.uint32(9)).astype(np.float64) + 0.5
+    u = torch.from_numpy(u / 8388608.0)
     return -torch.log(-torch.log(u))
 
 

@@ -148,6 +148,29 @@ def test_sample(dtype):
     assert torch.equal(ops.sample(logits, temp, seeds, pos).cpu(), tok)
 
 
+def test_sample_distribution():
+    """Token frequencies over many seeds match softmax(x / T) (the Gumbel-max identity),
+    and a vocab-sized row never yields a token whose noise overflowed (u rounding to 1)."""
+    torch.manual_seed(6)
+    V, R, T = 32, 32768, 0.7
+    row = torch.randn(V) * 1.5
+    logits = row.expand(R, V).contiguous().to(DEV)
+    temp = torch.full((R,), T, device=DEV)
+    seeds = torch.arange(R, device=DEV) * 2654435761 % (1 << 40)
+    pos = torch.full((R,), 17, device=DEV, dtype=torch.long)
+    tok = ops.sample(logits, temp, seeds, pos).cpu()
+    freq = torch.bincount(tok, minlength=V).double() / R
+    p = torch.softmax(row.double() / T, 0)
+    assert (freq - p).abs().max().item() < 4 * (p * (1 - p) / R).sqrt().max().item() + 1e-3
+    # 128k-vocab rows with one dominant logit: the noise is bounded (max ~17 nats), so a
+    # 40-nat lead always wins; an infinite noise value would hand the row to another column
+    big = torch.zeros(64, 128256, device=DEV, dtype=torch.bfloat16)
+    big[:, 1234] = 40.0
+    out = ops.sample(big, torch.ones(64, device=DEV), torch.arange(64, device=DEV) + 99,
+                     torch.arange(64, device=DEV)).cpu()
+    assert (out == 1234).all()
+
+
 @pytest.mark.parametrize("M", [64, 128, 192, 256])
 @pytest.mark.parametrize("N,K", [(256, 512), (640, 2048), (128, 4096)])
 def test_gemm_decode(M, N, K):
