@@ -83,15 +83,23 @@ __global__ void __launch_bounds__(NT) rmsnorm_kernel(
       }
     }
   }
+  // the weight vectors are requested before the block reduction, so their round trip
+  // overlaps the barrier instead of following it
+  const u16x8* wr = reinterpret_cast<const u16x8*>(w);
+  u16x8 wpre[MAXV];
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int vi = threadIdx.x + i * NT;
+    if (vi < nvec) wpre[i] = wr[vi];
+  }
   const float tot = block_sum<NT>(ss, scratch);
   const float rs = rsqrtf(tot / static_cast<float>(hidden) + eps);
-  const u16x8* wr = reinterpret_cast<const u16x8*>(w);
   u16x8* yr = reinterpret_cast<u16x8*>(y + row * y_stride);
 #pragma unroll
   for (int i = 0; i < MAXV; ++i) {
     const int vi = threadIdx.x + i * NT;
     if (vi < nvec) {
-      u16x8 wv = wr[vi];
+      const u16x8 wv = wpre[i];
       u16x8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {

@@ -48,7 +48,9 @@ struct CacheStore<uint8_t> {
   }
 };
 
-template <int D, typename KV>
+// SC: compile-time split-K slab count (0: runtime S), so all S slab loads of a group
+// are issued before the first add (a runtime-trip-count loop waited for each in turn).
+template <int D, typename KV, int SC>
 __global__ void __launch_bounds__(kRopeItems) rope_kv_kernel(
     const bf16_t* __restrict__ qkv, int64_t qkv_stride, const int64_t* __restrict__ pos,
     const float* __restrict__ cos_t, const float* __restrict__ sin_t, int Hq, int Hkv,
@@ -71,9 +73,23 @@ __global__ void __launch_bounds__(kRopeItems) rope_kv_kernel(
       const float* pr = xp + (int64_t)t * ncol + col;
       lo = *reinterpret_cast<const f32x4*>(pr);
       hi = *reinterpret_cast<const f32x4*>(pr + 4);
-      for (int sp = 1; sp < S; ++sp) {
-        lo += *reinterpret_cast<const f32x4*>(pr + sp * slab);
-        hi += *reinterpret_cast<const f32x4*>(pr + sp * slab + 4);
+      if constexpr (SC > 1) {
+        f32x4 pl[SC - 1], ph[SC - 1];
+#pragma unroll
+        for (int sp = 1; sp < SC; ++sp) {
+          pl[sp - 1] = *reinterpret_cast<const f32x4*>(pr + sp * slab);
+          ph[sp - 1] = *reinterpret_cast<const f32x4*>(pr + sp * slab + 4);
+        }
+#pragma unroll
+        for (int sp = 1; sp < SC; ++sp) {
+          lo += pl[sp - 1];
+          hi += ph[sp - 1];
+        }
+      } else if constexpr (SC == 0) {
+        for (int sp = 1; sp < S; ++sp) {
+          lo += *reinterpret_cast<const f32x4*>(pr + sp * slab);
+          hi += *reinterpret_cast<const f32x4*>(pr + sp * slab + 4);
+        }
       }
     } else {
       const u16x8 r = *reinterpret_cast<const u16x8*>(row + col);
@@ -175,14 +191,26 @@ int rope_kv(const bf16_t* qkv, int64_t qkv_stride, const int64_t* pos, const flo
   const int64_t slab = (int64_t)tokens * (Hq + 2 * Hkv) * head_dim;
   const int items = (Hq + Hkv) * (head_dim / 16) + Hkv * (head_dim / 8);
   const dim3 grid(tokens, (items + kRopeItems - 1) / kRopeItems);
-  if (fp8_cache)
-    rope_kv_kernel<128, uint8_t><<<grid, kRopeItems, 0, stream>>>(
-        qkv, qkv_stride, pos, cos_t, sin_t, Hq, Hkv, q_out, k_out, v_out, static_cast<uint8_t*>(k_cache),
-        static_cast<uint8_t*>(v_cache), slots, page_size, max_pos, xp, S, slab, bias, 1.f / k_scale, 1.f / v_scale);
-  else
-    rope_kv_kernel<128, bf16_t><<<grid, kRopeItems, 0, stream>>>(
-        qkv, qkv_stride, pos, cos_t, sin_t, Hq, Hkv, q_out, k_out, v_out, static_cast<bf16_t*>(k_cache),
-        static_cast<bf16_t*>(v_cache), slots, page_size, max_pos, xp, S, slab, bias, 1.f, 1.f);
+  const int sc = xp == nullptr ? 1 : S;
+#define OAMD_ROPE(KVT, SCC, KI, VI)                                                                              \
+  rope_kv_kernel<128, KVT, SCC><<<grid, kRopeItems, 0, stream>>>(                                               \
+      qkv, qkv_stride, pos, cos_t, sin_t, Hq, Hkv, q_out, k_out, v_out, static_cast<KVT*>(k_cache),            \
+      static_cast<KVT*>(v_cache), slots, page_size, max_pos, xp, S, slab, bias, KI, VI)
+#define OAMD_ROPE_S(KVT, KI, VI)                   \
+  switch (sc) {                                    \
+    case 1: OAMD_ROPE(KVT, 1, KI, VI); break;      \
+    case 2: OAMD_ROPE(KVT, 2, KI, VI); break;      \
+    case 4: OAMD_ROPE(KVT, 4, KI, VI); break;      \
+    case 8: OAMD_ROPE(KVT, 8, KI, VI); break;      \
+    default: OAMD_ROPE(KVT, 0, KI, VI); break;     \
+  }
+  if (fp8_cache) {
+    OAMD_ROPE_S(uint8_t, 1.f / k_scale, 1.f / v_scale)
+  } else {
+    OAMD_ROPE_S(bf16_t, 1.f, 1.f)
+  }
+#undef OAMD_ROPE_S
+#undef OAMD_ROPE
   OAMD_LAUNCH_CHECK();
   return 0;
 }
