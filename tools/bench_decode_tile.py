@@ -18,7 +18,7 @@ import torch  # noqa: E402
 from operator_amd import ops  # noqa: E402
 
 SHAPES = [("gate_up+silu", 28672, 4096, True), ("qkv", 6144, 4096, False), ("o", 4096, 4096, False),
-          ("down", 4096, 14336, False)]
+          ("down", 4096, 14336, False), ("lm_head", 128256, 4096, False)]
 
 
 def timeit(fn, iters):
@@ -39,32 +39,36 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--tile", action="store_true", help="also time gemm_tile split-K")
+    ap.add_argument("--shapes", default="gate_up+silu,qkv,o,down", help="comma list (lm_head: the vocab projection)")
     a = ap.parse_args()
     C = ops.kernels()
     for M in [int(x) for x in a.m.split(",")]:
         for name, N, K, silu in SHAPES:
+            if name not in a.shapes.split(","):
+                continue
             torch.manual_seed(0)
             x = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)
-            ws = [((torch.rand(N, K, device="cuda") * 2 - 1) * 0.05).to(torch.bfloat16) for _ in range(4)]
+            nw = 2 if N * K > (1 << 28) else 4   # rotating weight copies (the vocab projection is 1 GB each)
+            ws = [((torch.rand(N, K, device="cuda") * 2 - 1) * 0.05).to(torch.bfloat16) for _ in range(nw)]
             y = torch.empty(M, N // 2 if silu else N, dtype=torch.bfloat16, device="cuda")
-            P = torch.empty(16 * M * N, dtype=torch.float32, device="cuda")
+            P = torch.empty((4 if N > 65536 else 16) * M * N, dtype=torch.float32, device="cuda")
             it = {"i": 0}
 
             def cur():
-                w = ws[it["i"] % 4]
+                w = ws[it["i"] % len(ws)]
                 it["i"] += 1
                 return ops.gate_up_silu(x, w, 64) if silu else ops.linear(x, w)
 
             def tile(S):
                 def f():
-                    w = ws[it["i"] % 4]
+                    w = ws[it["i"] % len(ws)]
                     it["i"] += 1
                     C.gemm_tile(x, w, y, None, silu, 0, S, P if S > 1 else None)
                 return f
 
             def pp(S, bm, nt, one=False):
                 def f():
-                    w = ws[it["i"] % 4]
+                    w = ws[it["i"] % len(ws)]
                     it["i"] += 1
                     C.gemm_pp(x, w, y, P if S > 1 else None, S, bm, silu, nt, one)
                 return f
@@ -72,10 +76,10 @@ def main():
             cands = {"decode": cur}
             if a.tile:
                 for S in (1, 2, 4, 8, 16):
-                    if K % (64 * S) == 0:
+                    if K % (64 * S) == 0 and S * M * N <= P.numel():
                         cands[f"tile_s{S}"] = tile(S)
             for bm in ((128, 256) if M > 128 else (128,)):
-                for S in ((1,) if silu else (1, 2, 4, 8)):
+                for S in ((1,) if silu else (1, 2) if N > 65536 else (1, 2, 4, 8)):
                     if K % (64 * S) == 0:
                         for nt in (True, False):
                             cands[f"pp_bm{bm}_s{S}{'_nt' if nt else ''}"] = pp(S, bm, nt)
@@ -90,7 +94,7 @@ def main():
             ref = cur()
             errs = {}
             for S in ((1,) if silu else (1, 4)):
-                C.gemm_pp(x, ws[(it["i"] - 1) % 4], y, P if S > 1 else None, S, 128, silu, True)
+                C.gemm_pp(x, ws[(it["i"] - 1) % len(ws)], y, P if S > 1 else None, S, 128, silu, True)
                 errs[f"pp_s{S}"] = round((y.float() - ref.float()).abs().max().item(), 4)
             best = min(med, key=med.get)
             wb = N * K * 2
