@@ -13,8 +13,9 @@ from operator_amd import ops  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--batch", type=int, default=256)
 ap.add_argument("--vocab", type=int, default=128256)
+ap.add_argument("--scale", type=float, default=1.0, help="logit std (a trained model's rows are peaked: larger)")
 a = ap.parse_args()
-x = torch.randn(a.batch, a.vocab, device="cuda").to(torch.bfloat16)
+x = (torch.randn(a.batch, a.vocab, device="cuda") * a.scale).to(torch.bfloat16)
 t = torch.full((a.batch,), 0.3, device="cuda")
 sd = torch.arange(a.batch, device="cuda")
 ps = torch.arange(a.batch, device="cuda")
@@ -29,5 +30,5 @@ for _ in range(n):
 e1.record()
 torch.cuda.synchronize()
 us = e0.elapsed_time(e1) / n * 1e3
-print(json.dumps({"bench": "sample", "batch": a.batch, "vocab": a.vocab, "us": round(us, 1),
+print(json.dumps({"bench": "sample", "batch": a.batch, "vocab": a.vocab, "scale": a.scale, "us": round(us, 1),
                   "GBps": round(x.numel() * 2 / us / 1e3, 1)}))
