@@ -339,11 +339,16 @@ class ExplainEngine:
                 pend = self._admit_many(items, pend)
         else:
             pend = self._admit_many(items, self.build_prompts(items))
-        for x in pend:
-            if isinstance(x, BaseException):
-                raise x
+        if len(pend) == 1 and isinstance(pend[0], BaseException):
+            raise pend[0]
+        # several items: the ones admitted are already generating, so a failed admission is
+        # that item's ExplainError and every other item is still waited for (raising here
+        # would leave their requests decoding to max_tokens with no waiter)
         out: list[AIResponse | ExplainError] = []
         for p in pend:
+            if isinstance(p, BaseException):
+                out.append(p if isinstance(p, ExplainError) else ExplainError(str(p) or type(p).__name__))
+                continue
             if not isinstance(p, _Pending):
                 out.append(p)
                 continue

@@ -331,12 +331,16 @@ class EnginePool:
 
     # ---------------------------------------------------------------- lifecycle
     def _spawn(self, w: _Worker) -> None:
-        if self.log_arena_bytes and w.arena is None:
-            w.arena = _LogArena(self.log_arena_bytes)
-        if w.arena is not None:
-            w.arena.reset()
-        w.inq = self._ctx.Queue()
-        w.ready, w.alive, w.last_beat = False, True, time.time()
+        # under the pool lock: _handle may still release() a late reply of the killed
+        # process into this arena and _dispatch put() into it as soon as alive is set,
+        # so the ring reset and the alive/ready transition must not interleave with either
+        with self._lock:
+            if self.log_arena_bytes and w.arena is None:
+                w.arena = _LogArena(self.log_arena_bytes)
+            if w.arena is not None:
+                w.arena.reset()
+            w.inq = self._ctx.Queue()
+            w.ready, w.alive, w.last_beat = False, True, time.time()
         world = 1 + len(w.follower_devices)
         port = _free_port() if world > 1 else 0
         settings = self.settings.model_dump()

@@ -201,8 +201,17 @@ class Tokenizer:
                 cs.append(256 + n)
                 n += 1
         u2b = {chr(c): b for b, c in zip(bs, cs)}
+        # added tokens are decoded as their literal content, not through the byte-level
+        # alphabet; special ones (a checkpoint's 256 Llama-3 <|...|> ids) are dropped by
+        # decode(skip_special_tokens=True), so they stand for no bytes at all
+        added = {}
+        for i, at in self.tk.get_added_tokens_decoder().items():
+            added[i] = b"" if (at.special and self.from_checkpoint) else at.content.encode("utf-8")
         table = []
         for i in range(self.n_vocab):
+            if i in added:
+                table.append(added[i])
+                continue
             t = self.tk.id_to_token(i)
             if t is None or any(c not in u2b for c in t):
                 return None

@@ -9,9 +9,9 @@ file is read by the OS's page cache straight into the device tensors
 (``safe_open(device=...)``), no pickle, nothing executed from the file.
 
 The file name carries a key over everything that shapes the shard: architecture,
-TP rank / world, compute dtype, weight dtype, gate|up interleave and the source
-(HF files' sizes + mtimes, or the random-init seed), so a stale shard is never
-loaded. Writes go to a temporary name and are renamed into place (a crash mid-write
+TP rank / world, compute dtype, weight dtype, gate|up interleave, the source
+(HF files' sizes + mtimes, or the random-init seed) and the source text of the
+code that builds the layout (``layout_version``), so a stale shard is never loaded. Writes go to a temporary name and are renamed into place (a crash mid-write
 leaves no half file under the real name).
 """
 from __future__ import annotations
@@ -44,8 +44,27 @@ def source_id(model_path: str | None, seed: int) -> str:
     return "hf:" + os.path.abspath(model_path) + ":" + ",".join(parts)
 
 
+# the code that lays a shard out: TP slicing, QKV packing, gate|up interleave, fp8 scale
+# rounding, the random init. Its source text is part of the key, so an edit to any of it
+# misses every cache file written before the edit instead of mapping a stale layout back.
+LAYOUT_FUNCS = ("init_random", "_randn", "_quantize_layer", "_shard_layer", "split_gate_up", "load_hf")
+
+
+def layout_version(model_cls=None) -> str:
+    import inspect
+
+    from operator_amd import ops
+
+    if model_cls is None:
+        from .llama import LlamaModel as model_cls
+    src = "".join(inspect.getsource(getattr(model_cls, f)) for f in LAYOUT_FUNCS)
+    src += inspect.getsource(ops.interleave_gate_up) + inspect.getsource(ops.quantize_fp8)
+    return hashlib.sha256(src.encode()).hexdigest()[:16]
+
+
 def cache_path(cache_dir: str, model, source: str) -> str:
-    blob = json.dumps({"format": FORMAT, "cfg": dataclasses.asdict(model.cfg), "tp": [model.tp.rank, model.tp.world],
+    blob = json.dumps({"format": FORMAT, "layout": layout_version(type(model)), "cfg": dataclasses.asdict(model.cfg),
+                       "tp": [model.tp.rank, model.tp.world],
                        "dtype": str(model.dtype), "fp8": model.fp8, "gu_block": model.gu_block, "source": source},
                       sort_keys=True, default=str)
     key = hashlib.sha256(blob.encode()).hexdigest()[:24]

@@ -333,6 +333,14 @@ def tile_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
             and x.shape[0] >= 1)
 
 
+def tile_out_ok(out: torch.Tensor | None) -> bool:
+    """An explicit output gemm_tile can write: unit column stride, a row stride that is a
+    multiple of 4 elements and an 8-byte-aligned base (its epilogue stores 4 bf16 at once);
+    anything else falls back instead of tripping the binding's TORCH_CHECK."""
+    return out is None or (out.dim() == 2 and out.stride(1) == 1 and out.stride(0) % 4 == 0
+                           and out.data_ptr() % 8 == 0 and out.dtype == torch.bfloat16)
+
+
 def linear_tile(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None,
                 bias: torch.Tensor | None = None, silu_gu: bool = False) -> torch.Tensor:
     """Prefill / lm_head GEMM on the compute-bound gfx950 tile kernel (256 x 256 tiles,
@@ -356,7 +364,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None, sp
     N = w.shape[0]
     plan = None
     if bias is not None:
-        if tile_ok(x, w) and (out is None or out.stride(1) == 1):
+        if tile_ok(x, w) and tile_out_ok(out):
             return linear_tile(x, w, out, bias)
         return _blas(x, w, out, bias)
     if x.is_cuda and bm is None and bn is None and splits is None and _measured_blas(M, N, K):
@@ -378,7 +386,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None, sp
         if plan is None and (splits or bn or bm) and M % 64 == 0 and M <= 256 and N % 64 == 0 and K % 64 == 0:
             plan = (row_tile(M), 64, 1)  # explicit request (tests / tuning)
     if plan is None:
-        if tile_ok(x, w) and (out is None or out.stride(1) == 1):
+        if tile_ok(x, w) and tile_out_ok(out):
             return linear_tile(x, w, out)
         return _blas(x, w, out, None)
     bm, bn, S = bm or plan[0], bn or plan[1], splits or plan[2]

@@ -295,3 +295,36 @@ def test_weight_cache_roundtrip(tmp_path, wd):
     d = LlamaModel(cfg, device="cpu", dtype=torch.float32, weight_dtype=wd)
     assert weight_cache.load_or_build(d, str(tmp_path), None, 7) == "miss"
     assert torch.equal(d.embed, a.embed)
+
+
+def test_weight_cache_key_tracks_layout_code(tmp_path):
+    """A change to the code that lays a shard out (sharding / packing / quantization) is a
+    new cache key: an old file is never mapped back with a stale layout."""
+    from operator_amd.models import weight_cache
+
+    cfg = get_config("tiny-gqa4")
+    a = LlamaModel(cfg, device="cpu", dtype=torch.float32)
+    assert weight_cache.load_or_build(a, str(tmp_path), None, 7) == "miss"
+
+    class Relaid(LlamaModel):   # same everything, but a different shard layout routine
+        def _shard_layer(self, *args, **kw):
+            lw = super()._shard_layer(*args, **kw)
+            return lw
+
+    assert weight_cache.layout_version(Relaid) != weight_cache.layout_version(LlamaModel)
+    b = Relaid(cfg, device="cpu", dtype=torch.float32)
+    assert weight_cache.cache_path(str(tmp_path), b, "random:7") != weight_cache.cache_path(str(tmp_path), a, "random:7")
+    assert weight_cache.load_or_build(b, str(tmp_path), None, 7) == "miss"
+
+
+def test_tile_out_ok_rejects_outputs_gemm_tile_cannot_write():
+    """linear(): an explicit output gemm_tile's binding would refuse (row stride not a
+    multiple of 4, misaligned base, strided columns) falls back instead of raising."""
+    from operator_amd import ops
+
+    base = torch.empty(64, 132, dtype=torch.bfloat16)
+    assert ops.tile_out_ok(None) and ops.tile_out_ok(base[:, :128])
+    assert not ops.tile_out_ok(torch.empty(64, 130, dtype=torch.bfloat16)[:, :128])   # row stride 130
+    assert not ops.tile_out_ok(base[:, 1:129])                                        # base 2 B off
+    assert not ops.tile_out_ok(base.t())                                               # column stride
+    assert not ops.tile_out_ok(torch.empty(64, 128, dtype=torch.float32))

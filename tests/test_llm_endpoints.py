@@ -142,3 +142,32 @@ def test_finished_batch_is_detokenized_once_before_waiters_wake(server):
         ee.llm.finish_hook = real
     assert seen and not any(any(x) for x in seen)          # hook ran before the waiters were released
     assert all(r.text == ee.tok.decode(r.output) for r in reqs)
+
+
+def test_explain_many_item_failure_keeps_the_others(server):
+    """A batch item that cannot be admitted comes back as that item's ExplainError; the
+    items already submitted are still waited for (none is left decoding without a waiter)."""
+    from operator_amd.api.models import AIProviderConfig, AnalysisResult, AnalysisSummary
+    from operator_amd.engine.explain import ExplainError
+
+    _, svc = server
+    ee = svc.services["tiny"].ee
+    res = AnalysisResult(pod_name="p", pod_namespace="default",
+                         summary=AnalysisSummary(highest_severity="HIGH", significant_events=1))
+    real, calls = ee._start, {"n": 0}
+
+    def flaky(p, ids, notify=True):
+        calls["n"] += 1
+        if calls["n"] == 2:
+            raise ValueError("prompt exceeds max_context")
+        return real(p, ids, notify)
+
+    ee._start = flaky
+    try:
+        cfg = AIProviderConfig(max_tokens=4, temperature=0.0, caching_enabled=False)
+        out = ee.explain_many([(res, cfg)] * 3)
+    finally:
+        ee._start = real
+    assert isinstance(out[1], ExplainError) and "max_context" in str(out[1])
+    assert [o.tokens_generated for o in (out[0], out[2])] == [4, 4]
+    assert not ee.llm.running and not ee.llm.waiting

@@ -216,6 +216,36 @@ def test_several_local_models_routed_by_model_id(tmp_path):
         svc.close()
 
 
+def test_streaming_detokenization_with_checkpoint_special_tokens(tmp_path):
+    """A checkpoint-style byte-level BPE with special tokens (Llama-3 ships 256 <|...|> ids):
+    decode() skips them, so the byte table maps them to no bytes and streaming stays on."""
+    import random
+
+    import tokenizers
+    from tokenizers import decoders, models, pre_tokenizers, trainers
+
+    from operator_amd.engine.tokenizer import Tokenizer
+
+    tk = tokenizers.Tokenizer(models.BPE())
+    tk.pre_tokenizer = pre_tokenizers.ByteLevel(add_prefix_space=False)
+    tk.decoder = decoders.ByteLevel()
+    tr = trainers.BpeTrainer(vocab_size=400, show_progress=False, initial_alphabet=pre_tokenizers.ByteLevel.alphabet())
+    tk.train_from_iterator(["pod failed with OOMKilled", "Back-off restarting failed container"] * 50, trainer=tr)
+    tk.add_special_tokens(["<|begin_of_text|>", "<|eot_id|>"] + [f"<|reserved_special_token_{i}|>" for i in range(8)])
+    f = tmp_path / "tokenizer.json"
+    tk.save(str(f))
+    t = Tokenizer(tk.get_vocab_size(), tk.token_to_id("<|begin_of_text|>"), tk.token_to_id("<|eot_id|>"), path=str(f))
+    assert t.byte_table() is not None
+    specials = [tk.token_to_id(f"<|reserved_special_token_{i}|>") for i in range(8)]
+    rng = random.Random(5)
+    for _ in range(10):
+        ids = [rng.randrange(0, t.n_vocab) for _ in range(60)] + specials
+        rng.shuffle(ids)
+        buf = bytearray()
+        t.feed(buf, ids)
+        assert t.text_of(buf) == t.decode(ids)
+
+
 def test_streaming_detokenization_is_exact_or_off(tmp_path):
     """Tokenizer.byte_table: a byte-level BPE streams each request's bytes per decode window
     (LLMEngine.token_hook) and its text equals decode() for any ids (ids past the vocabulary,
