@@ -294,26 +294,37 @@ __global__ void __launch_bounds__(512) gemm_tile256_kernel(const bf16_t* __restr
     }
 }
 
-// Variant 1: four waves (one per SIMD), each owning a 128 x 128 output block: 64
-// accumulator fragments = all 256 AGPRs, so the LDS fragment traffic per MFMA is
-// 2/3 of the 8-wave layout (16 ds_read_b128 per 64 MFMAs) and far fewer waves wait
-// at barriers (rocprofv3: the 8-wave schedule spends 31 % of wave-cycles in waits).
-// The MFMAs are inline asm with the accumulator TIED in an AGPR ("+a"): with the
-// builtin, hipcc's register allocator shuffles the 256 accumulators through
-// v_accvgpr copies (hundreds per K-tile). Fragments are double-buffered in VGPRs
-// (substep s+1 is read while substep s computes) and ONE raw barrier per K-tile
-// separates "tile t+1 landed, every wave done reading tile t" from the DMA of tile
-// t+2 into tile t's buffer, which then has a whole K-tile to land.
+// Variant 1 ("ring-4"): four waves (one per SIMD), each owning a 128 x 128 output block
+// (64 accumulator fragments = 256 AGPRs, 0.25 KB of LDS fragment reads per MFMA), and a
+// 4-deep ring of BK = 32 stages (32 KiB each: 128 KiB of LDS) so two stages are always
+// in flight behind the one being computed and the one being read: the counted
+// vmcnt(8) at the end of a step leaves the youngest stage's DMA outstanding, never 0
+// inside the loop (round 3's 2-buffer BK = 64 version waited 15 % of its wave-cycles on
+// a vmcnt(0) per K-tile, profiles/gemm_tile_pmc_vs_hipblaslt.txt).
+//   * LDS image: a stage is 32 pieces of 1 KiB (16 rows x 64 B; pieces 0-15 X rows,
+//     16-31 W rows). Inside a piece, row r's four 16-B k-chunks c sit at slots
+//     4r + (c ^ f(r >> 2)), f = {0, 3, 2, 1}: the DMA (lane-linear: lane l writes slot l)
+//     reads each row's 64 B with four consecutive lanes (coalesced), and a fragment is ONE
+//     ds_read_b128 per lane (lane l: row l & 15, chunk l >> 4) whose four 16-lane groups
+//     each hit 16 distinct bank slots — conflict-free by the choice of f.
+//   * per step and wave: 64 MFMAs (v_mfma_f32_16x16x32_bf16, accumulator tied in an AGPR
+//     by inline asm: the builtin makes hipcc shuffle 256 accumulators through
+//     v_accvgpr copies), the 16 fragment reads of the NEXT stage (register double
+//     buffer) and 8 LDS-DMA pieces of the stage three ahead, spread one row of 8 MFMAs
+//     apart; one raw s_barrier per step.
+// Stage t lives in buffer t % 4; step t reads stage t+1 and refills buffer (t+3) % 4,
+// whose stage t-1 every wave finished reading before the barrier that ended step t-1.
 __device__ __forceinline__ void mfma_tied(f32x4& acc, const u16x8& a, const u16x8& b) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 
 template <int EPI>
-__global__ void __launch_bounds__(256) gemm_tile256_w4_kernel(const bf16_t* __restrict__ X,
+__global__ void __launch_bounds__(256) gemm_tile256_r4_kernel(const bf16_t* __restrict__ X,
                                                               const bf16_t* __restrict__ W, bf16_t* __restrict__ Y,
                                                               const bf16_t* __restrict__ bias, int M, int N, int K,
                                                               int ldy) {
-  __shared__ __attribute__((aligned(1024))) char lds[2 * kBuf];   // per buffer: X rows 0-255, then W rows 0-255
+  constexpr int kBK4 = 32, kNS = 4, kStage = 32768, kWOff = 16384;
+  __shared__ __attribute__((aligned(1024))) char lds[kNS * kStage];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = w >> 1, wn = w & 1;
@@ -328,123 +339,109 @@ __global__ void __launch_bounds__(256) gemm_tile256_w4_kernel(const bf16_t* __re
   const int tn = (lid % gsz) / gm;
   const int m0 = tm * kT, n0 = tn * kT;
 
-  // DMA: wave w issues image rows 8w + 32i + lane/8 (i < 8: X, i >= 8: W); the
-  // swizzle term ((row >> 1) & 7) is the same for every i
-  const int lrow = lane >> 3;
-  const int chunk = (lane & 7) ^ ((4 * w + (lrow >> 1)) & 7);
-  // 32-bit byte offsets of this lane's source rows (the launcher guarantees M*K*2 and
-  // N*K*2 < 4 GiB): half the VGPRs of 64-bit pointers, and the loads take the
-  // scalar-base + vector-offset form
-  uint32_t xs[8], ws[8];
+  // DMA: wave w issues pieces w + 4i (i < 4: X rows 16(w + 4i).., i >= 4: W rows
+  // 16(w + 4(i - 4))..); lane l -> row l >> 2, chunk (l & 3) ^ f(l >> 4). 32-bit byte offsets
+  // (the launcher guarantees M*K*2 and N*K*2 < 4 GiB): scalar base + vector offset loads.
+  const int r15 = lane >> 2, ck = (lane & 3) ^ ((4 - (lane >> 4)) & 3);
+  uint32_t xs[4], ws[4];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    xs[i] = ((uint32_t)min(m0 + 8 * w + 32 * i + lrow, M - 1) * (uint32_t)K + chunk * 8) * 2u;
-    ws[i] = ((uint32_t)min(n0 + 8 * w + 32 * i + lrow, N - 1) * (uint32_t)K + chunk * 8) * 2u;
+  for (int i = 0; i < 4; ++i) {
+    xs[i] = ((uint32_t)min(m0 + 16 * (w + 4 * i) + r15, M - 1) * (uint32_t)K + ck * 8) * 2u;
+    ws[i] = ((uint32_t)min(n0 + 16 * (w + 4 * i) + r15, N - 1) * (uint32_t)K + ck * 8) * 2u;
   }
   const char* Xb = reinterpret_cast<const char*>(X);
   const char* Wb = reinterpret_cast<const char*>(W);
-  auto issue = [&](int buf, int kt) {
-    char* dst = lds + buf * kBuf + w * 1024;
-    const int k0 = kt * kBK;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-      __builtin_amdgcn_global_load_lds(Xb + xs[i] + 2 * k0, (__attribute__((address_space(3))) void*)(dst + i * 4096),
+  auto dma = [&](int kt, int buf, int q) {   // piece q (0..7) of this wave for K-step kt, into buffer buf
+    char* dst = lds + buf * kStage + w * 1024;
+    const uint32_t k2 = (uint32_t)kt * (kBK4 * 2);
+    if (q < 4)
+      __builtin_amdgcn_global_load_lds(Xb + xs[q] + k2, (__attribute__((address_space(3))) void*)(dst + q * 4096),
                                        16, 0, 0);
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-      __builtin_amdgcn_global_load_lds(Wb + ws[i] + 2 * k0,
-                                       (__attribute__((address_space(3))) void*)(dst + 32768 + i * 4096), 16, 0, 0);
+    else
+      __builtin_amdgcn_global_load_lds(Wb + ws[q - 4] + k2,
+                                       (__attribute__((address_space(3))) void*)(dst + kWOff + (q - 4) * 4096), 16, 0,
+                                       0);
   };
 
-  const int l15 = lane & 15, lq = lane >> 4, sw = (l15 >> 1) & 7;
-  const int c0 = (lq ^ sw) << 4, c1 = ((4 + lq) ^ sw) << 4;
-  const int xrow = (wm * 128 + l15) * 128;            // + bt * 2048
-  const int wrow = 32768 + (wn * 32 + l15) * 128;     // + f * 16384 + type * 8192 + j * 2048
+  // fragment reads: X fragment i = piece wm*8 + i; W fragment j = the rows of feature
+  // block j = f*4 + type*2 + jj (128-row half f, gate/up 64-row type, wave's 32 rows)
+  const int l16 = 16 * (4 * (lane & 15) + ((lane >> 4) ^ ((4 - ((lane & 15) >> 2)) & 3)));
+  auto rd1 = [&](int kt, u16x8 (&xf)[8], u16x8 (&wf)[8], int q) {
+    constexpr int kOrd[16] = {8, 9, 0, 10, 11, 1, 12, 13, 2, 14, 15, 3, 4, 5, 6, 7};   // >= 8: W fragment
+    const char* buf = lds + (kt & (kNS - 1)) * kStage + l16;
+    const int o = kOrd[q];
+    if (o >= 8) {
+      const int j = o - 8;
+      const int piece = (j >> 2) * 8 + ((j >> 1) & 1) * 4 + wn * 2 + (j & 1);
+      wf[j] = *reinterpret_cast<const u16x8*>(buf + kWOff + piece * 1024);
+    } else {
+      xf[o] = *reinterpret_cast<const u16x8*>(buf + (wm * 8 + o) * 1024);
+    }
+  };
 
-  f32x4 acc[8][8];   // [token block][feature block fe = f*4 + type*2 + j]
+  f32x4 acc[8][8];   // [token block][feature block]
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   u16x8 xa[8], wa[8], xb[8], wb[8];
-  // fragment q of a substep's 16 reads, in the order the next substep consumes them
-  // (all W fragments feed its first MFMA row, X fragment i its row i)
-  auto rd1 = [&](const char* buf, int c, u16x8 (&xf)[8], u16x8 (&wf)[8], int q) {
-    constexpr int kOrd[16] = {8, 9, 0, 10, 11, 1, 12, 13, 2, 14, 15, 3, 4, 5, 6, 7};   // >= 8: W fragment
-    const int o = kOrd[q];
-    if (o >= 8) {
-      const int i = o - 8;
-      wf[i] = *reinterpret_cast<const u16x8*>(buf + wrow + (i >> 2) * 16384 + ((i >> 1) & 1) * 8192 + (i & 1) * 2048 + c);
-    } else {
-      xf[o] = *reinterpret_cast<const u16x8*>(buf + xrow + o * 2048 + c);
-    }
-  };
-  auto issue1 = [&](int buf, int kt, int q) {   // DMA instruction q (of 16) of K-tile kt
-    char* dst = lds + buf * kBuf + w * 1024;
-    const int k0 = kt * kBK;
-    if (q < 8)
-      __builtin_amdgcn_global_load_lds(Xb + xs[q] + 2 * k0, (__attribute__((address_space(3))) void*)(dst + q * 4096),
-                                       16, 0, 0);
-    else
-      __builtin_amdgcn_global_load_lds(Wb + ws[q - 8] + 2 * k0,
-                                       (__attribute__((address_space(3))) void*)(dst + 32768 + (q - 8) * 4096), 16, 0, 0);
-  };
-  // 64 MFMAs of one substep; after each 8-MFMA row, two fragment reads of the next
-  // substep (from `nbuf`) and, if `dma`, two DMA instructions of K-tile `kt`
-  // stage == 2: this substep also issues K-tile kt's LDS-DMA into buffer dbuf
-  auto mm = [&](u16x8 (&xf)[8], u16x8 (&wf)[8], const char* nbuf, int c, u16x8 (&nx)[8], u16x8 (&nw)[8],
-                bool rd_next, int stage, int dbuf, int kt) {
+  // one K-step: 64 MFMAs; after each 8-MFMA row, two fragment reads of step kt+1 and one
+  // DMA piece of step kt+3. Branch-free: past the last step the reads fetch a buffer no
+  // one uses and the DMA re-loads step T-1 into buffer (kt+3) % 4, whose stage (kt-1) is
+  // consumed and which no later step reads; the loop's exit drains those DMAs
+  const int T = K / kBK4;   // even (K % 64 == 0)
+  auto step = [&](u16x8 (&xf)[8], u16x8 (&wf)[8], u16x8 (&nx)[8], u16x8 (&nw)[8], int kt) {
+    const int ks = min(kt + 3, T - 1), kb = (kt + 3) & (kNS - 1);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) mfma_tied(acc[i][j], wf[j], xf[i]);
       __builtin_amdgcn_sched_barrier(0);
-      if (rd_next) {
-        rd1(nbuf, c, nx, nw, 2 * i);
-        rd1(nbuf, c, nx, nw, 2 * i + 1);
-      }
-      if (stage == 2) {
-        issue1(dbuf, kt, 2 * i);
-        issue1(dbuf, kt, 2 * i + 1);
-      }
+      dma(ks, kb, i);
+      rd1(kt + 1, nx, nw, 2 * i);
+      rd1(kt + 1, nx, nw, 2 * i + 1);
       __builtin_amdgcn_sched_barrier(0);
     }
   };
 
-  // the zero-initialised accumulators are read as SrcC by asm MFMAs, whose hazards
-  // hipcc does not pad: pin the writes above an explicit nop
+  // zero-initialised accumulators are read as SrcC by asm MFMAs, whose hazards hipcc
+  // does not pad: pin the writes above an explicit nop
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
   asm volatile("s_nop 4");
 
-  const int T = K / kBK;
-  issue(0, 0);
-  vm_wait<0>();
+#pragma unroll
+  for (int q = 0; q < 8; ++q) dma(0, 0, q);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) dma(min(1, T - 1), 1, q);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) dma(min(2, T - 1), 2, q);
+  vm_wait<8>();   // stages 0 and 1 landed (this wave's pieces); stage 2 in flight
   seg_barrier();
 #pragma unroll
-  for (int q = 0; q < 16; ++q) rd1(lds, c0, xa, wa, q);
-  if (T > 1) issue(1, 1);
+  for (int q = 0; q < 16; ++q) rd1(0, xa, wa, q);
   // one loop, no peeled copy: a second code path makes hipcc move accumulators with
   // v_accvgpr_write right before an asm MFMA reads them (an unpadded hazard)
-  for (int t = 0; t < T; ++t) {
-    const char* cur = lds + (t & 1) * kBuf;
-    const bool more = t + 1 < T;
-    // S0: substep 0 of tile t, reading substep 1's fragments of tile t
-    mm(xa, wa, cur, c1, xb, wb, true, 0, 0, t + 2);
-    // tile t+1 landed (this wave's DMA); every wave done reading tile t
+  for (int t = 0; t < T; t += 2) {
+    // step t: regs A hold stage t; read stage t+1 into B; DMA stage t+3
+    step(xa, wa, xb, wb, t);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    vm_wait<0>();
-    if (more) seg_barrier();
-    // S1: substep 1 of tile t, reading substep 0 of tile t+1; tile t+2 goes into
-    // tile t's buffer
-    mm(xb, wb, lds + ((t + 1) & 1) * kBuf, c0, xa, wa, more, t + 2 < T ? 2 : 0, t & 1, t + 2);
+    vm_wait<8>();   // stage t+2 landed (this wave's pieces); stage t+3 in flight
+    seg_barrier();
+    // step t+1: regs B hold stage t+1; read stage t+2 into A; DMA stage t+4
+    step(xb, wb, xa, wa, t + 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    vm_wait<8>();
+    seg_barrier();
   }
+  vm_wait<0>();   // the tail's dummy DMAs must land before the workgroup's LDS is released
   // the accumulators were written by asm MFMAs the hazard recognizer cannot see:
   // cover the MFMA-write -> accvgpr-read latency before the epilogue reads them
   asm volatile("s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
 
+  const int l15 = lane & 15, lq = lane >> 4;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int tok = m0 + wm * 128 + i * 16 + l15;
@@ -536,10 +533,10 @@ int gemm_tile(const bf16_t* X, const bf16_t* W, bf16_t* Y, const bf16_t* bias, i
     return splitk_reduce(P, Y, (int64_t)M * N, S, stream);
   }
   const bool off32 = (int64_t)M * K * 2 < (1LL << 32) && (int64_t)N * K * 2 < (1LL << 32);
-  if (variant == 1 && off32) {   // 4-wave 128x128 per wave (32-bit source offsets)
-    if (silu_gu) gemm_tile256_w4_kernel<kEpiSilu><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-    else if (bias) gemm_tile256_w4_kernel<kEpiBias><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-    else gemm_tile256_w4_kernel<kEpiStore><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+  if (variant == 1 && off32) {   // 4-wave, 4-stage BK = 32 ring (32-bit source offsets)
+    if (silu_gu) gemm_tile256_r4_kernel<kEpiSilu><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+    else if (bias) gemm_tile256_r4_kernel<kEpiBias><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+    else gemm_tile256_r4_kernel<kEpiStore><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
   } else if (variant == 2 || (variant == 0 && M > 256)) {
     // 8-wave ping-pong, two barrier segments per K-tile: 1.8-2.7 % over four segments on
     // the prefill shapes (M = 32k, profiles/gemm_tile_ph2_vs_ph4.jsonl); the lm_head at

@@ -178,11 +178,16 @@ def rbac(namespace: str = "podmortem-system", name: str = "podmortem-operator") 
 
 
 def deployment(namespace: str = "podmortem-system", image: str = "ghcr.io/podmortem/operator-amd:latest",
-               gpus: int = 1, name: str = "podmortem-operator", replicas: int = 1, shards: int = 1) -> list[dict]:
+               gpus: int = 1, name: str = "podmortem-operator", replicas: int = 1, shards: int = 1,
+               shard_per_gpu: bool = False) -> list[dict]:
     """PVC + operator Deployment + Service. ``replicas`` > 1 turns on Lease leader
     election (one active replica, the others warm standbys); ``shards`` > 1 runs that
     many operator processes in the pod, splitting the pods between them, each with
-    its own engines on the pod's GPUs (``run --shards``)."""
+    its own engines on the pod's GPUs (``run --shards``); ``shard_per_gpu`` runs one
+    operator process per GPU, each owning its GPU and its slice of the pods
+    (``run --shard-per-gpu``, the multi-GPU topology ``bench.py --gpus N`` measures)."""
+    if shard_per_gpu:
+        shards = max(1, gpus)
     labels = {"app.kubernetes.io/name": name}
     env = [{"name": "PODMORTEM_PATTERNS__CACHE_DIR", "value": "/shared/patterns"},
            {"name": "HSA_ENABLE_IPC_MODE_LEGACY", "value": "0"}]
@@ -204,7 +209,8 @@ def deployment(namespace: str = "podmortem-system", image: str = "ghcr.io/podmor
                       "containers": [{
                           "name": "operator", "image": image,
                           "command": ["python", "-m", "operator_amd", "run", "--gpus", str(gpus)] +
-                                     (["--shards", str(shards)] if shards > 1 else []),
+                                     (["--shard-per-gpu"] if shard_per_gpu else
+                                      ["--shards", str(shards)] if shards > 1 else []),
                           "env": env,
                           "ports": [{"containerPort": 8080, "name": "http"}],
                           "resources": {"limits": {"amd.com/gpu": gpus, "memory": f"{64 * max(1, shards)}Gi"},

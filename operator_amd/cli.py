@@ -45,7 +45,7 @@ def cmd_manifests(args) -> int:
     from operator_amd.api.crds import render_all
 
     text = render_all(namespace=args.namespace, image=args.image, gpus=args.gpus, replicas=args.replicas,
-                      shards=args.shards, compat=args.compat_services)
+                      shards=args.shards, shard_per_gpu=args.shard_per_gpu, compat=args.compat_services)
     if args.out:
         with open(args.out, "w") as f:
             f.write(text)
@@ -120,13 +120,16 @@ def _build_services(s, metrics):
     return matcher, factory, explainer
 
 
-def shard_env(base: dict, index: int, count: int, health_port: int) -> dict:
-    """Environment of operator shard ``index`` of ``count`` started by ``run --shards``:
-    its slice of the pods and its own health/metrics port (applied over the config and
-    the --set overrides by ``apply_shard_env``)."""
+def shard_env(base: dict, index: int, count: int, health_port: int, device: str | None = None) -> dict:
+    """Environment of operator shard ``index`` of ``count`` started by ``run --shards`` /
+    ``run --shard-per-gpu``: its slice of the pods, its own health/metrics port and, per
+    GPU, the one device its engines own (applied over the config and the --set overrides
+    by ``apply_shard_env``)."""
     env = dict(base)
     env.update({"OAMD_SHARD_CHILD": "1", "OAMD_SHARD_INDEX": str(index), "OAMD_SHARD_COUNT": str(count),
                 "OAMD_SHARD_PORT": str(health_port + index)})
+    if device is not None:
+        env["OAMD_SHARD_DEVICE"] = device
     return env
 
 
@@ -135,6 +138,14 @@ def apply_shard_env(s, env: dict) -> None:
         s.operator.shard_index = int(env["OAMD_SHARD_INDEX"])
         s.operator.shard_count = int(env["OAMD_SHARD_COUNT"])
         s.health.port = int(env["OAMD_SHARD_PORT"])
+        if env.get("OAMD_SHARD_DEVICE"):   # shard-per-GPU: this shard's engines on one device
+            s.engine.device = env["OAMD_SHARD_DEVICE"]
+            s.engine.gpus = 1
+
+
+def shard_device(base_device: str, index: int) -> str:
+    """The device shard ``index`` owns in shard-per-GPU mode (CPU stays CPU: tests)."""
+    return "cpu" if base_device == "cpu" else f"cuda:{index}"
 
 
 class ShardSupervisor:
@@ -149,9 +160,10 @@ class ShardSupervisor:
     ``poll`` return False so the whole pod fails and Kubernetes restarts it."""
 
     def __init__(self, argv: list[str], count: int, health_port: int, max_restarts: int = 5,
-                 window_s: float = 300.0, clock=time.monotonic):
+                 window_s: float = 300.0, clock=time.monotonic, devices: list[str] | None = None):
         self.argv, self.count, self.health_port = list(argv), count, health_port
         self.max_restarts, self.window_s, self.clock = max_restarts, window_s, clock
+        self.devices = devices   # shard-per-GPU: shard i's device (None: every shard on every GPU)
         self.restarts: list[float] = []
         self.kids = {i: self._start(i) for i in range(1, count)}
 
@@ -159,7 +171,8 @@ class ShardSupervisor:
         import subprocess
 
         return subprocess.Popen([sys.executable, "-m", "operator_amd", *self.argv],
-                                env=shard_env(os.environ, index, self.count, self.health_port))
+                                env=shard_env(os.environ, index, self.count, self.health_port,
+                                              self.devices[index] if self.devices else None))
 
     def poll(self) -> bool:
         """Restart exited shards; False once they crash-loop."""
@@ -210,12 +223,26 @@ def cmd_run(args) -> int:
         except OSError:
             pass
     sup = None
-    if args.shards and args.shards > 1:   # shards of this process's GPUs (config-only sharding: one pod each)
-        if not os.environ.get("OAMD_SHARD_CHILD"):
+    child = bool(os.environ.get("OAMD_SHARD_CHILD"))
+    if args.shard_per_gpu:
+        # production multi-GPU topology: one operator shard process per GPU, each owning
+        # that GPU's engines in-process and its hash slice of the pods, all against the
+        # same API server; the first process supervises (restarts) the others
+        n = max(1, args.gpus or s.engine.gpus)
+        if args.shards and args.shards > 1:
+            raise SystemExit("--shard-per-gpu and --shards are exclusive")
+        if not child:
+            devs = [shard_device(s.engine.device, i) for i in range(n)]
+            if n > 1:
+                sup = ShardSupervisor(sys.argv[1:], n, s.health.port, devices=devs)
+            s.operator.shard_count, s.operator.shard_index = n, 0
+            s.engine.device, s.engine.gpus = devs[0], 1
+    elif args.shards and args.shards > 1:   # shards of this process's GPUs (config-only sharding: one pod each)
+        if not child:
             sup = ShardSupervisor(sys.argv[1:], args.shards, s.health.port)
             s.operator.shard_count, s.operator.shard_index = args.shards, 0
         shard_sizing(s, args.shards)
-    if args.gpus and args.gpus > 1:
+    if args.gpus and args.gpus > 1 and not args.shard_per_gpu:
         s.engine.gpus = args.gpus
     if args.tp and args.tp > 1:
         s.engine.tp = args.tp
@@ -303,13 +330,17 @@ def main(argv: list[str] | None = None) -> int:
                    help="GPUs per explanation-model replica (engine.tp); --gpus 8 --tp 8 = one 70B replica")
     p.add_argument("--shards", type=int, default=0,
                    help="operator shards (processes splitting the pods, each with its own engines on the same "
-                        "GPUs); 2 fills an MI355X better than 1 (operator.shard_count)")
+                        "GPUs; operator.shard_count)")
+    p.add_argument("--shard-per-gpu", action="store_true",
+                   help="one operator shard process per GPU (--gpus N): shard i owns cuda:i and the pods hashing "
+                        "to it, all shards on the same API server (the multi-GPU production topology)")
     p = sub.add_parser("manifests")
     p.add_argument("--namespace", default="podmortem-system")
     p.add_argument("--image", default="ghcr.io/podmortem/operator-amd:latest")
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--replicas", type=int, default=1, help=">1 enables Lease leader election")
     p.add_argument("--shards", type=int, default=1, help="operator shards per pod (run --shards)")
+    p.add_argument("--shard-per-gpu", action="store_true", help="one operator shard per GPU (run --shard-per-gpu)")
     p.add_argument("--compat-services", action="store_true",
                    help="also emit log-parser / ai-interface Deployments+Services backed by serve-compat")
     p.add_argument("--out", default=None)

@@ -75,6 +75,11 @@ class StorageCfg(BaseModel):
     max_recent_failures: int = 10
     max_retries: int = 5
     initial_backoff_s: float = 0.1
+    # operator.shard_count > 1: N processes prepend to ONE Podmortem's recentFailures ring
+    # (GET + PATCH with resourceVersion), so conflicts are N-fold: a larger 409 budget and
+    # jittered delays for the status writes (the reference has a single writer)
+    sharded_max_retries: int = 12
+    sharded_jitter: float = 0.5
     failure_time_from_pod: bool = False  # Q5: reference records now(); true = container finishedAt
 
 

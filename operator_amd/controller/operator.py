@@ -76,8 +76,13 @@ class Operator:
         self.io_pool = TrackedExecutor(s.operator.io_workers, thread_name_prefix="kube-io")
         self.pool = TrackedExecutor(self.pipeline_workers(s), thread_name_prefix="analysis")
         retrier = Retrier(s.storage.max_retries, s.storage.initial_backoff_s)
-        self.status = StatusWriter(kube, retrier, s.storage.failure_time_from_pod)
-        self.storage = AnalysisStorage(kube, self.status, self.io_pool)
+        # the status ring is the one object every operator shard writes: a larger 409 budget
+        # with jittered delays there (pod annotations are per pod: one writer, no change)
+        status_retrier = retrier if s.operator.shard_count <= 1 else Retrier(
+            max(s.storage.max_retries, s.storage.sharded_max_retries), s.storage.initial_backoff_s,
+            jitter=s.storage.sharded_jitter)
+        self.status = StatusWriter(kube, status_retrier, s.storage.failure_time_from_pod)
+        self.storage = AnalysisStorage(kube, self.status, self.io_pool, retrier)
         self.events = EventEmitter(kube, self.io_pool, self.metrics)
         self.match_engine_factory = match_engine_factory
         self.matcher = match_service

@@ -72,8 +72,22 @@ def pattern_explanation(result: AnalysisResult) -> str:
 
 
 class Retrier:
-    def __init__(self, max_retries: int = 5, initial_delay_s: float = 0.1, sleep=time.sleep):
+    """409 retry schedule: ``max_retries`` retries, delays doubling from ``initial_delay_s``
+    (AnalysisStorageService.java:75-76: 5 x 100 ms). With several operator shards writing
+    one Podmortem's status, every shard's retry would land on the same doubling ticks
+    and collide again: ``jitter`` spreads each delay uniformly over ±jitter of its value,
+    and delays stop doubling at ``max_delay_s``."""
+
+    def __init__(self, max_retries: int = 5, initial_delay_s: float = 0.1, sleep=time.sleep, jitter: float = 0.0,
+                 max_delay_s: float = 1.6, rng=None):
         self.max_retries, self.initial_delay_s, self.sleep = max_retries, initial_delay_s, sleep
+        self.jitter, self.max_delay_s = jitter, max_delay_s
+        import random
+
+        self.rng = rng or random.Random()
+
+    def delay(self, nominal: float) -> float:
+        return nominal * (1.0 + self.jitter * (2.0 * self.rng.random() - 1.0)) if self.jitter else nominal
 
 
 class _Commit:
@@ -150,8 +164,8 @@ class StatusWriter:
         delay = self.retrier.initial_delay_s
         for attempt in range(self.retrier.max_retries + 1):
             if attempt:
-                self.retrier.sleep(delay)
-                delay *= 2
+                self.retrier.sleep(self.retrier.delay(delay))
+                delay = min(delay * 2, self.retrier.max_delay_s)
             try:
                 return fn()
             except ApiError as e:

@@ -145,6 +145,84 @@ def _error(code: int, body: bytes | str) -> ApiError:
         return ApiError(code, body.decode() if isinstance(body, bytes) else str(body))
 
 
+class _Pool:
+    """Keep-alive connection pool for unary requests on the stdlib ``http.client``: one
+    request costs ~0.25 ms of client CPU here against ~1.2 ms through httpx, and an
+    operator shard issues ~11 API calls per analysis under its GIL (watch streams stay on
+    httpx). A request that fails on a REUSED connection the server had already closed is
+    sent again once on a fresh one (nothing was processed for it)."""
+
+    def __init__(self, server: str, headers: dict, timeout_s: float, ca=None, cert=None):
+        import ssl
+        import threading
+        from urllib.parse import urlsplit
+
+        u = urlsplit(server)
+        self.https = u.scheme == "https"
+        self.host, self.port = u.hostname, u.port or (443 if self.https else 80)
+        self.prefix = u.path.rstrip("/")
+        self.headers, self.timeout = headers, timeout_s
+        self.ctx = None
+        if self.https:
+            if ca is False:
+                self.ctx = ssl.create_default_context()
+                self.ctx.check_hostname = False
+                self.ctx.verify_mode = ssl.CERT_NONE
+            else:
+                self.ctx = ssl.create_default_context(cafile=ca if isinstance(ca, str) else None)
+            if cert:
+                self.ctx.load_cert_chain(cert[0], cert[1])
+        self._idle: list = []
+        self._lock = threading.Lock()
+
+    def _new(self):
+        import http.client
+
+        if self.https:
+            return http.client.HTTPSConnection(self.host, self.port, timeout=self.timeout, context=self.ctx)
+        return http.client.HTTPConnection(self.host, self.port, timeout=self.timeout)
+
+    def request(self, method: str, path: str, body: bytes | None = None, headers: dict | None = None):
+        """(status, content-type, body bytes)."""
+        import http.client
+
+        h = dict(self.headers)
+        if headers:
+            h.update(headers)
+        for attempt in (0, 1):
+            with self._lock:
+                conn = self._idle.pop() if (self._idle and attempt == 0) else None
+            reused = conn is not None
+            if conn is None:
+                conn = self._new()
+            try:
+                conn.request(method, self.prefix + path, body=body, headers=h)
+                r = conn.getresponse()
+                data = r.read()
+            except (http.client.RemoteDisconnected, ConnectionResetError, BrokenPipeError,
+                    http.client.CannotSendRequest):
+                conn.close()
+                if reused and attempt == 0:
+                    continue
+                raise
+            except BaseException:
+                conn.close()
+                raise
+            if r.will_close:
+                conn.close()
+            else:
+                with self._lock:
+                    self._idle.append(conn)
+            return r.status, r.getheader("Content-Type", ""), data
+        raise OSError("unreachable")
+
+    def close(self) -> None:
+        with self._lock:
+            conns, self._idle = self._idle, []
+        for c in conns:
+            c.close()
+
+
 class KubeClient:
     def __init__(self, cfg: KubeConfig, timeout_s: float = 30.0):
         self.cfg = cfg
@@ -152,8 +230,15 @@ class KubeClient:
         if cfg.token:
             headers["Authorization"] = f"Bearer {cfg.token}"
         verify: Any = cfg.ca if cfg.ca is not None else True
+        # watch streams (long-lived, chunked)
         self.http = httpx.Client(base_url=cfg.server, headers=headers, verify=verify, cert=cfg.cert,
                                  timeout=timeout_s)
+        # unary requests
+        self.pool = _Pool(cfg.server, headers, timeout_s, cfg.ca, cfg.cert)
+
+    def close(self) -> None:
+        self.pool.close()
+        self.http.close()
 
     @staticmethod
     def auto(mode: str = "auto", kubeconfig: str | None = None, timeout_s: float = 30.0) -> "KubeClient":
@@ -163,14 +248,19 @@ class KubeClient:
         return KubeClient(KubeConfig.from_kubeconfig(kubeconfig), timeout_s)
 
     # ------------------------------------------------------------------ helpers
-    def _req(self, method: str, url: str, **kw) -> Any:
-        r = self.http.request(method, url, **kw)
-        if r.status_code >= 400:
-            raise _error(r.status_code, r.content)
-        if not r.content:
+    def _req(self, method: str, url: str, json_body: Any = None, content: bytes | str | None = None,
+             headers: dict | None = None) -> Any:
+        if json_body is not None:
+            content = json.dumps(json_body, separators=(",", ":"))
+            headers = dict(headers or {}, **{"Content-Type": "application/json"})
+        if isinstance(content, str):
+            content = content.encode()
+        status, ctype, data = self.pool.request(method, url, content, headers)
+        if status >= 400:
+            raise _error(status, data)
+        if not data:
             return None
-        ctype = r.headers.get("content-type", "")
-        return r.json() if "json" in ctype else r.text
+        return json.loads(data) if "json" in ctype else data.decode("utf-8", "replace")
 
     @staticmethod
     def _with_kind(o: dict, res: Resource) -> dict:
@@ -208,11 +298,11 @@ class KubeClient:
 
     def create(self, res: Resource, obj: dict, namespace: str | None = None) -> dict:
         ns = namespace or (obj.get("metadata") or {}).get("namespace")
-        return self._req("POST", res.base_path(ns), json=self._with_kind(dict(obj), res))
+        return self._req("POST", res.base_path(ns), json_body=self._with_kind(dict(obj), res))
 
     def replace(self, res: Resource, obj: dict, namespace: str | None = None) -> dict:
         ns = namespace or obj["metadata"].get("namespace")
-        return self._req("PUT", f"{res.base_path(ns)}/{obj['metadata']['name']}", json=obj)
+        return self._req("PUT", f"{res.base_path(ns)}/{obj['metadata']['name']}", json_body=obj)
 
     def _merge(self, url: str, patch: dict, rv: str | None) -> dict:
         if rv is not None:
@@ -231,7 +321,7 @@ class KubeClient:
 
     def replace_status(self, res: Resource, obj: dict, namespace: str | None = None) -> dict:
         ns = namespace or obj["metadata"].get("namespace")
-        return self._req("PUT", f"{res.base_path(ns)}/{obj['metadata']['name']}/status", json=obj)
+        return self._req("PUT", f"{res.base_path(ns)}/{obj['metadata']['name']}/status", json_body=obj)
 
     def delete(self, res: Resource, name: str, namespace: str | None = None) -> bool:
         try:
@@ -260,7 +350,7 @@ class KubeClient:
         if limit_bytes is not None:
             q["limitBytes"] = limit_bytes
         url = f"/api/v1/namespaces/{namespace}/pods/{name}/log" + (f"?{urlencode(q)}" if q else "")
-        r = self.http.get(url)
-        if r.status_code >= 400:
-            raise _error(r.status_code, r.content)
-        return r.text
+        status, _, data = self.pool.request("GET", url)
+        if status >= 400:
+            raise _error(status, data)
+        return data.decode("utf-8", "replace")

@@ -23,6 +23,7 @@ Thread-safe; every read returns a deep copy.
 from __future__ import annotations
 
 import itertools
+import json
 import queue
 import threading
 import uuid
@@ -69,9 +70,9 @@ class FakeWatch:
         self.q: queue.Queue = queue.Queue()
         self.closed = False
 
-    def push(self, typ: str, obj: dict) -> None:
+    def push(self, typ: str, obj: dict, ev: "_Event | None" = None) -> None:
         if not self.closed:
-            self.q.put((typ, obj))
+            self.q.put(ev if ev is not None else _Event(typ, obj))
 
     def fail(self, message: str = "watch stream error", code: int | None = None) -> None:
         self.q.put(WatchClosed(message, code))
@@ -85,7 +86,9 @@ class FakeWatch:
     def __iter__(self) -> Iterator[tuple[str, dict]]:
         return self
 
-    def __next__(self) -> tuple[str, dict]:
+    def next_event(self) -> "_Event":
+        """The next event as shared by every watch it went to (the REST server sends its
+        memoised wire bytes instead of copying and serialising the object per watcher)."""
         item = self.q.get()
         if item is self._END:
             raise StopIteration
@@ -93,13 +96,33 @@ class FakeWatch:
             self.closed = True
             self.fk._drop_watch(self)
             raise item
+        return item
+
+    def __next__(self) -> tuple[str, dict]:
+        ev = self.next_event()
         # events carry the stored (never mutated) object; each consumer gets its own
         # copy, made here on its thread rather than under the store's lock
-        return item[0], _jcopy(item[1])
+        return ev.typ, _jcopy(ev.obj)
+
+
+class _Event:
+    """One watch event, shared by every watch it is delivered to; ``wire()`` is its
+    serialised form, computed once (by whichever consumer asks first)."""
+    __slots__ = ("typ", "obj", "_wire")
+
+    def __init__(self, typ: str, obj: dict):
+        self.typ, self.obj, self._wire = typ, obj, None
+
+    def wire(self) -> bytes:
+        b = self._wire
+        if b is None:
+            b = self._wire = json.dumps({"type": self.typ, "object": self.obj}, separators=(",", ":")).encode() + b"\n"
+        return b
 
 
 class FakeKube:
-    def __init__(self):
+    def __init__(self, record_calls: bool = True):
+        self.record_calls = record_calls   # off for a long-running API server process (unbounded list)
         self._lock = threading.RLock()
         self._objs: dict[tuple[str, str, str], dict] = {}  # (plural-key, ns, name) -> obj
         self._by_kind: dict[str, dict[tuple[str, str], dict]] = {}
@@ -134,7 +157,8 @@ class FakeKube:
                                                                                 404: "NotFound"}.get(code, "Error"))
 
     def _log_call(self, verb, res, ns, name) -> None:
-        self.calls.append((verb, res.plural, ns, name))
+        if self.record_calls:
+            self.calls.append((verb, res.plural, ns, name))
 
     # ------------------------------------------------------------------ helpers
     @staticmethod
@@ -158,9 +182,12 @@ class FakeKube:
         # new dict), so the history can hold them by reference
         self._history.append((rv, self._key(res), typ, obj))
         self._last_rv = rv
+        ev = None
         for w in list(self._watches):
             if w.res == res and (w.namespace is None or w.namespace == obj["metadata"].get("namespace")):
-                w.push(typ, obj)
+                if ev is None:
+                    ev = _Event(typ, obj)
+                w.push(typ, obj, ev)
 
     def _drop_watch(self, w: FakeWatch) -> None:
         with self._lock:

@@ -3,7 +3,15 @@ KubeClient is exercised end-to-end without a cluster (tests, local demos).
 
 Supported: GET/LIST (label & field selectors), POST, PUT, PATCH
 (merge-patch, with metadata.resourceVersion -> 409), DELETE, the ``status``
-subresource, ``pods/{name}/log``, and ``?watch=1`` streaming.
+subresource, ``pods/{name}/log``, and ``?watch=1`` streaming. One extension a
+real apiserver does not have: ``PUT pods/{name}/log`` sets a pod's log text (what
+the container would have written), so a test or benchmark in another process can
+seed logs.
+
+Run standalone (the one API server several operator shard processes share, e.g.
+``bench.py --gpus N``): ``python -m operator_amd.kube.fake_server --port 0
+--port-file F`` writes its URL to F once it is listening. Each watch event is
+serialised once and the same bytes go to every watcher.
 """
 from __future__ import annotations
 
@@ -43,6 +51,10 @@ class FakeKubeServer:
 
         class H(BaseHTTPRequestHandler):
             protocol_version = "HTTP/1.1"
+            # one buffered write per response and TCP_NODELAY: unbuffered header lines under
+            # Nagle + the client's delayed ACK cost ~40 ms per keep-alive request
+            disable_nagle_algorithm = True
+            wbufsize = 1 << 16
 
             def log_message(self, *a):
                 pass
@@ -54,6 +66,7 @@ class FakeKubeServer:
                 self.send_header("Content-Length", str(len(b)))
                 self.end_headers()
                 self.wfile.write(b)
+                self.wfile.flush()
 
             def _err(self, e: ApiError) -> None:
                 self._json(e.code, {"kind": "Status", "code": e.code, "reason": e.reason, "message": e.message})
@@ -70,6 +83,10 @@ class FakeKubeServer:
                     return self._json(404, {"message": "not found", "reason": "NotFound", "code": 404})
                 res, ns, name, sub = rt
                 try:
+                    if method == "PUT" and sub == "log":
+                        n = int(self.headers.get("Content-Length", "0") or 0)
+                        srv.fk.set_log(ns or "default", name, self.rfile.read(n), q.get("container"))
+                        return self._json(200, {"kind": "Status", "status": "Success"})
                     if method == "GET" and sub == "log":
                         text = srv.fk.pod_log(name, ns, q.get("container"), q.get("previous") == "true",
                                               int(q["tailLines"]) if "tailLines" in q else None,
@@ -79,6 +96,7 @@ class FakeKubeServer:
                         self.send_header("Content-Length", str(len(text)))
                         self.end_headers()
                         self.wfile.write(text)
+                        self.wfile.flush()
                         return
                     if method == "GET" and name is None and q.get("watch") in ("1", "true"):
                         return self._watch(res, ns, q.get("resourceVersion"))
@@ -119,14 +137,19 @@ class FakeKubeServer:
                 self.send_header("Content-Type", "application/json")
                 self.send_header("Transfer-Encoding", "chunked")
                 self.end_headers()
+                self.wfile.flush()
 
                 def chunk(b: bytes) -> None:
                     self.wfile.write(f"{len(b):x}\r\n".encode() + b + b"\r\n")
                     self.wfile.flush()
 
                 try:
-                    for typ, obj in w:
-                        chunk(json.dumps({"type": typ, "object": obj}).encode() + b"\n")
+                    while True:
+                        try:
+                            ev = w.next_event()
+                        except StopIteration:
+                            break
+                        chunk(ev.wire())
                 except WatchClosed as e:
                     try:
                         chunk(json.dumps({"type": "ERROR", "object": {"code": e.code or 500, "message": str(e),
@@ -139,6 +162,7 @@ class FakeKubeServer:
                     return
                 try:
                     self.wfile.write(b"0\r\n\r\n")
+                    self.wfile.flush()
                 except OSError:
                     pass
 
@@ -157,7 +181,14 @@ class FakeKubeServer:
             def do_DELETE(self):  # noqa: N802
                 self._dispatch("DELETE")
 
-        self.httpd = ThreadingHTTPServer((host, port), H)
+        class Server(ThreadingHTTPServer):
+            def handle_error(self, request, client_address):   # a client gone mid-stream is not an error
+                import sys
+
+                if not isinstance(sys.exc_info()[1], (BrokenPipeError, ConnectionResetError)):
+                    super().handle_error(request, client_address)
+
+        self.httpd = Server((host, port), H)
         self.httpd.daemon_threads = True
         self.url = f"http://{host}:{self.httpd.server_address[1]}"
         self._t = threading.Thread(target=self.httpd.serve_forever, name="fakekube-http", daemon=True)
@@ -170,3 +201,73 @@ class FakeKubeServer:
         self.fk.fail_watches("server shutdown")
         self.httpd.shutdown()
         self.httpd.server_close()
+
+
+def main(argv: list[str] | None = None) -> int:
+    """A standalone FakeKube API server process (until SIGTERM / SIGINT)."""
+    import argparse
+    import os
+    import signal
+
+    ap = argparse.ArgumentParser(description="in-memory Kubernetes API server (test double)")
+    ap.add_argument("--host", default="127.0.0.1")
+    ap.add_argument("--port", type=int, default=0)
+    ap.add_argument("--port-file", default=None, help="write the URL here once listening")
+    a = ap.parse_args(argv)
+    if hasattr(os, "getppid"):   # exit with the process that started it
+        try:
+            import ctypes
+
+            ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, int(signal.SIGTERM))   # PR_SET_PDEATHSIG
+        except OSError:
+            pass
+    srv = FakeKubeServer(FakeKube(record_calls=False), a.host, a.port).start()
+    if a.port_file:
+        tmp = a.port_file + ".tmp"
+        with open(tmp, "w") as f:
+            f.write(srv.url)
+        os.replace(tmp, a.port_file)
+    stop = threading.Event()
+    signal.signal(signal.SIGTERM, lambda *_: stop.set())
+    signal.signal(signal.SIGINT, lambda *_: stop.set())
+    stop.wait()
+    srv.stop()
+    return 0
+
+
+def write_kubeconfig(url: str, path: str, namespace: str = "default") -> str:
+    """A kubeconfig (no credentials) for the API server at ``url``: what ``run`` /
+    ``KubeClient.auto`` read to reach a FakeKubeServer from another process."""
+    import yaml
+
+    doc = {"apiVersion": "v1", "kind": "Config", "current-context": "fake",
+           "clusters": [{"name": "fake", "cluster": {"server": url}}],
+           "users": [{"name": "fake", "user": {}}],
+           "contexts": [{"name": "fake", "context": {"cluster": "fake", "user": "fake", "namespace": namespace}}]}
+    with open(path, "w") as f:
+        yaml.safe_dump(doc, f)
+    return path
+
+
+def spawn(port_file: str, timeout_s: float = 60.0):
+    """Start ``main`` as a child process; returns (process, url) once it listens."""
+    import os
+    import subprocess
+    import sys
+    import time
+
+    if os.path.exists(port_file):
+        os.unlink(port_file)
+    p = subprocess.Popen([sys.executable, "-m", "operator_amd.kube.fake_server", "--port-file", port_file])
+    t0 = time.monotonic()
+    while not os.path.exists(port_file):
+        if p.poll() is not None or time.monotonic() - t0 > timeout_s:
+            p.kill()
+            raise RuntimeError(f"fake API server did not start (exit {p.poll()})")
+        time.sleep(0.05)
+    with open(port_file) as f:
+        return p, f.read().strip()
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -10,7 +10,7 @@ from operator_amd.ops import reference as ref
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-VARIANTS = (0, 1, 2, 3)   # gemm_tile schedules: auto (default), 4-wave 128x128 per wave, 8-wave 2-segment, 8-wave 4-segment
+VARIANTS = (0, 1, 2, 3)   # gemm_tile schedules: auto (default), 4-wave 4-stage ring, 8-wave 2-segment, 8-wave 4-segment
 
 
 def _rand(*shape, scale=1.0):
@@ -72,6 +72,30 @@ def test_gemm_tile_silu(M, inter, K):
         y = torch.empty(M, inter, dtype=torch.bfloat16, device=DEV)
         ops.kernels().gemm_tile(x, wgu, y, None, True, v)
         _close(y, r, 3e-2)
+
+
+@pytest.mark.parametrize("S", [2, 4])
+def test_gemm_tile_split_k(S):
+    """Split-K: fp32 slabs [S][M][N] (consumer-summed), the reduced bf16 output and the
+    fused-SwiGLU reduce of interleaved gate|up slabs, against fp32 references."""
+    M, N, K = 300, 512, 1024
+    torch.manual_seed(S)
+    x, w = _rand(M, K), _rand(N, K, scale=0.05)
+    r = x.float() @ w.float().t()
+    P = torch.empty(S * M * N, dtype=torch.float32, device=DEV)
+    ops.kernels().gemm_tile(x, w, None, None, False, 0, S, P)
+    torch.cuda.synchronize()
+    _close(P.view(S, M, N).sum(0), r, 1e-3)
+    y = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    ops.kernels().gemm_tile(x, w, y, None, False, 0, S, P)
+    _close(y, r)
+    g, u = _rand(256, K, scale=0.05), _rand(256, K, scale=0.05)
+    wgu = ops.interleave_gate_up(g, u)
+    gg = (x.float() @ g.float().t()).to(torch.bfloat16)
+    uu = (x.float() @ u.float().t()).to(torch.bfloat16)
+    ys = torch.empty(M, 256, dtype=torch.bfloat16, device=DEV)
+    ops.kernels().gemm_tile(x, wgu, ys, None, True, 0, S, P)
+    _close(ys, ref.silu_mul(torch.cat([gg, uu], 1), None), 3e-2)
 
 
 def test_gemm_tile_strided_output():

@@ -56,6 +56,99 @@ def wait(pred, timeout):
     return False
 
 
+def run_sharded(shards: int, failures: int, workdir: str, timeout_s: float = 600.0, log_kb: int = 0) -> dict:
+    """The production multi-GPU topology on the CPU: ONE API server process (the REST
+    FakeKube) and ``run --shard-per-gpu --gpus N`` (N operator shard processes, each
+    with its own stub log-parser + echo explainer, splitting the pods by hash). Fails
+    ``failures`` pods at once and waits until every one carries its analysis
+    annotation; returns the rate plus, per pod, how many PodmortemAnalysisComplete
+    Events it got (exactly one each = no double, no miss)."""
+    import signal
+    import socket
+    import subprocess
+    from collections import Counter
+
+    from operator_amd.kube.client import KubeClient, KubeConfig
+    from operator_amd.kube.fake_server import spawn, write_kubeconfig
+    from operator_amd.kube.resources import EVENTS
+
+    srv, url = spawn(os.path.join(workdir, "apiserver.url"))
+    kc = write_kubeconfig(url, os.path.join(workdir, "kubeconfig"))
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = dict(os.environ, PODMORTEM_LOG_LEVEL="WARNING")
+    op = None
+    kube = KubeClient(KubeConfig(url), 30.0)
+    try:
+        kube.create(AIPROVIDERS, {"metadata": {"name": "stub", "namespace": "default"},
+                                  "spec": {"providerId": "stub", "modelId": "echo"}})
+        kube.create(PODMORTEMS, {"metadata": {"name": "m0", "namespace": "default"},
+                                 "spec": {"podSelector": {"matchLabels": {"app": "demo"}},
+                                          "aiAnalysisEnabled": True, "aiProviderRef": {"name": "stub"}}})
+        log = LOG
+        if log_kb:
+            filler = b"INFO request served in 3 ms from cache shard 7\n"
+            log = filler * max(0, (log_kb * 1024 - len(LOG)) // len(filler)) + LOG
+        names = [f"p{i}" for i in range(failures)]
+        import httpx
+
+        with httpx.Client(base_url=url, timeout=30) as h:
+            for n in names:
+                kube.create(PODS, running_pod(n, labels={"app": "demo"}))
+                h.put(f"/api/v1/namespaces/default/pods/{n}/log", content=log).raise_for_status()
+        op = subprocess.Popen([sys.executable, "-m", "operator_amd", "run", "--shard-per-gpu", "--gpus", str(shards),
+                               "--set", "engine.device=cpu", "--set", "services.match=stub",
+                               "--set", "services.explain=echo", "--set", "kube.mode=kubeconfig",
+                               "--set", f"kube.kubeconfig={kc}", "--set", f"health.port={port}",
+                               "--set", "health.host=127.0.0.1", "--set", f"patterns.cache_dir={workdir}/patterns",
+                               "--set", "operator.workers=64"], env=env)
+        import urllib.request
+
+        def up(pt):
+            try:
+                return urllib.request.urlopen(f"http://127.0.0.1:{pt}/q/health/ready", timeout=1).status == 200
+            except OSError:
+                return False
+        assert wait(lambda: all(up(port + i) for i in range(shards)), 180), "shards did not come up"
+        t0 = time.perf_counter()
+        for n in names:
+            cur = kube.get(PODS, n, "default")
+            cur["status"] = failed_pod(n, finished_at="2025-08-29T10:00:00Z")["status"]
+            kube.replace(PODS, cur)
+        t_inj = time.perf_counter() - t0
+
+        def analysed():
+            return sum(1 for p in kube.list(PODS, "default")
+                       if "podmortem.io/analysis" in ((p.get("metadata") or {}).get("annotations") or {}))
+        end = time.perf_counter() + timeout_s
+        n_done = 0
+        while time.perf_counter() < end:
+            n_done = analysed()
+            if n_done >= failures:
+                break
+            time.sleep(0.1)
+        elapsed = time.perf_counter() - t0
+        time.sleep(2.0)   # let the last Events land before counting them
+        per_pod = Counter(e.get("regarding", {}).get("name") for e in kube.list(EVENTS, "default")
+                          if e.get("reason") == "PodmortemAnalysisComplete"
+                          and e.get("regarding", {}).get("kind") == "Pod")
+        return {"topology": f"shard-per-gpu x{shards} on one REST API server (stub log-parser + echo explainer)",
+                "failures": failures, "analysed": n_done, "analyses_per_s": round(failures / elapsed, 1),
+                "inject_s": round(t_inj, 2), "elapsed_s": round(elapsed, 2),
+                "complete_events_per_pod": dict(Counter(per_pod.get(n, 0) for n in names))}
+    finally:
+        if op is not None:
+            op.send_signal(signal.SIGTERM)
+            try:
+                op.wait(60)
+            except subprocess.TimeoutExpired:
+                op.kill()
+        kube.close() if hasattr(kube, "close") else None
+        srv.terminate()
+        srv.wait(30)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--failures", type=int, default=2000)
@@ -66,7 +159,17 @@ def main():
                     help="engines in N worker processes behind the EnginePool (the `run --gpus N` topology: "
                          "CPU matcher + echo explainer per worker) instead of in this process")
     ap.add_argument("--log-kb", type=int, default=0, help="pad every pod log to this size (KiB)")
+    ap.add_argument("--shard-per-gpu", type=int, default=0,
+                    help="N operator shard processes (`run --shard-per-gpu --gpus N`, CPU stub engines) on ONE REST "
+                         "API server process, instead of everything in this process")
     a = ap.parse_args()
+    if a.shard_per_gpu:
+        import tempfile
+
+        with tempfile.TemporaryDirectory() as d:
+            print(json.dumps({"bench": "plumbing (BASELINE config 1)", **run_sharded(a.shard_per_gpu, a.failures, d,
+                                                                                      log_kb=a.log_kb)}))
+        return
     s = load_settings(env={}, overrides={"patterns.cache_dir": "/tmp/oamd-plumbing", "health.enabled": False,
                                          "operator.workers": a.workers})
     fk = FakeKube()
