@@ -77,6 +77,11 @@ def parse_args():
                     help="operator.sink_concurrency: analyses writing results at once (0 = unbounded); a bound "
                          "keeps a finished wave's 256 result writers from starving the next wave's ramp "
                          "(GPU gap before its first prefill 230-440 -> 140-170 ms, profiles/wave_timeline_sinks_8b.jsonl)")
+    ap.add_argument("--apiserver", choices=["auto", "inproc", "rest"], default="auto",
+                    help="rest: ONE API server process (the REST FakeKube, kube/fake_server.py) that every rank's "
+                         "operator shard talks to over HTTP, each rank owning the pods that hash to it "
+                         "(`run --shard-per-gpu`); inproc: an in-memory FakeKube inside the rank process; "
+                         "auto: rest when --gpus > 1")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--cpu", action="store_true",
                     help="CPU rehearsal (gloo, tiny models): allows --gpus N > 1 on a host without N GPUs")
@@ -171,6 +176,17 @@ def main() -> int:
         # 3 x 128 (profiles/shards_equal_work_8b.jsonl)
         a.shards = 1
     a.shards = max(1, a.shards)
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    rest = a.mode == "pipeline" and (a.apiserver == "rest" or (a.apiserver == "auto" and world_env > 1))
+    if rest and a.shards > 1:
+        raise SystemExit("--apiserver rest runs one operator shard per rank (no --shards)")
+    apisrv = apiurl = None
+    if rest and int(os.environ.get("RANK", "0")) == 0:
+        # the one API server of the node: its own process, started before this rank
+        # touches the GPU; the URL reaches the other ranks over the process group
+        from operator_amd.kube.fake_server import spawn as spawn_apiserver
+
+        apisrv, apiurl = spawn_apiserver(f"/tmp/oamd-bench-apiserver-{os.getpid()}.url")
     kids = spawn_shards(a) if (a.shards > 1 and not child) else []
     shard = a.shard_index or 0
     a.batch = max(1, a.batch // a.shards)   # this shard's wave (--batch is per GPU, over all shards)
@@ -254,6 +270,12 @@ def main() -> int:
     from operator_amd.utils.tracing import mark, trace_range
 
     s = settings(dev, a.max_batch, int(os.environ.get("OAMD_BENCH_WORLD", world)) if child else world)
+    if rest:   # rank r = operator shard r of `world` (run --shard-per-gpu), all on one API server
+        s.operator.shard_count, s.operator.shard_index = world, rank
+        if world > 1:
+            box = [apiurl]
+            dist.broadcast_object_list(box, src=0)
+            apiurl = box[0]
 
     def note(msg: str) -> None:   # stage progress on stderr (the JSON line stays alone on stdout)
         tag = f"rank {rank}" + (f" shard {shard}" if a.shards > 1 else "")
@@ -315,7 +337,19 @@ def main() -> int:
     lock = threading.Lock()
 
     if a.mode == "pipeline":
-        fk = FakeKube()
+        if rest:
+            from operator_amd.controller.failures import in_shard
+            from operator_amd.kube.client import KubeClient, KubeConfig
+
+            fk = KubeClient(KubeConfig(apiurl), 120.0)
+
+            def set_log(name: str, text: bytes) -> None:
+                st, _, body = fk.pool.request("PUT", f"/api/v1/namespaces/default/pods/{name}/log", text)
+                if st >= 300:
+                    raise SystemExit(f"log upload failed: {st} {body[:200]!r}")
+        else:
+            fk = FakeKube()
+            set_log = lambda name, text: fk.set_log("default", name, text)  # noqa: E731
         if pool is not None:
             matcher, explainer = PoolMatchService(pool), PoolExplainService(pool)
         else:
@@ -344,13 +378,16 @@ def main() -> int:
                 return self.inner.ready()
 
         op = Operator(fk, s, match_service=matcher, explain_service=CountingExplainer(explainer))
-        fk.create(AIPROVIDERS, {"metadata": {"name": "local-llm", "namespace": "default"},
-                                "spec": {"providerId": "local", "modelId": a.model, "maxTokens": a.max_tokens,
-                                         "temperature": 0.3, "cachingEnabled": False,
-                                         "timeoutSeconds": 3600}})
-        fk.create(PODMORTEMS, {"metadata": {"name": "bench-monitor", "namespace": "default"},
-                               "spec": {"podSelector": {"matchLabels": {"app": "bench"}}, "aiAnalysisEnabled": True,
-                                        "aiProviderRef": {"name": "local-llm"}}})
+        if not rest or rank == 0:   # cluster state, created once
+            fk.create(AIPROVIDERS, {"metadata": {"name": "local-llm", "namespace": "default"},
+                                    "spec": {"providerId": "local", "modelId": a.model, "maxTokens": a.max_tokens,
+                                             "temperature": 0.3, "cachingEnabled": False,
+                                             "timeoutSeconds": 3600}})
+            fk.create(PODMORTEMS, {"metadata": {"name": "bench-monitor", "namespace": "default"},
+                                   "spec": {"podSelector": {"matchLabels": {"app": "bench"}},
+                                            "aiAnalysisEnabled": True, "aiProviderRef": {"name": "local-llm"}}})
+        if rest and world > 1:
+            dist.barrier()
 
         def on_done(monitor, pod, outcome):
             name = pod["metadata"]["name"]
@@ -373,13 +410,26 @@ def main() -> int:
         # not operator work, and is done here, untimed. A wave is the FAILURE of its
         # pods: each pod's status flips to a terminated, non-zero exit (the MODIFIED
         # watch event the operator reacts to), and its latency is timed from there.
+        def shard_name(base: str) -> str:
+            """``base`` or the first ``base-xJ`` whose ns/name hash puts it in this rank's
+            shard (rest: every rank's pods are the failures its own operator shard owns)."""
+            if not rest or world <= 1:
+                return base
+            j, name = 0, base
+            while not in_shard({"metadata": {"namespace": "default", "name": name}}, rank, world):
+                j += 1
+                name = f"{base}-x{j}"
+            return name
+
+        names_by_wave = [[shard_name(f"app-r{rank}-s{shard}-w{w}-{i}") for i in range(a.batch)] for w in range(waves)]
+
         def wave_names(w: int) -> list[str]:
-            return [f"app-r{rank}-s{shard}-w{w}-{i}" for i in range(a.batch)]
+            return names_by_wave[w]
 
         for w in range(waves):
             for name, log in zip(wave_names(w), logs[w]):
                 fk.create(PODS, running_pod(name, labels={"app": "bench"}))
-                fk.set_log("default", name, log)
+                set_log(name, log)
         logs.clear()
 
         def inject(w: int) -> None:
@@ -542,6 +592,8 @@ def main() -> int:
                    "mode": a.mode, "hipgraph": stats1["use_graphs"], "engine_procs_per_gpu": procs,
                    "operator_shards_per_gpu": a.shards,
                    "kv_cache_dtype": "fp8_e4m3fn" if a.kv_dtype == "fp8" else "bf16",
+                   "apiserver": ("one REST API server process, rank r = operator shard r (run --shard-per-gpu)"
+                                 if rest else "in-process FakeKube per rank"),
                    "waves": "serial" if (a.serial_waves or a.mode != "pipeline") else "pipelined"},
         "detail": {"init_s": round(init_s, 1), "prefill_tokens_per_gpu": ptoks, "decode_tokens_per_gpu": dtoks,
                    # workload check: every failure carries three signatures of the scanned library, so
@@ -578,6 +630,8 @@ def main() -> int:
                 json.dump(out, f, indent=1)
     if a.mode == "pipeline":
         op.stop()
+        if rest:
+            fk.close()
     if ee is not None:
         ee.close()
     if pool is not None:
@@ -585,6 +639,9 @@ def main() -> int:
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    if apisrv is not None:
+        apisrv.terminate()
+        apisrv.wait(30)
     return 0
 
 

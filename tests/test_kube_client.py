@@ -267,3 +267,38 @@ def test_shard_supervisor_restarts_then_gives_up(monkeypatch):
     now[0] = 200.0                 # the earlier restarts leave the window
     assert sup.poll()              # two more, two within the window
     assert sup.poll() is False     # the fifth exit is the fourth within the window
+
+
+def test_shard_per_gpu_topology_analyses_each_failure_exactly_once(tmp_path):
+    """The multi-GPU production topology on the CPU: `run --shard-per-gpu --gpus 8` (eight
+    operator shard processes with stub engines) against ONE REST API server process;
+    2000 pods fail at once and every one is analysed exactly once (one
+    PodmortemAnalysisComplete Event per pod: no double, no miss), with the shared
+    Podmortem status ring written by all eight."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    from bench_plumbing import run_sharded
+
+    r = run_sharded(8, 2000, str(tmp_path), timeout_s=400)
+    assert r["analysed"] == 2000, r
+    assert r["complete_events_per_pod"] == {1: 2000}, r
+
+
+def test_shard_per_gpu_env_and_jittered_retrier():
+    """--shard-per-gpu: shard i gets cuda:i (cpu stays cpu) and no engine pool; the
+    shared status ring's 409 schedule is jittered and its delays stop doubling."""
+    import random
+
+    from operator_amd.cli import apply_shard_env, shard_device, shard_env
+    from operator_amd.config import load_settings
+    from operator_amd.controller.storage import Retrier
+
+    s = load_settings(env={})
+    s.engine.gpus = 8
+    apply_shard_env(s, shard_env({}, 3, 8, 9000, shard_device("cuda", 3)))
+    assert (s.operator.shard_index, s.operator.shard_count, s.health.port) == (3, 8, 9003)
+    assert s.engine.device == "cuda:3" and s.engine.gpus == 1
+    assert shard_device("cpu", 5) == "cpu"
+    r = Retrier(12, 0.1, jitter=0.5, rng=random.Random(0))
+    ds = [r.delay(0.1) for _ in range(200)]
+    assert 0.05 <= min(ds) < 0.07 and 0.13 < max(ds) <= 0.15
+    assert Retrier(5, 0.1).delay(0.4) == 0.4

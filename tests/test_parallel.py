@@ -149,12 +149,14 @@ def test_bench_refuses_missing_gpus():
     assert r.returncode != 0 and "visible GPUs" in r.stderr
 
 
-@pytest.mark.parametrize("shards", [1, 2])
-def test_bench_two_ranks_gloo(shards):
+@pytest.mark.parametrize("shards,apiserver", [(1, "auto"), (2, "inproc")])
+def test_bench_two_ranks_gloo(shards, apiserver):
     """bench.py as the driver launches it for N > 1 (torch.distributed.run, one rank per
     device, 127.0.0.1 rendezvous), on the CPU tier with gloo and a tiny model: rank 0
-    prints exactly one JSON line with whole-job numbers; with 2 operator shards per
-    rank (a child process each) the counts cover both shards."""
+    prints exactly one JSON line with whole-job numbers. Default (auto): the ranks are
+    the shards of ONE operator deployment on ONE REST API server process (run
+    --shard-per-gpu); inproc with 2 operator shards per rank (a child process each):
+    the counts cover both shards."""
     import json
     import subprocess
     import sys
@@ -163,7 +165,8 @@ def test_bench_two_ranks_gloo(shards):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
            "--gpus", "2", "--steps", "2", "--warmup", "1", "--model", "tiny", "--batch", str(3 * shards),
-           "--max-tokens", "4", "--prompt-tokens", "128", "--log-kb", "4", "--patterns", "40", "--shards", str(shards)]
+           "--max-tokens", "4", "--prompt-tokens", "128", "--log-kb", "4", "--patterns", "40", "--shards", str(shards),
+           "--apiserver", apiserver]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=root)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
@@ -172,3 +175,4 @@ def test_bench_two_ranks_gloo(shards):
     assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 6 * shards and out["config"]["parallelism"] == "dp2"
     assert out["config"]["operator_shards_per_gpu"] == shards
     assert out["detail"]["outcomes"] == {"ai-complete": 6 * shards} and out["value"] > 0
+    assert out["config"]["apiserver"].startswith("one REST API server" if apiserver == "auto" else "in-process")
