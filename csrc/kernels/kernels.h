@@ -45,6 +45,11 @@ int gemm_tile(const bf16_t* X, const bf16_t* W, bf16_t* Y, const bf16_t* bias, i
 // nullptr); silu_gu: fused SwiGLU (S == 1), Y [M, N/2]; nt: non-temporal weight loads.
 int gemm_pp(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, int N, int K, int S, int bm, bool silu_gu,
             bool nt, hipStream_t stream, bool one_seg = false);
+// Decode GEMM for M <= 256 with the weight stream issued WD K-steps ahead by its own waves
+// (gemm_dw.hip): one 256-row tile, BN in {64, 128} columns (N % BN == 0), S-way split-K slabs P
+// (reduced into Y unless Y is nullptr); silu_gu: fused SwiGLU (S == 1, BN == 128), Y [M, N/2].
+int gemm_dw(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, int N, int K, int S, int BN, bool silu_gu,
+            hipStream_t stream);
 // Y[M, N] = bf16(sum_s P[s][M][N]) (fp32 split-K slabs).
 int splitk_reduce(const float* P, bf16_t* Y, int64_t MN, int S, hipStream_t stream);
 // Skinny-M decode GEMM (M <= 32, gemm_skinny.hip): N % 16 == 0, K % (128 S) == 0; S-way split-K slabs P

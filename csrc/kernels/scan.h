@@ -34,4 +34,15 @@ int scan_fixup(MatchRec* matches, const uint32_t* match_count, uint32_t match_ca
 
 int max_hot_states(int log2_classes);
 
+// line_index.hip (N3): exclusive prefix excl[0..n] (excl[n] = total) of the per-segment
+// newline counts (decoupled look-back; `state` holds line_prefix_state_words(n) uint64,
+// zeroed by the launcher), newlines per document, and the +-k context windows of reported
+// events located in the resident text (q [nq, 3] = doc, offset, k; out [nq, 4] = window
+// start, window end, line start, line end, document-relative).
+int64_t line_prefix_state_words(int64_t n);
+int line_prefix(const uint32_t* cnt, int64_t n, int64_t* excl, uint64_t* state, hipStream_t stream);
+int doc_lines(const int64_t* excl, const int64_t* first, int ndocs, int64_t* doc_nl, hipStream_t stream);
+int context_spans(const uint8_t* text, const int64_t* doc_base, const int64_t* doc_len, const int64_t* q, int nq,
+                  int64_t* out, hipStream_t stream);
+
 }  // namespace oamd

@@ -349,6 +349,37 @@ py::list contexts(const std::vector<py::bytes>& docs, const std::vector<int64_t>
   return out;
 }
 
+// The same (context lines, line) tuples from windows located on the GPU (line_index.hip
+// context_spans): spans [n, 4] = (window start, window end, line start, line end) of doc
+// doc_idx[i]; the window is split at every '\n' (the GPU already found the k lines).
+py::list contexts_from_spans(const std::vector<py::bytes>& docs, const std::vector<int64_t>& doc_idx,
+                             py::array_t<int64_t, py::array::c_style | py::array::forcecast> spans) {
+  const auto dv = views(docs);
+  if (spans.ndim() != 2 || spans.shape(1) != 4 || (size_t)spans.shape(0) < doc_idx.size())
+    throw std::invalid_argument("contexts_from_spans: spans [n, 4]");
+  const int64_t* sp = spans.data();
+  py::list out(doc_idx.size());
+  for (size_t i = 0; i < doc_idx.size(); ++i) {
+    if (doc_idx[i] < 0 || doc_idx[i] >= (int64_t)dv.size()) throw std::out_of_range("contexts_from_spans: doc");
+    const auto d = dv[doc_idx[i]];
+    const int64_t* r = sp + 4 * i;
+    if (r[0] < 0 || r[0] > r[2] || r[2] > r[3] || r[3] > r[1] || r[1] > (int64_t)d.size())
+      throw std::out_of_range("contexts_from_spans: span outside its document");
+    py::list ctx;
+    size_t a = (size_t)r[0];
+    const size_t we = (size_t)r[1];
+    while (true) {
+      const void* f = a < we ? std::memchr(d.data() + a, '\n', we - a) : nullptr;
+      const size_t b = f ? (size_t)(static_cast<const char*>(f) - d.data()) : we;
+      ctx.append(decode(d.substr(a, b - a)));
+      if (!f) break;
+      a = b + 1;
+    }
+    out[i] = py::make_tuple(ctx, decode(d.substr((size_t)r[2], (size_t)(r[3] - r[2]))));
+  }
+  return out;
+}
+
 }  // namespace
 
 void register_verify(py::module_& m) {
@@ -361,4 +392,5 @@ void register_verify(py::module_& m) {
         py::arg("docs"), py::arg("regexes"));
   m.def("line_scan", &line_scan, py::arg("docs"), py::arg("regexes"), py::arg("matcher"));
   m.def("contexts", &contexts, py::arg("docs"), py::arg("doc_idx"), py::arg("offsets"), py::arg("k"));
+  m.def("contexts_from_spans", &contexts_from_spans, py::arg("docs"), py::arg("doc_idx"), py::arg("spans"));
 }

@@ -72,9 +72,56 @@ void scan_fixup(at::Tensor& matches, const at::Tensor& match_count, const at::Te
   TORCH_CHECK(rc == 0, "scan_fixup launch failed rc=", rc);
 }
 
+void line_prefix(const at::Tensor& cnt, at::Tensor& excl, at::Tensor& state) {
+  CHECK_T(cnt, at::kInt);
+  CHECK_T(excl, at::kLong);
+  CHECK_T(state, at::kLong);
+  const int64_t n = cnt.numel();
+  TORCH_CHECK(n >= 1 && excl.numel() >= n + 1, "line_prefix: excl needs n + 1 entries");
+  TORCH_CHECK(state.numel() >= ((oamd::line_prefix_state_words(n) + 1) & ~1ll), "line_prefix: state too small");
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(cnt.device());
+  const int rc = oamd::line_prefix(reinterpret_cast<const uint32_t*>(cnt.data_ptr()), n, excl.data_ptr<int64_t>(),
+                                   reinterpret_cast<uint64_t*>(state.data_ptr()),
+                                   c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream());
+  TORCH_CHECK(rc == 0, "line_prefix launch failed rc=", rc);
+}
+
+void doc_lines(const at::Tensor& excl, const at::Tensor& first, at::Tensor& doc_nl) {
+  CHECK_T(excl, at::kLong);
+  CHECK_T(first, at::kLong);
+  CHECK_T(doc_nl, at::kLong);
+  const int64_t nd = first.numel() - 1;
+  TORCH_CHECK(nd >= 1 && doc_nl.numel() >= nd, "doc_lines: doc_nl needs one entry per doc");
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(excl.device());
+  const int rc = oamd::doc_lines(excl.data_ptr<int64_t>(), first.data_ptr<int64_t>(), (int)nd,
+                                 doc_nl.data_ptr<int64_t>(), c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream());
+  TORCH_CHECK(rc == 0, "doc_lines launch failed rc=", rc);
+}
+
+void context_spans(const at::Tensor& text, const at::Tensor& doc_base, const at::Tensor& doc_len,
+                   const at::Tensor& q, at::Tensor& out) {
+  CHECK_T(text, at::kByte);
+  CHECK_T(doc_base, at::kLong);
+  CHECK_T(doc_len, at::kLong);
+  CHECK_T(q, at::kLong);
+  CHECK_T(out, at::kLong);
+  TORCH_CHECK(q.dim() == 2 && q.size(1) == 3 && out.dim() == 2 && out.size(1) == 4 && out.size(0) >= q.size(0),
+              "context_spans: q [n, 3], out [n, 4]");
+  TORCH_CHECK(doc_base.numel() == doc_len.numel(), "context_spans: doc_base / doc_len");
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(text.device());
+  const int rc = oamd::context_spans(text.data_ptr<uint8_t>(), doc_base.data_ptr<int64_t>(),
+                                     doc_len.data_ptr<int64_t>(), q.data_ptr<int64_t>(), (int)q.size(0),
+                                     out.data_ptr<int64_t>(), c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream());
+  TORCH_CHECK(rc == 0, "context_spans launch failed rc=", rc);
+}
+
 }  // namespace
 
 void register_scan_bindings(pybind11::module_& m) {
+  m.def("line_prefix", &line_prefix);
+  m.def("doc_lines", &doc_lines);
+  m.def("context_spans", &context_spans);
+  m.def("line_prefix_state_words", [](int64_t n) { return (oamd::line_prefix_state_words(n) + 1) & ~1ll; });
   m.def("ac_scan", &ac_scan);
   m.def("scan_fixup", &scan_fixup);
   m.def("max_hot_states", [](int64_t log2c) { return oamd::max_hot_states((int)log2c); });

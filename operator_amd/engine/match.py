@@ -6,10 +6,17 @@ GPU path (one call per batch of failures):
   host  : plan + pack logs into a pinned staging buffer (native, threaded)
   H2D   : one contiguous async copy
   device: ac_scan (DFA walk, LDS hot states) -> per-segment newline counts
-          -> exclusive prefix (cumsum) -> scan_fixup (doc, factor, line, offset)
+          -> line_prefix (decoupled look-back exclusive prefix) -> scan_fixup
+          (doc, factor, line, offset) -> doc_lines (newlines per doc)
   D2H   : the (small) match list
   host  : factor -> matcher expansion, regex verification of candidate lines
-          only, native event scoring, result assembly with context lines.
+          only, native event scoring (or the score_reduce kernel)
+  device: context_spans: the +-k line window of every reported event, located in
+          the text still resident from the scan; the host slices and decodes them
+          (csrc/kernels/line_index.hip, verify.cpp contexts_from_spans).
+The scan tail is eager: a captured hipGraph of it (round 3) scanned a bucket-padded
+length and cost more than the handful of launches it replaced (0.59 vs 0.40 ms per
+64-log batch, profiles/scan_graph_vs_eager.jsonl); it was removed (docs/PARITY.md).
 CPU path: the same post-processing fed by the pure-Python oracle.
 """
 from __future__ import annotations
@@ -141,7 +148,7 @@ class MatchEngine:
     def __init__(self, patterns: PatternSet | CompiledPatterns, device: str | torch.device = "cuda",
                  seg_bytes: int = 1024, max_events: int = 50, significance: float = 0.5,
                  match_cap: int = 1 << 20, grid_blocks: int = 0, use_native_scorer: bool = True,
-                 gpu_scorer: bool | None = None, profile_bytes: int = 1 << 20, scan_graphs: bool = False):
+                 gpu_scorer: bool | None = None, profile_bytes: int = 1 << 20):
         self.cp = patterns if isinstance(patterns, CompiledPatterns) else compile_patterns(patterns)
         # DFA states are renumbered by visit count over the first `profile_bytes` of
         # text scanned (0: keep breadth-first numbering), see _profile_states
@@ -164,9 +171,9 @@ class MatchEngine:
         # scan -> line index -> fixup -> per-doc newlines -> D2H as ONE captured hipGraph per
         # (segment size, segment-count bucket, doc-count bucket): one launch and one sync
         # per batch instead of ~10 launches and 3 syncs
-        self.scan_graphs = bool(scan_graphs)
-        self._graphs: dict[tuple, dict] = {}
-        self.graph_replays = 0
+        # the scan's text and doc layout stay on the GPU until the next scan: the context
+        # windows of the reported events are located there (line_index.hip context_spans)
+        self._resident: tuple | None = None
         self._lock = threading.Lock()
         self._pinned: torch.Tensor | None = None
         self._text: torch.Tensor | None = None
@@ -306,9 +313,7 @@ class MatchEngine:
         total, first = P.plan_docs([len(d) for d in docs], seg)
         n_segs = total // seg
         pinned = self._ensure("_pinned", total, torch.uint8, pinned=True)
-        use_graph = self.scan_graphs and (self._profiled or self.profile_bytes <= 0)
-        # a graph scans a bucketed length: the text buffer must hold it before the upload
-        text = self._ensure("_text", self._bucket(n_segs, 1024) * seg if self.scan_graphs else total, torch.uint8)
+        text = self._ensure("_text", total, torch.uint8)
         # pack and upload in doc-aligned chunks of >= PACK_CHUNK bytes: the host packs
         # chunk k+1 (native threads) while chunk k's DMA runs, so a large batch pays
         # max(pack, H2D) rather than the sum (BASELINE config 2: 1.2 GB)
@@ -326,12 +331,14 @@ class MatchEngine:
             text[lo:hi].copy_(pinned[lo:hi], non_blocking=True)
             a = b
         C = kernels()
-        if use_graph:
-            out = self._scan_graph(docs, first, seg, n_segs)
-            if out is not None:
-                return out
         seg_nl = self._ensure("_seg_nl", 2 * n_segs, torch.int32)   # totals, then split-segment heads
         first_t = torch.tensor(first, dtype=torch.int64).to(self.device, non_blocking=True)
+        # N3 on the GPU: exclusive newline prefix per segment (decoupled look-back scan),
+        # match records -> (doc, factor, line, offset), newlines per doc
+        excl = self._ensure("_nl_excl", n_segs + 1, torch.int64)
+        lp_state = self._ensure("_lp_state", C.line_prefix_state_words(n_segs), torch.int64)
+        doc_nl = self._ensure("_doc_nl", len(docs), torch.int64)
+        doc_nl_h = self._ensure("_doc_nl_h", len(docs), torch.int64, pinned=True)
         while True:
             if self._matches is None or self._matches.shape[0] < self.match_cap:
                 self._matches = torch.empty(self.match_cap, 4, dtype=torch.int32, device=self.device)
@@ -340,10 +347,8 @@ class MatchEngine:
             self._count.zero_()
             C.ac_scan(text[:total], seg, self.cls_map, self.table, self.log2c, self.hot_states, self.out_off,
                       self.out_ids, self._matches, self._count, seg_nl, self.grid_blocks, self.hot_table)
-            nl = seg_nl[:n_segs].to(torch.int64)
-            incl = torch.cumsum(nl, 0)
-            excl = incl - nl
-            C.scan_fixup(self._matches, self._count, excl, first_t, seg, seg_nl[n_segs:2 * n_segs])
+            C.line_prefix(seg_nl[:n_segs], excl, lp_state)
+            C.scan_fixup(self._matches, self._count, excl[:n_segs], first_t, seg, seg_nl[n_segs:2 * n_segs])
             cnt = int(self._count.item())
             if cnt <= self._matches.shape[0]:
                 break
@@ -351,101 +356,34 @@ class MatchEngine:
             self._matches = None
         # newlines per doc from the per-segment counts the scan already produced (the
         # host would otherwise re-read every byte for AnalysisResult.metadata.totalLines)
-        pre = torch.cat([incl.new_zeros(1), incl])
-        doc_nl = pre[first_t[1:]] - pre[first_t[:-1]]
+        C.doc_lines(excl, first_t, doc_nl)
+        doc_nl_h[:len(docs)].copy_(doc_nl[:len(docs)], non_blocking=True)
         self.stats.raw_matches += cnt
         self.stats.bytes_scanned += sum(len(d) for d in docs)
         hits = self._matches[:cnt].cpu().numpy().astype(np.int64) if cnt else np.zeros((0, 4), np.int64)
-        self._doc_newlines = (docs, doc_nl.cpu().tolist())
+        self._doc_newlines = (docs, doc_nl_h[:len(docs)].tolist())
+        self._resident = (docs, first_t, seg, text)
         return hits
 
-    GRAPH_MATCH_ROWS = 1 << 15   # match records copied back inside the graph (more: one extra copy)
-    MAX_GRAPHS = 16
+    def _contexts_gpu(self, docs: list[bytes], q_doc: list[int], q_off: list[int], q_k: list[int]):
+        """Context windows of the reported events located in the text the last GPU scan
+        left resident (None when that scan was not of ``docs``: the host path)."""
+        from operator_amd.ops import kernels, patterns
 
-    @staticmethod
-    def _bucket(n: int, floor: int) -> int:
-        """n rounded up to a 1/8-octave step (<= 12.5 % padding), at least ``floor``."""
-        n = max(n, floor)
-        step = max(1, 1 << max(0, n.bit_length() - 4))
-        return -(-n // step) * step
-
-    def _scan_graph(self, docs: list[bytes], first: list[int], seg: int, n_segs: int) -> np.ndarray | None:
-        """The captured-graph form of the scan tail (the text is already uploaded)."""
-        from operator_amd.ops import kernels
-
-        C = kernels()
-        nsb = self._bucket(n_segs, 1024)
-        ndb = self._bucket(len(first), 8)           # doc boundaries (docs + 1)
-        total, total_b = n_segs * seg, nsb * seg
-        key = (seg, nsb, ndb, self.match_cap)
-        text = self._text                             # sized for the bucket by _scan_gpu, text uploaded
-        g = self._graphs.get(key)
-        if g is not None and g["text_ptr"] != text.data_ptr():
-            self._graphs.clear()                      # buffers moved: every graph is stale
-            g = None
-        if total_b > total:                           # padding segments must scan as NULs
-            text[total:total_b].zero_()
-        fpad = first + [first[-1]] * (ndb - len(first))
-        if g is None:
-            if len(self._graphs) >= self.MAX_GRAPHS:
-                self._graphs.pop(next(iter(self._graphs)))
-            if self._matches is None or self._matches.shape[0] < self.match_cap:
-                self._matches = torch.empty(self.match_cap, 4, dtype=torch.int32, device=self.device)
-            if self._count is None:
-                self._count = torch.zeros(1, dtype=torch.int32, device=self.device)
-            K = min(self.match_cap, self.GRAPH_MATCH_ROWS)
-            g = {"text_ptr": text.data_ptr(), "K": K,
-                 "first_h": torch.empty(ndb, dtype=torch.int64, pin_memory=True),
-                 "first_d": torch.empty(ndb, dtype=torch.int64, device=self.device),
-                 "seg_nl": torch.empty(2 * nsb, dtype=torch.int32, device=self.device),
-                 "cnt_h": torch.empty(1, dtype=torch.int32, pin_memory=True),
-                 "m_h": torch.empty(K, 4, dtype=torch.int32, pin_memory=True),
-                 "nl_h": torch.empty(ndb - 1, dtype=torch.int64, pin_memory=True)}
-            g["first_h"].copy_(torch.tensor(fpad, dtype=torch.int64))
-            g["first_d"].copy_(g["first_h"], non_blocking=True)
-            matches, count = self._matches, self._count
-
-            def body():
-                count.zero_()
-                C.ac_scan(text[:total_b], seg, self.cls_map, self.table, self.log2c, self.hot_states, self.out_off,
-                          self.out_ids, matches, count, g["seg_nl"], self.grid_blocks, self.hot_table)
-                nl = g["seg_nl"][:nsb].to(torch.int64)
-                incl = torch.cumsum(nl, 0)
-                C.scan_fixup(matches, count, incl - nl, g["first_d"], seg, g["seg_nl"][nsb:2 * nsb])
-                pre = torch.cat([incl.new_zeros(1), incl])
-                fd = g["first_d"]
-                g["cnt_h"].copy_(count, non_blocking=True)
-                g["m_h"].copy_(matches[:K], non_blocking=True)
-                g["nl_h"].copy_(pre[fd[1:]] - pre[fd[:-1]], non_blocking=True)
-
-            body()                                    # warm-up run on the stream, then capture
-            self._stream.synchronize()
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph, stream=self._stream):
-                body()
-            g["graph"] = graph
-            # the graph holds raw pointers: keep every buffer it reads or writes alive
-            g["refs"] = (matches, count, self.cls_map, self.table, self.out_off, self.out_ids, self.hot_table)
-            self._graphs[key] = g
-        else:
-            g["first_h"].copy_(torch.tensor(fpad, dtype=torch.int64))
-            g["first_d"].copy_(g["first_h"], non_blocking=True)
-        g["graph"].replay()
-        self._stream.synchronize()
-        self.graph_replays += 1
-        cnt = int(g["cnt_h"][0])
-        if cnt > self._matches.shape[0]:              # overflow: grow, and the eager path rescans
-            self.match_cap = int(cnt * 1.25) + 1024
-            self._matches = None
+        r = self._resident
+        if r is None or r[0] is not docs or not q_doc:
             return None
-        if cnt <= g["K"]:
-            hits = g["m_h"][:cnt].numpy().astype(np.int64)
-        else:
-            hits = self._matches[:cnt].cpu().numpy().astype(np.int64)
-        self.stats.raw_matches += cnt
-        self.stats.bytes_scanned += sum(len(d) for d in docs)
-        self._doc_newlines = (docs, g["nl_h"][:len(docs)].tolist())
-        return hits
+        _, first_t, seg, text = r
+        n = len(q_doc)
+        q = torch.tensor(np.stack([np.asarray(q_doc, np.int64), np.asarray(q_off, np.int64),
+                                   np.asarray(q_k, np.int64)], 1)).to(self.device, non_blocking=True)
+        lens = torch.tensor([len(d) for d in docs], dtype=torch.int64).to(self.device, non_blocking=True)
+        base = first_t[:-1] * seg
+        out = torch.empty(n, 4, dtype=torch.int64, device=self.device)
+        with self._on_stream():
+            kernels().context_spans(text, base, lens, q, out)
+            spans = out.cpu().numpy()
+        return patterns().contexts_from_spans(docs, q_doc, spans)
 
     def scan_cpu(self, docs: list[bytes]) -> np.ndarray:
         """Same contract as scan_gpu, computed with Python (used without a GPU)."""
@@ -638,7 +576,9 @@ class MatchEngine:
                 q_doc.extend([di] * len(o_))
                 q_off.extend(o_)
                 q_k.extend(k_)
-            ctxs = patterns().contexts(docs, q_doc, q_off, q_k) if q_doc else []
+            ctxs = self._contexts_gpu(docs, q_doc, q_off, q_k)
+            if ctxs is None:
+                ctxs = patterns().contexts(docs, q_doc, q_off, q_k) if q_doc else []
             t_ctx = time.perf_counter()
             out = []
             j = 0

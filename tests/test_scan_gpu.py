@@ -138,23 +138,102 @@ def test_profiled_state_order_gives_identical_scan():
     assert _rows(b.scan_gpu(docs[::-1])) == _rows(a.scan_gpu(docs[::-1]))
 
 
-def test_scan_graph_replays_equal_eager_scans():
-    """The captured scan tail (scan_graphs=True) returns what the eager launches return,
-    across batches that share a graph bucket and batches that need a new one, and it
-    falls back to the eager rescan on match overflow."""
-    ps = synthetic_library(400, seed=1)
-    fac = LogFactory(n_patterns=400, seed=6)
-    batches = [fac.batch(n, kb * 1024, n_failures=3, seed=s)[0]
-               for n, kb, s in ((32, 16, 1), (32, 16, 2), (30, 17, 3), (64, 64, 4), (5, 3, 5))]
-    eager = MatchEngine(ps, device="cuda", seg_bytes=1024, scan_graphs=False, profile_bytes=0)
-    graph = MatchEngine(ps, device="cuda", seg_bytes=1024, scan_graphs=True, profile_bytes=0)
-    for docs in batches + batches[:2]:
-        assert _rows(graph.scan_gpu(docs)) == _rows(eager.scan_gpu(docs))
-        ra = [r.metadata["totalLines"] for r in graph.analyze(docs)]
-        assert ra == [d.count(b"\n") + 1 for d in docs]
-    assert graph.graph_replays >= 10 and eager.graph_replays == 0
-    assert len(graph._graphs) < 2 * len(batches)
+def test_line_prefix_equals_cumsum_and_replays():
+    """line_prefix (decoupled look-back scan, line_index.hip) == an exclusive cumsum for
+    tile-boundary lengths, twice on the same state buffer (the launcher's memset makes it
+    replay-safe); doc_lines == per-doc differences."""
+    from operator_amd.ops import kernels
+
+    C = kernels()
+    g = torch.Generator(device="cpu").manual_seed(7)
+    for n in (1, 100, 4095, 4096, 4097, 262145, 1000003):
+        cnt = torch.randint(0, 50, (n,), generator=g, dtype=torch.int32).cuda()
+        ref = torch.cat([torch.zeros(1, dtype=torch.int64), torch.cumsum(cnt.cpu().to(torch.int64), 0)])
+        excl = torch.full((n + 1,), -1, dtype=torch.int64, device="cuda")
+        st = torch.empty(C.line_prefix_state_words(n), dtype=torch.int64, device="cuda")
+        for _ in range(2):
+            C.line_prefix(cnt, excl, st)
+            assert torch.equal(excl.cpu(), ref), n
+        first = torch.tensor(sorted({0, n} | set(torch.randint(0, n + 1, (5,), generator=g).tolist())),
+                             dtype=torch.int64)
+        dn = torch.empty(len(first) - 1, dtype=torch.int64, device="cuda")
+        C.doc_lines(excl, first.cuda(), dn)
+        assert dn.cpu().tolist() == [int(ref[b] - ref[a]) for a, b in zip(first[:-1], first[1:])]
+
+
+def test_context_spans_equal_host_contexts():
+    """The +-k windows located on the GPU (context_spans + contexts_from_spans) equal the
+    host's native `contexts` for every kind of edge: empty lines, lines longer than a
+    64-byte step, a leading newline, no trailing newline, offsets at 0 / len / on a
+    newline, k = 0..5 — and MatchEngine.analyze uses them for its results."""
+    import random
+
+    from operator_amd.ops import kernels, patterns
+
+    rng = random.Random(11)
+
+    def line():
+        n = rng.choice([0, 0, 3, 20, 63, 64, 65, 130, 700])
+        return bytes(rng.choice(b"abcdefgh \t\xc3\xa9") for _ in range(n))
+
+    docs = []
+    for i in range(40):
+        ls = [line() for _ in range(rng.randrange(0, 30))]
+        d = b"\n".join(ls)
+        if i % 3 == 0:
+            d = b"\n" + d
+        if i % 4 == 1:
+            d = d + b"\n"
+        docs.append(d)
+    docs[5] = b""
+    docs[6] = b"\n\n\n"
+    seg = 256
+    P = patterns()
+    total, first = P.plan_docs([len(d) for d in docs], seg)
+    buf = bytearray(total)
+    for d, f in zip(docs, first):
+        buf[f * seg:f * seg + len(d)] = d
+    text = torch.frombuffer(buf, dtype=torch.uint8).cuda()
+    q_doc, q_off, q_k = [], [], []
+    for di, d in enumerate(docs):
+        offs = {0, len(d)} | {rng.randrange(0, len(d) + 1) for _ in range(6)} | \
+               {i for i, c in enumerate(d) if c == 10 and rng.random() < 0.3}
+        for o in sorted(offs):
+            q_doc.append(di)
+            q_off.append(o)
+            q_k.append(rng.randrange(0, 6))
+    q = torch.tensor(list(zip(q_doc, q_off, q_k)), dtype=torch.int64).cuda()
+    out = torch.empty(len(q_doc), 4, dtype=torch.int64, device="cuda")
+    base = torch.tensor(first[:-1], dtype=torch.int64).cuda() * seg
+    lens = torch.tensor([len(d) for d in docs], dtype=torch.int64).cuda()
+    kernels().context_spans(text, base, lens, q, out)
+    got = P.contexts_from_spans(docs, q_doc, out.cpu().numpy())
+    want = P.contexts(docs, q_doc, q_off, q_k)
+    assert got == want
+    # through the engine: eager analyze locates its windows on the GPU, same results as the host
+    ps = synthetic_library(200, seed=3)
+    fac = LogFactory(n_patterns=200, seed=9)
+    bdocs = fac.batch(24, 8 * 1024, n_failures=3, seed=2)[0]
+    eng = MatchEngine(ps, device="cuda", seg_bytes=1024, profile_bytes=0)
+    calls = {"n": 0}
+    orig = eng._contexts_gpu
+
+    def spy(*a):
+        r = orig(*a)
+        calls["n"] += r is not None
+        return r
+    eng._contexts_gpu = spy
+    gpu = [r.to_obj() for r in eng.analyze(bdocs)]
+    assert calls["n"] == 1
+    host = MatchEngine(ps, device="cpu").analyze(bdocs)
+    for a, b in zip(gpu, host):
+        b = b.to_obj()
+        assert [e["context"] for e in a["events"]] == [e["context"] for e in b["events"]]
+        assert a["metadata"]["totalLines"] == b["metadata"]["totalLines"]
+
+
+def test_scan_match_overflow_regrows():
     small = MatchEngine(PatternSet.from_dicts([{"id": "e", "primary_pattern": {"literal": "e"}}]), device="cuda",
                         seg_bytes=256, match_cap=64, profile_bytes=0)
     assert small.scan_gpu([b"eee\n" * 500]).shape[0] == 1500 and small.match_cap >= 1500
-    assert small.scan_gpu([b"eee\n" * 500]).shape[0] == 1500   # the grown cap: a graph again
+    assert small.scan_gpu([b"eee\n" * 500]).shape[0] == 1500
