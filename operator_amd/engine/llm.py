@@ -21,7 +21,6 @@ from __future__ import annotations
 import contextlib
 import gc
 import itertools
-import os
 import threading
 import time
 from collections import deque
@@ -89,11 +88,10 @@ class EngineStats:
     no_pipeline: dict = field(default_factory=dict)   # why a window was not queued ahead
 
 
-# Decode-window waits spin (the default event). OAMD_BLOCKING_WAIT=1 parks the engine
-# thread in the driver instead (hipEventBlockingSync); measured A/B on one MI355X box,
-# 5-step flagship: blocking 29.37 / 29.25 vs spinning 29.43 / 29.44 analyses/s
-# (profiles/blocking_wait_ab.txt), so spinning stays the default.
-_BLOCKING_WAIT = os.environ.get("OAMD_BLOCKING_WAIT", "0") == "1"
+# Decode-window waits spin (the default event). Parking the engine thread in the driver
+# (hipEventBlockingSync) measured slower on one MI355X box, 5-step flagship: blocking
+# 29.37 / 29.25 vs spinning 29.43 / 29.44 analyses/s (profiles/blocking_wait_ab.txt), so
+# the blocking variant was removed.
 
 
 @dataclass
@@ -727,7 +725,7 @@ class LLMEngine:
             self._hb ^= 1
             host = self._host_bufs[self._hb]
             host[:B, :k].copy_(st.hist[:B, :k], non_blocking=True)
-            ev = torch.cuda.Event(blocking=_BLOCKING_WAIT)
+            ev = torch.cuda.Event()
             ev.record()
         else:
             host, ev = st.hist, None
