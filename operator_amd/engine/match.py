@@ -178,6 +178,10 @@ class MatchEngine:
         self._pinned: torch.Tensor | None = None
         self._text: torch.Tensor | None = None
         self._seg_nl: torch.Tensor | None = None
+        self._nl_excl: torch.Tensor | None = None
+        self._lp_state: torch.Tensor | None = None
+        self._doc_nl: torch.Tensor | None = None
+        self._doc_nl_h: torch.Tensor | None = None
         self._matches: torch.Tensor | None = None
         self._count: torch.Tensor | None = None
         self._doc_newlines: tuple[list[bytes], list[int]] | None = None   # (docs, newlines) of the last GPU scan
