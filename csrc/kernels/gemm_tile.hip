@@ -318,7 +318,10 @@ __device__ __forceinline__ void mfma_tied(f32x4& acc, const u16x8& a, const u16x
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 
-template <int EPI>
+// DM: how the stages are loaded — 0: global_load_lds (flat address per lane), 1: buffer_load
+// ... lds (SGPR descriptor, 32-bit lane offset, K step in soffset), 2: timing experiment only,
+// no loads inside the loop (wrong results; isolates the loop's DMA issue cost)
+template <int EPI, int DM = 0>
 __global__ void __launch_bounds__(256) gemm_tile256_r4_kernel(const bf16_t* __restrict__ X,
                                                               const bf16_t* __restrict__ W, bf16_t* __restrict__ Y,
                                                               const bf16_t* __restrict__ bias, int M, int N, int K,
@@ -351,16 +354,27 @@ __global__ void __launch_bounds__(256) gemm_tile256_r4_kernel(const bf16_t* __re
   }
   const char* Xb = reinterpret_cast<const char*>(X);
   const char* Wb = reinterpret_cast<const char*>(W);
+  const auto xr = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)((uint32_t)M * (uint32_t)K * 2u), 0x00020000);
+  const auto wr = __builtin_amdgcn_make_buffer_rsrc((void*)W, (short)0, (int)((uint32_t)N * (uint32_t)K * 2u), 0x00020000);
   auto dma = [&](int kt, int buf, int q) {   // piece q (0..7) of this wave for K-step kt, into buffer buf
     char* dst = lds + buf * kStage + w * 1024;
     const uint32_t k2 = (uint32_t)kt * (kBK4 * 2);
-    if (q < 4)
-      __builtin_amdgcn_global_load_lds(Xb + xs[q] + k2, (__attribute__((address_space(3))) void*)(dst + q * 4096),
-                                       16, 0, 0);
-    else
-      __builtin_amdgcn_global_load_lds(Wb + ws[q - 4] + k2,
-                                       (__attribute__((address_space(3))) void*)(dst + kWOff + (q - 4) * 4096), 16, 0,
-                                       0);
+    if constexpr (DM == 1) {
+      if (q < 4)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)(dst + q * 4096), 16,
+                                                 (int)xs[q], (int)k2, 0, 0);
+      else
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (__attribute__((address_space(3))) void*)(dst + kWOff + (q - 4) * 4096),
+                                                 16, (int)ws[q - 4], (int)k2, 0, 0);
+    } else {
+      if (q < 4)
+        __builtin_amdgcn_global_load_lds(Xb + xs[q] + k2, (__attribute__((address_space(3))) void*)(dst + q * 4096),
+                                         16, 0, 0);
+      else
+        __builtin_amdgcn_global_load_lds(Wb + ws[q - 4] + k2,
+                                         (__attribute__((address_space(3))) void*)(dst + kWOff + (q - 4) * 4096), 16, 0,
+                                         0);
+    }
   };
 
   // fragment reads: X fragment i = piece wm*8 + i; W fragment j = the rows of feature
@@ -397,7 +411,7 @@ __global__ void __launch_bounds__(256) gemm_tile256_r4_kernel(const bf16_t* __re
 #pragma unroll
       for (int j = 0; j < 8; ++j) mfma_tied(acc[i][j], wf[j], xf[i]);
       __builtin_amdgcn_sched_barrier(0);
-      dma(ks, kb, i);
+      if constexpr (DM != 2) dma(ks, kb, i);
       rd1(kt + 1, nx, nw, 2 * i);
       rd1(kt + 1, nx, nw, 2 * i + 1);
       __builtin_amdgcn_sched_barrier(0);
@@ -537,6 +551,9 @@ int gemm_tile(const bf16_t* X, const bf16_t* W, bf16_t* Y, const bf16_t* bias, i
     if (silu_gu) gemm_tile256_r4_kernel<kEpiSilu><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
     else if (bias) gemm_tile256_r4_kernel<kEpiBias><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
     else gemm_tile256_r4_kernel<kEpiStore><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+  } else if ((variant == 4 || variant == 5) && off32 && !silu_gu && !bias) {   // ring-4 load experiments
+    if (variant == 4) gemm_tile256_r4_kernel<kEpiStore, 1><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+    else gemm_tile256_r4_kernel<kEpiStore, 2><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
   } else if (variant == 2 || (variant == 0 && M > 256)) {
     // 8-wave ping-pong, two barrier segments per K-tile: 1.8-2.7 % over four segments on
     // the prefill shapes (M = 32k, profiles/gemm_tile_ph2_vs_ph4.jsonl); the lm_head at

@@ -40,10 +40,16 @@ def ai_enabled(monitor: dict) -> bool:
     return enabled is True and spec.get("aiProviderRef") is not None
 
 
-def get_provider(kube, monitor: dict) -> dict | None:
+def get_provider(kube, monitor: dict, cache=None) -> dict | None:
+    """The monitor's AIProvider: from the informer cache when it holds it, else a GET (the
+    reference GETs on every analysis, PodFailureWatcher.java:510-559)."""
     name, ns = provider_ref(monitor)
     if name is None:
         return None
+    if cache is not None:
+        p = cache.get(name, ns)
+        if p is not None:
+            return p
     try:
         p = kube.get(AIPROVIDERS, name, ns)
         if p is None:

@@ -110,6 +110,8 @@ class Operator:
         """Watcher, informer and reconcilers: what only the leader runs."""
         s, kube = self.settings, self.kube
         self.monitors = MonitorCache(kube)
+        self.providers = MonitorCache(kube, res=AIPROVIDERS)   # AIProvider lookups of the analysis pipeline
+        self.pipeline.provider_cache = self.providers
         shard = (s.operator.shard_index, s.operator.shard_count)
         if not 0 <= shard[0] < max(1, shard[1]):
             raise ValueError(f"operator.shard_index {shard[0]} outside 0..{shard[1] - 1}")
@@ -135,6 +137,7 @@ class Operator:
             self._workers_used = True
             # watch before the controllers' first reconcile pass, so a failure is seen by one or the other
             self.monitors.start()
+            self.providers.start()
             self.watcher.start()
             for c in self.controllers:
                 c.start()
@@ -148,6 +151,7 @@ class Operator:
             for c in self.controllers:
                 c.stop()
             self.monitors.stop()
+            self.providers.stop()
             self._workers_running = False
 
     @property

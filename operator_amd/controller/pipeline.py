@@ -45,6 +45,7 @@ class AnalysisPipeline:
                  status: StatusWriter, executor: Executor | None = None, metrics=None,
                  log_container: str | None = None, log_previous: bool = False, log_limit_bytes: int | None = None,
                  sink_concurrency: int = 0):
+        self.provider_cache = None   # Operator sets its AIProvider informer cache (MonitorCache)
         self.kube, self.matcher, self.explainer = kube, matcher, explainer
         self._sinks = threading.BoundedSemaphore(sink_concurrency) if sink_concurrency > 0 else None
         self.events, self.storage, self.status = events, storage, status
@@ -129,7 +130,7 @@ class AnalysisPipeline:
                 self.events.emit_analysis_complete(pod, monitor, result, "AI disabled")
             return "pattern-only"
         try:
-            provider = ai_client.get_provider(self.kube, monitor)
+            provider = ai_client.get_provider(self.kube, monitor, self.provider_cache)
         except Exception as e:  # noqa: BLE001 (executor-level failure)
             md = pod.get("metadata") or {}
             log.warning("AI provider lookup for pod %s/%s failed: %s", md.get("namespace"), md.get("name"), e)

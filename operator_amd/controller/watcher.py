@@ -39,14 +39,17 @@ def parse_namespaces(value: str | None) -> list[str]:
 
 
 class MonitorCache:
-    """Informer-style cache of Podmortem objects (list + watch, kube/informer.WatchLoop)."""
+    """Informer-style cache of Podmortem objects (list + watch, kube/informer.WatchLoop);
+    with ``res`` = AIPROVIDERS the same cache serves the analysis pipeline's AIProvider
+    lookups (one API GET per analysis saved; a miss still falls back to a GET)."""
 
-    def __init__(self, kube, restart_delay_s: float = 1.0):
+    def __init__(self, kube, restart_delay_s: float = 1.0, res=PODMORTEMS):
         self.kube = kube
+        self.res = res
         self._objs: dict[tuple, dict] = {}
         self._lock = threading.Lock()
-        self._loop = WatchLoop(kube, PODMORTEMS, None, self._on_event, relist=self._replace_all,
-                               name="podmortem-cache", restart_delay_s=restart_delay_s, max_delay_s=30.0)
+        self._loop = WatchLoop(kube, res, None, self._on_event, relist=self._replace_all,
+                               name=f"{res.plural}-cache", restart_delay_s=restart_delay_s, max_delay_s=30.0)
         self._thread: threading.Thread | None = None
         self.synced = threading.Event()
 
@@ -56,7 +59,7 @@ class MonitorCache:
 
     def start(self) -> None:
         self._replace_all(self._loop.list_now())
-        self._thread = threading.Thread(target=self._loop.run, name="podmortem-cache", daemon=True)
+        self._thread = threading.Thread(target=self._loop.run, name=f"{self.res.plural}-cache", daemon=True)
         self._thread.start()
 
     def _replace_all(self, items: list[dict]) -> None:
@@ -77,6 +80,10 @@ class MonitorCache:
     def list(self) -> list[dict]:
         with self._lock:
             return list(self._objs.values())
+
+    def get(self, name: str, namespace: str | None) -> dict | None:
+        with self._lock:
+            return self._objs.get((namespace or "", name))
 
 
 class PodFailureWatcher:

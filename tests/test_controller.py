@@ -551,7 +551,7 @@ def test_sink_concurrency_bounds_result_writers(monkeypatch):
     from operator_amd.controller import ai_client
     from operator_amd.controller.pipeline import AnalysisPipeline
 
-    monkeypatch.setattr(ai_client, "get_provider", lambda kube, m: {"spec": {}})
+    monkeypatch.setattr(ai_client, "get_provider", lambda kube, m, cache=None: {"spec": {}})
     monkeypatch.setattr(ai_client, "to_provider_config", lambda kube, p: AIProviderConfig())
     state = {"now": 0, "max": 0, "stored": 0}
     lock = threading.Lock()
