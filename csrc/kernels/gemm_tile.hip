@@ -319,8 +319,9 @@ __device__ __forceinline__ void mfma_tied(f32x4& acc, const u16x8& a, const u16x
 }
 
 // DM: how the stages are loaded — 0: global_load_lds (flat address per lane), 1: buffer_load
-// ... lds (SGPR descriptor, 32-bit lane offset, K step in soffset), 2: timing experiment only,
-// no loads inside the loop (wrong results; isolates the loop's DMA issue cost)
+// ... lds (SGPR descriptor, 32-bit lane offset, K step in soffset). Timing experiments only
+// (wrong results): 2 no loads inside the loop; 3 every piece read from 1 KiB of contiguous
+// memory; 4 the 8 pieces issued back to back after the first MFMA row; 5 W pieces only
 template <int EPI, int DM = 0>
 __global__ void __launch_bounds__(256) gemm_tile256_r4_kernel(const bf16_t* __restrict__ X,
                                                               const bf16_t* __restrict__ W, bf16_t* __restrict__ Y,
@@ -366,6 +367,10 @@ __global__ void __launch_bounds__(256) gemm_tile256_r4_kernel(const bf16_t* __re
       else
         __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (__attribute__((address_space(3))) void*)(dst + kWOff + (q - 4) * 4096),
                                                  16, (int)ws[q - 4], (int)k2, 0, 0);
+    } else if constexpr (DM == 3) {
+      const char* base = (q < 4 ? Xb : Wb) + (uint32_t)(w * 8 + q) * 1024u + (uint32_t)lane * 16u + k2 * 64u;
+      __builtin_amdgcn_global_load_lds(base, (__attribute__((address_space(3))) void*)(dst + (q < 4 ? q * 4096 : kWOff + (q - 4) * 4096)),
+                                       16, 0, 0);
     } else {
       if (q < 4)
         __builtin_amdgcn_global_load_lds(Xb + xs[q] + k2, (__attribute__((address_space(3))) void*)(dst + q * 4096),
@@ -411,7 +416,15 @@ __global__ void __launch_bounds__(256) gemm_tile256_r4_kernel(const bf16_t* __re
 #pragma unroll
       for (int j = 0; j < 8; ++j) mfma_tied(acc[i][j], wf[j], xf[i]);
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (DM != 2) dma(ks, kb, i);
+      if constexpr (DM == 4) {
+        if (i == 0)
+#pragma unroll
+          for (int q = 0; q < 8; ++q) dma(ks, kb, q);
+      } else if constexpr (DM == 5) {
+        if (i >= 4) dma(ks, kb, i);
+      } else if constexpr (DM != 2) {
+        dma(ks, kb, i);
+      }
       rd1(kt + 1, nx, nw, 2 * i);
       rd1(kt + 1, nx, nw, 2 * i + 1);
       __builtin_amdgcn_sched_barrier(0);
@@ -456,6 +469,182 @@ __global__ void __launch_bounds__(256) gemm_tile256_r4_kernel(const bf16_t* __re
   asm volatile("s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
 
   const int l15 = lane & 15, lq = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int tok = m0 + wm * 128 + i * 16 + l15;
+    if (tok >= M) continue;
+    bf16_t* yrow = Y + (int64_t)tok * ldy;
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        if constexpr (EPI == kEpiSilu) {
+          const int col = (n0 >> 1) + f * 64 + wn * 32 + j * 16 + 4 * lq;
+          if (2 * col >= N) continue;
+          const f32x4 gt = acc[i][f * 4 + j], up = acc[i][f * 4 + 2 + j];
+          f32x4 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float gg = bf2f(f2bf(gt[r]));
+            const float uu = bf2f(f2bf(up[r]));
+            const float sg = bf2f(f2bf(gg / (1.f + __expf(-gg))));
+            o[r] = sg * uu;
+          }
+          *reinterpret_cast<uint2*>(yrow + col) = pack4(o);
+        } else {
+#pragma unroll
+          for (int ty = 0; ty < 2; ++ty) {
+            const int col = n0 + f * 128 + ty * 64 + wn * 32 + j * 16 + 4 * lq;
+            if (col >= N) continue;
+            f32x4 v = acc[i][f * 4 + ty * 2 + j];
+            if constexpr (EPI == kEpiBias) {
+              const uint2 bb = *reinterpret_cast<const uint2*>(bias + col);
+              v[0] += __uint_as_float(bb.x << 16);
+              v[1] += __uint_as_float(bb.x & 0xffff0000u);
+              v[2] += __uint_as_float(bb.y << 16);
+              v[3] += __uint_as_float(bb.y & 0xffff0000u);
+            }
+            *reinterpret_cast<uint2*>(yrow + col) = pack4(v);
+          }
+        }
+      }
+  }
+}
+
+// Variant 9 ("region ring"): four waves (one per SIMD, 128 x 128 outputs each, 256 tied
+// AGPR accumulators) with BK = 64 K-tiles loaded in full 128-B row segments: measured on
+// the ring-4 kernel, an LDS-DMA instruction of 16 rows x 64 B costs about twice what one of
+// 8 rows x 128 B does (the memory pipeline's request count, not the bytes: M 16384, N 4096,
+// K 14336: 1.25 PF/s with 64-B segments, 1.57 with 1-KiB contiguous pieces, 1.80 with no
+// loads at all; tools/gemm_tile_variants.py). A 64-deep tile is 64 KiB, so the ring is cut
+// into 16 KiB regions (X rows 0-127, X 128-255, W 0-127, W 128-255 of a tile): 10 regions
+// (160 KiB) = 2.5 tiles. Region i = 4 * tile + r lives in slot i % 10; while tile t is
+// computed the waves issue regions 4t+6 .. 4t+9 (tile t+1's second half, tile t+2's first)
+// into tile t-1's slots, and the counted vmcnt(8) at the end of tile t leaves exactly the
+// two youngest regions in flight. One raw barrier per tile. LDS image: 128-B rows with the
+// chunk ^ ((row >> 1) & 7) swizzle on the DMA source and the read (conflict-free b128).
+template <int EPI>
+__global__ void __launch_bounds__(256) gemm_tile256_q4_kernel(const bf16_t* __restrict__ X,
+                                                              const bf16_t* __restrict__ W, bf16_t* __restrict__ Y,
+                                                              const bf16_t* __restrict__ bias, int M, int N, int K,
+                                                              int ldy) {
+  constexpr int kSlots = 10;
+  __shared__ __attribute__((aligned(1024))) char lds[kSlots * kRegion];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 1, wn = w & 1;
+
+  const int mt = (M + kT - 1) / kT, nt = (N + kT - 1) / kT;
+  const int nwg = mt * nt;
+  const int lid = xcd_remap(blockIdx.x, nwg);
+  const int gsz = kGroupM * nt;
+  const int first_m = (lid / gsz) * kGroupM;
+  const int gm = min(mt - first_m, kGroupM);
+  const int tm = first_m + (lid % gsz) % gm;
+  const int tn = (lid % gsz) / gm;
+  const int m0 = tm * kT, n0 = tn * kT;
+
+  // DMA: region r (0: X rows 0-127, 1: X 128-255, 2: W 0-127, 3: W 128-255), piece q (0..3)
+  // of wave w = region rows 8 (w + 4q) .. +7; lane l -> row + l/8, LDS slot l%8, source
+  // chunk slot ^ ((row >> 1) & 7). 32-bit byte offsets (the launcher checks the extents).
+  const int lrow = lane >> 3, lslot = lane & 7;
+  uint32_t so[4][4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = 8 * (w + 4 * q) + lrow;
+      const int chunk = lslot ^ ((row >> 1) & 7);
+      const int g = (r < 2) ? min(m0 + 128 * r + row, M - 1) : min(n0 + 128 * (r - 2) + row, N - 1);
+      so[r][q] = ((uint32_t)g * (uint32_t)K + chunk * 8) * 2u;
+    }
+  const char* Xb = reinterpret_cast<const char*>(X);
+  const char* Wb = reinterpret_cast<const char*>(W);
+  const int T = K / kBK;
+  // region i (tile i / 4, part i % 4); past the last tile it re-loads tile T-1 (its slot is
+  // free and never read again), so every tile issues the same number of DMAs
+  auto dma = [&](int i, int q) {
+    const int r = i & 3;
+    const int kt = min(i >> 2, T - 1);
+    char* dst = lds + (i % kSlots) * kRegion + (w + 4 * q) * 1024;
+    const char* src = (r < 2 ? Xb : Wb) + so[r][q] + (uint32_t)kt * (kBK * 2);
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+  };
+
+  const int l15 = lane & 15, lq = lane >> 4, sw = (l15 >> 1) & 7;
+  const int c0 = (lq ^ sw) << 4, c1 = ((4 + lq) ^ sw) << 4;
+  // fragment rows: X fragment i = rows 16 i + l15 of region wm; W fragment j (f = j / 4,
+  // type = (j / 2) % 2, jj = j % 2) = rows type*64 + wn*32 + jj*16 + l15 of region 2 + f
+  auto rd1 = [&](int t, int c, u16x8 (&xf)[8], u16x8 (&wf)[8], int q) {
+    constexpr int kOrd[16] = {8, 9, 0, 10, 11, 1, 12, 13, 2, 14, 15, 3, 4, 5, 6, 7};   // >= 8: W fragment
+    const int o = kOrd[q];
+    if (o >= 8) {
+      const int j = o - 8;
+      const char* reg = lds + ((4 * t + 2 + (j >> 2)) % kSlots) * kRegion;
+      wf[j] = *reinterpret_cast<const u16x8*>(reg + (((j >> 1) & 1) * 64 + wn * 32 + (j & 1) * 16 + l15) * 128 + c);
+    } else {
+      const char* reg = lds + ((4 * t + wm) % kSlots) * kRegion;
+      xf[o] = *reinterpret_cast<const u16x8*>(reg + (16 * o + l15) * 128 + c);
+    }
+  };
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  u16x8 xa[8], wa[8], xb[8], wb[8];
+  // one k-substep of tile t: 64 MFMAs; after each 8-MFMA row two fragment reads of the next
+  // substep (from tile tn, chunk cn) and, in the first substep, one DMA piece of regions
+  // 4t+6 .. 4t+9 (2 per row: the 16 pieces of the four regions over the 8 rows)
+  auto mm = [&](u16x8 (&xf)[8], u16x8 (&wf)[8], int tn, int cn, u16x8 (&nx)[8], u16x8 (&nw)[8], int t,
+                bool first) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) mfma_tied(acc[i][j], wf[j], xf[i]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (first) {
+        dma(4 * t + 6 + (i >> 1), (2 * i) & 3);
+        dma(4 * t + 6 + (i >> 1), (2 * i + 1) & 3);
+      }
+      rd1(tn, cn, nx, nw, 2 * i);
+      rd1(tn, cn, nx, nw, 2 * i + 1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
+  asm volatile("s_nop 4");
+
+  // prologue: regions 0 .. 5 (tile 0, tile 1's first half); tile 0 landed, 2 regions in flight
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dma(i, q);
+  vm_wait<8>();
+  seg_barrier();
+#pragma unroll
+  for (int q = 0; q < 16; ++q) rd1(0, c0, xa, wa, q);
+  // one loop, no peeled copy (a second code path makes hipcc move accumulators with
+  // v_accvgpr_write right before an asm MFMA reads them)
+  for (int t = 0; t < T; ++t) {
+    // substep 0 of tile t (regs A), reading substep 1 of tile t; issues regions 4t+6 .. 4t+9
+    mm(xa, wa, t, c1, xb, wb, t, true);
+    // substep 1 of tile t (regs B), reading substep 0 of tile t+1 (landed: see below)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    vm_wait<8>();      // tile t+1 landed (this wave's pieces); regions 4t+8, 4t+9 in flight
+    seg_barrier();     // ... every wave's pieces; tile t-1's reads long done
+    mm(xb, wb, t + 1, c0, xa, wa, t, false);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    seg_barrier();     // every wave done reading tile t: its slots are refilled next tile
+  }
+  vm_wait<0>();        // the tail's re-loads land before the workgroup's LDS is released
+  asm volatile("s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
+
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int tok = m0 + wm * 128 + i * 16 + l15;
@@ -551,9 +740,16 @@ int gemm_tile(const bf16_t* X, const bf16_t* W, bf16_t* Y, const bf16_t* bias, i
     if (silu_gu) gemm_tile256_r4_kernel<kEpiSilu><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
     else if (bias) gemm_tile256_r4_kernel<kEpiBias><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
     else gemm_tile256_r4_kernel<kEpiStore><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-  } else if ((variant == 4 || variant == 5) && off32 && !silu_gu && !bias) {   // ring-4 load experiments
+  } else if (variant == 9 && off32) {   // 4-wave, BK = 64 region ring
+    if (silu_gu) gemm_tile256_q4_kernel<kEpiSilu><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+    else if (bias) gemm_tile256_q4_kernel<kEpiBias><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+    else gemm_tile256_q4_kernel<kEpiStore><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+  } else if (variant >= 4 && variant <= 8 && off32 && !silu_gu && !bias) {   // ring-4 load experiments
     if (variant == 4) gemm_tile256_r4_kernel<kEpiStore, 1><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-    else gemm_tile256_r4_kernel<kEpiStore, 2><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+    else if (variant == 5) gemm_tile256_r4_kernel<kEpiStore, 2><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+    else if (variant == 6) gemm_tile256_r4_kernel<kEpiStore, 3><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+    else if (variant == 7) gemm_tile256_r4_kernel<kEpiStore, 4><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+    else gemm_tile256_r4_kernel<kEpiStore, 5><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
   } else if (variant == 2 || (variant == 0 && M > 256)) {
     // 8-wave ping-pong, two barrier segments per K-tile: 1.8-2.7 % over four segments on
     // the prefill shapes (M = 32k, profiles/gemm_tile_ph2_vs_ph4.jsonl); the lm_head at
