@@ -71,8 +71,6 @@ def parse_args():
                          "others as child processes")
     ap.add_argument("--shard-index", type=int, default=None, help=argparse.SUPPRESS)  # internal: child shard
     ap.add_argument("--multi-step", type=int, default=8, help="decode steps per graph window (engine.multi_step)")
-    ap.add_argument("--phase-streams", action="store_true",
-                    help="prefill on a normal-priority, decode on a high-priority HIP stream (engine.phase_streams)")
     ap.add_argument("--sink-concurrency", type=int, default=16,
                     help="operator.sink_concurrency: analyses writing results at once (0 = unbounded); a bound "
                          "keeps a finished wave's 256 result writers from starving the next wave's ramp "
@@ -223,7 +221,7 @@ def main() -> int:
             "engine.max_prefill_tokens": a.prefill_tokens,
             "engine.max_context": a.prompt_tokens + a.max_tokens + 64, "engine.max_prompt_tokens": a.prompt_tokens,
             "engine.kv_cache_gb": kv, "engine.kv_dtype": a.kv_dtype, "engine.use_graphs": not a.no_graphs,
-            "engine.ignore_eos": True, "engine.phase_streams": a.phase_streams,
+            "engine.ignore_eos": True,
             "engine.multi_step": a.multi_step,
             "engine.seed": 0, "health.enabled": False, "operator.workers": 2 * a.batch + 16, "operator.io_workers": 16,
             "operator.sink_concurrency": a.sink_concurrency,

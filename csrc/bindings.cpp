@@ -473,77 +473,6 @@ void attn_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tenso
                        (int)num_splits, (float)scale, (int)variant, cur_stream(), q8p, sxp));
 }
 
-// Decode attention with the step's RoPE + KV write fused in (kernels.h DecodeRope): the
-// QKV projection output (bf16 rows, or `partial` = `splits` fp32 split-K slabs) replaces
-// q; `out` is [B, Hq, D].
-void attn_decode_rope(const at::Tensor& qkv, const c10::optional<at::Tensor>& partial, int64_t splits,
-                      const c10::optional<at::Tensor>& bias, const at::Tensor& cos_t, const at::Tensor& sin_t,
-                      const at::Tensor& k_cache, const at::Tensor& v_cache, const at::Tensor& block_tables,
-                      const at::Tensor& seq_lens, at::Tensor& out, at::Tensor& o_part, at::Tensor& ml_part,
-                      int64_t num_splits, double scale, int64_t variant, double k_scale, double v_scale,
-                      const c10::optional<at::Tensor>& q8, const c10::optional<at::Tensor>& sx) {
-  CHECK_BF16(out); CHECK_CONTIG(out); CHECK_DEV(out);
-  const bool fp8 = kv_is_fp8(k_cache);
-  TORCH_CHECK(fp8 ? kv_is_fp8(v_cache) : (k_cache.scalar_type() == at::kBFloat16 &&
-                                          v_cache.scalar_type() == at::kBFloat16),
-              "KV cache must be bf16 or float8_e4m3fn (both K and V)");
-  CHECK_DEV(k_cache); CHECK_DEV(v_cache); CHECK_CONTIG(k_cache); CHECK_CONTIG(v_cache);
-  CHECK_DT(block_tables, at::kInt); CHECK_CONTIG(block_tables); CHECK_DT(seq_lens, at::kInt); CHECK_CONTIG(seq_lens);
-  CHECK_DT(o_part, at::kFloat); CHECK_DT(ml_part, at::kFloat); CHECK_CONTIG(o_part); CHECK_CONTIG(ml_part);
-  CHECK_DT(cos_t, at::kFloat); CHECK_DT(sin_t, at::kFloat); CHECK_CONTIG(cos_t); CHECK_CONTIG(sin_t);
-  TORCH_CHECK(out.dim() == 3, "out must be [B, Hq, D]");
-  const int64_t B = out.size(0), Hq = out.size(1), D = out.size(2);
-  TORCH_CHECK(k_cache.dim() == 4 && k_cache.sizes() == v_cache.sizes() && k_cache.size(3) == D, "cache shape");
-  const int64_t Hkv = k_cache.size(1), page = k_cache.size(2);
-  TORCH_CHECK(D == 128 && Hq % Hkv == 0 && cos_t.size(1) * 2 == D && sin_t.sizes() == cos_t.sizes(),
-              "head_dim 128, Hq % Hkv == 0, cos/sin [max_pos, 64]");
-  const int64_t ncol = (Hq + 2 * Hkv) * D;
-  oamd::DecodeRope rp{};
-  if (partial.has_value()) {
-    CHECK_DT(*partial, at::kFloat); CHECK_CONTIG(*partial); CHECK_DEV(*partial);
-    TORCH_CHECK(splits >= 1 && splits <= oamd::kRopeMaxS && partial->numel() >= splits * B * ncol,
-                "attn_decode_rope: slabs [splits <= kRopeMaxS][B][(Hq+2Hkv)D]");
-    rp.xp = partial->data_ptr<float>();
-    rp.S = (int)splits;
-    rp.slab = B * ncol;
-  } else {
-    CHECK_DEV(qkv); CHECK_BF16(qkv); CHECK_CONTIG(qkv);
-    TORCH_CHECK(qkv.dim() == 2 && qkv.size(0) == B && qkv.size(1) == ncol, "qkv must be [B, (Hq+2Hkv)*D]");
-    rp.qkv = ptr<bf16_t>(qkv);
-    rp.S = 1;
-  }
-  if (bias.has_value()) {
-    CHECK_BF16(*bias); CHECK_CONTIG(*bias); CHECK_DEV(*bias);
-    TORCH_CHECK(bias->numel() == ncol, "attn_decode_rope: bias must be [(Hq + 2 Hkv) * D]");
-    rp.bias = ptr<bf16_t>(*bias);
-  }
-  rp.cos_t = ptr<float>(cos_t);
-  rp.sin_t = ptr<float>(sin_t);
-  rp.max_pos = (int)cos_t.size(0);
-  TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) == B && seq_lens.numel() == B, "tables shape");
-  TORCH_CHECK(num_splits >= 1 && block_tables.size(1) <= 1024, "num_splits >= 1, at most 1024 pages per sequence");
-  TORCH_CHECK(num_splits == 1 ||
-                  (o_part.numel() >= B * Hq * num_splits * D && ml_part.numel() >= B * Hq * num_splits * 2),
-              "partial buffers too small");
-  TORCH_CHECK(k_scale > 0 && v_scale > 0, "KV scales must be positive");
-  TORCH_CHECK(q8.has_value() == sx.has_value(), "q8 and sx together");
-  uint8_t* q8p = nullptr;
-  float* sxp = nullptr;
-  if (q8.has_value()) {
-    CHECK_CONTIG(*q8); CHECK_CONTIG(*sx); CHECK_DT(*sx, at::kFloat);
-    TORCH_CHECK((q8->scalar_type() == at::kByte || q8->scalar_type() == at::kFloat8_e4m3fn) &&
-                    q8->numel() == B * Hq * D && sx->numel() == B && Hq * D <= 8192,
-                "q8 e4m3fn [B, Hq*D], sx fp32 [B], Hq*D <= 8192");
-    q8p = static_cast<uint8_t*>(q8->data_ptr());
-    sxp = sx->data_ptr<float>();
-  }
-  const c10::hip::HIPGuardMasqueradingAsCUDA g(out.device());
-  RC(oamd::attn_decode(nullptr, k_cache.data_ptr(), v_cache.data_ptr(), fp8, (float)k_scale, (float)v_scale,
-                       ptr<int>(block_tables), ptr<int>(seq_lens), ptr<bf16_t>(out), ptr<float>(o_part),
-                       ptr<float>(ml_part), (int)B, (int)Hq, (int)Hkv, (int)D, (int)page, (int)block_tables.size(1),
-                       (int)num_splits, (float)scale, (int)variant, cur_stream(), q8p, sxp, &rp));
-}
-
 void attn_prefill(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor& o,
                   const at::Tensor& cu_seqlens, const at::Tensor& work_seq, const at::Tensor& work_q0,
                   double scale, int64_t variant) {
@@ -616,12 +545,6 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("ml_part"), pybind11::arg("num_splits"), pybind11::arg("scale"), pybind11::arg("variant") = 0,
         pybind11::arg("k_scale") = 1.0, pybind11::arg("v_scale") = 1.0, pybind11::arg("q8") = pybind11::none(),
         pybind11::arg("sx") = pybind11::none());
-  m.def("attn_decode_rope", &attn_decode_rope, pybind11::arg("qkv"), pybind11::arg("partial"),
-        pybind11::arg("splits"), pybind11::arg("bias"), pybind11::arg("cos_t"), pybind11::arg("sin_t"),
-        pybind11::arg("k_cache"), pybind11::arg("v_cache"), pybind11::arg("block_tables"), pybind11::arg("seq_lens"),
-        pybind11::arg("out"), pybind11::arg("o_part"), pybind11::arg("ml_part"), pybind11::arg("num_splits"),
-        pybind11::arg("scale"), pybind11::arg("variant") = 0, pybind11::arg("k_scale") = 1.0,
-        pybind11::arg("v_scale") = 1.0, pybind11::arg("q8") = pybind11::none(), pybind11::arg("sx") = pybind11::none());
   m.def("decode_slots", &decode_slots);
   m.def("decode_advance", &decode_advance);
   m.def("quantize_fp8", &quantize_fp8);

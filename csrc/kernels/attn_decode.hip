@@ -106,37 +106,6 @@ struct KVT<uint8_t> {
   }
 };
 
-// 8 bf16 values -> the cache element type (bf16 as is; fp8: e4m3(x * inv), saturated),
-// exactly as rope.hip stores them
-template <typename KV>
-__device__ __forceinline__ void cache_put8(KV* dst, const u16x8& v, float inv) {
-  if constexpr (sizeof(KV) == 2) {
-    *reinterpret_cast<u16x8*>(dst) = v;
-  } else {
-    auto f = [&](int j) { return fminf(fmaxf(bf2f(v[j]) * inv, -448.f), 448.f); };
-    int lo = 0, hi = 0;
-    lo = __builtin_amdgcn_cvt_pk_fp8_f32(f(0), f(1), lo, false);
-    lo = __builtin_amdgcn_cvt_pk_fp8_f32(f(2), f(3), lo, true);
-    hi = __builtin_amdgcn_cvt_pk_fp8_f32(f(4), f(5), hi, false);
-    hi = __builtin_amdgcn_cvt_pk_fp8_f32(f(6), f(7), hi, true);
-    *reinterpret_cast<uint2*>(dst) = uint2{(unsigned)lo, (unsigned)hi};
-  }
-}
-
-// One bf16 value as the attention kernel sees it once it is in the cache: bf16 as is;
-// fp8: the e4m3 code of x * inv as a float (the scale is applied by the caller, as for
-// streamed K / V)
-template <typename KV>
-__device__ __forceinline__ float kv_value(bf16_t x, float inv) {
-  if constexpr (sizeof(KV) == 2) {
-    return bf2f(x);
-  } else {
-    const float v = fminf(fmaxf(bf2f(x) * inv, -448.f), 448.f);
-    const int pk = __builtin_amdgcn_cvt_pk_fp8_f32(v, 0.f, 0, false);
-    return __builtin_amdgcn_cvt_pk_f32_fp8(pk, false)[0];
-  }
-}
-
 // Token range of split s of a sequence of `len` tokens cut into at most
 // `num_splits` pieces of a multiple of `chunk` tokens. Shared with the combine
 // kernel so both agree on how many splits a sequence really has.
@@ -153,12 +122,11 @@ struct KVRegs {
 
 template <int G, int NT, typename KV = bf16_t>
 __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2)
-    // kc / vc not __restrict__: the fused RoPE stores the new token's K/V through them
-    attn_decode_kernel(const bf16_t* __restrict__ q, const KV* kc, const KV* vc,
+    attn_decode_kernel(const bf16_t* __restrict__ q, const KV* __restrict__ kc, const KV* __restrict__ vc,
                        const int* __restrict__ block_tables, const int* __restrict__ seq_lens,
                        bf16_t* __restrict__ out, float* __restrict__ o_part, float* __restrict__ ml_part, int Hkv,
                        int page_size, int log2_page, int max_pages, int num_splits, float scale_log2,
-                       float v_scale, int head_minor, DecodeRope rp, float k_inv, float v_inv) {
+                       float v_scale, int head_minor) {
   using T = KVT<KV>;
   constexpr int D = 128;
   constexpr int TW = 16 * NT;  // tokens per wave per chunk
@@ -170,12 +138,6 @@ __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2)
   __shared__ __attribute__((aligned(16))) float red[4][G][D];
   __shared__ float mls[4][G][2];
   __shared__ u16x8 q_lds[4][64];
-  // fused RoPE (rp.cos_t set): items = G query-head + 1 key-head rotations (8 per head,
-  // 8 + 8 dims each) and 16 value copies (8 dims); per (item, split-K slab) fp32 partials
-  constexpr int NI = (G + 1) * 8 + 16;
-  __shared__ __attribute__((aligned(16))) float rp_part[NI * kRopeMaxS * 16];
-  __shared__ u16x8 kv_new[2][16];   // the new token's k, v (bf16, dims 8i..8i+7)
-  __shared__ float s_new[G];        // its scores (log2 domain) per head
 
   // work item of this workgroup: (sequence, split, kv-head); head_minor dispatches the
   // kv-heads of one sequence back to back (they read different head slices of the
@@ -207,9 +169,6 @@ __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2)
   const int end = min(len, start + per);
   const int ns_b = (len + per - 1) / per;
   const int nch = (end - start + CH - 1) / CH;
-  const bool fused = rp.cos_t != nullptr;
-  const bool writer = fused && end == len;   // this split holds the new token (position len - 1)
-  const int end_s = writer ? len - 1 : end;  // the streamed cache tokens (the new one is not there yet)
 
   // Page ids of the split -> LDS: the steady-state data loads depend only on LDS
   // (lgkmcnt), never on a global load that would share vmcnt with them. The first
@@ -219,60 +178,9 @@ __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2)
   const int page0 = start >> log2_page;
   const int npg = ((end - 1) >> log2_page) - page0 + 1;
   const int* btb = block_tables + (int64_t)b * max_pages + page0;
-  // Fused RoPE, phase 1: every (item, slab) pair loads its 16 fp32 partials (x1: dims
-  // g..g+7 of the head, x2: dims 64+g..; a value copy only x1), at most 2 pairs per
-  // thread, all issued before any K/V load so their LDS writes never wait for K/V
-  const int ncol = (Hq + 2 * Hkv) * D;
-  const int nS = rp.xp ? rp.S : 1;
-  f32x4 rv[2][4];
-  f32x4 csv[4];   // cos (g..g+7) | sin (g..g+7) of a rotation item's position, prefetched
-  auto rp_col = [&](int item) -> int {   // first column of an item's x1
-    if (item < (G + 1) * 8) {
-      const int h = item >> 3, g = (item & 7) * 8;
-      return (h < G ? (kvh * G + h) : (Hq + kvh)) * D + g;
-    }
-    return (Hq + Hkv + kvh) * D + (item - (G + 1) * 8) * 8;
-  };
-  if (fused) {
-    if (tid < (G + 1) * 8) {
-      const int pp = min(len - 1, rp.max_pos - 1), g = (tid & 7) * 8;
-      const float* cr = rp.cos_t + (int64_t)pp * (D / 2) + g;
-      const float* sr = rp.sin_t + (int64_t)pp * (D / 2) + g;
-      csv[0] = *reinterpret_cast<const f32x4*>(cr);
-      csv[1] = *reinterpret_cast<const f32x4*>(cr + 4);
-      csv[2] = *reinterpret_cast<const f32x4*>(sr);
-      csv[3] = *reinterpret_cast<const f32x4*>(sr + 4);
-    }
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int pr = tid + 256 * k;
-      if (pr < NI * nS) {
-        const int item = pr % NI, sl = pr / NI, col = rp_col(item);
-        const bool rot = item < (G + 1) * 8;
-        if (rp.xp) {
-          const float* src = rp.xp + (int64_t)sl * rp.slab + (int64_t)b * ncol + col;
-          rv[k][0] = *reinterpret_cast<const f32x4*>(src);
-          rv[k][1] = *reinterpret_cast<const f32x4*>(src + 4);
-          rv[k][2] = rot ? *reinterpret_cast<const f32x4*>(src + 64) : f32x4{0.f, 0.f, 0.f, 0.f};
-          rv[k][3] = rot ? *reinterpret_cast<const f32x4*>(src + 68) : f32x4{0.f, 0.f, 0.f, 0.f};
-        } else {
-          const bf16_t* src = rp.qkv + (int64_t)b * ncol + col;
-          const u16x8 x1 = *reinterpret_cast<const u16x8*>(src);
-          const u16x8 x2 = rot ? *reinterpret_cast<const u16x8*>(src + 64) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            rv[k][0][j] = bf2f(x1[j]);
-            rv[k][1][j] = bf2f(x1[4 + j]);
-            rv[k][2][j] = bf2f(x2[j]);
-            rv[k][3][j] = bf2f(x2[4 + j]);
-          }
-        }
-      }
-    }
-  }
   const int pid0 = tid < npg ? btb[tid] : 0;   // issued before any K/V load (vmcnt is in order)
   u16x8 qv[4];
-  if (w == 0 && !fused) {
+  if (w == 0) {
     const int hq = kvh * G + (l15 < G ? l15 : 0);
     const bf16_t* qp = q + ((int64_t)b * Hq + hq) * D + 32 * lg;
 #pragma unroll
@@ -331,96 +239,11 @@ __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2)
   for (int i = tid + 256; i < npg; i += 256) pg_lds[i] = btb[i];   // > 256 pages: rare
   // q as the MFMA B operand (column = head, zero past G), staged once in LDS and read per
   // k-step (16 VGPRs fewer per lane than q in registers)
-  if (fused) {
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int pr = tid + 256 * k;
-      if (pr < NI * nS) {
-        float* dst = rp_part + ((pr % NI) * kRopeMaxS + pr / NI) * 16;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) *reinterpret_cast<f32x4*>(dst + 4 * j) = rv[k][j];
-      }
-    }
-    if (l15 >= G && w == 0) {
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) q_lds[ks][lane] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-    }
-  } else if (w == 0) {
+  if (w == 0) {
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) q_lds[ks][lane] = l15 < G ? qv[ks] : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
   }
   __syncthreads();
-  if (fused) {
-    // Fused RoPE, phase 2: one thread per item sums its slabs in order (+ bias), rounds
-    // to bf16 and rotates (neox form) exactly as rope_kv does; q goes to the MFMA operand,
-    // the new token's k / v to LDS (its attention term is merged after the stream, its
-    // cache store issued at the very end: no store -> load hazard inside the kernel)
-    if (tid < NI) {
-      const int item = tid, col = rp_col(item);
-      const bool rot = item < (G + 1) * 8;
-      float x1[8], x2[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) x1[j] = x2[j] = 0.f;
-      for (int sl = 0; sl < nS; ++sl) {
-        const f32x4* src = reinterpret_cast<const f32x4*>(rp_part + (item * kRopeMaxS + sl) * 16);
-        const f32x4 p0 = src[0], p1 = src[1], p2 = src[2], p3 = src[3];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          x1[j] += p0[j];
-          x1[4 + j] += p1[j];
-          x2[j] += p2[j];
-          x2[4 + j] += p3[j];
-        }
-      }
-      if (rp.bias) {
-        const u16x8 b1 = *reinterpret_cast<const u16x8*>(rp.bias + col);
-        const u16x8 b2 = rot ? *reinterpret_cast<const u16x8*>(rp.bias + col + 64) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          x1[j] += bf2f(b1[j]);
-          x2[j] += bf2f(b2[j]);
-        }
-      }
-      if (rot) {
-        const int h = item >> 3, g = (item & 7) * 8;
-        u16x8 o1, o2;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float c = csv[j >> 2][j & 3], sn = csv[2 + (j >> 2)][j & 3];
-          const float a = bf2f(f2bf(x1[j])), bb = bf2f(f2bf(x2[j]));
-          o1[j] = f2bf(a * c - bb * sn);
-          o2[j] = f2bf(bb * c + a * sn);
-        }
-        if (h < G) {
-          q_lds[(g & 31) >> 3][h + 16 * (g >> 5)] = o1;
-          q_lds[(g & 31) >> 3][h + 16 * (2 + (g >> 5))] = o2;
-        } else {
-          kv_new[0][g >> 3] = o1;
-          kv_new[0][8 + (g >> 3)] = o2;
-        }
-      } else {
-        u16x8 o;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = f2bf(x1[j]);
-        kv_new[1][item - (G + 1) * 8] = o;
-      }
-    }
-    __syncthreads();
-    if (writer && tid >= 64 && tid < 96) {   // the new token into the cache, for the next steps:
-      // issued here (wave 1; nothing in this kernel reads it) instead of delaying the end
-      const int ti = tid - 64, pos_new = len - 1;
-      const int64_t page = block_tables[(int64_t)b * max_pages + (pos_new >> log2_page)];
-      const int off = pos_new & (page_size - 1), t16 = off & 15;
-      const int64_t row = page * page_stride + head_off + (int64_t)off * D;
-      if (ti < 16) {   // tiled K: [16-token tile][ks][lg][token][8 dims], dim d = 32 lg + 8 ks + j
-        const int d = 8 * ti;
-        cache_put8(const_cast<KV*>(kc) + row - (int64_t)t16 * D + ((((d & 31) >> 3) * 4 + (d >> 5)) * 16 + t16) * 8,
-                   kv_new[0][ti], k_inv);
-      } else {
-        cache_put8(const_cast<KV*>(vc) + row + 8 * (ti - 16), kv_new[1][ti - 16], v_inv);
-      }
-    }
-  }
 
   // Online softmax per (head, token group): lane (l15, lg) of the S = K Q^T tile holds head
   // l15 of tokens 4lg..4lg+3 of every 16-token tile, and the P.V lanes (dims 8 l15.., lg)
@@ -450,7 +273,7 @@ __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2)
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const int tok = base + 16 * i + 4 * lg + rr;
-        sc[i][rr] = (tok < end_s) ? a[rr] * scale_log2 : -INFINITY;
+        sc[i][rr] = (tok < end) ? a[rr] * scale_log2 : -INFINITY;
         m_new = fmaxf(m_new, sc[i][rr]);
       }
     }
@@ -555,40 +378,18 @@ __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2)
       mls[w][l15][1] = l_run;
     }
   }
-  if (writer && w == 0) {   // the new token's scores: q . k over 128 dims, 16 lanes per head
-#pragma unroll
-    for (int h0 = 0; h0 < G; h0 += 4) {
-      const int h = h0 + lg;
-      float sdot = 0.f;
-      if (h < G) {
-        const u16x8 qv8 = q_lds[l15 & 3][h + 16 * (l15 >> 2)];
-        const u16x8 kv8 = kv_new[0][l15];
-#pragma unroll
-        for (int t = 0; t < 8; ++t) sdot += bf2f(qv8[t]) * kv_value<KV>(kv8[t], k_inv);
-      }
-#pragma unroll
-      for (int o = 8; o > 0; o >>= 1) sdot += __shfl_xor(sdot, o, 16);
-      if (h < G && l15 == 0) s_new[h] = sdot * scale_log2;
-    }
-  }
   __syncthreads();
   for (int e = tid; e < G * D; e += 256) {
     const int h = e / D, d = e % D;
     float M = mls[0][h][0];
 #pragma unroll
     for (int ww = 1; ww < 4; ++ww) M = fmaxf(M, mls[ww][h][0]);
-    if (writer) M = fmaxf(M, s_new[h]);
     float o = 0.f, L = 0.f;
 #pragma unroll
     for (int ww = 0; ww < 4; ++ww) {
       const float f = exp2f(mls[ww][h][0] - M);
       o += f * red[ww][h][d];
       L += f * mls[ww][h][1];
-    }
-    if (writer) {   // + the new token (p = exp2(s - M), its v as the cache holds it)
-      const float f = exp2f(s_new[h] - M);
-      o += f * kv_value<KV>(kv_new[1][d >> 3][d & 7], v_inv);
-      L += f;
     }
     o *= v_scale;
     const int hq = kvh * G + h;
@@ -696,15 +497,8 @@ __global__ void __launch_bounds__(1024) attn_decode_combine_q8_kernel(
 int attn_decode(const bf16_t* q, const void* k_cache, const void* v_cache, bool fp8, float k_scale, float v_scale,
                 const int* block_tables, const int* seq_lens, bf16_t* out, float* o_part, float* ml_part, int B,
                 int Hq, int Hkv, int head_dim, int page_size, int max_pages, int num_splits, float scale, int variant,
-                hipStream_t stream, uint8_t* q8, float* sx, const DecodeRope* rope) {
+                hipStream_t stream, uint8_t* q8, float* sx) {
   if (B == 0) return 0;
-  DecodeRope rp{};
-  if (rope != nullptr) {
-    if (rope->cos_t == nullptr || rope->sin_t == nullptr || (rope->qkv == nullptr && rope->xp == nullptr)) return -7;
-    if (rope->xp != nullptr && (rope->S < 1 || rope->S > kRopeMaxS)) return -8;
-    if ((Hq / Hkv + 1) * 8 + 16 > 256 || ((Hq / Hkv + 1) * 8 + 16) * (rope->xp ? rope->S : 1) > 512) return -9;
-    rp = *rope;
-  }
   if (head_dim != 128) return -1;
   if (page_size < 16 || (page_size & (page_size - 1)) != 0) return -2;
   if (max_pages > kMaxPagesLds) return -4;
@@ -723,8 +517,7 @@ int attn_decode(const bf16_t* q, const void* k_cache, const void* v_cache, bool 
   do {                                                                                                    \
     attn_decode_kernel<GG, NTT, KVT_><<<grid, 256, 0, stream>>>(                                         \
         q, static_cast<const KVT_*>(k_cache), static_cast<const KVT_*>(v_cache), block_tables, seq_lens, \
-        out, o_part, ml_part, Hkv, page_size, log2p, max_pages, num_splits, scale_log2, v_scale, hm, rp,  \
-        1.f / k_scale, 1.f / v_scale);                                                                   \
+        out, o_part, ml_part, Hkv, page_size, log2p, max_pages, num_splits, scale_log2, v_scale, hm);      \
     chunk = 64 * NTT;                                                                                     \
   } while (0)
   const bool nt2 = (variant & 3) == 2;

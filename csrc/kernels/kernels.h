@@ -76,29 +76,11 @@ int score_events(const int64_t* keys, const int* hit_doc, const int* doc_ptr, in
                  const double* conf, const int* severity, int num_matchers, double significance, double* ev_score,
                  int* ev_pat, int* ev_line, int* order, int* summary, hipStream_t stream);
 
-// Fused RoPE + KV write of the decode step's new token (attn_decode with `rope`): the
-// attention workgroup of (sequence b, kv-head) reads the QKV projection's row b (bf16 row
-// of `qkv`, or the sum of S fp32 split-K slabs `xp`, + optional bias), rotates its G query
-// heads straight into the MFMA operand and its kv-head's k, and the split holding the
-// new token (position seq_lens[b] - 1) stores k / v at that position's page slot, so the
-// rope_kv kernel (and q in global memory) disappear from the decode step.
-constexpr int kRopeMaxS = 8;
-struct DecodeRope {
-  const bf16_t* qkv;     // [B, (Hq + 2 Hkv) * D] bf16 rows (when xp == nullptr)
-  const float* xp;       // [S][B][(Hq + 2 Hkv) * D] fp32 split-K slabs, or nullptr
-  int S;                 // <= kRopeMaxS
-  int64_t slab;          // elements per slab (B * (Hq + 2 Hkv) * D)
-  const bf16_t* bias;    // [(Hq + 2 Hkv) * D] or nullptr
-  const float* cos_t;    // [max_pos, D / 2]
-  const float* sin_t;
-  int max_pos;
-};
-
 // k_cache / v_cache: bf16, or (fp8) OCP e4m3fn bytes holding x / k_scale, x / v_scale
 int attn_decode(const bf16_t* q, const void* k_cache, const void* v_cache, bool fp8, float k_scale, float v_scale,
                 const int* block_tables, const int* seq_lens, bf16_t* out, float* o_part, float* ml_part, int B,
                 int Hq, int Hkv, int head_dim, int page_size, int max_pages, int num_splits, float scale, int variant,
-                hipStream_t stream, uint8_t* q8 = nullptr, float* sx = nullptr, const DecodeRope* rope = nullptr);
+                hipStream_t stream, uint8_t* q8 = nullptr, float* sx = nullptr);
 // (q8, sx non-null: the output rows are also emitted as per-token e4m3fn [B, Hq*128] + fp32 scales,
 // == quantize_fp8_rows(out); `out` then holds valid bf16 only for rows of a single split.)
 // Causal prefill attention; the work list holds one item per attn_prefill_block_q(Hq, Hkv, variant)

@@ -133,7 +133,6 @@ class EngineCfg(BaseModel):
     use_graphs: bool = True
     prefill_graphs: bool = True       # full-ish prefill batches replay a captured bucket graph
     warmup_graphs: bool = True        # engine processes capture their graphs before reporting ready
-    phase_streams: bool = False       # prefill on a normal-, decode on a high-priority stream (several engines per GPU)
     multi_step: int = 8
     ignore_eos: bool = False
 

@@ -170,7 +170,7 @@ def _no_gc():
     """No Python garbage collection while a hipGraph is being captured. Recent PyTorch
     no longer collects on entering ``torch.cuda.graph``, so a collection triggered by
     an allocation inside the capture could free a dead cycle's GPU tensors there; a
-    tensor used on another stream (engine.phase_streams, the scan stream) then
+    tensor used on another stream (the scan stream) then
     records an event on that stream mid-capture, which aborts the process. Dead
     cycles are collected first, then collection waits until the capture ends."""
     gc.collect()
@@ -347,7 +347,7 @@ class _PendingPrefill:
 class LLMEngine:
     def __init__(self, model: LlamaModel, kv: PagedKVCache, max_batch: int = 256, max_prefill_tokens: int = 16384,
                  max_context: int | None = None, use_graphs: bool = True, multi_step: int = 8,
-                 admit_wait_s: float = 0.0, prefill_graphs: bool = True, phase_streams: bool = False):
+                 admit_wait_s: float = 0.0, prefill_graphs: bool = True):
         self.model, self.kv = model, kv
         # arrival batching window used by the loop that drives step() (EngineLoop):
         # an idle engine given less than a full prefill batch waits this long for more
@@ -402,15 +402,6 @@ class LLMEngine:
         # called after every engine step; raise to fail the engine (e.g. a TP collective
         # that timed out: TPLLMEngine registers the one-shot all-reduce's check)
         self.health_checks: list = []
-        # phase_streams: prefills on a normal-priority stream, decode windows on a
-        # high-priority one (ordered by stream waits at each phase change), so that with
-        # several engines on one GPU (operator shards) another engine's large prefill
-        # GEMM grids do not hold the CUs ahead of this engine's short decode kernels
-        self._pstream = self._dstream = None
-        if phase_streams and self.device.type == "cuda":
-            lo, hi = torch.cuda.Stream.priority_range() if hasattr(torch.cuda.Stream, "priority_range") else (0, -1)
-            self._pstream = torch.cuda.Stream(self.device, priority=lo)
-            self._dstream = torch.cuda.Stream(self.device, priority=hi)
         self._host_bufs = None
         if self.device.type == "cuda":
             self._host_bufs = [torch.empty(max_batch, self.multi_step, dtype=torch.long, pin_memory=True)
@@ -514,24 +505,14 @@ class LLMEngine:
             # while this batch is already queued on the GPU behind it (no host gap
             # between prefill batches)
             prev = self._pf
-            if self._pstream is not None:
-                self._pstream.wait_stream(self._dstream)
-                with torch.cuda.stream(self._pstream):
-                    self._pf = self._prefill(batch)
-                self._dstream.wait_stream(self._pstream)
-            else:
-                self._pf = self._prefill(batch)
+            self._pf = self._prefill(batch)
             if prev is not None:
                 self._finish_prefill(prev)
         elif self._pf is not None:
             prev, self._pf = self._pf, None
             self._finish_prefill(prev)
         elif self.running:
-            if self._dstream is not None:
-                with torch.cuda.stream(self._dstream):
-                    self._decode()
-            else:
-                self._decode()
+            self._decode()
         for chk in self.health_checks:
             chk()
         return self._reap()

@@ -258,12 +258,6 @@ class LlamaModel:
                 q, k, v = ops.rope_kv(qkv, fb.positions, self.cos, self.sin, self.hq, self.hkv, kc, vc, fb.slots,
                                       want_kv=True, bias=bias, k_scale=kv.k_scale, v_scale=kv.v_scale)
                 o = ops.attn_prefill(q, k, v, fb.seq_lens, self.scale, work=fb.prefill_work)
-            elif h.is_cuda and ops.decode_rope_fusable(qkv, self.hq, self.hkv, fb.num_splits):
-                # the new token's RoPE + KV write run inside the attention kernel; fp8: the
-                # split-combine kernel also emits the o-projection's e4m3fn rows
-                o = ops.attn_decode_rope(qkv, self.cos, self.sin, self.hq, self.hkv, kc, vc, fb.block_tables,
-                                         fb.context_lens, self.scale, fb.num_splits, bias=bias, workspace=ws,
-                                         k_scale=kv.k_scale, v_scale=kv.v_scale, quant=q8)
             else:
                 q, _, _ = ops.rope_kv(qkv, fb.positions, self.cos, self.sin, self.hq, self.hkv, kc, vc, fb.slots,
                                       want_kv=False, bias=bias, k_scale=kv.k_scale, v_scale=kv.v_scale)

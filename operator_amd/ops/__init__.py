@@ -541,64 +541,6 @@ def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, b
     return (q8, sx) if quant else o
 
 
-ROPE_MAX_SPLITS = 8   # kernels.h kRopeMaxS
-# Model routing only (decode_rope_fusable); attn_decode_rope itself always fuses when it can.
-# Off by default: measured on the flagship (rocprofv3 --stats, 2 waves each way) the fused
-# attention kernel took 199.9 us vs 191.7 us + 7 us of rope_kv unfused, i.e. the rotation in
-# every workgroup's prologue (slab loads -> LDS -> rotate -> barrier) costs what the separate
-# kernel did, and the whole step came out 0.4 % slower.
-FUSED_DECODE_ROPE = os.environ.get("OAMD_FUSED_ROPE", "0") == "1"
-
-
-def decode_rope_fusable(qkv, Hq: int, Hkv: int, num_splits: int) -> bool:
-    """The decode step's RoPE + KV write can run inside attn_decode: a GPU batch, at most
-    kRopeMaxS split-K slabs and 512 (item, slab) pairs per workgroup, and one attention
-    workgroup per (sequence, kv-head) — with split-KV every split would redo the rotation
-    (the TP8 shard of a 70B: 8 splits x 8 slabs), so rope_kv stays the cheaper pass there."""
-    S = qkv.S if isinstance(qkv, SplitK) else 1
-    return (FUSED_DECODE_ROPE and qkv.is_cuda and num_splits == 1 and S <= ROPE_MAX_SPLITS
-            and ((Hq // Hkv + 1) * 8 + 16) * S <= 512)
-
-
-def attn_decode_rope(qkv, cos: torch.Tensor, sin: torch.Tensor, Hq: int, Hkv: int, k_cache: torch.Tensor,
-                     v_cache: torch.Tensor, block_tables: torch.Tensor, seq_lens: torch.Tensor, scale: float,
-                     num_splits: int, bias: torch.Tensor | None = None,
-                     workspace: tuple[torch.Tensor, torch.Tensor] | None = None, variant: int = 0,
-                     k_scale: float = 1.0, v_scale: float = 1.0, quant: bool = False):
-    """Decode step attention with the step's RoPE + KV-cache write fused in: ``qkv`` is the
-    QKV projection output (bf16 [B, (Hq+2Hkv)D] rows or split-K ``SplitK`` slabs); each
-    sequence's new token sits at position ``seq_lens - 1`` and is stored at that position's
-    page slot. Same result as ``rope_kv`` (positions seq_lens - 1) + ``attn_decode``, without
-    the rope_kv kernel or q in memory. Falls back to exactly that pair off the GPU."""
-    B = qkv.shape[0]
-    D = cos.shape[1] * 2
-    S = qkv.S if isinstance(qkv, SplitK) else 1
-    if not seq_lens.is_cuda or S > ROPE_MAX_SPLITS or ((Hq // Hkv + 1) * 8 + 16) * S > 512:
-        P = k_cache.shape[2]
-        pos = (seq_lens.to(torch.long) - 1).clamp_min(0)
-        pg = torch.gather(block_tables, 1, (pos // P).clamp(max=block_tables.shape[1] - 1).unsqueeze(1)).squeeze(1)
-        slots = torch.where(seq_lens > 0, pg.to(torch.long) * P + pos % P, torch.full_like(pos, -1))
-        q, _, _ = rope_kv(qkv, pos, cos, sin, Hq, Hkv, k_cache, v_cache, slots, want_kv=False, bias=bias,
-                          k_scale=k_scale, v_scale=v_scale)
-        return attn_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, num_splits, workspace=workspace,
-                           variant=variant, k_scale=k_scale, v_scale=v_scale, quant=quant)
-    dev = seq_lens.device
-    o = torch.empty(B, Hq, D, dtype=torch.bfloat16, device=dev)
-    if workspace is None:
-        workspace = decode_workspace(B, Hq, num_splits, dev)
-    q8 = sx = None
-    if quant:
-        q8 = torch.empty(B, Hq * D, dtype=torch.float8_e4m3fn, device=dev)
-        sx = torch.empty(B, dtype=torch.float32, device=dev)
-    if isinstance(qkv, SplitK):
-        kernels().attn_decode_rope(o, qkv.p, qkv.S, bias, cos, sin, k_cache, v_cache, block_tables, seq_lens, o,
-                                   workspace[0], workspace[1], num_splits, scale, variant, k_scale, v_scale, q8, sx)
-    else:
-        kernels().attn_decode_rope(qkv, None, 1, bias, cos, sin, k_cache, v_cache, block_tables, seq_lens, o,
-                                   workspace[0], workspace[1], num_splits, scale, variant, k_scale, v_scale, q8, sx)
-    return (q8, sx) if quant else o
-
-
 def sample(logits: torch.Tensor, temperature: torch.Tensor, seeds: torch.Tensor, positions: torch.Tensor,
            out: torch.Tensor | None = None, col_offset: int = 0, out_val: torch.Tensor | None = None) -> torch.Tensor:
     """Temperature / Gumbel-max sampling (greedy rows where temperature <= 0).

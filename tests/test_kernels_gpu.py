@@ -471,57 +471,6 @@ def test_attn_decode_fused_quant_matches_quantized_output(Hq, Hkv, splits, varia
     assert torch.equal(q8.view(torch.uint8), q0.view(torch.uint8))
 
 
-@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (28, 4), (16, 16), (24, 8)])
-@pytest.mark.parametrize("src", ["rows", "slabs2", "slabs4", "rows_bias", "slabs4_bias"])
-@pytest.mark.parametrize("fp8", [False, True])
-def test_attn_decode_fused_rope_matches_rope_kv_then_attention(Hq, Hkv, src, fp8):
-    """attn_decode_rope (RoPE + KV write of the new token inside the attention kernel) ==
-    rope_kv at positions seq_lens - 1 followed by attn_decode: the same KV cache bit for bit
-    (the new token's K tile piece and V row), and the same attention output up to fp32
-    summation order (the new token's term is merged after the cache stream instead of
-    inside it), for bf16 rows or split-K slabs, with a Qwen2-style bias, for every split
-    count, one-token and short contexts, padding rows and a bf16 or e4m3fn cache."""
-    torch.manual_seed(21)
-    D, P = 128, 64
-    lens = [1, 40, 129, 300, 0, 1500, 64]
-    B = len(lens)
-    maxp = (max(lens) + P - 1) // P + 1
-    pages = B * maxp + 2
-    cos, sin = ref.rope_tables(4096, D, 500000.0, device=DEV)
-    kc0 = _rand(pages, Hkv, P, D)
-    vc0 = _rand(pages, Hkv, P, D)
-    ks = vs = 1.0
-    if fp8:
-        ks, vs = 0.05, 0.04
-        kc0 = (kc0.float() / ks).clamp(-448, 448).to(torch.float8_e4m3fn)
-        vc0 = (vc0.float() / vs).clamp(-448, 448).to(torch.float8_e4m3fn)
-    bt = torch.randperm(pages, device=DEV)[: B * maxp].reshape(B, maxp).int()
-    sl = torch.tensor(lens, dtype=torch.int32, device=DEV)
-    W = (Hq + 2 * Hkv) * D
-    bias = _rand(W, scale=0.5) if src.endswith("bias") else None
-    if src.startswith("slabs"):
-        S = int(src[5])
-        qkv = ops.SplitK(torch.randn(S * B * W, device=DEV) * 0.5, S, B, W)
-    else:
-        qkv = _rand(B, W)
-    scale = 1 / math.sqrt(D)
-    pos = (sl.long() - 1).clamp_min(0)
-    pg = torch.gather(bt, 1, (pos // P).unsqueeze(1)).squeeze(1)
-    slots = torch.where(sl > 0, pg.long() * P + pos % P, torch.full_like(pos, -1))
-    for ns in (1, 2, 8):
-        kc1, vc1, kc2, vc2 = kc0.clone(), vc0.clone(), kc0.clone(), vc0.clone()
-        q, _, _ = ops.rope_kv(qkv, pos, cos, sin, Hq, Hkv, kc1, vc1, slots, want_kv=False, bias=bias,
-                              k_scale=ks, v_scale=vs)
-        o1 = ops.attn_decode(q, kc1, vc1, bt, sl, scale, ns, k_scale=ks, v_scale=vs)
-        o2 = ops.attn_decode_rope(qkv, cos, sin, Hq, Hkv, kc2, vc2, bt, sl, scale, ns, bias=bias,
-                                  k_scale=ks, v_scale=vs)
-        torch.cuda.synchronize()
-        assert torch.equal(kc1.view(torch.uint8), kc2.view(torch.uint8)), ("K cache", ns)
-        assert torch.equal(vc1.view(torch.uint8), vc2.view(torch.uint8)), ("V cache", ns)
-        torch.testing.assert_close(o2.float(), o1.float(), atol=1e-2, rtol=1e-2)
-        assert torch.equal(o2[sl == 0], torch.zeros_like(o2[sl == 0]))
-
-
 def test_decode_step_bookkeeping_kernels_match_torch():
     """decode_slots / decode_advance (one thread per row) == the torch formulation of a
     decode step's slot computation and state advance, padding rows (ctx 0) included."""

@@ -149,7 +149,7 @@ def test_graph_capture_with_dead_cycles_holding_multi_stream_tensors():
     gc.set_threshold(1, 1, 1)
     try:
         kv = PagedKVCache(cfg.layers, 64, cfg.kv_heads, 128, 16, device="cuda")
-        eng = LLMEngine(m, kv, max_batch=4, max_context=512, use_graphs=True, multi_step=2, phase_streams=True)
+        eng = LLMEngine(m, kv, max_batch=4, max_context=512, use_graphs=True, multi_step=2)
         reqs = [GenRequest(list(range(2, 2 + n)), max_tokens=6, temperature=0.0, ignore_eos=True) for n in (7, 30)]
         eng.generate(reqs)
     finally:
@@ -158,19 +158,16 @@ def test_graph_capture_with_dead_cycles_holding_multi_stream_tensors():
     assert all(len(r.output) == 6 for r in reqs) and eng.stats.graph_replays > 0
 
 
-@pytest.mark.parametrize("phase_streams", [False, True])
-def test_pipelined_windows_eos_and_arrivals(phase_streams):
+def test_pipelined_windows_eos_and_arrivals():
     """Pipelined multi-step decode windows (graphs) must produce exactly the eager
     engine's tokens with staggered lengths, EOS inside a window and requests that
-    arrive while others decode — also with prefill / decode on their own priority
-    streams (engine.phase_streams)."""
+    arrive while others decode."""
     cfg = get_config("tiny-gqa4")
     m = LlamaModel(cfg, device="cuda").init_random(seed=6)
 
     def run(graphs, eos):
         kv = PagedKVCache(cfg.layers, 256, cfg.kv_heads, 128, 16, device="cuda")
-        eng = LLMEngine(m, kv, max_batch=8, max_context=1024, use_graphs=graphs, multi_step=4,
-                        phase_streams=phase_streams and graphs)
+        eng = LLMEngine(m, kv, max_batch=8, max_context=1024, use_graphs=graphs, multi_step=4)
         if eos is not None:
             eng.eos = {eos}
         first = [GenRequest(list(range(3, 3 + n)), max_tokens=mt, temperature=0.8, seed=s)
