@@ -35,6 +35,7 @@ namespace oamd {
 namespace {
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kT = 256;          // tile rows / cols
 constexpr int kBK = 64;          // K per tile step (one 128-B line per row)
@@ -319,7 +320,9 @@ __device__ __forceinline__ void mfma_tied(f32x4& acc, const u16x8& a, const u16x
 }
 
 // DM: how the stages are loaded — 0: global_load_lds (flat address per lane), 1: buffer_load
-// ... lds (SGPR descriptor, 32-bit lane offset, K step in soffset). Timing experiments only
+// ... lds (SGPR descriptor, 32-bit lane offset, K step in soffset), 6: register staging
+// (global_load_dwordx4 into one of two register sets in step t, ds_write_b128 of that set
+// into the LDS image in step t+1, same image as the DMA). Timing experiments only
 // (wrong results): 2 no loads inside the loop; 3 every piece read from 1 KiB of contiguous
 // memory; 4 the 8 pieces issued back to back after the first MFMA row; 5 W pieces only
 template <int EPI, int DM = 0>
@@ -398,25 +401,51 @@ __global__ void __launch_bounds__(256) gemm_tile256_r4_kernel(const bf16_t* __re
     }
   };
 
+  // register staging (DM 6): piece q of stage kt -> set[q]; set -> this wave's LDS slot
+  auto gload = [&](int kt, u32x4 (&st)[8], int q) {
+    const uint32_t k2 = (uint32_t)kt * (kBK4 * 2);
+    st[q] = q < 4 ? __builtin_amdgcn_raw_buffer_load_b128(xr, (int)xs[q], (int)k2, 0)
+                  : __builtin_amdgcn_raw_buffer_load_b128(wr, (int)ws[q - 4], (int)k2, 0);
+  };
+  auto lwrite = [&](int buf, const u32x4 (&st)[8], int q) {
+    char* dst = lds + buf * kStage + w * 1024 + (q < 4 ? q * 4096 : kWOff + (q - 4) * 4096) + lane * 16;
+    *reinterpret_cast<u32x4*>(dst) = st[q];
+  };
+
   f32x4 acc[8][8];   // [token block][feature block]
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   u16x8 xa[8], wa[8], xb[8], wb[8];
+  u32x4 sa[8], sb[8];
   // one K-step: 64 MFMAs; after each 8-MFMA row, two fragment reads of step kt+1 and one
   // DMA piece of step kt+3. Branch-free: past the last step the reads fetch a buffer no
   // one uses and the DMA re-loads step T-1 into buffer (kt+3) % 4, whose stage (kt-1) is
-  // consumed and which no later step reads; the loop's exit drains those DMAs
+  // consumed and which no later step reads; the loop's exit drains those DMAs.
+  // DM 6: the row's global load of stage kt+3 goes to set `ld`, and the row writes piece i
+  // of set `wr` (stage kt+2, loaded in step kt-1) into buffer (kt+2) % 4 (stage kt-2's,
+  // whose fragments were read in step kt-3); the barrier ending step kt publishes it for
+  // the fragment reads of step kt+1.
   const int T = K / kBK4;   // even (K % 64 == 0)
-  auto step = [&](u16x8 (&xf)[8], u16x8 (&wf)[8], u16x8 (&nx)[8], u16x8 (&nw)[8], int kt) {
+  auto step = [&](u16x8 (&xf)[8], u16x8 (&wf)[8], u16x8 (&nx)[8], u16x8 (&nw)[8], int kt, u32x4 (&ld)[8],
+                  u32x4 (&wr)[8]) {
     const int ks = min(kt + 3, T - 1), kb = (kt + 3) & (kNS - 1);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) mfma_tied(acc[i][j], wf[j], xf[i]);
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (DM == 4) {
+      if constexpr (DM == 6) {
+        gload(ks, ld, i);
+        lwrite((kt + 2) & (kNS - 1), wr, i);
+      } else if constexpr (DM == 7) {   // timing: loads only (the set kept live, never written)
+        gload(ks, ld, i);
+        asm volatile("" ::"v"(wr[i]));
+      } else if constexpr (DM == 8) {   // timing: LDS writes only (of registers never loaded)
+        asm volatile("" : "+v"(wr[i]));
+        lwrite((kt + 2) & (kNS - 1), wr, i);
+      } else if constexpr (DM == 4) {
         if (i == 0)
 #pragma unroll
           for (int q = 0; q < 8; ++q) dma(ks, kb, q);
@@ -439,13 +468,27 @@ __global__ void __launch_bounds__(256) gemm_tile256_r4_kernel(const bf16_t* __re
     for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
   asm volatile("s_nop 4");
 
+  if constexpr (DM >= 6) {   // stages 0, 1 into LDS; stage 2 in set B (written by step 0)
 #pragma unroll
-  for (int q = 0; q < 8; ++q) dma(0, 0, q);
+    for (int q = 0; q < 8; ++q) gload(0, sa, q);
 #pragma unroll
-  for (int q = 0; q < 8; ++q) dma(min(1, T - 1), 1, q);
+    for (int q = 0; q < 8; ++q) gload(min(1, T - 1), sb, q);
 #pragma unroll
-  for (int q = 0; q < 8; ++q) dma(min(2, T - 1), 2, q);
-  vm_wait<8>();   // stages 0 and 1 landed (this wave's pieces); stage 2 in flight
+    for (int q = 0; q < 8; ++q) lwrite(0, sa, q);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) lwrite(1, sb, q);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) gload(min(2, T - 1), sb, q);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  } else {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) dma(0, 0, q);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) dma(min(1, T - 1), 1, q);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) dma(min(2, T - 1), 2, q);
+    vm_wait<8>();   // stages 0 and 1 landed (this wave's pieces); stage 2 in flight
+  }
   seg_barrier();
 #pragma unroll
   for (int q = 0; q < 16; ++q) rd1(0, xa, wa, q);
@@ -453,14 +496,14 @@ __global__ void __launch_bounds__(256) gemm_tile256_r4_kernel(const bf16_t* __re
   // v_accvgpr_write right before an asm MFMA reads them (an unpadded hazard)
   for (int t = 0; t < T; t += 2) {
     // step t: regs A hold stage t; read stage t+1 into B; DMA stage t+3
-    step(xa, wa, xb, wb, t);
+    step(xa, wa, xb, wb, t, sa, sb);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    vm_wait<8>();   // stage t+2 landed (this wave's pieces); stage t+3 in flight
+    if constexpr (DM < 6) vm_wait<8>();   // stage t+2 landed (this wave's pieces); stage t+3 in flight
     seg_barrier();
     // step t+1: regs B hold stage t+1; read stage t+2 into A; DMA stage t+4
-    step(xb, wb, xa, wa, t + 1);
+    step(xb, wb, xa, wa, t + 1, sb, sa);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    vm_wait<8>();
+    if constexpr (DM < 6) vm_wait<8>();
     seg_barrier();
   }
   vm_wait<0>();   // the tail's dummy DMAs must land before the workgroup's LDS is released
@@ -744,6 +787,13 @@ int gemm_tile(const bf16_t* X, const bf16_t* W, bf16_t* Y, const bf16_t* bias, i
     if (silu_gu) gemm_tile256_q4_kernel<kEpiSilu><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
     else if (bias) gemm_tile256_q4_kernel<kEpiBias><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
     else gemm_tile256_q4_kernel<kEpiStore><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+  } else if (variant == 10 && off32) {   // 4-wave ring, register-staged loads
+    if (silu_gu) gemm_tile256_r4_kernel<kEpiSilu, 6><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+    else if (bias) gemm_tile256_r4_kernel<kEpiBias, 6><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+    else gemm_tile256_r4_kernel<kEpiStore, 6><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+  } else if ((variant == 11 || variant == 12) && off32 && !silu_gu && !bias) {   // register-staging timing splits
+    if (variant == 11) gemm_tile256_r4_kernel<kEpiStore, 7><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+    else gemm_tile256_r4_kernel<kEpiStore, 8><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
   } else if (variant >= 4 && variant <= 8 && off32 && !silu_gu && !bias) {   // ring-4 load experiments
     if (variant == 4) gemm_tile256_r4_kernel<kEpiStore, 1><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
     else if (variant == 5) gemm_tile256_r4_kernel<kEpiStore, 2><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);

@@ -251,24 +251,44 @@ __global__ void __launch_bounds__(NT) ac_scan_wide_kernel(
   };
 
   // Exact walk of one chunk of stream k from state s (cold states through the
-  // global table) with match emission when `own`: the rare path. Rolled loop,
-  // bytes re-read from global memory (the chunk was just loaded: L2-resident).
-  auto slow = [&](int k, int64_t at, uint32_t s, uint32_t nl_now, bool own) -> uint32_t {
-    const uint8_t* tp = text + at;
-    const int lim = static_cast<int>(end[k] - at < CH ? end[k] - at : CH);  // bytes before the stream end
+  // global table) with match emission when `own`: the rare path. The chunk's bytes
+  // come from the registers the fast walk used (zeros outside the stream, as there);
+  // each byte step is one LDS read unless a lane of the wave is in a cold state
+  // (wave-uniform branch to the global table), and emission sits behind another.
+  // Rolled over the chunk's dwords (a dword picked by a 4-level select, no scratch),
+  // unrolled over the 4 bytes of each.
+  auto slow = [&](int k, const u32x4_t (&cu)[NV], int64_t at, uint32_t s, uint32_t nl_now, bool own) -> uint32_t {
 #pragma unroll 1
-    for (int i = 0; i < CH; ++i) {
-      const uint32_t b = (at + i >= 0 && i < lim) ? tp[i] : 0u;
-      const uint32_t sk = s & 0x7fffu;
-      const uint32_t e = sk < Hs ? static_cast<uint32_t>(tl[b * kWideStride + sk])
-                                 : static_cast<uint32_t>(tg[(sk << log2C) | cls[b]]);
-      if (own && (e & 0x8000u)) {
-        const uint64_t p = static_cast<uint64_t>(at + i);
-        emit_matches(e & 0x7fffu, static_cast<uint32_t>(p >> seg_shift), static_cast<uint32_t>(p) & seg_mask,
-                     nl_now | ((mid >> k & 1u) << 31), out_off, out_ids, matches, count, cap);
+    for (int d = 0; d < CH / 4; ++d) {
+      u32x4_t v4 = cu[0];
+      if constexpr (NV == 4) {
+        const u32x4_t v01 = (d & 4) ? cu[1] : cu[0];
+        const u32x4_t v23 = (d & 4) ? cu[3] : cu[2];
+        v4 = (d & 8) ? v23 : v01;
+      } else if constexpr (NV == 2) {
+        v4 = (d & 4) ? cu[1] : cu[0];
       }
-      nl_now += (own && b == 10u);
-      s = e;
+      const uint32_t w01 = (d & 1) ? v4[1] : v4[0];
+      const uint32_t w23 = (d & 1) ? v4[3] : v4[2];
+      const uint32_t wv = (d & 2) ? w23 : w01;
+#pragma unroll
+      for (int by = 0; by < 4; ++by) {
+        const uint32_t b = (wv >> (8 * by)) & 0xffu;
+        const uint32_t sk = s & 0x7fffu;
+        uint32_t e = tl[b * kWideStride + (sk & 0xffu)];
+        if (__ballot(sk >= Hs)) {
+          if (sk >= Hs) e = tg[(sk << log2C) | cls[b]];
+        }
+        if (__ballot(own && (e & 0x8000u))) {
+          if (own && (e & 0x8000u)) {
+            const uint64_t p = static_cast<uint64_t>(at + 4 * d + by);
+            emit_matches(e & 0x7fffu, static_cast<uint32_t>(p >> seg_shift), static_cast<uint32_t>(p) & seg_mask,
+                         nl_now | ((mid >> k & 1u) << 31), out_off, out_ids, matches, count, cap);
+          }
+        }
+        nl_now += (own && b == 10u);
+        s = e;
+      }
     }
     return s;
   };
@@ -317,7 +337,7 @@ __global__ void __launch_bounds__(NT) ac_scan_wide_kernel(
     if (__ballot(flag != 0)) {
 #pragma unroll   // compile-time k: a runtime index would put st[]/pos[] in scratch
       for (int k = 0; k < NS; ++k)
-        if (flag >> k & 1u) st[k] = slow(k, pos[k] + delta, s0[k], nl0[k], own >> k & 1u);
+        if (flag >> k & 1u) st[k] = slow(k, cur[k], pos[k] + delta, s0[k], nl0[k], own >> k & 1u);
     }
   };
 
