@@ -246,36 +246,6 @@ void gemm_tile(const at::Tensor& x, const at::Tensor& w, const c10::optional<at:
                      silu_gu, (int)variant, (int)splits, pp, cur_stream()));
 }
 
-void gemm_dw(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& y_opt,
-             const c10::optional<at::Tensor>& p, int64_t splits, int64_t bn, bool silu_gu) {
-  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
-  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && w.size(1) == x.size(1), "x [M,K], w [N,K]");
-  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
-  TORCH_CHECK(M >= 1 && M <= 256, "gemm_dw: 1 <= M <= 256");
-  TORCH_CHECK((bn == 64 || bn == 128) && N % bn == 0, "gemm_dw: bn in {64, 128}, N % bn == 0");
-  TORCH_CHECK(splits >= 1 && splits <= 32 && K % (64 * splits) == 0, "gemm_dw: K % (64 * splits) == 0");
-  TORCH_CHECK(!silu_gu || (splits == 1 && bn == 128), "gemm_dw: fused SwiGLU needs splits == 1, bn == 128");
-  bf16_t* yp = nullptr;
-  if (y_opt.has_value()) {
-    CHECK_BF16(*y_opt); CHECK_CONTIG(*y_opt);
-    TORCH_CHECK(y_opt->dim() == 2 && y_opt->size(0) == M && y_opt->size(1) == (silu_gu ? N / 2 : N), "gemm_dw: y");
-    yp = ptr<bf16_t>(*y_opt);
-  } else {
-    TORCH_CHECK(splits > 1 && !silu_gu, "y may be omitted only for split-K slabs summed by the consumer");
-  }
-  float* pp = nullptr;
-  if (splits > 1) {
-    TORCH_CHECK(p.has_value(), "split-K needs a partial buffer");
-    CHECK_DT(*p, at::kFloat); CHECK_CONTIG(*p);
-    TORCH_CHECK(p->numel() >= splits * M * N, "partial buffer too small");
-    pp = p->data_ptr<float>();
-  }
-  TORCH_CHECK(M * K < (1LL << 40) && N * K < (1LL << 40), "gemm too large");
-  const c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
-  RC(oamd::gemm_dw(ptr<bf16_t>(x), ptr<bf16_t>(w), yp, pp, (int)M, (int)N, (int)K, (int)splits, (int)bn, silu_gu,
-                   cur_stream()));
-}
-
 void gemm_pp(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& y_opt,
              const c10::optional<at::Tensor>& p, int64_t splits, int64_t bm, bool silu_gu, bool nt, bool one_seg) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
@@ -561,8 +531,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_tile", &gemm_tile, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"),
         pybind11::arg("bias") = pybind11::none(), pybind11::arg("silu_gu") = false, pybind11::arg("variant") = 0,
         pybind11::arg("splits") = 1, pybind11::arg("partial") = pybind11::none());
-  m.def("gemm_dw", &gemm_dw, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"), pybind11::arg("p"),
-        pybind11::arg("splits") = 1, pybind11::arg("bn") = 128, pybind11::arg("silu_gu") = false);
   m.def("gemm_pp", &gemm_pp, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"),
         pybind11::arg("p") = pybind11::none(), pybind11::arg("splits") = 1, pybind11::arg("bm") = 256,
         pybind11::arg("silu_gu") = false, pybind11::arg("nt") = true, pybind11::arg("one_seg") = false);

@@ -104,10 +104,6 @@ def gate_up_silu(x: torch.Tensor, wgu: torch.Tensor, block: int | None) -> torch
     if (x.is_cuda and block == 64 and x.dtype == torch.bfloat16 and M % 64 == 0 and M <= 256 and N % 128 == 0
             and K % 64 == 0 and x.is_contiguous() and wgu.is_contiguous()):
         t = _gemm_table_get().get(("silu", M, N, K))
-        if t == "dw":   # deep weight stream, one 256-row tile (gemm_dw.hip)
-            y = torch.empty(M, N // 2, dtype=x.dtype, device=x.device)
-            kernels().gemm_dw(x, wgu, y, None, 1, 128, True)
-            return y
         if isinstance(t, str) and t.startswith("pp"):   # ping-pong kernel, nt weight loads (bm 128 / 256)
             y = torch.empty(M, N // 2, dtype=x.dtype, device=x.device)
             kernels().gemm_pp(x, wgu, y, None, 1, int(t[2:]), True, True)
@@ -292,7 +288,7 @@ def gemm_plan(M: int, N: int, K: int):
     if t in ("blas", "tile"):   # hipBLASLt / the 256x256-tile kernel (linear decides which)
         return None
     if t is not None:
-        return tuple(t)   # (bm, bn, S[, stages]) for gemm_decode, or ("dw", bn, S) for gemm_dw
+        return tuple(t)   # (bm, bn, S[, stages]) for gemm_decode
     return (row_tile(M), 64, gemm_splits(M, N, K))
 
 
@@ -393,18 +389,6 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None, sp
         if tile_ok(x, w) and tile_out_ok(out):
             return linear_tile(x, w, out)
         return _blas(x, w, out, None)
-    if plan[0] == "dw" and bm is None and bn is None:   # deep weight stream, all rows in one tile
-        bn, S = plan[1], splits or plan[2]
-        if S > 1 and (partial is None or partial.numel() < S * M * N):
-            partial = torch.empty(S * M * N, dtype=torch.float32, device=x.device)
-        if defer_reduce and S > 1 and out is None:
-            kernels().gemm_dw(x, w, None, partial, S, bn, False)
-            return SplitK(partial, S, M, N)
-        y = out if out is not None else torch.empty(M, N, dtype=x.dtype, device=x.device)
-        kernels().gemm_dw(x, w, y, partial if S > 1 else None, S, bn, False)
-        return y
-    if plan[0] == "dw":
-        plan = (row_tile(M), 64, plan[2])
     bm, bn, S = bm or plan[0], bn or plan[1], splits or plan[2]
     ns = stages or (plan[3] if len(plan) > 3 else 3)
     if S > 1 and (partial is None or partial.numel() < S * M * N):

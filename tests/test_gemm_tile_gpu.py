@@ -157,43 +157,3 @@ def test_gemm_pp_silu(M):
         y = torch.empty(M, inter, dtype=torch.bfloat16, device=DEV)
         ops.kernels().gemm_pp(x, wgu, y, None, 1, bm, True, True, one)
         _close(y, r, 3e-2)
-
-
-@pytest.mark.parametrize("M", [1, 77, 256])
-@pytest.mark.parametrize("N,K", [(128, 64), (384, 448), (1024, 1024), (6144, 4096)])
-def test_gemm_dw_decode(M, N, K):
-    """Deep-weight-stream decode GEMM (gemm_dw.hip): both column tiles, every split count
-    (fewer K-steps than the weight prefetch depth included), bf16 store, reduced and
-    deferred (slab) outputs, against the fp32 reference."""
-    torch.manual_seed(M + N + K)
-    x = _rand(M, K)
-    w = _rand(N, K, scale=0.05)
-    r = x.float() @ w.float().t()
-    P = torch.empty(8 * M * N, dtype=torch.float32, device=DEV)
-    for bn in (64, 128):
-        for S in (1, 2, 4, 8):
-            if K % (64 * S) or N % bn:
-                continue
-            y = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
-            ops.kernels().gemm_dw(x, w, y, P if S > 1 else None, S, bn, False)
-            _close(y, r)
-            if S > 1:
-                ops.kernels().gemm_dw(x, w, None, P, S, bn, False)
-                torch.cuda.synchronize()
-                _close(P[:S * M * N].view(S, M, N).sum(0), r)
-
-
-@pytest.mark.parametrize("M", [3, 200, 256])
-def test_gemm_dw_silu(M):
-    inter, K = 1024, 2048
-    torch.manual_seed(M)
-    x = _rand(M, K)
-    g = _rand(inter, K, scale=0.05)
-    u = _rand(inter, K, scale=0.05)
-    wgu = ops.interleave_gate_up(g, u)
-    gg = (x.float() @ g.float().t()).to(torch.bfloat16)
-    uu = (x.float() @ u.float().t()).to(torch.bfloat16)
-    r = ref.silu_mul(torch.cat([gg, uu], 1), None)
-    y = torch.empty(M, inter, dtype=torch.bfloat16, device=DEV)
-    ops.kernels().gemm_dw(x, wgu, y, None, 1, 128, True)
-    _close(y, r, 3e-2)

@@ -1,11 +1,11 @@
 #!/usr/bin/env python3
 """Decode-bucket projections of Llama-3-8B at M = 256 (qkv, o, down, gate|up + SwiGLU):
 the production plan (ops.linear / ops.gate_up_silu as the model calls them, split-K slabs
-deferred to the consumer) against gemm_dw (csrc/kernels/gemm_dw.hip) for every feasible
-(BN, S). Weights are COLD as in a real decode step (each step streams 16 GB of weights +
+deferred to the consumer), alone and paired with the consumer that sums its slabs. Weights are COLD as in a real decode step (each step streams 16 GB of weights +
 the KV cache through a 256 MiB Infinity Cache): every call uses the next of enough
-rotating weight copies to exceed 512 MB. Split-K variants are also timed with a reduce
-of their fp32 slabs (what the consumer's extra reads cost). Interleaved rounds, medians.
+rotating weight copies to exceed 512 MB. Interleaved rounds, medians. (Round 4 also timed a
+deep-weight-stream kernel here, gemm_dw: slower on every shape,
+profiles/decode_gemm_dw_vs_table_m256_cold.jsonl, and deleted.)
 One JSON line per shape.
 
     python tools/bench_decode_gemm.py [--m 256] [--rounds 5]
@@ -23,7 +23,6 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from operator_amd import ops  # noqa: E402
-from operator_amd.ops import SplitK  # noqa: E402
 
 SHAPES = [("qkv", 6144, 4096, False), ("o", 4096, 4096, False), ("down", 4096, 14336, False),
           ("gate_up+silu", 28672, 4096, True)]
@@ -49,7 +48,6 @@ def main() -> int:
     ap.add_argument("--shapes", default="qkv,o,down,gate_up+silu")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
-    C = ops.kernels()
     M = a.m
     rows = []
     for name, N, K, silu in SHAPES:
@@ -59,9 +57,6 @@ def main() -> int:
         x = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)
         ncopy = max(2, -(-512 * 2**20 // (N * K * 2)))
         ws = [((torch.rand(N, K, device="cuda") * 2 - 1) * 0.05).to(torch.bfloat16) for _ in range(ncopy)]
-        NO = N // 2 if silu else N
-        y = torch.empty(M, NO, dtype=torch.bfloat16, device="cuda")
-        P = torch.empty(16 * M * N, dtype=torch.float32, device="cuda")
         it = {"i": 0}
 
         def nxt():
@@ -71,7 +66,6 @@ def main() -> int:
         cands = {}
         if silu:
             cands["table"] = lambda: ops.gate_up_silu(x, nxt(), ops.GU_BLOCK)
-            cands["dw_bn128_s1"] = lambda: C.gemm_dw(x, nxt(), y, None, 1, 128, True)
         else:
             # "+norm": the pair as the model runs it, the projection then a residual RMSNorm that
             # reads its output (summing the fp32 slabs of a split-K plan)
@@ -81,41 +75,13 @@ def main() -> int:
             norm = lambda r: ops.rmsnorm(r, nw, 1e-5, residual=res, out=yn)  # noqa: E731
             cands["table"] = lambda: ops.linear(x, nxt(), defer_reduce=True)
             cands["table+norm"] = lambda: norm(ops.linear(x, nxt(), defer_reduce=True))
-            for bn in (64, 128):
-                for S in (1, 2, 4, 8):
-                    if N % bn or K % (64 * S):
-                        continue
-                    if S == 1:
-                        cands[f"dw_bn{bn}_s1"] = (lambda bn=bn: C.gemm_dw(x, nxt(), y, None, 1, bn, False))
-                        cands[f"dw_bn{bn}_s1+norm"] = (lambda bn=bn: norm(C.gemm_dw(x, nxt(), y, None, 1, bn, False)
-                                                                          or y))
-                    else:
-                        cands[f"dw_bn{bn}_s{S}"] = (lambda bn=bn, S=S: C.gemm_dw(x, nxt(), None, P, S, bn, False))
-                        cands[f"dw_bn{bn}_s{S}+norm"] = (
-                            lambda bn=bn, S=S: norm(C.gemm_dw(x, nxt(), None, P, S, bn, False) or SplitK(P, S, M, N)))
-        # numerics of every gemm_dw variant against fp32
-        w0 = ws[0]
-        ref = x.float() @ w0.float().t()
-        if silu:
-            g = ref.view(M, -1, 2, ops.GU_BLOCK)[:, :, 0].reshape(M, -1).to(torch.bfloat16).float()
-            u = ref.view(M, -1, 2, ops.GU_BLOCK)[:, :, 1].reshape(M, -1).to(torch.bfloat16).float()
-            ref = (torch.nn.functional.silu(g).to(torch.bfloat16).float() * u)
-        errs = {}
-        for k in cands:
-            if not k.startswith("dw") or k.endswith("+norm"):
-                continue
-            bn, S = int(k.split("_")[1][2:]), int(k.split("_")[2][1:])
-            yy = torch.empty_like(y)
-            C.gemm_dw(x, w0, yy, P if S > 1 else None, S, bn, silu)
-            errs[k] = round((yy.float() - ref).abs().max().item(), 4)
         times = {k: [] for k in cands}
         for _ in range(a.rounds):
             for k, fn in cands.items():
                 times[k].append(timeit(fn, a.iters))
         us = {k: round(statistics.median(v), 2) for k, v in times.items()}
-        best = min((k for k in us if not k.endswith("+norm")), key=us.get)
-        r = {"M": M, "shape": name, "N": N, "K": K, "weight_copies": ncopy, "us": dict(sorted(us.items(), key=lambda t: t[1])),
-             "best": best, "best_weight_tb_s": round(N * K * 2 / us[best] / 1e6, 2), "dw_max_abs_err_vs_fp32": errs}
+        r = {"M": M, "shape": name, "N": N, "K": K, "weight_copies": ncopy, "us": us,
+             "weight_tb_s": round(N * K * 2 / us["table"] / 1e6, 2)}
         print(json.dumps(r), flush=True)
         rows.append(r)
         del ws
