@@ -33,6 +33,18 @@ int rope_kv(const bf16_t* qkv, int64_t qkv_stride, const int64_t* pos, const flo
 int gemm_decode(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, int N, int K, int S, int BN,
                 int BM, bool silu_gu, bool w_tiled, int stages, hipStream_t stream);
 
+// Compute-bound 256x256-tile GEMM (prefill projections, lm_head; gemm_tile.hip): Y[M, N] = X[M,K] W[N,K]^T
+// (+ bias[N]) for any M >= 1, N % 16 == 0, K % 64 == 0; silu_gu: fused SwiGLU over the 64-row interleaved
+// gate|up weight (N % 128 == 0), Y [M, N/2]. ldy = Y's row stride in elements.
+// S > 1: S-way split-K into fp32 slabs P[S][M][N], then reduced into Y (SwiGLU applied when silu_gu);
+// Y == nullptr leaves the slabs to the consumer (rmsnorm / rope_kv sum them).
+int gemm_tile(const bf16_t* X, const bf16_t* W, bf16_t* Y, const bf16_t* bias, int M, int N, int K, int ldy,
+              bool silu_gu, int variant, int S, float* P, hipStream_t stream);
+// Decode-bucket GEMM on the ping-pong schedule (gemm_pp.hip): Y[M,N] = X[M,K] W[N,K]^T, bm-row tiles
+// (128 / 256), 128-column tiles (N % 128 == 0), S-way split-K slabs P (S > 1; reduced into Y unless Y is
+// nullptr); silu_gu: fused SwiGLU (S == 1), Y [M, N/2]; nt: non-temporal weight loads.
+int gemm_pp(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, int N, int K, int S, int bm, bool silu_gu,
+            bool nt, hipStream_t stream, bool one_seg = false);
 // Y[M, N] = bf16(sum_s P[s][M][N]) (fp32 split-K slabs).
 int splitk_reduce(const float* P, bf16_t* Y, int64_t MN, int S, hipStream_t stream);
 // Skinny-M decode GEMM (M <= 32, gemm_skinny.hip): N % 16 == 0, K % (128 S) == 0; S-way split-K slabs P
