@@ -730,6 +730,209 @@ __global__ void __launch_bounds__(256) gemm_tile256_q4_kernel(const bf16_t* __re
   }
 }
 
+// Variant 13 ("two buffers, four phases"): four waves (one per SIMD, 128 x 128 outputs
+// each, 256 tied AGPR accumulators), BK = 64 tiles in two 64 KiB LDS buffers filled by
+// LDS-DMA pieces of 8 rows x 128 B (buffer_load ... lds: per-lane 32-bit row offsets fixed
+// for the kernel, the K step in soffset) — half the memory requests of 16 x 64-B pieces
+// (profiles/gemm_tile_pmc_l2_r4.txt: TCC_HIT 2.2e8 vs 9.9e7, TA_BUSY 2.5x). Tile t (buffer
+// t & 1) runs in four 32-MFMA phases:
+//   1. k-half 0 from registers A; read k-half 1 (registers B) — the tile's last reads;
+//      lgkmcnt(0) + barrier: every wave is done with buffer t & 1
+//   2. k-half 0 cont.; 8 X pieces of tile t+2 into buffer t & 1;
+//      vmcnt(16) + barrier: tile t+1's X pieces (issued in phase 2 of tile t-1) landed
+//   3. k-half 1 from registers B; 8 W pieces of tile t+2; read X of tile t+1, k-half 0;
+//      vmcnt(16) + barrier: tile t+1's W pieces landed
+//   4. k-half 1 cont.; read W of tile t+1, k-half 0 (registers A)
+// so every piece has a whole tile (128 MFMAs per wave) to land, a buffer is refilled only
+// after the barrier that follows its last read, and each staged piece is read one phase
+// after the wait + barrier that retire it. DMAs and fragment reads sit between MFMAs (one
+// per two). LDS image: 128-B rows, chunk slot = chunk ^ ((row >> 1) & 7) on the DMA
+// source and the read (conflict-free ds_read_b128, as variant 9).
+template <int EPI>
+__global__ void __launch_bounds__(256) gemm_tile256_h4_kernel(const bf16_t* __restrict__ X,
+                                                              const bf16_t* __restrict__ W, bf16_t* __restrict__ Y,
+                                                              const bf16_t* __restrict__ bias, int M, int N, int K,
+                                                              int ldy) {
+  constexpr int kHalf = 32768;       // one operand of a tile: 256 rows x 128 B
+  constexpr int kTile = 2 * kHalf;   // X then W
+  __shared__ __attribute__((aligned(1024))) char lds[2 * kTile];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 1, wn = w & 1;
+
+  const int mt = (M + kT - 1) / kT, nt = (N + kT - 1) / kT;
+  const int nwg = mt * nt;
+  const int lid = xcd_remap(blockIdx.x, nwg);
+  const int gsz = kGroupM * nt;
+  const int first_m = (lid / gsz) * kGroupM;
+  const int gm = min(mt - first_m, kGroupM);
+  const int tm = first_m + (lid % gsz) % gm;
+  const int tn = (lid % gsz) / gm;
+  const int m0 = tm * kT, n0 = tn * kT;
+
+  // DMA piece q (0..7) of an operand for wave w = rows 8 (w + 4q) .. +7; lane l -> row + l/8,
+  // LDS slot l % 8, source chunk slot ^ ((row >> 1) & 7). 32-bit byte offsets (launcher checks)
+  const int lrow = lane >> 3, lslot = lane & 7;
+  uint32_t xo[8], wo[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int row = 8 * (w + 4 * q) + lrow;
+    const int chunk = lslot ^ ((row >> 1) & 7);
+    xo[q] = ((uint32_t)min(m0 + row, M - 1) * (uint32_t)K + chunk * 8) * 2u;
+    wo[q] = ((uint32_t)min(n0 + row, N - 1) * (uint32_t)K + chunk * 8) * 2u;
+  }
+  const auto xr = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)((uint32_t)M * (uint32_t)K * 2u), 0x00020000);
+  const auto wr = __builtin_amdgcn_make_buffer_rsrc((void*)W, (short)0, (int)((uint32_t)N * (uint32_t)K * 2u), 0x00020000);
+  const int T = K / kBK;
+  auto dma_x = [&](int kt, int buf, int q) {
+    char* dst = lds + buf * kTile + (w + 4 * q) * 1024;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)dst, 16, (int)xo[q],
+                                             min(kt, T - 1) * (kBK * 2), 0, 0);
+  };
+  auto dma_w = [&](int kt, int buf, int q) {
+    char* dst = lds + buf * kTile + kHalf + (w + 4 * q) * 1024;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (__attribute__((address_space(3))) void*)dst, 16, (int)wo[q],
+                                             min(kt, T - 1) * (kBK * 2), 0, 0);
+  };
+
+  // fragments: X fragment i = rows wm*128 + 16 i + l15; W fragment j (f = j / 4, type =
+  // (j / 2) % 2, jj = j % 2) = rows f*128 + type*64 + wn*32 + jj*16 + l15; k-half h reads
+  // chunk 4h + lane/16 of the row, at its swizzled slot
+  const int l15 = lane & 15, lq = lane >> 4, sw = (l15 >> 1) & 7;
+  const int c0 = (lq ^ sw) << 4, c1 = ((4 + lq) ^ sw) << 4;
+  const int xrow = (wm * 128 + l15) * 128, wrow = (wn * 32 + l15) * 128;
+  auto rdx = [&](int buf, int c, u16x8 (&xf)[8], int i) {
+    xf[i] = *reinterpret_cast<const u16x8*>(lds + buf * kTile + xrow + i * 2048 + c);
+  };
+  auto rdw = [&](int buf, int c, u16x8 (&wf)[8], int j) {
+    const int r = (j >> 2) * 128 + ((j >> 1) & 1) * 64 + (j & 1) * 16;
+    wf[j] = *reinterpret_cast<const u16x8*>(lds + buf * kTile + kHalf + wrow + r * 128 + c);
+  };
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  u16x8 xa[8], wa[8], xb[8], wb[8];
+  // one MFMA row (token block i: 8 MFMAs) with up to four other instructions, one after
+  // every second MFMA (op(k), k = 0..3)
+  auto row = [&](const u16x8 (&xf)[8], const u16x8 (&wf)[8], int i, auto op) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      mfma_tied(acc[i][j], wf[j], xf[i]);
+      if (j & 1) {
+        __builtin_amdgcn_sched_barrier(0);
+        op(j >> 1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
+  asm volatile("s_nop 4");
+
+  // prologue: tiles 0 and 1 (buffers 0, 1); tile 0 landed; k-half 0 of tile 0 into A
+#pragma unroll
+  for (int q = 0; q < 8; ++q) dma_x(0, 0, q);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) dma_w(0, 0, q);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) dma_x(1, 1, q);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) dma_w(1, 1, q);
+  vm_wait<16>();
+  seg_barrier();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) rdx(0, c0, xa, i);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) rdw(0, c0, wa, j);
+
+  // one loop, no peeled copy (a second code path makes hipcc move accumulators with
+  // v_accvgpr_write right before an asm MFMA reads them)
+  for (int t = 0; t < T; ++t) {
+    const int b = t & 1, nb = b ^ 1;
+    // phase 1: rows 0-3 of k-half 0; read k-half 1 of tile t (X 8, W 8)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      row(xa, wa, i, [&](int k) {
+        if (k < 2) rdx(b, c1, xb, 2 * i + k);
+        else rdw(b, c1, wb, 2 * i + k - 2);
+      });
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    seg_barrier();
+    // phase 2: rows 4-7 of k-half 0; X pieces of tile t+2 into buffer b
+#pragma unroll
+    for (int i = 4; i < 8; ++i)
+      row(xa, wa, i, [&](int k) {
+        if (k < 2) dma_x(t + 2, b, 2 * (i - 4) + k);
+      });
+    vm_wait<16>();   // tile t+1's X pieces (this wave's)
+    seg_barrier();   // ... every wave's
+    // phase 3: rows 0-3 of k-half 1; W pieces of tile t+2; X of tile t+1, k-half 0
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      row(xb, wb, i, [&](int k) {
+        if (k < 2) dma_w(t + 2, b, 2 * i + k);
+        else rdx(nb, c0, xa, 2 * i + k - 2);
+      });
+    vm_wait<16>();   // tile t+1's W pieces
+    seg_barrier();
+    // phase 4: rows 4-7 of k-half 1; W of tile t+1, k-half 0
+#pragma unroll
+    for (int i = 4; i < 8; ++i)
+      row(xb, wb, i, [&](int k) {
+        if (k < 2) rdw(nb, c0, wa, 2 * (i - 4) + k);
+      });
+  }
+  vm_wait<0>();   // the tail's clamped re-loads land before the workgroup's LDS is released
+  asm volatile("s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
+
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int tok = m0 + wm * 128 + i * 16 + l15;
+    if (tok >= M) continue;
+    bf16_t* yrow = Y + (int64_t)tok * ldy;
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        if constexpr (EPI == kEpiSilu) {
+          const int col = (n0 >> 1) + f * 64 + wn * 32 + j * 16 + 4 * lq;
+          if (2 * col >= N) continue;
+          const f32x4 gt = acc[i][f * 4 + j], up = acc[i][f * 4 + 2 + j];
+          f32x4 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float gg = bf2f(f2bf(gt[r]));
+            const float uu = bf2f(f2bf(up[r]));
+            const float sg = bf2f(f2bf(gg / (1.f + __expf(-gg))));
+            o[r] = sg * uu;
+          }
+          *reinterpret_cast<uint2*>(yrow + col) = pack4(o);
+        } else {
+#pragma unroll
+          for (int ty = 0; ty < 2; ++ty) {
+            const int col = n0 + f * 128 + ty * 64 + wn * 32 + j * 16 + 4 * lq;
+            if (col >= N) continue;
+            f32x4 v = acc[i][f * 4 + ty * 2 + j];
+            if constexpr (EPI == kEpiBias) {
+              const uint2 bb = *reinterpret_cast<const uint2*>(bias + col);
+              v[0] += __uint_as_float(bb.x << 16);
+              v[1] += __uint_as_float(bb.x & 0xffff0000u);
+              v[2] += __uint_as_float(bb.y << 16);
+              v[3] += __uint_as_float(bb.y & 0xffff0000u);
+            }
+            *reinterpret_cast<uint2*>(yrow + col) = pack4(v);
+          }
+        }
+      }
+  }
+}
+
 // y[m, f] = SwiGLU of the split-K sums of the interleaved gate|up slabs (64-feature
 // blocks): g = bf16(sum_s P[s][m][128 b + j]), u = bf16(sum_s P[s][m][128 b + 64 + j]),
 // y = bf16(bf16(silu(g)) * u) — the numerics of the fused epilogue. 4 features per thread.
@@ -787,6 +990,10 @@ int gemm_tile(const bf16_t* X, const bf16_t* W, bf16_t* Y, const bf16_t* bias, i
     if (silu_gu) gemm_tile256_q4_kernel<kEpiSilu><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
     else if (bias) gemm_tile256_q4_kernel<kEpiBias><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
     else gemm_tile256_q4_kernel<kEpiStore><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+  } else if (variant == 13 && off32) {   // 4-wave, two 64 KiB buffers, four phases per K-tile
+    if (silu_gu) gemm_tile256_h4_kernel<kEpiSilu><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+    else if (bias) gemm_tile256_h4_kernel<kEpiBias><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+    else gemm_tile256_h4_kernel<kEpiStore><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
   } else if (variant == 10 && off32) {   // 4-wave ring, register-staged loads
     if (silu_gu) gemm_tile256_r4_kernel<kEpiSilu, 6><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
     else if (bias) gemm_tile256_r4_kernel<kEpiBias, 6><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);

@@ -1,5 +1,8 @@
 set -e
 cd $GRAFT_REPO_ROOT
-bash tools/gpu_scan.sh
-timeout -k 10 300 python -u tools/gemm_tile_variants.py --variants 10,11,12,5,1 > gpurun_out/gtv2.jsonl
+timeout -k 10 300 python -u -m pytest tests/test_gemm_tile_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/gt_tests.log 2>&1 || { tail -30 gpurun_out/gt_tests.log; exit 1; }
+tail -1 gpurun_out/gt_tests.log
+timeout -k 10 300 python -u tools/gemm_tile_variants.py --variants 13,2,1,4,10,11,12,5 > gpurun_out/gtv2.jsonl
+timeout -k 10 300 python -u tools/gemm_tile_variants.py --variants 13,2 --m 16384 --n 6144 --k 4096 >> gpurun_out/gtv2.jsonl
 cat gpurun_out/gtv2.jsonl
+bash tools/gpu_scan.sh
