@@ -748,7 +748,7 @@ __global__ void __launch_bounds__(256) gemm_tile256_q4_kernel(const bf16_t* __re
 // after the wait + barrier that retire it. DMAs and fragment reads sit between MFMAs (one
 // per two). LDS image: 128-B rows, chunk slot = chunk ^ ((row >> 1) & 7) on the DMA
 // source and the read (conflict-free ds_read_b128, as variant 9).
-template <int EPI>
+template <int EPI, int AUX = 0>
 __global__ void __launch_bounds__(256) gemm_tile256_h4_kernel(const bf16_t* __restrict__ X,
                                                               const bf16_t* __restrict__ W, bf16_t* __restrict__ Y,
                                                               const bf16_t* __restrict__ bias, int M, int N, int K,
@@ -787,12 +787,12 @@ __global__ void __launch_bounds__(256) gemm_tile256_h4_kernel(const bf16_t* __re
   auto dma_x = [&](int kt, int buf, int q) {
     char* dst = lds + buf * kTile + (w + 4 * q) * 1024;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)dst, 16, (int)xo[q],
-                                             min(kt, T - 1) * (kBK * 2), 0, 0);
+                                             min(kt, T - 1) * (kBK * 2), 0, AUX);
   };
   auto dma_w = [&](int kt, int buf, int q) {
     char* dst = lds + buf * kTile + kHalf + (w + 4 * q) * 1024;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (__attribute__((address_space(3))) void*)dst, 16, (int)wo[q],
-                                             min(kt, T - 1) * (kBK * 2), 0, 0);
+                                             min(kt, T - 1) * (kBK * 2), 0, AUX);
   };
 
   // fragments: X fragment i = rows wm*128 + 16 i + l15; W fragment j (f = j / 4, type =
@@ -868,7 +868,7 @@ __global__ void __launch_bounds__(256) gemm_tile256_h4_kernel(const bf16_t* __re
 #pragma unroll
     for (int i = 4; i < 8; ++i)
       row(xa, wa, i, [&](int k) {
-        if (k < 2) dma_x(t + 2, b, 2 * (i - 4) + k);
+        if (!(k & 1)) dma_x(t + 2, b, 2 * (i - 4) + (k >> 1));
       });
     vm_wait<16>();   // tile t+1's X pieces (this wave's)
     seg_barrier();   // ... every wave's
@@ -876,8 +876,8 @@ __global__ void __launch_bounds__(256) gemm_tile256_h4_kernel(const bf16_t* __re
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       row(xb, wb, i, [&](int k) {
-        if (k < 2) dma_w(t + 2, b, 2 * i + k);
-        else rdx(nb, c0, xa, 2 * i + k - 2);
+        if (!(k & 1)) dma_w(t + 2, b, 2 * i + (k >> 1));
+        else rdx(nb, c0, xa, 2 * i + (k >> 1));
       });
     vm_wait<16>();   // tile t+1's W pieces
     seg_barrier();
@@ -885,7 +885,7 @@ __global__ void __launch_bounds__(256) gemm_tile256_h4_kernel(const bf16_t* __re
 #pragma unroll
     for (int i = 4; i < 8; ++i)
       row(xb, wb, i, [&](int k) {
-        if (k < 2) rdw(nb, c0, wa, 2 * (i - 4) + k);
+        if (!(k & 1)) rdw(nb, c0, wa, 2 * (i - 4) + (k >> 1));
       });
   }
   vm_wait<0>();   // the tail's clamped re-loads land before the workgroup's LDS is released
@@ -994,6 +994,10 @@ int gemm_tile(const bf16_t* X, const bf16_t* W, bf16_t* Y, const bf16_t* bias, i
     if (silu_gu) gemm_tile256_h4_kernel<kEpiSilu><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
     else if (bias) gemm_tile256_h4_kernel<kEpiBias><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
     else gemm_tile256_h4_kernel<kEpiStore><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+  } else if (variant >= 14 && variant <= 16 && off32 && !silu_gu && !bias) {   // variant 13, DMA cache policy
+    if (variant == 14) gemm_tile256_h4_kernel<kEpiStore, 16><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+    else if (variant == 15) gemm_tile256_h4_kernel<kEpiStore, 2><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+    else gemm_tile256_h4_kernel<kEpiStore, 18><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
   } else if (variant == 10 && off32) {   // 4-wave ring, register-staged loads
     if (silu_gu) gemm_tile256_r4_kernel<kEpiSilu, 6><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
     else if (bias) gemm_tile256_r4_kernel<kEpiBias, 6><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
