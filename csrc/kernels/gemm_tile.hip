@@ -3,29 +3,28 @@
 // (SURVEY.md §2.4 N7 "prefill is compute-bound tiles (256² 8-phase template)";
 // replaces the external LLM behind J/service/AIInterfaceRestClient.java:37-39).
 //
-// Structure (cdna_hip_programming.md §5 "The 256² 8-phase template", T1-T5):
-//   * one 256 x 256 output tile per 512-thread workgroup (8 waves, 2 per SIMD),
-//     BK = 64, both operands staged global -> LDS by LDS-DMA
-//     (global_load_lds_dwordx4) into two 64 KiB buffers; every tile is split
-//     into four 16 KiB regions (X rows 0-127, W rows 0-127, W rows 128-255,
-//     X rows 128-255) that are loaded, waited for and recycled one at a time;
-//   * the K-tile is computed in four phases, one per (X half, W half) quadrant,
-//     16 MFMA v_mfma_f32_16x16x32_bf16 per wave each; a phase issues one region
-//     of the NEXT K-tile, so 1.5 tiles stay in flight with only 2 buffers and
-//     the LDS-DMA never drains inside the loop (counted vmcnt, raw s_barrier);
-//   * ping-pong: waves 4-7 run one barrier segment behind waves 0-3, so on
-//     every SIMD one wave issues its LDS fragment reads + DMA while the other
-//     runs its MFMA cluster (s_setprio 1 around it, T5);
-//   * the LDS image is lane-linear (DMA) with the st_16x32-style XOR swizzle
-//     applied to the global SOURCE chunk and the read address (rule 21):
-//     slot = chunk ^ ((row >> 1) & 7), conflict-free for ds_read_b128;
-//   * operands swapped in the MFMA (A = W fragment, B = X fragment) so each
-//     lane's accumulator holds 4 consecutive OUTPUT FEATURES of one token:
-//     8-byte stores, and a fused SwiGLU epilogue in registers when the gate|up
-//     weight is interleaved in 64-row blocks (wave wc owns gate rows
-//     wc*16..+16 and the matching up rows 64 + wc*16..+16 of every 128 rows);
-//   * XCD-aware, grouped tile order (T1 bijective remap, then GROUP_M m-tiles
-//     per n-tile) so the 32 tiles an XCD runs at once share X/W panels in L2.
+// Two schedules of one 256 x 256 output tile per workgroup, BK = 64, both operands staged
+// global -> LDS by LDS-DMA into two 64 KiB buffers (128-B rows; the st_16x32-style XOR
+// swizzle slot = chunk ^ ((row >> 1) & 7) applied to the global SOURCE chunk and to the read
+// address, rule 21: conflict-free ds_read_b128), v_mfma_f32_16x16x32_bf16 with operands
+// swapped (A = W fragment, B = X fragment) so each lane's accumulator holds 4 consecutive
+// OUTPUT FEATURES of one token: 8-byte stores, and a fused SwiGLU epilogue in registers when
+// the gate|up weight is interleaved in 64-row blocks. XCD-aware, grouped tile order (T1
+// bijective remap, then GROUP_M m-tiles per n-tile) so the 32 tiles an XCD runs at once
+// share X/W panels in L2.
+//   * h4 (default, gemm_tile256_h4_kernel below): 4 waves, one per SIMD, 128 x 128 outputs
+//     each in 256 tied AGPRs; four 32-MFMA phases per K-tile with the next tile's DMA and
+//     fragment reads between the MFMAs and 3 barriers (details at the kernel);
+//   * ping-pong (gemm_tile256_kernel, variants 2 / 3 and the split-K slabs): 8 waves, two
+//     per SIMD; every tile split into four 16 KiB regions (X rows 0-127, W rows 0-127, W rows
+//     128-255, X rows 128-255) loaded, waited for and recycled one at a time; the K-tile in
+//     four (or two, PH2) phases, one per (X half, W half) quadrant; waves 4-7 run one
+//     barrier segment behind waves 0-3 so on every SIMD one wave issues its LDS reads + DMA
+//     while the other runs its MFMA cluster (s_setprio 1 around it, T5).
+// Round 4 measured and deleted three other 4-wave schedules (a 4-stage BK = 32 ring with
+// LDS-DMA or register staging, a BK = 64 region ring): 16 x 64-B DMA pieces cost twice the
+// memory requests of 8 x 128-B ones and register-staged loads cost as much as LDS-DMA
+// (profiles/gemm_tile_pmc_l2_r4.txt, gemm_tile_variants_r4*.jsonl).
 // M and N tails are handled by clamped loads and masked stores; K % 64 == 0.
 #include "common.h"
 #include "kernels.h"
@@ -35,7 +34,6 @@ namespace oamd {
 namespace {
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kT = 256;          // tile rows / cols
 constexpr int kBK = 64;          // K per tile step (one 128-B line per row)
@@ -295,442 +293,13 @@ __global__ void __launch_bounds__(512) gemm_tile256_kernel(const bf16_t* __restr
     }
 }
 
-// Variant 1 ("ring-4"): four waves (one per SIMD), each owning a 128 x 128 output block
-// (64 accumulator fragments = 256 AGPRs, 0.25 KB of LDS fragment reads per MFMA), and a
-// 4-deep ring of BK = 32 stages (32 KiB each: 128 KiB of LDS) so two stages are always
-// in flight behind the one being computed and the one being read: the counted
-// vmcnt(8) at the end of a step leaves the youngest stage's DMA outstanding, never 0
-// inside the loop (round 3's 2-buffer BK = 64 version waited 15 % of its wave-cycles on
-// a vmcnt(0) per K-tile, profiles/gemm_tile_pmc_vs_hipblaslt.txt).
-//   * LDS image: a stage is 32 pieces of 1 KiB (16 rows x 64 B; pieces 0-15 X rows,
-//     16-31 W rows). Inside a piece, row r's four 16-B k-chunks c sit at slots
-//     4r + (c ^ f(r >> 2)), f = {0, 3, 2, 1}: the DMA (lane-linear: lane l writes slot l)
-//     reads each row's 64 B with four consecutive lanes (coalesced), and a fragment is ONE
-//     ds_read_b128 per lane (lane l: row l & 15, chunk l >> 4) whose four 16-lane groups
-//     each hit 16 distinct bank slots — conflict-free by the choice of f.
-//   * per step and wave: 64 MFMAs (v_mfma_f32_16x16x32_bf16, accumulator tied in an AGPR
-//     by inline asm: the builtin makes hipcc shuffle 256 accumulators through
-//     v_accvgpr copies), the 16 fragment reads of the NEXT stage (register double
-//     buffer) and 8 LDS-DMA pieces of the stage three ahead, spread one row of 8 MFMAs
-//     apart; one raw s_barrier per step.
-// Stage t lives in buffer t % 4; step t reads stage t+1 and refills buffer (t+3) % 4,
-// whose stage t-1 every wave finished reading before the barrier that ended step t-1.
+// 16x16x32 bf16 MFMA with the accumulator tied in AGPRs by inline asm: the builtin makes
+// hipcc shuffle 256 accumulators through v_accvgpr copies.
 __device__ __forceinline__ void mfma_tied(f32x4& acc, const u16x8& a, const u16x8& b) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 
-// DM: how the stages are loaded — 0: global_load_lds (flat address per lane), 1: buffer_load
-// ... lds (SGPR descriptor, 32-bit lane offset, K step in soffset), 6: register staging
-// (global_load_dwordx4 into one of two register sets in step t, ds_write_b128 of that set
-// into the LDS image in step t+1, same image as the DMA). Timing experiments only
-// (wrong results): 2 no loads inside the loop; 3 every piece read from 1 KiB of contiguous
-// memory; 4 the 8 pieces issued back to back after the first MFMA row; 5 W pieces only
-template <int EPI, int DM = 0>
-__global__ void __launch_bounds__(256) gemm_tile256_r4_kernel(const bf16_t* __restrict__ X,
-                                                              const bf16_t* __restrict__ W, bf16_t* __restrict__ Y,
-                                                              const bf16_t* __restrict__ bias, int M, int N, int K,
-                                                              int ldy) {
-  constexpr int kBK4 = 32, kNS = 4, kStage = 32768, kWOff = 16384;
-  __shared__ __attribute__((aligned(1024))) char lds[kNS * kStage];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = w >> 1, wn = w & 1;
-
-  const int mt = (M + kT - 1) / kT, nt = (N + kT - 1) / kT;
-  const int nwg = mt * nt;
-  const int lid = xcd_remap(blockIdx.x, nwg);
-  const int gsz = kGroupM * nt;
-  const int first_m = (lid / gsz) * kGroupM;
-  const int gm = min(mt - first_m, kGroupM);
-  const int tm = first_m + (lid % gsz) % gm;
-  const int tn = (lid % gsz) / gm;
-  const int m0 = tm * kT, n0 = tn * kT;
-
-  // DMA: wave w issues pieces w + 4i (i < 4: X rows 16(w + 4i).., i >= 4: W rows
-  // 16(w + 4(i - 4))..); lane l -> row l >> 2, chunk (l & 3) ^ f(l >> 4). 32-bit byte offsets
-  // (the launcher guarantees M*K*2 and N*K*2 < 4 GiB): scalar base + vector offset loads.
-  const int r15 = lane >> 2, ck = (lane & 3) ^ ((4 - (lane >> 4)) & 3);
-  uint32_t xs[4], ws[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    xs[i] = ((uint32_t)min(m0 + 16 * (w + 4 * i) + r15, M - 1) * (uint32_t)K + ck * 8) * 2u;
-    ws[i] = ((uint32_t)min(n0 + 16 * (w + 4 * i) + r15, N - 1) * (uint32_t)K + ck * 8) * 2u;
-  }
-  const char* Xb = reinterpret_cast<const char*>(X);
-  const char* Wb = reinterpret_cast<const char*>(W);
-  const auto xr = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)((uint32_t)M * (uint32_t)K * 2u), 0x00020000);
-  const auto wr = __builtin_amdgcn_make_buffer_rsrc((void*)W, (short)0, (int)((uint32_t)N * (uint32_t)K * 2u), 0x00020000);
-  auto dma = [&](int kt, int buf, int q) {   // piece q (0..7) of this wave for K-step kt, into buffer buf
-    char* dst = lds + buf * kStage + w * 1024;
-    const uint32_t k2 = (uint32_t)kt * (kBK4 * 2);
-    if constexpr (DM == 1) {
-      if (q < 4)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)(dst + q * 4096), 16,
-                                                 (int)xs[q], (int)k2, 0, 0);
-      else
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (__attribute__((address_space(3))) void*)(dst + kWOff + (q - 4) * 4096),
-                                                 16, (int)ws[q - 4], (int)k2, 0, 0);
-    } else if constexpr (DM == 3) {
-      const char* base = (q < 4 ? Xb : Wb) + (uint32_t)(w * 8 + q) * 1024u + (uint32_t)lane * 16u + k2 * 64u;
-      __builtin_amdgcn_global_load_lds(base, (__attribute__((address_space(3))) void*)(dst + (q < 4 ? q * 4096 : kWOff + (q - 4) * 4096)),
-                                       16, 0, 0);
-    } else {
-      if (q < 4)
-        __builtin_amdgcn_global_load_lds(Xb + xs[q] + k2, (__attribute__((address_space(3))) void*)(dst + q * 4096),
-                                         16, 0, 0);
-      else
-        __builtin_amdgcn_global_load_lds(Wb + ws[q - 4] + k2,
-                                         (__attribute__((address_space(3))) void*)(dst + kWOff + (q - 4) * 4096), 16, 0,
-                                         0);
-    }
-  };
-
-  // fragment reads: X fragment i = piece wm*8 + i; W fragment j = the rows of feature
-  // block j = f*4 + type*2 + jj (128-row half f, gate/up 64-row type, wave's 32 rows)
-  const int l16 = 16 * (4 * (lane & 15) + ((lane >> 4) ^ ((4 - ((lane & 15) >> 2)) & 3)));
-  auto rd1 = [&](int kt, u16x8 (&xf)[8], u16x8 (&wf)[8], int q) {
-    constexpr int kOrd[16] = {8, 9, 0, 10, 11, 1, 12, 13, 2, 14, 15, 3, 4, 5, 6, 7};   // >= 8: W fragment
-    const char* buf = lds + (kt & (kNS - 1)) * kStage + l16;
-    const int o = kOrd[q];
-    if (o >= 8) {
-      const int j = o - 8;
-      const int piece = (j >> 2) * 8 + ((j >> 1) & 1) * 4 + wn * 2 + (j & 1);
-      wf[j] = *reinterpret_cast<const u16x8*>(buf + kWOff + piece * 1024);
-    } else {
-      xf[o] = *reinterpret_cast<const u16x8*>(buf + (wm * 8 + o) * 1024);
-    }
-  };
-
-  // register staging (DM 6): piece q of stage kt -> set[q]; set -> this wave's LDS slot
-  auto gload = [&](int kt, u32x4 (&st)[8], int q) {
-    const uint32_t k2 = (uint32_t)kt * (kBK4 * 2);
-    st[q] = q < 4 ? __builtin_amdgcn_raw_buffer_load_b128(xr, (int)xs[q], (int)k2, 0)
-                  : __builtin_amdgcn_raw_buffer_load_b128(wr, (int)ws[q - 4], (int)k2, 0);
-  };
-  auto lwrite = [&](int buf, const u32x4 (&st)[8], int q) {
-    char* dst = lds + buf * kStage + w * 1024 + (q < 4 ? q * 4096 : kWOff + (q - 4) * 4096) + lane * 16;
-    *reinterpret_cast<u32x4*>(dst) = st[q];
-  };
-
-  f32x4 acc[8][8];   // [token block][feature block]
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  u16x8 xa[8], wa[8], xb[8], wb[8];
-  u32x4 sa[8], sb[8];
-  // one K-step: 64 MFMAs; after each 8-MFMA row, two fragment reads of step kt+1 and one
-  // DMA piece of step kt+3. Branch-free: past the last step the reads fetch a buffer no
-  // one uses and the DMA re-loads step T-1 into buffer (kt+3) % 4, whose stage (kt-1) is
-  // consumed and which no later step reads; the loop's exit drains those DMAs.
-  // DM 6: the row's global load of stage kt+3 goes to set `ld`, and the row writes piece i
-  // of set `wr` (stage kt+2, loaded in step kt-1) into buffer (kt+2) % 4 (stage kt-2's,
-  // whose fragments were read in step kt-3); the barrier ending step kt publishes it for
-  // the fragment reads of step kt+1.
-  const int T = K / kBK4;   // even (K % 64 == 0)
-  auto step = [&](u16x8 (&xf)[8], u16x8 (&wf)[8], u16x8 (&nx)[8], u16x8 (&nw)[8], int kt, u32x4 (&ld)[8],
-                  u32x4 (&wr)[8]) {
-    const int ks = min(kt + 3, T - 1), kb = (kt + 3) & (kNS - 1);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) mfma_tied(acc[i][j], wf[j], xf[i]);
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (DM == 6) {
-        gload(ks, ld, i);
-        lwrite((kt + 2) & (kNS - 1), wr, i);
-      } else if constexpr (DM == 7) {   // timing: loads only (the set kept live, never written)
-        gload(ks, ld, i);
-        asm volatile("" ::"v"(wr[i]));
-      } else if constexpr (DM == 8) {   // timing: LDS writes only (of registers never loaded)
-        asm volatile("" : "+v"(wr[i]));
-        lwrite((kt + 2) & (kNS - 1), wr, i);
-      } else if constexpr (DM == 4) {
-        if (i == 0)
-#pragma unroll
-          for (int q = 0; q < 8; ++q) dma(ks, kb, q);
-      } else if constexpr (DM == 5) {
-        if (i >= 4) dma(ks, kb, i);
-      } else if constexpr (DM != 2) {
-        dma(ks, kb, i);
-      }
-      rd1(kt + 1, nx, nw, 2 * i);
-      rd1(kt + 1, nx, nw, 2 * i + 1);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-
-  // zero-initialised accumulators are read as SrcC by asm MFMAs, whose hazards hipcc
-  // does not pad: pin the writes above an explicit nop
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
-  asm volatile("s_nop 4");
-
-  if constexpr (DM >= 6) {   // stages 0, 1 into LDS; stage 2 in set B (written by step 0)
-#pragma unroll
-    for (int q = 0; q < 8; ++q) gload(0, sa, q);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) gload(min(1, T - 1), sb, q);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) lwrite(0, sa, q);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) lwrite(1, sb, q);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) gload(min(2, T - 1), sb, q);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  } else {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) dma(0, 0, q);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) dma(min(1, T - 1), 1, q);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) dma(min(2, T - 1), 2, q);
-    vm_wait<8>();   // stages 0 and 1 landed (this wave's pieces); stage 2 in flight
-  }
-  seg_barrier();
-#pragma unroll
-  for (int q = 0; q < 16; ++q) rd1(0, xa, wa, q);
-  // one loop, no peeled copy: a second code path makes hipcc move accumulators with
-  // v_accvgpr_write right before an asm MFMA reads them (an unpadded hazard)
-  for (int t = 0; t < T; t += 2) {
-    // step t: regs A hold stage t; read stage t+1 into B; DMA stage t+3
-    step(xa, wa, xb, wb, t, sa, sb);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if constexpr (DM < 6) vm_wait<8>();   // stage t+2 landed (this wave's pieces); stage t+3 in flight
-    seg_barrier();
-    // step t+1: regs B hold stage t+1; read stage t+2 into A; DMA stage t+4
-    step(xb, wb, xa, wa, t + 1, sb, sa);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if constexpr (DM < 6) vm_wait<8>();
-    seg_barrier();
-  }
-  vm_wait<0>();   // the tail's dummy DMAs must land before the workgroup's LDS is released
-  // the accumulators were written by asm MFMAs the hazard recognizer cannot see:
-  // cover the MFMA-write -> accvgpr-read latency before the epilogue reads them
-  asm volatile("s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
-
-  const int l15 = lane & 15, lq = lane >> 4;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int tok = m0 + wm * 128 + i * 16 + l15;
-    if (tok >= M) continue;
-    bf16_t* yrow = Y + (int64_t)tok * ldy;
-#pragma unroll
-    for (int f = 0; f < 2; ++f)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        if constexpr (EPI == kEpiSilu) {
-          const int col = (n0 >> 1) + f * 64 + wn * 32 + j * 16 + 4 * lq;
-          if (2 * col >= N) continue;
-          const f32x4 gt = acc[i][f * 4 + j], up = acc[i][f * 4 + 2 + j];
-          f32x4 o;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float gg = bf2f(f2bf(gt[r]));
-            const float uu = bf2f(f2bf(up[r]));
-            const float sg = bf2f(f2bf(gg / (1.f + __expf(-gg))));
-            o[r] = sg * uu;
-          }
-          *reinterpret_cast<uint2*>(yrow + col) = pack4(o);
-        } else {
-#pragma unroll
-          for (int ty = 0; ty < 2; ++ty) {
-            const int col = n0 + f * 128 + ty * 64 + wn * 32 + j * 16 + 4 * lq;
-            if (col >= N) continue;
-            f32x4 v = acc[i][f * 4 + ty * 2 + j];
-            if constexpr (EPI == kEpiBias) {
-              const uint2 bb = *reinterpret_cast<const uint2*>(bias + col);
-              v[0] += __uint_as_float(bb.x << 16);
-              v[1] += __uint_as_float(bb.x & 0xffff0000u);
-              v[2] += __uint_as_float(bb.y << 16);
-              v[3] += __uint_as_float(bb.y & 0xffff0000u);
-            }
-            *reinterpret_cast<uint2*>(yrow + col) = pack4(v);
-          }
-        }
-      }
-  }
-}
-
-// Variant 9 ("region ring"): four waves (one per SIMD, 128 x 128 outputs each, 256 tied
-// AGPR accumulators) with BK = 64 K-tiles loaded in full 128-B row segments: measured on
-// the ring-4 kernel, an LDS-DMA instruction of 16 rows x 64 B costs about twice what one of
-// 8 rows x 128 B does (the memory pipeline's request count, not the bytes: M 16384, N 4096,
-// K 14336: 1.25 PF/s with 64-B segments, 1.57 with 1-KiB contiguous pieces, 1.80 with no
-// loads at all; tools/gemm_tile_variants.py). A 64-deep tile is 64 KiB, so the ring is cut
-// into 16 KiB regions (X rows 0-127, X 128-255, W 0-127, W 128-255 of a tile): 10 regions
-// (160 KiB) = 2.5 tiles. Region i = 4 * tile + r lives in slot i % 10; while tile t is
-// computed the waves issue regions 4t+6 .. 4t+9 (tile t+1's second half, tile t+2's first)
-// into tile t-1's slots, and the counted vmcnt(8) at the end of tile t leaves exactly the
-// two youngest regions in flight. One raw barrier per tile. LDS image: 128-B rows with the
-// chunk ^ ((row >> 1) & 7) swizzle on the DMA source and the read (conflict-free b128).
-template <int EPI>
-__global__ void __launch_bounds__(256) gemm_tile256_q4_kernel(const bf16_t* __restrict__ X,
-                                                              const bf16_t* __restrict__ W, bf16_t* __restrict__ Y,
-                                                              const bf16_t* __restrict__ bias, int M, int N, int K,
-                                                              int ldy) {
-  constexpr int kSlots = 10;
-  __shared__ __attribute__((aligned(1024))) char lds[kSlots * kRegion];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = w >> 1, wn = w & 1;
-
-  const int mt = (M + kT - 1) / kT, nt = (N + kT - 1) / kT;
-  const int nwg = mt * nt;
-  const int lid = xcd_remap(blockIdx.x, nwg);
-  const int gsz = kGroupM * nt;
-  const int first_m = (lid / gsz) * kGroupM;
-  const int gm = min(mt - first_m, kGroupM);
-  const int tm = first_m + (lid % gsz) % gm;
-  const int tn = (lid % gsz) / gm;
-  const int m0 = tm * kT, n0 = tn * kT;
-
-  // DMA: region r (0: X rows 0-127, 1: X 128-255, 2: W 0-127, 3: W 128-255), piece q (0..3)
-  // of wave w = region rows 8 (w + 4q) .. +7; lane l -> row + l/8, LDS slot l%8, source
-  // chunk slot ^ ((row >> 1) & 7). 32-bit byte offsets (the launcher checks the extents).
-  const int lrow = lane >> 3, lslot = lane & 7;
-  uint32_t so[4][4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int row = 8 * (w + 4 * q) + lrow;
-      const int chunk = lslot ^ ((row >> 1) & 7);
-      const int g = (r < 2) ? min(m0 + 128 * r + row, M - 1) : min(n0 + 128 * (r - 2) + row, N - 1);
-      so[r][q] = ((uint32_t)g * (uint32_t)K + chunk * 8) * 2u;
-    }
-  const char* Xb = reinterpret_cast<const char*>(X);
-  const char* Wb = reinterpret_cast<const char*>(W);
-  const int T = K / kBK;
-  // region i (tile i / 4, part i % 4); past the last tile it re-loads tile T-1 (its slot is
-  // free and never read again), so every tile issues the same number of DMAs
-  auto dma = [&](int i, int q) {
-    const int r = i & 3;
-    const int kt = min(i >> 2, T - 1);
-    char* dst = lds + (i % kSlots) * kRegion + (w + 4 * q) * 1024;
-    const char* src = (r < 2 ? Xb : Wb) + so[r][q] + (uint32_t)kt * (kBK * 2);
-    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
-  };
-
-  const int l15 = lane & 15, lq = lane >> 4, sw = (l15 >> 1) & 7;
-  const int c0 = (lq ^ sw) << 4, c1 = ((4 + lq) ^ sw) << 4;
-  // fragment rows: X fragment i = rows 16 i + l15 of region wm; W fragment j (f = j / 4,
-  // type = (j / 2) % 2, jj = j % 2) = rows type*64 + wn*32 + jj*16 + l15 of region 2 + f
-  auto rd1 = [&](int t, int c, u16x8 (&xf)[8], u16x8 (&wf)[8], int q) {
-    constexpr int kOrd[16] = {8, 9, 0, 10, 11, 1, 12, 13, 2, 14, 15, 3, 4, 5, 6, 7};   // >= 8: W fragment
-    const int o = kOrd[q];
-    if (o >= 8) {
-      const int j = o - 8;
-      const char* reg = lds + ((4 * t + 2 + (j >> 2)) % kSlots) * kRegion;
-      wf[j] = *reinterpret_cast<const u16x8*>(reg + (((j >> 1) & 1) * 64 + wn * 32 + (j & 1) * 16 + l15) * 128 + c);
-    } else {
-      const char* reg = lds + ((4 * t + wm) % kSlots) * kRegion;
-      xf[o] = *reinterpret_cast<const u16x8*>(reg + (16 * o + l15) * 128 + c);
-    }
-  };
-
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  u16x8 xa[8], wa[8], xb[8], wb[8];
-  // one k-substep of tile t: 64 MFMAs; after each 8-MFMA row two fragment reads of the next
-  // substep (from tile tn, chunk cn) and, in the first substep, one DMA piece of regions
-  // 4t+6 .. 4t+9 (2 per row: the 16 pieces of the four regions over the 8 rows)
-  auto mm = [&](u16x8 (&xf)[8], u16x8 (&wf)[8], int tn, int cn, u16x8 (&nx)[8], u16x8 (&nw)[8], int t,
-                bool first) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) mfma_tied(acc[i][j], wf[j], xf[i]);
-      __builtin_amdgcn_sched_barrier(0);
-      if (first) {
-        dma(4 * t + 6 + (i >> 1), (2 * i) & 3);
-        dma(4 * t + 6 + (i >> 1), (2 * i + 1) & 3);
-      }
-      rd1(tn, cn, nx, nw, 2 * i);
-      rd1(tn, cn, nx, nw, 2 * i + 1);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
-  asm volatile("s_nop 4");
-
-  // prologue: regions 0 .. 5 (tile 0, tile 1's first half); tile 0 landed, 2 regions in flight
-#pragma unroll
-  for (int i = 0; i < 6; ++i)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) dma(i, q);
-  vm_wait<8>();
-  seg_barrier();
-#pragma unroll
-  for (int q = 0; q < 16; ++q) rd1(0, c0, xa, wa, q);
-  // one loop, no peeled copy (a second code path makes hipcc move accumulators with
-  // v_accvgpr_write right before an asm MFMA reads them)
-  for (int t = 0; t < T; ++t) {
-    // substep 0 of tile t (regs A), reading substep 1 of tile t; issues regions 4t+6 .. 4t+9
-    mm(xa, wa, t, c1, xb, wb, t, true);
-    // substep 1 of tile t (regs B), reading substep 0 of tile t+1 (landed: see below)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    vm_wait<8>();      // tile t+1 landed (this wave's pieces); regions 4t+8, 4t+9 in flight
-    seg_barrier();     // ... every wave's pieces; tile t-1's reads long done
-    mm(xb, wb, t + 1, c0, xa, wa, t, false);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    seg_barrier();     // every wave done reading tile t: its slots are refilled next tile
-  }
-  vm_wait<0>();        // the tail's re-loads land before the workgroup's LDS is released
-  asm volatile("s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
-
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int tok = m0 + wm * 128 + i * 16 + l15;
-    if (tok >= M) continue;
-    bf16_t* yrow = Y + (int64_t)tok * ldy;
-#pragma unroll
-    for (int f = 0; f < 2; ++f)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        if constexpr (EPI == kEpiSilu) {
-          const int col = (n0 >> 1) + f * 64 + wn * 32 + j * 16 + 4 * lq;
-          if (2 * col >= N) continue;
-          const f32x4 gt = acc[i][f * 4 + j], up = acc[i][f * 4 + 2 + j];
-          f32x4 o;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float gg = bf2f(f2bf(gt[r]));
-            const float uu = bf2f(f2bf(up[r]));
-            const float sg = bf2f(f2bf(gg / (1.f + __expf(-gg))));
-            o[r] = sg * uu;
-          }
-          *reinterpret_cast<uint2*>(yrow + col) = pack4(o);
-        } else {
-#pragma unroll
-          for (int ty = 0; ty < 2; ++ty) {
-            const int col = n0 + f * 128 + ty * 64 + wn * 32 + j * 16 + 4 * lq;
-            if (col >= N) continue;
-            f32x4 v = acc[i][f * 4 + ty * 2 + j];
-            if constexpr (EPI == kEpiBias) {
-              const uint2 bb = *reinterpret_cast<const uint2*>(bias + col);
-              v[0] += __uint_as_float(bb.x << 16);
-              v[1] += __uint_as_float(bb.x & 0xffff0000u);
-              v[2] += __uint_as_float(bb.y << 16);
-              v[3] += __uint_as_float(bb.y & 0xffff0000u);
-            }
-            *reinterpret_cast<uint2*>(yrow + col) = pack4(v);
-          }
-        }
-      }
-  }
-}
-
-// Variant 13 ("two buffers, four phases"): four waves (one per SIMD, 128 x 128 outputs
+// Variant 1, the default ("h4": two buffers, four phases): four waves (one per SIMD, 128 x 128 outputs
 // each, 256 tied AGPR accumulators), BK = 64 tiles in two 64 KiB LDS buffers filled by
 // LDS-DMA pieces of 8 rows x 128 B (buffer_load ... lds: per-lane 32-bit row offsets fixed
 // for the kernel, the K step in soffset) — half the memory requests of 16 x 64-B pieces
@@ -747,8 +316,10 @@ __global__ void __launch_bounds__(256) gemm_tile256_q4_kernel(const bf16_t* __re
 // after the barrier that follows its last read, and each staged piece is read one phase
 // after the wait + barrier that retire it. DMAs and fragment reads sit between MFMAs (one
 // per two). LDS image: 128-B rows, chunk slot = chunk ^ ((row >> 1) & 7) on the DMA
-// source and the read (conflict-free ds_read_b128, as variant 9).
-template <int EPI, int AUX = 0>
+// source and the read (conflict-free ds_read_b128). The DMAs carry the sc1
+// cache policy (AUX 16: 1-3 % over the default on down / qkv; nt costs 4-20 %,
+// profiles/gemm_tile_variants_r4_c.jsonl).
+template <int EPI, int AUX = 16>
 __global__ void __launch_bounds__(256) gemm_tile256_h4_kernel(const bf16_t* __restrict__ X,
                                                               const bf16_t* __restrict__ W, bf16_t* __restrict__ Y,
                                                               const bf16_t* __restrict__ bias, int M, int N, int K,
@@ -982,43 +553,18 @@ int gemm_tile(const bf16_t* X, const bf16_t* W, bf16_t* Y, const bf16_t* bias, i
     return splitk_reduce(P, Y, (int64_t)M * N, S, stream);
   }
   const bool off32 = (int64_t)M * K * 2 < (1LL << 32) && (int64_t)N * K * 2 < (1LL << 32);
-  if (variant == 1 && off32) {   // 4-wave, 4-stage BK = 32 ring (32-bit source offsets)
-    if (silu_gu) gemm_tile256_r4_kernel<kEpiSilu><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-    else if (bias) gemm_tile256_r4_kernel<kEpiBias><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-    else gemm_tile256_r4_kernel<kEpiStore><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-  } else if (variant == 9 && off32) {   // 4-wave, BK = 64 region ring
-    if (silu_gu) gemm_tile256_q4_kernel<kEpiSilu><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-    else if (bias) gemm_tile256_q4_kernel<kEpiBias><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-    else gemm_tile256_q4_kernel<kEpiStore><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-  } else if (variant == 13 && off32) {   // 4-wave, two 64 KiB buffers, four phases per K-tile
+  if ((variant == 0 || variant == 1) && off32) {   // 4-wave, two 64 KiB buffers, four phases per K-tile
     if (silu_gu) gemm_tile256_h4_kernel<kEpiSilu><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
     else if (bias) gemm_tile256_h4_kernel<kEpiBias><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
     else gemm_tile256_h4_kernel<kEpiStore><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-  } else if (variant >= 14 && variant <= 16 && off32 && !silu_gu && !bias) {   // variant 13, DMA cache policy
-    if (variant == 14) gemm_tile256_h4_kernel<kEpiStore, 16><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-    else if (variant == 15) gemm_tile256_h4_kernel<kEpiStore, 2><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-    else gemm_tile256_h4_kernel<kEpiStore, 18><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-  } else if (variant == 10 && off32) {   // 4-wave ring, register-staged loads
-    if (silu_gu) gemm_tile256_r4_kernel<kEpiSilu, 6><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-    else if (bias) gemm_tile256_r4_kernel<kEpiBias, 6><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-    else gemm_tile256_r4_kernel<kEpiStore, 6><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-  } else if ((variant == 11 || variant == 12) && off32 && !silu_gu && !bias) {   // register-staging timing splits
-    if (variant == 11) gemm_tile256_r4_kernel<kEpiStore, 7><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-    else gemm_tile256_r4_kernel<kEpiStore, 8><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-  } else if (variant >= 4 && variant <= 8 && off32 && !silu_gu && !bias) {   // ring-4 load experiments
-    if (variant == 4) gemm_tile256_r4_kernel<kEpiStore, 1><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-    else if (variant == 5) gemm_tile256_r4_kernel<kEpiStore, 2><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-    else if (variant == 6) gemm_tile256_r4_kernel<kEpiStore, 3><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-    else if (variant == 7) gemm_tile256_r4_kernel<kEpiStore, 4><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-    else gemm_tile256_r4_kernel<kEpiStore, 5><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
   } else if (variant == 2 || (variant == 0 && M > 256)) {
-    // 8-wave ping-pong, two barrier segments per K-tile: 1.8-2.7 % over four segments on
-    // the prefill shapes (M = 32k, profiles/gemm_tile_ph2_vs_ph4.jsonl); the lm_head at
-    // M <= 256 keeps four (weight-streaming bound there, 1 % the other way)
+    // 8-wave ping-pong, two barrier segments per K-tile (the round-3 default; 2-8 % behind
+    // variant 1 on the prefill shapes, profiles/gemm_tile_h4_vs_ph2_m32k.jsonl); also the
+    // fallback for operands past 32-bit offsets
     if (silu_gu) gemm_tile256_kernel<kEpiSilu, true><<<nwg, 512, 0, stream>>>(X, W, Y, bias, M, N, K, ldy, nullptr);
     else if (bias) gemm_tile256_kernel<kEpiBias, true><<<nwg, 512, 0, stream>>>(X, W, Y, bias, M, N, K, ldy, nullptr);
     else gemm_tile256_kernel<kEpiStore, true><<<nwg, 512, 0, stream>>>(X, W, Y, bias, M, N, K, ldy, nullptr);
-  } else {   // 8-wave ping-pong, four segments per K-tile (variant 3, or 0 at M <= 256)
+  } else {   // 8-wave ping-pong, four segments per K-tile (variant 3, or 0 at M <= 256 past 32-bit offsets)
     if (silu_gu) gemm_tile256_kernel<kEpiSilu><<<nwg, 512, 0, stream>>>(X, W, Y, bias, M, N, K, ldy, nullptr);
     else if (bias) gemm_tile256_kernel<kEpiBias><<<nwg, 512, 0, stream>>>(X, W, Y, bias, M, N, K, ldy, nullptr);
     else gemm_tile256_kernel<kEpiStore><<<nwg, 512, 0, stream>>>(X, W, Y, bias, M, N, K, ldy, nullptr);

@@ -2,6 +2,6 @@ set -e
 cd $GRAFT_REPO_ROOT
 timeout -k 10 300 python -u -m pytest tests/test_gemm_tile_gpu.py -x -q --timeout 120 --timeout-method thread -k "gemm_tile" > gpurun_out/gt_tests.log 2>&1 || { tail -30 gpurun_out/gt_tests.log; exit 1; }
 tail -1 gpurun_out/gt_tests.log
-timeout -k 10 300 python -u tools/gemm_tile_variants.py --variants ${GTV:-9,2,6} > gpurun_out/gtv.jsonl
-timeout -k 10 300 python -u tools/gemm_tile_variants.py --variants ${GTV:-9,2,6} --m 16384 --n 6144 --k 4096 >> gpurun_out/gtv.jsonl
+timeout -k 10 300 python -u tools/gemm_tile_variants.py --variants ${GTV:-1,2,3} > gpurun_out/gtv.jsonl
+timeout -k 10 300 python -u tools/gemm_tile_variants.py --variants ${GTV:-1,2,3} --m 16384 --n 6144 --k 4096 >> gpurun_out/gtv.jsonl
 cat gpurun_out/gtv.jsonl
