@@ -65,22 +65,26 @@ class FakeWatch:
 
     _END = object()
 
-    def __init__(self, fk: "FakeKube", res: Resource, namespace: str | None):
+    def __init__(self, fk: "FakeKube", res: Resource, namespace: str | None, sink=None):
         self.fk, self.res, self.namespace = fk, res, namespace
         self.q: queue.Queue = queue.Queue()
+        # sink(item): deliver events / end / failure markers somewhere else than self.q
+        # (the asyncio REST server feeds its watch coroutines this way)
+        self._put = sink if sink is not None else self.q.put
         self.closed = False
+        self._held = None   # an end / failure marker met while draining (next_events)
 
     def push(self, typ: str, obj: dict, ev: "_Event | None" = None) -> None:
         if not self.closed:
-            self.q.put(ev if ev is not None else _Event(typ, obj))
+            self._put(ev if ev is not None else _Event(typ, obj))
 
     def fail(self, message: str = "watch stream error", code: int | None = None) -> None:
-        self.q.put(WatchClosed(message, code))
+        self._put(WatchClosed(message, code))
 
     def close(self) -> None:
         if not self.closed:
             self.closed = True
-            self.q.put(self._END)
+            self._put(self._END)
             self.fk._drop_watch(self)
 
     def __iter__(self) -> Iterator[tuple[str, dict]]:
@@ -89,7 +93,7 @@ class FakeWatch:
     def next_event(self) -> "_Event":
         """The next event as shared by every watch it went to (the REST server sends its
         memoised wire bytes instead of copying and serialising the object per watcher)."""
-        item = self.q.get()
+        item, self._held = (self._held, None) if self._held is not None else (self.q.get(), None)
         if item is self._END:
             raise StopIteration
         if isinstance(item, WatchClosed):
@@ -97,6 +101,21 @@ class FakeWatch:
             self.fk._drop_watch(self)
             raise item
         return item
+
+    def next_events(self, max_n: int = 64) -> list["_Event"]:
+        """The next event (blocking) plus every one already queued behind it, up to
+        ``max_n``: the REST server writes them with one flush."""
+        out = [self.next_event()]
+        while len(out) < max_n:
+            try:
+                item = self.q.get_nowait()
+            except queue.Empty:
+                break
+            if item is self._END or isinstance(item, WatchClosed):
+                self._held = item   # delivered by the next call
+                break
+            out.append(item)
+        return out
 
     def __next__(self) -> tuple[str, dict]:
         ev = self.next_event()
@@ -206,15 +225,16 @@ class FakeKube:
         with self._lock:
             return self.list(res, namespace, label_selector, field_selector), self.current_resource_version()
 
-    def get(self, res: Resource, name: str, namespace: str | None = None) -> dict | None:
+    def get(self, res: Resource, name: str, namespace: str | None = None, *, copy: bool = True) -> dict | None:
         self._log_call("get", res, namespace, name)
         self._fault("get", res)
         with self._lock:
             o = self._objs.get((self._key(res), namespace or "", name))
-        return _jcopy(o) if o is not None else None   # stored objects are immutable: copy unlocked
+        # stored objects are immutable: copy unlocked (copy=False: the REST server only encodes it)
+        return _jcopy(o) if o is not None and copy else o
 
     def list(self, res: Resource, namespace: str | None = None, label_selector: dict | str | None = None,
-             field_selector: str | None = None) -> list[dict]:
+             field_selector: str | None = None, *, copy: bool = True) -> list[dict]:
         self._log_call("list", res, namespace, None)
         self._fault("list", res)
         sel = parse_selector(label_selector) if isinstance(label_selector, str) else label_selector
@@ -229,9 +249,9 @@ class FakeKube:
                 if not match_fields(field_selector, o):
                     continue
                 out.append(o)
-        return [_jcopy(o) for o in out]
+        return [_jcopy(o) for o in out] if copy else out
 
-    def create(self, res: Resource, obj: dict, namespace: str | None = None) -> dict:
+    def create(self, res: Resource, obj: dict, namespace: str | None = None, *, copy: bool = True) -> dict:
         ns = namespace or obj.get("metadata", {}).get("namespace") or ("default" if res.namespaced else "")
         name = obj.get("metadata", {}).get("name")
         self._log_call("create", res, ns, name)
@@ -258,10 +278,10 @@ class FakeKube:
             o.setdefault("kind", res.kind)
             self._store(k, o)
             self._emit(res, "ADDED", o)
-        return _jcopy(o)
+        return _jcopy(o) if copy else o
 
     def _update(self, res: Resource, name: str, namespace: str | None, fn, resource_version: str | None,
-                status: bool) -> dict:
+                status: bool, copy: bool = True) -> dict:
         with self._lock:
             k = (self._key(res), namespace or "", name)
             cur = self._objs.get(k)
@@ -298,31 +318,31 @@ class FakeKube:
             new["metadata"]["resourceVersion"] = str(next(self._rv))
             self._store(k, new)
             self._emit(res, "MODIFIED", new)
-        return _jcopy(new)
+        return _jcopy(new) if copy else new
 
     def patch(self, res: Resource, name: str, namespace: str | None, patch: dict,
-              resource_version: str | None = None) -> dict:
+              resource_version: str | None = None, *, copy: bool = True) -> dict:
         self._log_call("patch", res, namespace, name)
         self._fault("patch", res)
         rv = resource_version or (patch.get("metadata") or {}).get("resourceVersion")
-        return self._update(res, name, namespace, lambda o: merge_patch(o, patch), rv, status=False)
+        return self._update(res, name, namespace, lambda o: merge_patch(o, patch), rv, status=False, copy=copy)
 
-    def replace(self, res: Resource, obj: dict, namespace: str | None = None) -> dict:
+    def replace(self, res: Resource, obj: dict, namespace: str | None = None, *, copy: bool = True) -> dict:
         name = obj["metadata"]["name"]
         ns = namespace or obj["metadata"].get("namespace")
         self._log_call("replace", res, ns, name)
         self._fault("replace", res)
         rv = obj["metadata"].get("resourceVersion")
-        return self._update(res, name, ns, lambda o: _jcopy(obj), rv, status=False)
+        return self._update(res, name, ns, lambda o: _jcopy(obj), rv, status=False, copy=copy)
 
     def patch_status(self, res: Resource, name: str, namespace: str | None, status_patch: dict,
-                     resource_version: str | None = None) -> dict:
+                     resource_version: str | None = None, *, copy: bool = True) -> dict:
         self._log_call("patch_status", res, namespace, name)
         self._fault("patch_status", res)
         return self._update(res, name, namespace, lambda o: merge_patch(o, {"status": status_patch}),
-                            resource_version, status=True)
+                            resource_version, status=True, copy=copy)
 
-    def replace_status(self, res: Resource, obj: dict, namespace: str | None = None) -> dict:
+    def replace_status(self, res: Resource, obj: dict, namespace: str | None = None, *, copy: bool = True) -> dict:
         name = obj["metadata"]["name"]
         ns = namespace or obj["metadata"].get("namespace")
         self._log_call("replace_status", res, ns, name)
@@ -333,7 +353,7 @@ class FakeKube:
             o["status"] = _jcopy(obj.get("status"))
             return o
 
-        return self._update(res, name, ns, fn, rv, status=True)
+        return self._update(res, name, ns, fn, rv, status=True, copy=copy)
 
     def delete(self, res: Resource, name: str, namespace: str | None = None) -> bool:
         self._log_call("delete", res, namespace, name)
@@ -350,11 +370,12 @@ class FakeKube:
             self._emit(res, "DELETED", o)
             return True
 
-    def watch(self, res: Resource, namespace: str | None = None, resource_version: str | None = None) -> FakeWatch:
+    def watch(self, res: Resource, namespace: str | None = None, resource_version: str | None = None,
+              sink=None) -> FakeWatch:
         self._log_call("watch", res, namespace, None)
         self._fault("watch", res)
         with self._lock:
-            w = FakeWatch(self, res, namespace)
+            w = FakeWatch(self, res, namespace, sink)
             if resource_version and int(resource_version) < self._compacted:
                 w.fail(f"too old resource version: {resource_version} ({self._compacted})", 410)
                 return w

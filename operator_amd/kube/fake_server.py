@@ -96,6 +96,9 @@ class _Conn(socketserver.StreamRequestHandler):
 class _Server(socketserver.ThreadingTCPServer):
     daemon_threads = True
     allow_reuse_address = True
+    # listen backlog: eight operator shards' worker pools plus bursts of failing pods connect
+    # at once (the socketserver default of 5 resets connections under that load)
+    request_queue_size = 1024
 
     def handle_error(self, request, client_address):   # a client gone mid-stream is not an error
         import sys
@@ -113,6 +116,13 @@ class FakeKubeServer:
         self._t = threading.Thread(target=self.httpd.serve_forever, name="fakekube-http", daemon=True)
 
     def dispatch(self, c: _Conn, method: str, target: str, raw: bytes) -> None:
+        w = self.route(c, method, target, raw)
+        if w is not None:
+            self._watch(c, *w)
+
+    def route(self, c, method: str, target: str, raw: bytes):
+        """Serve one unary request into ``c`` (``respond`` / ``json``); a watch request
+        is returned as (resource, namespace, resourceVersion) for the caller to stream."""
         fk = self.fk
         u = urlparse(target)
         q = {k: v[0] for k, v in parse_qs(u.query).items()}
@@ -131,29 +141,29 @@ class FakeKubeServer:
                                   int(q["limitBytes"]) if "limitBytes" in q else None).encode()
                 return c.respond(200, text, b"text/plain")
             if method == "GET" and name is None and q.get("watch") in ("1", "true"):
-                return self._watch(c, res, ns, q.get("resourceVersion"))
+                return res, ns, q.get("resourceVersion")
             if method == "GET" and name is None:
-                items = fk.list(res, ns, q.get("labelSelector"), q.get("fieldSelector"))
+                items = fk.list(res, ns, q.get("labelSelector"), q.get("fieldSelector"), copy=False)
                 return c.json(200, {"kind": res.kind + "List", "apiVersion": res.api_version,
                                     "metadata": {"resourceVersion": fk.current_resource_version()},
                                     "items": items})
             if method == "GET":
-                o = fk.get(res, name, ns)
+                o = fk.get(res, name, ns, copy=False)
                 if o is None:
                     raise ApiError(404, f"{res.plural} {name} not found", "NotFound")
                 return c.json(200, o)
             if method == "POST":
-                return c.json(201, fk.create(res, body(), ns))
+                return c.json(201, fk.create(res, body(), ns, copy=False))
             if method == "PUT":
                 if sub == "status":
-                    return c.json(200, fk.replace_status(res, body(), ns))
-                return c.json(200, fk.replace(res, body(), ns))
+                    return c.json(200, fk.replace_status(res, body(), ns, copy=False))
+                return c.json(200, fk.replace(res, body(), ns, copy=False))
             if method == "PATCH":
                 b = body()
                 rv = (b.get("metadata") or {}).get("resourceVersion")
                 if sub == "status":
-                    return c.json(200, fk.patch_status(res, name, ns, b.get("status") or {}, rv))
-                return c.json(200, fk.patch(res, name, ns, b, rv))
+                    return c.json(200, fk.patch_status(res, name, ns, b.get("status") or {}, rv, copy=False))
+                return c.json(200, fk.patch(res, name, ns, b, rv, copy=False))
             if method == "DELETE":
                 if not fk.delete(res, name, ns):
                     raise ApiError(404, f"{res.plural} {name} not found", "NotFound")
@@ -175,10 +185,13 @@ class FakeKubeServer:
         try:
             while True:
                 try:
-                    ev = w.next_event()
+                    evs = w.next_events()
                 except StopIteration:
                     break
-                chunk(ev.wire())
+                # every event already queued goes out in one write + flush (under load one
+                # wake-up and one syscall per burst instead of per event)
+                wf.write(b"".join(b"%x\r\n%s\r\n" % (len(b), b) for b in (ev.wire() for ev in evs)))
+                wf.flush()
         except WatchClosed as e:
             try:
                 chunk(json.dumps({"type": "ERROR", "object": {"code": e.code or 500, "message": str(e),
@@ -215,6 +228,7 @@ def main(argv: list[str] | None = None) -> int:
     ap.add_argument("--host", default="127.0.0.1")
     ap.add_argument("--port", type=int, default=0)
     ap.add_argument("--port-file", default=None, help="write the URL here once listening")
+    ap.add_argument("--threaded", action="store_true", help="one thread per connection (the in-process server)")
     a = ap.parse_args(argv)
     try:   # exit with the process that started it
         import ctypes
@@ -222,7 +236,12 @@ def main(argv: list[str] | None = None) -> int:
         ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, int(signal.SIGTERM))   # PR_SET_PDEATHSIG
     except OSError:
         pass
-    srv = FakeKubeServer(FakeKube(record_calls=False), a.host, a.port).start()
+    if a.threaded:
+        srv = FakeKubeServer(FakeKube(record_calls=False), a.host, a.port).start()
+    else:
+        from .fake_aserver import AsyncFakeKubeServer
+
+        srv = AsyncFakeKubeServer(FakeKube(record_calls=False), a.host, a.port).start()
     if a.port_file:
         tmp = a.port_file + ".tmp"
         with open(tmp, "w") as f:

@@ -17,6 +17,7 @@ from operator_amd.engine.server import CompatServer
 from operator_amd.engine.service import EchoExplainService, LocalMatchService
 from operator_amd.kube.client import KubeClient, KubeConfig
 from operator_amd.kube.fake import FakeKube, failed_pod, running_pod
+from operator_amd.kube.fake_aserver import AsyncFakeKubeServer
 from operator_amd.kube.fake_server import FakeKubeServer
 from operator_amd.kube.resources import EVENTS, PODMORTEMS, PODS, ApiError, WatchClosed
 from operator_amd.patterns.synth import catalog_library
@@ -32,10 +33,12 @@ def wait_for(fn, timeout=20.0):
     raise AssertionError("timed out")
 
 
-@pytest.fixture
-def server():
+@pytest.fixture(params=["threaded", "asyncio"])
+def server(request):
+    """The REST FakeKube in both process models: a thread per connection (in-process
+    tests) and one asyncio loop (the standalone API server of shard-per-GPU runs)."""
     fk = FakeKube()
-    srv = FakeKubeServer(fk).start()
+    srv = (FakeKubeServer(fk) if request.param == "threaded" else AsyncFakeKubeServer(fk)).start()
     kc = KubeClient(KubeConfig(srv.url, token="test-token"), timeout_s=10)
     yield fk, srv, kc
     srv.stop()

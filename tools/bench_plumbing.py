@@ -56,6 +56,31 @@ def wait(pred, timeout):
     return False
 
 
+def free_port_block(n: int) -> int:
+    """First of ``n`` consecutive free TCP ports (shard i serves health on base + i), taken
+    below the kernel's ephemeral range so the shards' and harness's outgoing connections
+    cannot occupy one between this check and the shard binding it."""
+    import random
+    import socket
+
+    rng = random.Random()
+    for _ in range(200):
+        base = rng.randrange(20000, 32000 - n)
+        socks = []
+        try:
+            for i in range(n):
+                sk = socket.socket()
+                socks.append(sk)
+                sk.bind(("127.0.0.1", base + i))
+            return base
+        except OSError:
+            continue
+        finally:
+            for sk in socks:
+                sk.close()
+    raise RuntimeError(f"no block of {n} free ports")
+
+
 def run_sharded(shards: int, failures: int, workdir: str, timeout_s: float = 600.0, log_kb: int = 0) -> dict:
     """The production multi-GPU topology on the CPU: ONE API server process (the REST
     FakeKube) and ``run --shard-per-gpu --gpus N`` (N operator shard processes, each
@@ -64,7 +89,6 @@ def run_sharded(shards: int, failures: int, workdir: str, timeout_s: float = 600
     annotation; returns the rate plus, per pod, how many PodmortemAnalysisComplete
     Events it got (exactly one each = no double, no miss)."""
     import signal
-    import socket
     import subprocess
     from collections import Counter
 
@@ -74,9 +98,7 @@ def run_sharded(shards: int, failures: int, workdir: str, timeout_s: float = 600
 
     srv, url = spawn(os.path.join(workdir, "apiserver.url"))
     kc = write_kubeconfig(url, os.path.join(workdir, "kubeconfig"))
-    with socket.socket() as sk:
-        sk.bind(("127.0.0.1", 0))
-        port = sk.getsockname()[1]
+    port = free_port_block(shards)
     env = dict(os.environ, PODMORTEM_LOG_LEVEL="WARNING")
     op = None
     kube = KubeClient(KubeConfig(url), 30.0)
@@ -111,11 +133,13 @@ def run_sharded(shards: int, failures: int, workdir: str, timeout_s: float = 600
             except OSError:
                 return False
         assert wait(lambda: all(up(port + i) for i in range(shards)), 180), "shards did not come up"
+        # the failures arrive as they would from many kubelets: concurrent status merge patches
+        from concurrent.futures import ThreadPoolExecutor
+
+        st = failed_pod("x", finished_at="2025-08-29T10:00:00Z")["status"]
         t0 = time.perf_counter()
-        for n in names:
-            cur = kube.get(PODS, n, "default")
-            cur["status"] = failed_pod(n, finished_at="2025-08-29T10:00:00Z")["status"]
-            kube.replace(PODS, cur)
+        with ThreadPoolExecutor(16) as ex:
+            list(ex.map(lambda n: kube.patch_status(PODS, n, "default", st), names))
         t_inj = time.perf_counter() - t0
 
         def analysed():
@@ -124,10 +148,12 @@ def run_sharded(shards: int, failures: int, workdir: str, timeout_s: float = 600
         end = time.perf_counter() + timeout_s
         n_done = 0
         while time.perf_counter() < end:
+            # a LIST of every pod is the API server's most expensive request: poll it sparingly
+            # (the server is shared with the shards under test)
+            time.sleep(0.5)
             n_done = analysed()
             if n_done >= failures:
                 break
-            time.sleep(0.1)
         elapsed = time.perf_counter() - t0
         time.sleep(2.0)   # let the last Events land before counting them
         per_pod = Counter(e.get("regarding", {}).get("name") for e in kube.list(EVENTS, "default")
