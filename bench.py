@@ -310,6 +310,7 @@ def main() -> int:
             return {"prefill_tokens": st.prefill_tokens, "decode_tokens": st.decode_tokens,
                     "prefill_graph_replays": st.prefill_graph_replays, "use_graphs": bool(llm.use_graphs),
                     "prefill_padded_tokens": st.prefill_padded_tokens, "prefill_eager": st.prefill_eager,
+                    "prefix_hits": st.prefix_hits, "prefix_tokens": st.prefix_tokens, "prefix_builds": st.prefix_builds,
                     "decode_launch_s": st.decode_launch_s, "decode_wait_s": st.decode_wait_s,
                     "decode_windows": st.decode_windows, "decode_windows_ahead": st.decode_windows_ahead,
                     "no_pipeline": dict(st.no_pipeline),
@@ -317,7 +318,8 @@ def main() -> int:
                     "dfa_states": getattr(meng, "dfa_states", None)}
         ws = pool.worker_stats()
         out = {k: sum(w["llm"].get(k, 0) for w in ws) for k in ("prefill_tokens", "decode_tokens", "prefill_graph_replays",
-                                                                 "prefill_padded_tokens", "prefill_eager")}
+                                                                 "prefill_padded_tokens", "prefill_eager", "prefix_hits",
+                                                                 "prefix_tokens", "prefix_builds")}
         out.update(use_graphs=all(w.get("use_graphs") for w in ws),
                    prefill_graph_buckets=sorted({b for w in ws for b in w.get("prefill_graph_buckets", [])}),
                    dfa_states=ws[0].get("dfa_states") if ws else None)
@@ -523,6 +525,7 @@ def main() -> int:
         print(f"{SHARD_TAG} RESULT " + json.dumps({
             "t0": mono0, "t1": mono1, "lat": lat, "outcomes": counter["outcomes"],
             "ptoks": st1["prefill_tokens"] - stats0["prefill_tokens"],
+            "xtoks": st1.get("prefix_tokens", 0) - stats0.get("prefix_tokens", 0),
             "dtoks": st1["decode_tokens"] - stats0["decode_tokens"],
             "replays": st1["prefill_graph_replays"] - stats0["prefill_graph_replays"]}), flush=True)
         if a.mode == "pipeline":
@@ -575,6 +578,8 @@ def main() -> int:
     value = total / elapsed
     stats1 = engine_stats()
     ptoks = stats1["prefill_tokens"] - stats0["prefill_tokens"] + sum(r["ptoks"] for r in results)
+    # prompt tokens served from the shared prompt-prefix pages (computed once, not per request)
+    xtoks = stats1.get("prefix_tokens", 0) - stats0.get("prefix_tokens", 0) + sum(r.get("xtoks", 0) for r in results)
     dtoks = stats1["decode_tokens"] - stats0["decode_tokens"] + sum(r["dtoks"] for r in results)
     replays = stats1["prefill_graph_replays"] - stats0["prefill_graph_replays"] + sum(r["replays"] for r in results)
     out = {
@@ -595,8 +600,12 @@ def main() -> int:
                    "waves": "serial" if (a.serial_waves or a.mode != "pipeline") else "pipelined"},
         "detail": {"init_s": round(init_s, 1), "prefill_tokens_per_gpu": ptoks, "decode_tokens_per_gpu": dtoks,
                    # workload check: every failure carries three signatures of the scanned library, so
-                   # this stays ~895 whatever the rank / shard layout (README "Correction")
-                   "prompt_tokens_per_analysis": round(ptoks / max(1, a.batch * a.shards * a.steps), 1),
+                   # this stays ~885 whatever the rank / shard layout (README "Correction"); it counts
+                   # the prompt tokens read from shared prompt-prefix pages too
+                   "prompt_tokens_per_analysis": round((ptoks + xtoks) / max(1, a.batch * a.shards * a.steps), 1),
+                   "shared_prefix": {"requests": stats1.get("prefix_hits", 0) - stats0.get("prefix_hits", 0),
+                                     "prompt_tokens_not_prefilled": xtoks,
+                                     "prefixes_computed": stats1.get("prefix_builds", 0) - stats0.get("prefix_builds", 0)},
                    "prefill_graph_replays": replays,
                    "prefill_graph_buckets": stats1["prefill_graph_buckets"],
                    "prefill_padded_tokens": stats1.get("prefill_padded_tokens", 0) - stats0.get("prefill_padded_tokens", 0),

@@ -443,9 +443,12 @@ void attn_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tenso
                        (int)num_splits, (float)scale, (int)variant, cur_stream(), q8p, sxp));
 }
 
+// pk / pv / seq_pfx: a shared prompt prefix (kernels.h attn_prefill, variant 3): seq_pfx[s] prefix
+// keys (a multiple of 64, at most pk.size(0)) precede sequence s's own keys.
 void attn_prefill(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor& o,
                   const at::Tensor& cu_seqlens, const at::Tensor& work_seq, const at::Tensor& work_q0,
-                  double scale, int64_t variant) {
+                  double scale, int64_t variant, const c10::optional<at::Tensor>& pk,
+                  const c10::optional<at::Tensor>& pv, const c10::optional<at::Tensor>& seq_pfx) {
   CHECK_DEV(q); for (auto* t : {&q, &k, &v}) { CHECK_BF16(*t); CHECK_CONTIG(*t); }
   CHECK_BF16(o); CHECK_CONTIG(o);
   for (auto* t : {&cu_seqlens, &work_seq, &work_q0}) { CHECK_DT(*t, at::kInt); CHECK_CONTIG(*t); }
@@ -453,10 +456,23 @@ void attn_prefill(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
   TORCH_CHECK(q.size(0) == k.size(0) && q.size(2) == 128 && k.size(2) == 128, "T / head_dim mismatch");
   TORCH_CHECK(q.size(1) % k.size(1) == 0, "Hq % Hkv");
   TORCH_CHECK(work_seq.numel() == work_q0.numel(), "work list shape");
+  const bf16_t *pkp = nullptr, *pvp = nullptr;
+  const int* pfx = nullptr;
+  if (seq_pfx.has_value()) {
+    TORCH_CHECK(pk.has_value() && pv.has_value() && variant == 3, "a prefix needs pk, pv and variant 3");
+    for (const auto* t : {&*pk, &*pv}) { CHECK_DEV(*t); CHECK_BF16(*t); CHECK_CONTIG(*t); }
+    TORCH_CHECK(pk->dim() == 3 && pv->sizes() == pk->sizes() && pk->size(1) == k.size(1) && pk->size(2) == 128,
+                "pk / pv [prefix, Hkv, 128]");
+    CHECK_DEV(*seq_pfx); CHECK_DT(*seq_pfx, at::kInt); CHECK_CONTIG(*seq_pfx);
+    TORCH_CHECK(seq_pfx->numel() >= cu_seqlens.numel() - 1, "seq_pfx: one prefix length per sequence");
+    pkp = ptr<bf16_t>(*pk);
+    pvp = ptr<bf16_t>(*pv);
+    pfx = ptr<int>(*seq_pfx);
+  }
   const c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
   RC(oamd::attn_prefill(ptr<bf16_t>(q), ptr<bf16_t>(k), ptr<bf16_t>(v), ptr<bf16_t>(o), ptr<int>(cu_seqlens),
                         ptr<int>(work_seq), ptr<int>(work_q0), (int)work_seq.numel(), (int)q.size(1),
-                        (int)k.size(1), 128, (float)scale, (int)variant, cur_stream()));
+                        (int)k.size(1), 128, (float)scale, (int)variant, cur_stream(), pkp, pvp, pfx));
 }
 
 void sample(const at::Tensor& logits, const at::Tensor& temperature, const at::Tensor& seeds,
@@ -538,7 +554,8 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("p") = pybind11::none(), pybind11::arg("splits") = 1, pybind11::arg("silu_gu") = false);
   m.def("attn_prefill", &attn_prefill, pybind11::arg("q"), pybind11::arg("k"), pybind11::arg("v"),
         pybind11::arg("o"), pybind11::arg("cu_seqlens"), pybind11::arg("work_seq"), pybind11::arg("work_q0"),
-        pybind11::arg("scale"), pybind11::arg("block_q") = 64);
+        pybind11::arg("scale"), pybind11::arg("block_q") = 64, pybind11::arg("pk") = pybind11::none(),
+        pybind11::arg("pv") = pybind11::none(), pybind11::arg("seq_pfx") = pybind11::none());
   m.def("attn_prefill_block_q", &oamd::attn_prefill_block_q);
   m.def("sample", &sample, pybind11::arg("logits"), pybind11::arg("temperature"), pybind11::arg("seeds"),
         pybind11::arg("positions"), pybind11::arg("out"), pybind11::arg("col_offset") = 0,

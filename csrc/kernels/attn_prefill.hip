@@ -400,11 +400,16 @@ __device__ __forceinline__ s16x4 ds_read_tr16(const char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
 }
 
+// Shared prompt prefix (seq_pfx != nullptr): sequence seq's keys are seq_pfx[seq] prefix
+// keys (a multiple of 64, rows of pk / pv [prefix, Hkv, D], the cached K/V of a prompt
+// prefix many requests share) followed by its own slen keys; its query rows are its own
+// tokens, at positions seq_pfx[seq] + row. Prefix keys are visible to every row (no mask).
 template <int G>
 __global__ void __launch_bounds__(512) attn_prefill_mfma32_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     bf16_t* __restrict__ o, const int* __restrict__ cu_seqlens, const int* __restrict__ work_seq,
-    const int* __restrict__ work_q0, int Hq, int Hkv, float scale_log2) {
+    const int* __restrict__ work_q0, int Hq, int Hkv, float scale_log2, const bf16_t* __restrict__ pk,
+    const bf16_t* __restrict__ pv, const int* __restrict__ seq_pfx) {
   constexpr int D = 128, BK = 64, RG = 8 / G, BQ = 32 * RG;
   __shared__ __attribute__((aligned(16))) char Ks[BK * 256];
   __shared__ __attribute__((aligned(16))) char Vs[BK * 256];
@@ -438,9 +443,10 @@ __global__ void __launch_bounds__(512) attn_prefill_mfma32_kernel(
   float mrow = -INFINITY, lpart = 0.f;
 
   const int kend = min(slen, q0 + BQ);
-  const int ntiles = (kend + BK - 1) / BK;
+  const int npt = seq_pfx != nullptr ? seq_pfx[seq] / BK : 0;   // shared-prefix key tiles first
+  const int ntiles = npt + (kend + BK - 1) / BK;
   const bool active = wave_used && rbase < slen;
-  const int wend = min(slen, rbase + 32);  // keys this wave can see: < wend
+  const int wend = min(slen, rbase + 32);  // own keys this wave can see: < wend
 
   // transposed-read addressing: 16-lane group g reads rows r0 + q (q = i >> 2) at
   // columns d0 + 4p .. +3 (p = i & 3), d0 = 32 dd + 16 (g & 1); lane i gets column d0 + i
@@ -448,14 +454,18 @@ __global__ void __launch_bounds__(512) attn_prefill_mfma32_kernel(
   const int trq = gi >> 2, trp = gi & 3;
 
   u16x8 kr[2], vr[2];
-  auto load_tile = [&](int kb) {
+  auto load_tile = [&](int kt) {   // key tile kt: a prefix tile (kt < npt) or own tile kt - npt
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
       const int c = tid + r * 512;
       const int key = c >> 4, ch = c & 15;
       kr[r] = vr[r] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      if (kb + key < slen) {
-        const int64_t off = ((int64_t)(s0 + kb + key) * Hkv + kvh) * D + ch * 8;
+      if (kt < npt) {
+        const int64_t off = ((int64_t)(kt * BK + key) * Hkv + kvh) * D + ch * 8;
+        kr[r] = *reinterpret_cast<const u16x8*>(pk + off);
+        vr[r] = *reinterpret_cast<const u16x8*>(pv + off);
+      } else if ((kt - npt) * BK + key < slen) {
+        const int64_t off = ((int64_t)(s0 + (kt - npt) * BK + key) * Hkv + kvh) * D + ch * 8;
         kr[r] = *reinterpret_cast<const u16x8*>(k + off);
         vr[r] = *reinterpret_cast<const u16x8*>(v + off);
       }
@@ -473,11 +483,11 @@ __global__ void __launch_bounds__(512) attn_prefill_mfma32_kernel(
 
   load_tile(0);
   for (int kt = 0; kt < ntiles; ++kt) {
-    const int kb = kt * BK;
+    const int kb = (kt - npt) * BK;   // own-key coordinates (negative: a prefix tile)
     __syncthreads();  // previous tile fully consumed
     store_tile();
     __syncthreads();
-    if (kt + 1 < ntiles) load_tile(kb + BK);  // in flight during this tile's MFMAs
+    if (kt + 1 < ntiles) load_tile(kt + 1);   // in flight during this tile's MFMAs
     if (!active || kb >= wend) continue;      // wave-uniform: no visible key for this wave
 
     // ---- S^T = K Q^T (two 32-key blocks) ----
@@ -494,7 +504,7 @@ __global__ void __launch_bounds__(512) attn_prefill_mfma32_kernel(
       }
     }
     // ---- online softmax: register i of block b is key kb + 32b + (i&3) + 8(i>>2) + 4h ----
-    const bool mask = (kb + BK > rbase + 1) || (kb + BK > slen);
+    const bool mask = kb >= 0 && ((kb + BK > rbase + 1) || (kb + BK > slen));
     float mx = -INFINITY;
 #pragma unroll
     for (int b = 0; b < 2; ++b)
@@ -581,11 +591,13 @@ int attn_prefill_block_q(int Hq, int Hkv, int variant) {
 
 int attn_prefill(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, const int* cu_seqlens,
                  const int* work_seq, const int* work_q0, int num_work, int Hq, int Hkv, int head_dim,
-                 float scale, int variant, hipStream_t stream) {
+                 float scale, int variant, hipStream_t stream, const bf16_t* pk, const bf16_t* pv,
+                 const int* seq_pfx) {
   if (num_work == 0) return 0;
   if (head_dim != 128) return -1;
   if (Hq % Hkv != 0) return -3;
   if (attn_prefill_block_q(Hq, Hkv, variant) < 0) return -4;
+  if (seq_pfx != nullptr && (variant != 3 || pk == nullptr || pv == nullptr)) return -5;   // v3 only
   const float sl2 = scale * 1.4426950408889634f;
   const int G = Hq / Hkv;
   if (variant == 1) {
@@ -594,6 +606,8 @@ int attn_prefill(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, c
   } else {
     dim3 grid(num_work, Hkv);
 #define OAMD_PF(KERN, GG) KERN<GG><<<grid, 512, 0, stream>>>(q, k, v, o, cu_seqlens, work_seq, work_q0, Hq, Hkv, sl2)
+#define OAMD_PF3(GG) \
+  attn_prefill_mfma32_kernel<GG><<<grid, 512, 0, stream>>>(q, k, v, o, cu_seqlens, work_seq, work_q0, Hq, Hkv, sl2, pk, pv, seq_pfx)
 #define OAMD_PF_G(KERN)            \
   switch (G) {                     \
     case 1: OAMD_PF(KERN, 1); break; \
@@ -605,13 +619,17 @@ int attn_prefill(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, c
       OAMD_PF_G(attn_prefill_gqa_kernel)
     } else {
       switch (G) {  // groups of Llama-3.2-3B (3), Qwen2.5-32B (5), Qwen2.5-7B (7)
-        case 3: OAMD_PF(attn_prefill_mfma32_kernel, 3); break;
-        case 5: OAMD_PF(attn_prefill_mfma32_kernel, 5); break;
-        case 6: OAMD_PF(attn_prefill_mfma32_kernel, 6); break;
-        case 7: OAMD_PF(attn_prefill_mfma32_kernel, 7); break;
-        default: OAMD_PF_G(attn_prefill_mfma32_kernel)
+        case 1: OAMD_PF3(1); break;
+        case 2: OAMD_PF3(2); break;
+        case 3: OAMD_PF3(3); break;
+        case 4: OAMD_PF3(4); break;
+        case 5: OAMD_PF3(5); break;
+        case 6: OAMD_PF3(6); break;
+        case 7: OAMD_PF3(7); break;
+        default: OAMD_PF3(8); break;
       }
     }
+#undef OAMD_PF3
 #undef OAMD_PF_G
 #undef OAMD_PF
   }

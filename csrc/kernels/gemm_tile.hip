@@ -307,11 +307,12 @@ __device__ __forceinline__ void mfma_tied(f32x4& acc, const u16x8& a, const u16x
 // t & 1) runs in four 32-MFMA phases:
 //   1. k-half 0 from registers A; read k-half 1 (registers B) — the tile's last reads;
 //      lgkmcnt(0) + barrier: every wave is done with buffer t & 1
-//   2. k-half 0 cont.; 8 X pieces of tile t+2 into buffer t & 1;
-//      vmcnt(16) + barrier: tile t+1's X pieces (issued in phase 2 of tile t-1) landed
-//   3. k-half 1 from registers B; 8 W pieces of tile t+2; read X of tile t+1, k-half 0;
-//      vmcnt(16) + barrier: tile t+1's W pieces landed
-//   4. k-half 1 cont.; read W of tile t+1, k-half 0 (registers A)
+//   2. k-half 0 cont.; 8 W pieces of tile t+2 into buffer t & 1;
+//      vmcnt(16) + barrier: tile t+1's W pieces (issued in phase 2 of tile t-1) landed
+//   3. k-half 1 from registers B; 8 X pieces of tile t+2; read W of tile t+1, k-half 0;
+//      vmcnt(16) + barrier: tile t+1's X pieces landed
+//   4. k-half 1 cont.; read X of tile t+1, k-half 0 (registers A) — X last: every MFMA row
+//      of the next phase 1 needs all 8 W fragments but only its own X fragment
 // so every piece has a whole tile (128 MFMAs per wave) to land, a buffer is refilled only
 // after the barrier that follows its last read, and each staged piece is read one phase
 // after the wait + barrier that retire it. DMAs and fragment reads sit between MFMAs (one
@@ -319,7 +320,7 @@ __device__ __forceinline__ void mfma_tied(f32x4& acc, const u16x8& a, const u16x
 // source and the read (conflict-free ds_read_b128). The DMAs carry the sc1
 // cache policy (AUX 16: 1-3 % over the default on down / qkv; nt costs 4-20 %,
 // profiles/gemm_tile_variants_r4_c.jsonl).
-template <int EPI, int AUX = 16>
+template <int EPI, int AUX = 16, bool XFIRST = false>
 __global__ void __launch_bounds__(256) gemm_tile256_h4_kernel(const bf16_t* __restrict__ X,
                                                               const bf16_t* __restrict__ W, bf16_t* __restrict__ Y,
                                                               const bf16_t* __restrict__ bias, int M, int N, int K,
@@ -408,13 +409,18 @@ __global__ void __launch_bounds__(256) gemm_tile256_h4_kernel(const bf16_t* __re
 
   // prologue: tiles 0 and 1 (buffers 0, 1); tile 0 landed; k-half 0 of tile 0 into A
 #pragma unroll
-  for (int q = 0; q < 8; ++q) dma_x(0, 0, q);
+  for (int tt = 0; tt < 2; ++tt) {   // per tile in the order the loop issues them
 #pragma unroll
-  for (int q = 0; q < 8; ++q) dma_w(0, 0, q);
+    for (int q = 0; q < 8; ++q) {
+      if constexpr (XFIRST) dma_x(tt, tt, q);
+      else dma_w(tt, tt, q);
+    }
 #pragma unroll
-  for (int q = 0; q < 8; ++q) dma_x(1, 1, q);
-#pragma unroll
-  for (int q = 0; q < 8; ++q) dma_w(1, 1, q);
+    for (int q = 0; q < 8; ++q) {
+      if constexpr (XFIRST) dma_w(tt, tt, q);
+      else dma_x(tt, tt, q);
+    }
+  }
   vm_wait<16>();
   seg_barrier();
 #pragma unroll
@@ -435,28 +441,39 @@ __global__ void __launch_bounds__(256) gemm_tile256_h4_kernel(const bf16_t* __re
       });
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     seg_barrier();
-    // phase 2: rows 4-7 of k-half 0; X pieces of tile t+2 into buffer b
+    // phase 2: rows 4-7 of k-half 0; W pieces of tile t+2 into buffer b
 #pragma unroll
     for (int i = 4; i < 8; ++i)
       row(xa, wa, i, [&](int k) {
-        if (!(k & 1)) dma_x(t + 2, b, 2 * (i - 4) + (k >> 1));
+        if (!(k & 1)) {
+          if constexpr (XFIRST) dma_x(t + 2, b, 2 * (i - 4) + (k >> 1));
+          else dma_w(t + 2, b, 2 * (i - 4) + (k >> 1));
+        }
       });
-    vm_wait<16>();   // tile t+1's X pieces (this wave's)
+    vm_wait<16>();   // tile t+1's W pieces (this wave's)
     seg_barrier();   // ... every wave's
-    // phase 3: rows 0-3 of k-half 1; W pieces of tile t+2; X of tile t+1, k-half 0
+    // phase 3: rows 0-3 of k-half 1; X pieces of tile t+2; W of tile t+1, k-half 0
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       row(xb, wb, i, [&](int k) {
-        if (!(k & 1)) dma_w(t + 2, b, 2 * i + (k >> 1));
-        else rdx(nb, c0, xa, 2 * i + (k >> 1));
+        if constexpr (XFIRST) {
+          if (!(k & 1)) dma_w(t + 2, b, 2 * i + (k >> 1));
+          else rdx(nb, c0, xa, 2 * i + (k >> 1));
+        } else {
+          if (!(k & 1)) dma_x(t + 2, b, 2 * i + (k >> 1));
+          else rdw(nb, c0, wa, 2 * i + (k >> 1));
+        }
       });
-    vm_wait<16>();   // tile t+1's W pieces
+    vm_wait<16>();   // tile t+1's X pieces
     seg_barrier();
-    // phase 4: rows 4-7 of k-half 1; W of tile t+1, k-half 0
+    // phase 4: rows 4-7 of k-half 1; X of tile t+1, k-half 0
 #pragma unroll
     for (int i = 4; i < 8; ++i)
       row(xb, wb, i, [&](int k) {
-        if (!(k & 1)) rdw(nb, c0, wa, 2 * (i - 4) + (k >> 1));
+        if (!(k & 1)) {
+          if constexpr (XFIRST) rdw(nb, c0, wa, 2 * (i - 4) + (k >> 1));
+          else rdx(nb, c0, xa, 2 * (i - 4) + (k >> 1));
+        }
       });
   }
   vm_wait<0>();   // the tail's clamped re-loads land before the workgroup's LDS is released
@@ -557,6 +574,8 @@ int gemm_tile(const bf16_t* X, const bf16_t* W, bf16_t* Y, const bf16_t* bias, i
     if (silu_gu) gemm_tile256_h4_kernel<kEpiSilu><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
     else if (bias) gemm_tile256_h4_kernel<kEpiBias><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
     else gemm_tile256_h4_kernel<kEpiStore><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+  } else if (variant == 4 && off32 && !silu_gu && !bias) {   // h4 with the X pieces / fragments first (timing)
+    gemm_tile256_h4_kernel<kEpiStore, 16, true><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
   } else if (variant == 2 || (variant == 0 && M > 256)) {
     // 8-wave ping-pong, two barrier segments per K-tile (the round-3 default; 2-8 % behind
     // variant 1 on the prefill shapes, profiles/gemm_tile_h4_vs_ph2_m32k.jsonl); also the

@@ -84,7 +84,8 @@ int attn_decode(const bf16_t* q, const void* k_cache, const void* v_cache, bool 
 int attn_prefill_block_q(int Hq, int Hkv, int variant);
 int attn_prefill(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, const int* cu_seqlens,
                  const int* work_seq, const int* work_q0, int num_work, int Hq, int Hkv, int head_dim,
-                 float scale, int variant, hipStream_t stream);
+                 float scale, int variant, hipStream_t stream,
+                 const bf16_t* pk = nullptr, const bf16_t* pv = nullptr, const int* seq_pfx = nullptr);
 int sample_tokens(const void* logits, bool logits_bf16, int64_t stride, int rows, int vocab,
                   const float* temperature, const int64_t* seeds, const int64_t* positions,
                   int64_t* out_tokens, int64_t col_offset, float* out_val, hipStream_t stream);

@@ -132,6 +132,7 @@ class EngineCfg(BaseModel):
     page_size: int = 64
     use_graphs: bool = True
     prefill_graphs: bool = True       # full-ish prefill batches replay a captured bucket graph
+    prefix_sharing: bool = True       # prompts starting with the same whole KV pages share them (computed once)
     warmup_graphs: bool = True        # engine processes capture their graphs before reporting ready
     multi_step: int = 8
     ignore_eos: bool = False

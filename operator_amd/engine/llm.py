@@ -15,6 +15,10 @@ hipGraph-captured decode steps.
 * Under tensor parallelism every rank of the TP group must receive the same
   requests in the same order; scheduling is deterministic, so ranks stay in
   lockstep without broadcasting decisions.
+* Shared prompt prefixes: requests whose first whole KV pages hold the same tokens
+  (every explanation prompt starts with the same instructions) map ONE set of pages,
+  computed once, at the head of their block tables; their prefill computes only their
+  own tokens, attending to the cached prefix K/V (``_SharedPrefix``).
 """
 from __future__ import annotations
 
@@ -52,6 +56,7 @@ class GenRequest:
     rid: int = -1
     # runtime state
     pages: list[int] = field(default_factory=list)
+    prefix: "_SharedPrefix | None" = None   # shared prompt-prefix pages at the head of ``pages``
     output: list[int] = field(default_factory=list)
     done: bool = False
     cancelled: bool = False
@@ -81,6 +86,9 @@ class EngineStats:
     prefill_graph_replays: int = 0
     prefill_padded_tokens: int = 0   # bucket padding computed by prefill-graph replays
     prefill_eager: int = 0           # prefill batches no graph bucket fit (<= 15 % padding)
+    prefix_hits: int = 0             # requests whose prompt started with the shared prefix
+    prefix_tokens: int = 0           # ... prompt tokens they did not prefill
+    prefix_builds: int = 0           # shared prefixes computed
     decode_launch_s: float = 0.0     # host time inside decode-window graph launches (a launch that
     decode_wait_s: float = 0.0       # ... blocks means the GPU queue is full) / waiting for windows
     decode_windows: int = 0          # decode windows launched
@@ -266,7 +274,7 @@ class _PrefillGraph:
         self.dev = {n: torch.zeros(k, dtype=dt, device=dev) for n, k, dt in (
             ("ids", T, i64), ("pos", T, i64), ("slots", T, i64), ("last", S, i64), ("seeds", S, i64),
             ("spos", S, i64), ("cu", S + 1, i32), ("ws", self.W, i32), ("wq", self.W, i32),
-            ("temp", S, torch.float32))}
+            ("temp", S, torch.float32), ("pfx", S, i32))}
         # two pinned input sets + sampled-token buffers, used alternately: a launch
         # returns without waiting for the GPU, so the engine can queue the next
         # prefill batch before reading this one's tokens (LLMEngine._prefill); a set is
@@ -281,8 +289,9 @@ class _PrefillGraph:
 
     def _run(self) -> None:
         e, d = self.eng, self.dev
+        pre = (e._pk, e._pv, d["pfx"], None) if e.prefix_sharing else None
         fb = ForwardBatch(d["ids"], d["pos"], d["slots"], True, d["last"], seq_lens=[],
-                          prefill_work=(d["cu"], d["ws"], d["wq"], self.variant))
+                          prefill_work=(d["cu"], d["ws"], d["wq"], self.variant), prefix=pre)
         logits = e.model.forward(fb, e.kv)
         self.tok = e.model.sample(logits, d["temp"], d["seeds"], d["spos"])
 
@@ -301,7 +310,7 @@ class _PrefillGraph:
             self._run()
         self.graph = g
 
-    def launch(self, ids, pos, slots, cu, ws, wq, last, temp, seeds, spos):
+    def launch(self, ids, pos, slots, cu, ws, wq, last, temp, seeds, spos, pfx=None):
         """Queue one replay for the real batch (numpy inputs, <= T tokens, <= S
         sequences); returns (pinned token buffer, event): ``event`` completes when the
         batch's sampled first tokens are in the buffer."""
@@ -313,7 +322,7 @@ class _PrefillGraph:
         b = len(last)
         for name, arr, fill in (("ids", ids, 0), ("pos", pos, 0), ("slots", slots, -1), ("last", last, 0),
                                 ("seeds", seeds, 0), ("spos", spos, 0), ("temp", temp, 0.0), ("ws", ws, -1),
-                                ("wq", wq, 0), ("cu", cu, int(cu[-1]))):
+                                ("wq", wq, 0), ("cu", cu, int(cu[-1])), ("pfx", pfx if pfx is not None else [], 0)):
             v = h[name].numpy()
             v[:len(arr)] = arr
             v[len(arr):] = fill
@@ -334,6 +343,19 @@ class _PrefillGraph:
         return out.tolist()
 
 
+class _SharedPrefix:
+    """The first ``n`` prompt tokens (whole KV pages) many requests share: their KV pages,
+    written once by a prefill of just these tokens and mapped at the head of every such
+    request's block table (read-only: a request's own tokens start on its own pages), and
+    their post-RoPE K/V per layer in ``LLMEngine._pk`` / ``_pv`` for the prefill attention
+    of the requests' own tokens. Freed when replaced and no request holds it."""
+
+    def __init__(self, tokens: tuple, pages: list[int]):
+        self.tokens, self.pages, self.n = tokens, pages, len(tokens)
+        self.users = 0
+        self.retired = False
+
+
 @dataclass
 class _PendingPrefill:
     """A launched prefill batch whose first tokens are still on the device."""
@@ -345,9 +367,15 @@ class _PendingPrefill:
 
 
 class LLMEngine:
+    # shared prompt prefixes: at most this many whole pages, built once a page-aligned
+    # prefix has been seen at the head of this many of the last PREFIX_WINDOW prompts
+    PREFIX_MAX_PAGES = 4
+    PREFIX_MIN_SEEN = 2
+    PREFIX_WINDOW = 64
+
     def __init__(self, model: LlamaModel, kv: PagedKVCache, max_batch: int = 256, max_prefill_tokens: int = 16384,
                  max_context: int | None = None, use_graphs: bool = True, multi_step: int = 8,
-                 admit_wait_s: float = 0.0, prefill_graphs: bool = True):
+                 admit_wait_s: float = 0.0, prefill_graphs: bool = True, prefix_sharing: bool = True):
         self.model, self.kv = model, kv
         # arrival batching window used by the loop that drives step() (EngineLoop):
         # an idle engine given less than a full prefill batch waits this long for more
@@ -406,6 +434,20 @@ class LLMEngine:
         if self.device.type == "cuda":
             self._host_bufs = [torch.empty(max_batch, self.multi_step, dtype=torch.long, pin_memory=True)
                                for _ in range(2)]
+        # shared prompt prefix: the GPU path needs the v3 prefill attention kernel; TP
+        # engines replay the leader's steps and keep it off
+        self.prefix_sharing = prefix_sharing and (
+            self.device.type != "cuda" or ops.prefill_variant(model.hq, model.hkv) == 3)
+        self._pfx: _SharedPrefix | None = None
+        self._pfx_seen: deque = deque()
+        self._pfx_count: dict = {}
+        self._pfx_last: list = []   # the page-aligned prefixes of the last admitted prompt
+        self._pk = self._pv = None
+        if self.prefix_sharing:
+            n = self.PREFIX_MAX_PAGES * kv.page_size
+            shape = (model.cfg.layers, n, model.hkv, model.cfg.head_dim)
+            self._pk = torch.zeros(shape, dtype=torch.bfloat16, device=self.device)
+            self._pv = torch.zeros(shape, dtype=torch.bfloat16, device=self.device)
 
     # ------------------------------------------------------------------ API
     def submit(self, req: GenRequest) -> GenRequest:
@@ -445,14 +487,95 @@ class LLMEngine:
             self.running, self.waiting, self._prefilling = [], deque(), []
             self._pf = None
         for r in reqs:
-            if r.pages:
-                self.kv.allocator.release(r.pages)
-                r.pages = []
+            self._release(r)
             r.error = reason
             r.done = True
             r.event.set()
         self._inflight = None
         self._active = None
+
+    @property
+    def prefix_pages(self) -> int:
+        """KV pages the current shared prompt prefix holds (outside any request)."""
+        return len(self._pfx.pages) if self._pfx is not None else 0
+
+    def _release(self, r: GenRequest) -> None:
+        """Return a request's own KV pages; shared prefix pages stay with the prefix."""
+        pf = r.prefix
+        own = r.pages[len(pf.pages):] if pf is not None else r.pages
+        if own:
+            self.kv.allocator.release(own)
+        r.pages = []
+        if pf is not None:
+            r.prefix = None
+            pf.users -= 1
+            if pf.retired and pf.users == 0:
+                self.kv.allocator.release(pf.pages)
+
+    # ------------------------------------------------------------------ shared prompt prefixes
+    def _prefix_keys(self, prompt: list[int]) -> list[tuple]:
+        """Page-aligned prompt prefixes a request could share (longest last), each leaving
+        at least one token of its own to prefill (its logits sample the first output)."""
+        P = self.kv.page_size
+        k = min(self.PREFIX_MAX_PAGES, (len(prompt) - 1) // P)
+        return [tuple(prompt[:j * P]) for j in range(1, k + 1)]
+
+    def _note_prefix(self, prompt: list[int]) -> None:
+        self._pfx_last = self._prefix_keys(prompt)
+        for key in self._pfx_last:
+            self._pfx_seen.append(key)
+            self._pfx_count[key] = self._pfx_count.get(key, 0) + 1
+        while len(self._pfx_seen) > self.PREFIX_WINDOW * self.PREFIX_MAX_PAGES:
+            old = self._pfx_seen.popleft()
+            c = self._pfx_count[old] - 1
+            if c:
+                self._pfx_count[old] = c
+            else:
+                del self._pfx_count[old]
+
+    def _maybe_build_prefix(self) -> None:
+        """Compute a shared prefix when the latest admitted prompt starts with a page-aligned
+        prefix seen at the head of PREFIX_MIN_SEEN recent prompts (the longest such) that
+        is not the one in place, and no request holds the current one. One eager prefill of
+        just the prefix tokens writes its KV pages and hands each layer's K/V to
+        ``_pk`` / ``_pv``."""
+        best = None
+        for key in self._pfx_last:
+            if self._pfx_count.get(key, 0) >= self.PREFIX_MIN_SEEN:
+                best = key   # keys are shortest first
+        cur = self._pfx
+        if best is None or (cur is not None and (cur.tokens == best or cur.users > 0)):
+            return
+        npages = len(best) // self.kv.page_size
+        if npages + 1 > self.kv.allocator.free:
+            return
+        pages = self.kv.allocator.alloc(npages)
+        n = len(best)
+        dev = self.device
+        P = self.kv.page_size
+        slots = torch.tensor([pages[j // P] * P + j % P for j in range(n)], dtype=torch.long, device=dev)
+
+        def sink(i, k, v):
+            self._pk[i, :n].copy_(k.reshape(n, *self._pk.shape[2:]))
+            self._pv[i, :n].copy_(v.reshape(n, *self._pv.shape[2:]))
+
+        work = None
+        if dev.type == "cuda":
+            var = ops.prefill_variant(self.model.hq, self.model.hkv)
+            ws, wq = ops.prefill_work_list([n], ops.prefill_block_q(self.model.hq, self.model.hkv, var))
+            work = (torch.tensor([0, n], dtype=torch.int32, device=dev), torch.tensor(ws, dtype=torch.int32, device=dev),
+                    torch.tensor(wq, dtype=torch.int32, device=dev), var)
+        fb = ForwardBatch(torch.tensor(best, dtype=torch.long, device=dev), torch.arange(n, device=dev), slots, True,
+                          torch.tensor([n - 1], dtype=torch.long, device=dev), seq_lens=[n], prefill_work=work,
+                          kv_sink=sink)
+        with trace_range(f"prefix[{n}]"):
+            self.model.forward(fb, self.kv)
+        if cur is not None:
+            cur.retired = True
+            if cur.users == 0:
+                self.kv.allocator.release(cur.pages)
+        self._pfx = _SharedPrefix(best, pages)
+        self.stats.prefix_builds += 1
 
     def has_work(self) -> bool:
         return bool(self.waiting or self.running or self._pf is not None)
@@ -541,6 +664,9 @@ class LLMEngine:
         out, toks = [], 0
         rows = self._rows()
         cap = self._prefill_cap()
+        if self.prefix_sharing and self._pfx_count:
+            self._maybe_build_prefix()
+        pf = self._pfx
         with self._lock:
             while self.waiting and rows + len(out) < self.max_batch:
                 r = self.waiting[0]
@@ -549,7 +675,9 @@ class LLMEngine:
                     continue
                 if out and toks + len(r.prompt) > cap:
                     break
-                need = self.kv.pages_needed(len(r.prompt) + r.max_tokens)
+                shared = (pf is not None and len(r.prompt) > pf.n and r.prompt[0] == pf.tokens[0]
+                          and tuple(r.prompt[:pf.n]) == pf.tokens)
+                need = self.kv.pages_needed(len(r.prompt) + r.max_tokens) - (len(pf.pages) if shared else 0)
                 if need > self.kv.allocator.free:
                     if not rows and not out:
                         r.error = "KV cache too small for request"
@@ -559,6 +687,14 @@ class LLMEngine:
                         continue
                     break
                 r.pages = self.kv.allocator.alloc(need)
+                if shared:
+                    r.pages = pf.pages + r.pages
+                    r.prefix = pf
+                    pf.users += 1
+                    self.stats.prefix_hits += 1
+                    self.stats.prefix_tokens += pf.n
+                if self.prefix_sharing:
+                    self._note_prefix(r.prompt)
                 self.waiting.popleft()
                 out.append(r)
                 self._prefilling = (self._pf.batch if self._pf is not None else []) + out
@@ -593,13 +729,17 @@ class LLMEngine:
         # packed token ids / positions / cache slots built with numpy: this runs on the
         # engine thread between prefill batches, while the GPU waits for it
         P = self.kv.page_size
-        lens = [len(r.prompt) for r in batch]
-        ar = [np.arange(n, dtype=np.int64) for n in lens]
-        ids = np.concatenate([np.asarray(r.prompt, dtype=np.int64) for r in batch])
+        # a request holding the shared prefix prefills only its own tokens (positions n..)
+        skip = [r.prefix.n if r.prefix is not None else 0 for r in batch]
+        full = [len(r.prompt) for r in batch]
+        lens = [f - n for f, n in zip(full, skip)]
+        ar = [np.arange(n, f, dtype=np.int64) for n, f in zip(skip, full)]
+        ids = np.concatenate([np.asarray(r.prompt[n:], dtype=np.int64) for r, n in zip(batch, skip)])
         pos = np.concatenate(ar)
         slots = np.concatenate([np.asarray(r.pages, dtype=np.int64)[a // P] * P + a % P for r, a in zip(batch, ar)])
         cu = np.zeros(len(lens) + 1, dtype=np.int64)
         cu[1:] = np.cumsum(lens)
+        pfx = skip if any(skip) else None
         last = cu[1:] - 1
         var = ops.prefill_variant(self.model.hq, self.model.hkv)
         ws, wq = ops.prefill_work_list(lens, ops.prefill_block_q(self.model.hq, self.model.hkv, var))
@@ -607,16 +747,17 @@ class LLMEngine:
         seeds = [r.seed for r in batch]
         g = self._prefill_graph_for(len(ids), len(batch))
         if g is not None:
-            toks, ev = g.launch(ids, pos, slots, cu, ws, wq, last, temps, seeds, lens)
+            toks, ev = g.launch(ids, pos, slots, cu, ws, wq, last, temps, seeds, full, skip)
             self.stats.prefill_graph_replays += 1
             self.stats.prefill_padded_tokens += g.T - len(ids)
         else:
             self.stats.prefill_eager += 1
             t = lambda x, dt=torch.long: torch.as_tensor(np.asarray(x)).to(dtype=dt).to(dev, non_blocking=True)  # noqa: E731
             work = (t(cu, torch.int32), t(ws, torch.int32), t(wq, torch.int32), var) if dev.type == "cuda" else None
-            fb = ForwardBatch(t(ids), t(pos), t(slots), True, t(last), seq_lens=lens, prefill_work=work)
+            pre = None if pfx is None else (self._pk, self._pv, t(pfx, torch.int32), pfx)
+            fb = ForwardBatch(t(ids), t(pos), t(slots), True, t(last), seq_lens=lens, prefill_work=work, prefix=pre)
             logits = self.model.forward(fb, self.kv)
-            tk = self.model.sample(logits, t(temps, torch.float32), t(seeds), t(lens))
+            tk = self.model.sample(logits, t(temps, torch.float32), t(seeds), t(full))
             if dev.type == "cuda":
                 toks = torch.empty(len(batch), dtype=torch.long, pin_memory=True)
                 toks.copy_(tk, non_blocking=True)
@@ -767,8 +908,7 @@ class LLMEngine:
             if len(r.output) >= r.max_tokens or hit_eos or r.cancelled:
                 r.done = True
                 r.t_done = now
-                self.kv.allocator.release(r.pages)
-                r.pages = []
+                self._release(r)
                 fin.append(r)
             else:
                 keep.append(r)

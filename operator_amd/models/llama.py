@@ -53,6 +53,10 @@ class ForwardBatch:
     # prefill
     seq_lens: list[int] = field(default_factory=list)
     prefill_work: tuple | None = None
+    # shared prompt prefix (LLMEngine prefix sharing): (pk, pv, seq_pfx, pfx_lens), pk / pv the
+    # cached post-RoPE K/V [layers, P, Hkv, D]; sequence s's tokens follow pfx_lens[s] of them
+    prefix: tuple | None = None
+    kv_sink: object = None   # called (layer, k, v) with each prefill layer's K/V (prefix capture)
     # decode
     block_tables: torch.Tensor | None = None   # [B, max_pages] int32
     context_lens: torch.Tensor | None = None   # [B] int32 (including the new token)
@@ -257,7 +261,12 @@ class LlamaModel:
             if fb.is_prefill:
                 q, k, v = ops.rope_kv(qkv, fb.positions, self.cos, self.sin, self.hq, self.hkv, kc, vc, fb.slots,
                                       want_kv=True, bias=bias, k_scale=kv.k_scale, v_scale=kv.v_scale)
-                o = ops.attn_prefill(q, k, v, fb.seq_lens, self.scale, work=fb.prefill_work)
+                if fb.kv_sink is not None:
+                    fb.kv_sink(i, k, v)
+                pre = None
+                if fb.prefix is not None:
+                    pre = (fb.prefix[0][i], fb.prefix[1][i], fb.prefix[2], fb.prefix[3])
+                o = ops.attn_prefill(q, k, v, fb.seq_lens, self.scale, work=fb.prefill_work, prefix=pre)
             else:
                 q, _, _ = ops.rope_kv(qkv, fb.positions, self.cos, self.sin, self.hq, self.hkv, kc, vc, fb.slots,
                                       want_kv=False, bias=bias, k_scale=kv.k_scale, v_scale=kv.v_scale)

@@ -205,13 +205,22 @@ def prefill_work_list(seq_lens: list[int], block_q: int = 64) -> tuple[list[int]
 
 
 def attn_prefill(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, seq_lens: list[int], scale: float,
-                 out: torch.Tensor | None = None, work: tuple[torch.Tensor, torch.Tensor, torch.Tensor] | None = None):
-    """Causal attention over packed sequences (q [T,Hq,D], k/v [T,Hkv,D])."""
+                 out: torch.Tensor | None = None, work: tuple[torch.Tensor, torch.Tensor, torch.Tensor] | None = None,
+                 prefix: tuple | None = None):
+    """Causal attention over packed sequences (q [T,Hq,D], k/v [T,Hkv,D]).
+
+    ``prefix`` = (pk, pv, seq_pfx, pfx_lens): a shared prompt prefix (LLMEngine prefix
+    sharing) whose cached K/V rows pk / pv [P, Hkv, D] come before sequence s's own keys
+    for its first pfx_lens[s] keys (0 or a multiple of 64, <= P); the own query rows sit at
+    positions pfx_lens[s] + row and see every prefix key. seq_pfx: the same lengths as an
+    int32 device tensor (GPU), pfx_lens: as a host list (CPU reference; may be None on
+    the GPU)."""
     cu = [0]
     for L in seq_lens:
         cu.append(cu[-1] + int(L))
     if not q.is_cuda:
-        r = reference.attn_prefill(q, k, v, cu, scale)
+        r = reference.attn_prefill(q, k, v, cu, scale,
+                                   prefix=None if prefix is None else (prefix[0], prefix[1], prefix[3]))
         if out is not None:
             out.copy_(r)
             return out
@@ -224,7 +233,13 @@ def attn_prefill(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, seq_lens: li
         work = (torch.tensor(cu, dtype=torch.int32, device=dev), torch.tensor(ws, dtype=torch.int32, device=dev),
                 torch.tensor(wq, dtype=torch.int32, device=dev), var)
     # work = (cu_seqlens, work_seq, work_q0, variant); the work list must be cut at that variant's block_q
-    kernels().attn_prefill(q, k, v, o, work[0], work[1], work[2], scale, work[3] if len(work) > 3 else 1)
+    var = work[3] if len(work) > 3 else 1
+    if prefix is not None:
+        if var != 3:
+            raise ValueError("a shared prefix needs attn_prefill variant 3")
+        kernels().attn_prefill(q, k, v, o, work[0], work[1], work[2], scale, var, prefix[0], prefix[1], prefix[2])
+    else:
+        kernels().attn_prefill(q, k, v, o, work[0], work[1], work[2], scale, var)
     return o
 
 

@@ -143,8 +143,10 @@ def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, cos: torch.Tensor, sin: torch.
 
 
 def attn_prefill(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cu_seqlens: list[int] | torch.Tensor,
-                 scale: float) -> torch.Tensor:
-    """Causal GQA attention over packed variable-length sequences. q [T,Hq,D], k/v [T,Hkv,D]."""
+                 scale: float, prefix: tuple | None = None) -> torch.Tensor:
+    """Causal GQA attention over packed variable-length sequences. q [T,Hq,D], k/v [T,Hkv,D].
+    ``prefix`` = (pk, pv, lens): sequence i's keys start with the rows pk[:lens[i]] /
+    pv[:lens[i]] (a cached shared prompt prefix), visible to all of its query rows."""
     cu = [int(x) for x in cu_seqlens]
     Hq, Hkv = q.shape[1], k.shape[1]
     G = Hq // Hkv
@@ -153,12 +155,18 @@ def attn_prefill(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cu_seqlens: 
         a, b = cu[i], cu[i + 1]
         if b == a:
             continue
+        pl = int(prefix[2][i]) if prefix is not None else 0
+        kk, vv = k[a:b], v[a:b]
+        if pl:
+            kk, vv = torch.cat([prefix[0][:pl].to(k.dtype), kk]), torch.cat([prefix[1][:pl].to(v.dtype), vv])
         qs = q[a:b].float().transpose(0, 1)                      # [Hq, L, D]
-        ks = k[a:b].float().transpose(0, 1).repeat_interleave(G, 0)
-        vs = v[a:b].float().transpose(0, 1).repeat_interleave(G, 0)
+        ks = kk.float().transpose(0, 1).repeat_interleave(G, 0)
+        vs = vv.float().transpose(0, 1).repeat_interleave(G, 0)
         s = torch.matmul(qs, ks.transpose(1, 2)) * scale
         L = b - a
         mask = torch.ones(L, L, dtype=torch.bool, device=q.device).triu(1)
+        if pl:
+            mask = torch.cat([torch.zeros(L, pl, dtype=torch.bool, device=q.device), mask], 1)
         s.masked_fill_(mask, float("-inf"))
         p = torch.softmax(s, -1)
         out[a:b] = torch.matmul(p, vs).transpose(0, 1).to(q.dtype)

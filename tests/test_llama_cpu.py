@@ -64,7 +64,7 @@ def test_cached_decode_equals_recompute(name):
             nxt = int(torch.argmax(_full_logits(m, kv, seq)[-1]))
             seq.append(nxt)
         assert r.output == seq[len(r.prompt):], (r.output, seq[len(r.prompt):])
-    assert kv.allocator.free == kv.num_pages  # every page returned
+    assert kv.allocator.free + eng.prefix_pages == kv.num_pages  # every page returned
 
 
 def test_sampling_is_seeded_and_batch_invariant():
@@ -141,12 +141,12 @@ def test_engine_prefill_failure_releases_pages():
         for r in first:
             assert r.event.wait(60)
         assert all(r.error and "out of memory" in r.error for r in first)
-        assert kv.allocator.free == kv.num_pages and loop.fatal is None
+        assert kv.allocator.free + eng.prefix_pages == kv.num_pages and loop.fatal is None
         again = GenRequest(list(range(1, 30)), max_tokens=4, temperature=0.0, ignore_eos=True)
         eng.submit(again)
         loop.notify()
         assert again.event.wait(60) and again.error is None and len(again.output) == 4
-        assert kv.allocator.free == kv.num_pages
+        assert kv.allocator.free + eng.prefix_pages == kv.num_pages
     finally:
         loop.stop()
         loop.join(10)
@@ -180,12 +180,12 @@ def test_engine_step_failure_releases_pages_and_keeps_serving():
         for r in first:
             assert r.event.wait(60)
         assert all(r.error and "out of memory" in r.error for r in first)
-        assert kv.allocator.free == kv.num_pages and loop.fatal is None and loop.is_alive()
+        assert kv.allocator.free + eng.prefix_pages == kv.num_pages and loop.fatal is None and loop.is_alive()
         again = GenRequest(list(range(1, 30)), max_tokens=8, temperature=0.0, ignore_eos=True)
         eng.submit(again)
         loop.notify()
         assert again.event.wait(60) and again.error is None and len(again.output) == 8
-        assert kv.allocator.free == kv.num_pages
+        assert kv.allocator.free + eng.prefix_pages == kv.num_pages
     finally:
         loop.stop()
         loop.join(10)
@@ -217,7 +217,7 @@ def test_pipelined_prefill_batches_match_one_at_a_time():
         eng.step()
     assert [r.output for r in reqs] == alone
     assert len(launched) == 4 and sum(p for _, p in launched) == 3   # batches 2-4 queued behind a pending one
-    assert kv.allocator.free == kv.num_pages
+    assert kv.allocator.free + eng.prefix_pages == kv.num_pages
 
 
 def test_pipelined_prefill_failure_releases_both_batches():
@@ -249,12 +249,12 @@ def test_pipelined_prefill_failure_releases_both_batches():
         for r in reqs:
             assert r.event.wait(60)
         assert all(r.error and "out of memory" in r.error for r in reqs)
-        assert kv.allocator.free == kv.num_pages and loop.fatal is None and eng._pf is None
+        assert kv.allocator.free + eng.prefix_pages == kv.num_pages and loop.fatal is None and eng._pf is None
         again = GenRequest(list(range(1, 30)), max_tokens=4, temperature=0.0, ignore_eos=True)
         eng.submit(again)
         loop.notify()
         assert again.event.wait(60) and again.error is None and len(again.output) == 4
-        assert kv.allocator.free == kv.num_pages
+        assert kv.allocator.free + eng.prefix_pages == kv.num_pages
     finally:
         loop.stop()
         loop.join(10)

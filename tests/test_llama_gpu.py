@@ -54,7 +54,7 @@ def test_graph_decode_equals_eager_decode():
                 for n, t, s in [(5, 0.0, 0), (300, 0.7, 1), (17, 0.3, 2)]]
         eng.generate(reqs)
         outs.append([r.output for r in reqs])
-        assert kv.allocator.free == kv.num_pages
+        assert kv.allocator.free + eng.prefix_pages == kv.num_pages
     assert outs[0] == outs[1]
 
 
@@ -182,7 +182,7 @@ def test_pipelined_windows_eos_and_arrivals():
             eng.submit(r)
         while any(not r.done for r in first + late):
             eng.step()
-        assert kv.allocator.free == kv.num_pages
+        assert kv.allocator.free + eng.prefix_pages == kv.num_pages
         return [r.output for r in first + late]
 
     base = run(False, None)
