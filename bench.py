@@ -59,6 +59,9 @@ def parse_args():
     ap.add_argument("--serial-waves", action="store_true",
                     help="wait for every sink write of a wave before writing the next one")
     ap.add_argument("--kv-gb", type=float, default=None, help="KV-cache budget (default 96 GB on GPU, 1 GB on CPU)")
+    ap.add_argument("--page-size", type=int, default=64, help="KV page size in tokens (engine.page_size)")
+    ap.add_argument("--no-prefix-sharing", action="store_true",
+                    help="prefill every prompt whole (engine.prefix_sharing off: no shared prompt-prefix pages)")
     ap.add_argument("--kv-dtype", choices=["auto", "fp8"], default="auto",
                     help="fp8: e4m3fn KV cache (reduced precision: not the headline configuration)")
     ap.add_argument("--engine-procs", type=int, default=1,
@@ -222,7 +225,8 @@ def main() -> int:
             "engine.max_context": a.prompt_tokens + a.max_tokens + 64, "engine.max_prompt_tokens": a.prompt_tokens,
             "engine.kv_cache_gb": kv, "engine.kv_dtype": a.kv_dtype, "engine.use_graphs": not a.no_graphs,
             "engine.ignore_eos": True,
-            "engine.multi_step": a.multi_step,
+            "engine.multi_step": a.multi_step, "engine.page_size": a.page_size,
+            "engine.prefix_sharing": not a.no_prefix_sharing,
             "engine.seed": 0, "health.enabled": False, "operator.workers": 2 * a.batch + 16, "operator.io_workers": 16,
             "operator.sink_concurrency": a.sink_concurrency,
             "patterns.cache_dir": f"/tmp/oamd-bench-{os.getpid()}", "services.match_max_batch": 64,
@@ -595,6 +599,7 @@ def main() -> int:
                    "mode": a.mode, "hipgraph": stats1["use_graphs"], "engine_procs_per_gpu": procs,
                    "operator_shards_per_gpu": a.shards,
                    "kv_cache_dtype": "fp8_e4m3fn" if a.kv_dtype == "fp8" else "bf16",
+                   "kv_page_tokens": a.page_size, "shared_prompt_prefix": not a.no_prefix_sharing,
                    "apiserver": ("one REST API server process, rank r = operator shard r (run --shard-per-gpu)"
                                  if rest else "in-process FakeKube per rank"),
                    "waves": "serial" if (a.serial_waves or a.mode != "pipeline") else "pipelined"},

@@ -673,10 +673,11 @@ class LLMEngine:
                 if r.cancelled:
                     self.waiting.popleft()
                     continue
-                if out and toks + len(r.prompt) > cap:
-                    break
                 shared = (pf is not None and len(r.prompt) > pf.n and r.prompt[0] == pf.tokens[0]
                           and tuple(r.prompt[:pf.n]) == pf.tokens)
+                own = len(r.prompt) - (pf.n if shared else 0)   # tokens this batch prefills for r
+                if out and toks + own > cap:
+                    break
                 need = self.kv.pages_needed(len(r.prompt) + r.max_tokens) - (len(pf.pages) if shared else 0)
                 if need > self.kv.allocator.free:
                     if not rows and not out:
@@ -698,7 +699,7 @@ class LLMEngine:
                 self.waiting.popleft()
                 out.append(r)
                 self._prefilling = (self._pf.batch if self._pf is not None else []) + out
-                toks += len(r.prompt)
+                toks += own
         return out
 
     def _prefill(self, batch: list[GenRequest]) -> _PendingPrefill:
