@@ -444,7 +444,7 @@ void attn_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tenso
 }
 
 // pk / pv / seq_pfx: a shared prompt prefix (kernels.h attn_prefill, variant 3): seq_pfx[s] prefix
-// keys (a multiple of 64, at most pk.size(0)) precede sequence s's own keys.
+// keys (at most pk.size(0)) precede sequence s's own keys.
 void attn_prefill(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor& o,
                   const at::Tensor& cu_seqlens, const at::Tensor& work_seq, const at::Tensor& work_q0,
                   double scale, int64_t variant, const c10::optional<at::Tensor>& pk,

@@ -401,9 +401,10 @@ __device__ __forceinline__ s16x4 ds_read_tr16(const char* p) {
 }
 
 // Shared prompt prefix (seq_pfx != nullptr): sequence seq's keys are seq_pfx[seq] prefix
-// keys (a multiple of 64, rows of pk / pv [prefix, Hkv, D], the cached K/V of a prompt
-// prefix many requests share) followed by its own slen keys; its query rows are its own
-// tokens, at positions seq_pfx[seq] + row. Prefix keys are visible to every row (no mask).
+// keys (rows of pk / pv [prefix, Hkv, D], the cached K/V of a prompt prefix many requests
+// share) followed by its own slen keys; its query rows are its own tokens, at positions
+// seq_pfx[seq] + row. Prefix keys are visible to every row; a last, partial prefix tile is
+// masked past the prefix length.
 template <int G>
 __global__ void __launch_bounds__(512) attn_prefill_mfma32_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
@@ -443,7 +444,8 @@ __global__ void __launch_bounds__(512) attn_prefill_mfma32_kernel(
   float mrow = -INFINITY, lpart = 0.f;
 
   const int kend = min(slen, q0 + BQ);
-  const int npt = seq_pfx != nullptr ? seq_pfx[seq] / BK : 0;   // shared-prefix key tiles first
+  const int pl = seq_pfx != nullptr ? seq_pfx[seq] : 0;   // shared-prefix keys first
+  const int npt = (pl + BK - 1) / BK;
   const int ntiles = npt + (kend + BK - 1) / BK;
   const bool active = wave_used && rbase < slen;
   const int wend = min(slen, rbase + 32);  // own keys this wave can see: < wend
@@ -461,9 +463,11 @@ __global__ void __launch_bounds__(512) attn_prefill_mfma32_kernel(
       const int key = c >> 4, ch = c & 15;
       kr[r] = vr[r] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
       if (kt < npt) {
-        const int64_t off = ((int64_t)(kt * BK + key) * Hkv + kvh) * D + ch * 8;
-        kr[r] = *reinterpret_cast<const u16x8*>(pk + off);
-        vr[r] = *reinterpret_cast<const u16x8*>(pv + off);
+        if (kt * BK + key < pl) {
+          const int64_t off = ((int64_t)(kt * BK + key) * Hkv + kvh) * D + ch * 8;
+          kr[r] = *reinterpret_cast<const u16x8*>(pk + off);
+          vr[r] = *reinterpret_cast<const u16x8*>(pv + off);
+        }
       } else if ((kt - npt) * BK + key < slen) {
         const int64_t off = ((int64_t)(s0 + (kt - npt) * BK + key) * Hkv + kvh) * D + ch * 8;
         kr[r] = *reinterpret_cast<const u16x8*>(k + off);
@@ -504,7 +508,9 @@ __global__ void __launch_bounds__(512) attn_prefill_mfma32_kernel(
       }
     }
     // ---- online softmax: register i of block b is key kb + 32b + (i&3) + 8(i>>2) + 4h ----
-    const bool mask = kb >= 0 && ((kb + BK > rbase + 1) || (kb + BK > slen));
+    const bool ptile = kb < 0;
+    const int pend = pl - kt * BK;   // prefix tile: its keys below pend are prefix keys
+    const bool mask = ptile ? (pend < BK) : ((kb + BK > rbase + 1) || (kb + BK > slen));
     float mx = -INFINITY;
 #pragma unroll
     for (int b = 0; b < 2; ++b)
@@ -512,8 +518,8 @@ __global__ void __launch_bounds__(512) attn_prefill_mfma32_kernel(
       for (int i = 0; i < 16; ++i) {
         float sv = sacc[b][i] * scale_log2;
         if (mask) {
-          const int key = kb + 32 * b + (i & 3) + 8 * (i >> 2) + 4 * h;
-          if (key > qrow || key >= slen) sv = -INFINITY;
+          const int j = 32 * b + (i & 3) + 8 * (i >> 2) + 4 * h;   // key within the tile
+          if (ptile ? (j >= pend) : (kb + j > qrow || kb + j >= slen)) sv = -INFINITY;
         }
         sacc[b][i] = sv;
         mx = fmaxf(mx, sv);

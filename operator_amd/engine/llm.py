@@ -367,9 +367,10 @@ class _PendingPrefill:
 
 
 class LLMEngine:
-    # shared prompt prefixes: at most this many whole pages, built once a page-aligned
-    # prefix has been seen at the head of this many of the last PREFIX_WINDOW prompts
-    PREFIX_MAX_PAGES = 4
+    # shared prompt prefixes: whole pages, at most PREFIX_MAX_TOKENS tokens, built once a
+    # page-aligned prefix has been seen at the head of PREFIX_MIN_SEEN of the last
+    # PREFIX_WINDOW prompts
+    PREFIX_MAX_TOKENS = 256
     PREFIX_MIN_SEEN = 2
     PREFIX_WINDOW = 64
 
@@ -444,7 +445,7 @@ class LLMEngine:
         self._pfx_last: list = []   # the page-aligned prefixes of the last admitted prompt
         self._pk = self._pv = None
         if self.prefix_sharing:
-            n = self.PREFIX_MAX_PAGES * kv.page_size
+            n = max(kv.page_size, self.PREFIX_MAX_TOKENS // kv.page_size * kv.page_size)
             shape = (model.cfg.layers, n, model.hkv, model.cfg.head_dim)
             self._pk = torch.zeros(shape, dtype=torch.bfloat16, device=self.device)
             self._pv = torch.zeros(shape, dtype=torch.bfloat16, device=self.device)
@@ -517,7 +518,7 @@ class LLMEngine:
         """Page-aligned prompt prefixes a request could share (longest last), each leaving
         at least one token of its own to prefill (its logits sample the first output)."""
         P = self.kv.page_size
-        k = min(self.PREFIX_MAX_PAGES, (len(prompt) - 1) // P)
+        k = min(self._pk.shape[1] // P, (len(prompt) - 1) // P)
         return [tuple(prompt[:j * P]) for j in range(1, k + 1)]
 
     def _note_prefix(self, prompt: list[int]) -> None:
@@ -525,7 +526,7 @@ class LLMEngine:
         for key in self._pfx_last:
             self._pfx_seen.append(key)
             self._pfx_count[key] = self._pfx_count.get(key, 0) + 1
-        while len(self._pfx_seen) > self.PREFIX_WINDOW * self.PREFIX_MAX_PAGES:
+        while len(self._pfx_seen) > self.PREFIX_WINDOW * (self._pk.shape[1] // self.kv.page_size):
             old = self._pfx_seen.popleft()
             c = self._pfx_count[old] - 1
             if c:

@@ -211,7 +211,7 @@ def attn_prefill(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, seq_lens: li
 
     ``prefix`` = (pk, pv, seq_pfx, pfx_lens): a shared prompt prefix (LLMEngine prefix
     sharing) whose cached K/V rows pk / pv [P, Hkv, D] come before sequence s's own keys
-    for its first pfx_lens[s] keys (0 or a multiple of 64, <= P); the own query rows sit at
+    for its first pfx_lens[s] keys (<= P); the own query rows sit at
     positions pfx_lens[s] + row and see every prefix key. seq_pfx: the same lengths as an
     int32 device tensor (GPU), pfx_lens: as a host list (CPU reference; may be None on
     the GPU)."""

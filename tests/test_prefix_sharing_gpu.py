@@ -17,11 +17,12 @@ pytestmark = pytest.mark.gpu
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (28, 4)])
 def test_prefill_attention_with_prefix_matches_fp32(Hq, Hkv):
     """attn_prefill variant 3 with pk / pv / seq_pfx == fp32 attention over [prefix ++ own]
-    keys (prefix 0, 64 or 192 keys per sequence; own lengths around the 32-row blocks)."""
+    keys (prefix 0 - 192 keys per sequence, partial last prefix tiles included; own
+    lengths around the 32-row blocks)."""
     torch.manual_seed(3)
     D, P = 128, 256
-    own = [1, 33, 64, 200, 97, 5]
-    pl = [64, 0, 192, 64, 128, 0]
+    own = [1, 33, 64, 200, 97, 5, 40]
+    pl = [64, 0, 192, 96, 128, 0, 112]   # whole 64-key tiles and partial ones (page sizes 32, 16)
     T = sum(own)
     r = lambda *s: (torch.randn(*s, device="cuda") * 0.5).to(torch.bfloat16)  # noqa: E731
     q, k, v = r(T, Hq, D), r(T, Hkv, D), r(T, Hkv, D)
