@@ -59,7 +59,7 @@ def parse_args():
     ap.add_argument("--serial-waves", action="store_true",
                     help="wait for every sink write of a wave before writing the next one")
     ap.add_argument("--kv-gb", type=float, default=None, help="KV-cache budget (default 96 GB on GPU, 1 GB on CPU)")
-    ap.add_argument("--page-size", type=int, default=64, help="KV page size in tokens (engine.page_size)")
+    ap.add_argument("--page-size", type=int, default=16, help="KV page size in tokens (engine.page_size)")
     ap.add_argument("--no-prefix-sharing", action="store_true",
                     help="prefill every prompt whole (engine.prefix_sharing off: no shared prompt-prefix pages)")
     ap.add_argument("--kv-dtype", choices=["auto", "fp8"], default="auto",

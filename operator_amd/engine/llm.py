@@ -395,6 +395,9 @@ class LLMEngine:
         self.max_prefill_tokens = max_prefill_tokens
         self.max_context = min(max_context or model.cfg.max_position, model.cfg.max_position)
         self.max_pages = kv.pages_needed(self.max_context)
+        if model.device.type == "cuda" and self.max_pages > 1024:   # attn_decode.hip kMaxPagesLds
+            raise ValueError(f"max_context {self.max_context} needs {self.max_pages} KV pages of "
+                             f"{kv.page_size} tokens per sequence (at most 1024): raise engine.page_size")
         self.hkv = model.hkv
         self.use_graphs = use_graphs and self.device.type == "cuda"
         self.multi_step = max(1, multi_step)
@@ -586,11 +589,17 @@ class LLMEngine:
         return not self.running and self._inflight is None and self._pf is None
 
     def queued_prompt_tokens(self) -> int:
-        """Prompt tokens waiting for admission (stops counting at one full prefill batch)."""
+        """Prompt tokens waiting for admission that a prefill would compute (a prompt that
+        starts with the shared prefix counts its own tokens only; stops counting at one
+        full prefill batch)."""
         n = 0
+        pf = self._pfx
         with self._lock:
             for r in self.waiting:
                 n += len(r.prompt)
+                if pf is not None and len(r.prompt) > pf.n and r.prompt[0] == pf.tokens[0] \
+                        and tuple(r.prompt[:pf.n]) == pf.tokens:
+                    n -= pf.n
                 if n >= self.max_prefill_tokens:
                     break
         return n

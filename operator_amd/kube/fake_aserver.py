@@ -106,9 +106,11 @@ class AsyncFakeKubeServer:
                 except Exception as e:  # noqa: BLE001 - a malformed request must not end the server
                     w = None
                     sink.json(500, {"kind": "Status", "code": 500, "message": f"{type(e).__name__}: {e}"})
-                if w is not None:   # a watch owns the connection until it ends
+                if w is not None:   # a watch owns the connection until it ends; then keep-alive
+                    # goes on (a client pool reuses the connection: closing it here would
+                    # reset the next request sent on it)
                     await self._watch(writer, *w)
-                    return
+                    continue
                 writer.write(sink.out)
                 if writer.transport.get_write_buffer_size() > (1 << 20):
                     await writer.drain()
