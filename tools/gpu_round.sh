@@ -8,6 +8,6 @@ timeout -k 10 400 python -u bench.py "$@" > gpurun_out/bench.json 2> gpurun_out/
 cat gpurun_out/bench.json
 PMC="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TA_BUSY_avr GRBM_GUI_ACTIVE" bash tools/pmc_gemm_tile.sh "1 2 blas"
 cat gpurun_out/pmc_summary.txt
-timeout -k 10 300 python -u tools/gemm_tile_variants.py --variants ${GTV:-1,4,2} > gpurun_out/gtv.jsonl
-timeout -k 10 300 python -u tools/gemm_tile_variants.py --variants ${GTV:-1,4,2} --m 16384 --n 6144 --k 4096 >> gpurun_out/gtv.jsonl
+timeout -k 10 300 python -u tools/gemm_tile_variants.py --variants ${GTV:-1,2,3} > gpurun_out/gtv.jsonl
+timeout -k 10 300 python -u tools/gemm_tile_variants.py --variants ${GTV:-1,2,3} --m 16384 --n 6144 --k 4096 >> gpurun_out/gtv.jsonl
 cat gpurun_out/gtv.jsonl
