@@ -320,7 +320,10 @@ __device__ __forceinline__ void mfma_tied(f32x4& acc, const u16x8& a, const u16x
 // source and the read (conflict-free ds_read_b128). The DMAs carry the sc1
 // cache policy (AUX 16: 1-3 % over the default on down / qkv; nt costs 4-20 %,
 // profiles/gemm_tile_variants_r4_c.jsonl).
-template <int EPI, int AUX = 16>
+// COLS: the MFMA groups run over W fragments (A operand fixed for 8 MFMAs, as hipBLASLt's
+// MT256x256x64 loop does) instead of X fragments; every group then needs all 8 X fragments,
+// so the X pieces / fragments of the next tile come first (phases 2-3) and W last.
+template <int EPI, int AUX = 16, bool COLS = false>
 __global__ void __launch_bounds__(256) gemm_tile256_h4_kernel(const bf16_t* __restrict__ X,
                                                               const bf16_t* __restrict__ W, bf16_t* __restrict__ Y,
                                                               const bf16_t* __restrict__ bias, int M, int N, int K,
@@ -392,7 +395,8 @@ __global__ void __launch_bounds__(256) gemm_tile256_h4_kernel(const bf16_t* __re
   auto row = [&](const u16x8 (&xf)[8], const u16x8 (&wf)[8], int i, auto op) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      mfma_tied(acc[i][j], wf[j], xf[i]);
+      if constexpr (COLS) mfma_tied(acc[j][i], wf[i], xf[j]);
+      else mfma_tied(acc[i][j], wf[j], xf[i]);
       if (j & 1) {
         __builtin_amdgcn_sched_barrier(0);
         op(j >> 1);
@@ -409,11 +413,17 @@ __global__ void __launch_bounds__(256) gemm_tile256_h4_kernel(const bf16_t* __re
 
   // prologue: tiles 0 and 1 (buffers 0, 1); tile 0 landed; k-half 0 of tile 0 into A
 #pragma unroll
-  for (int tt = 0; tt < 2; ++tt) {   // per tile in the order the loop issues them: W, then X
+  for (int tt = 0; tt < 2; ++tt) {   // per tile in the order the loop issues them
 #pragma unroll
-    for (int q = 0; q < 8; ++q) dma_w(tt, tt, q);
+    for (int q = 0; q < 8; ++q) {
+      if constexpr (COLS) dma_x(tt, tt, q);
+      else dma_w(tt, tt, q);
+    }
 #pragma unroll
-    for (int q = 0; q < 8; ++q) dma_x(tt, tt, q);
+    for (int q = 0; q < 8; ++q) {
+      if constexpr (COLS) dma_w(tt, tt, q);
+      else dma_x(tt, tt, q);
+    }
   }
   vm_wait<16>();
   seg_barrier();
@@ -439,7 +449,10 @@ __global__ void __launch_bounds__(256) gemm_tile256_h4_kernel(const bf16_t* __re
 #pragma unroll
     for (int i = 4; i < 8; ++i)
       row(xa, wa, i, [&](int k) {
-        if (!(k & 1)) dma_w(t + 2, b, 2 * (i - 4) + (k >> 1));
+        if (!(k & 1)) {
+          if constexpr (COLS) dma_x(t + 2, b, 2 * (i - 4) + (k >> 1));
+          else dma_w(t + 2, b, 2 * (i - 4) + (k >> 1));
+        }
       });
     vm_wait<16>();   // tile t+1's W pieces (this wave's)
     seg_barrier();   // ... every wave's
@@ -447,8 +460,13 @@ __global__ void __launch_bounds__(256) gemm_tile256_h4_kernel(const bf16_t* __re
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       row(xb, wb, i, [&](int k) {
-        if (!(k & 1)) dma_x(t + 2, b, 2 * i + (k >> 1));
-        else rdw(nb, c0, wa, 2 * i + (k >> 1));
+        if constexpr (COLS) {
+          if (!(k & 1)) dma_w(t + 2, b, 2 * i + (k >> 1));
+          else rdx(nb, c0, xa, 2 * i + (k >> 1));
+        } else {
+          if (!(k & 1)) dma_x(t + 2, b, 2 * i + (k >> 1));
+          else rdw(nb, c0, wa, 2 * i + (k >> 1));
+        }
       });
     vm_wait<16>();   // tile t+1's X pieces
     seg_barrier();
@@ -456,7 +474,10 @@ __global__ void __launch_bounds__(256) gemm_tile256_h4_kernel(const bf16_t* __re
 #pragma unroll
     for (int i = 4; i < 8; ++i)
       row(xb, wb, i, [&](int k) {
-        if (!(k & 1)) rdx(nb, c0, xa, 2 * (i - 4) + (k >> 1));
+        if (!(k & 1)) {
+          if constexpr (COLS) rdw(nb, c0, wa, 2 * (i - 4) + (k >> 1));
+          else rdx(nb, c0, xa, 2 * (i - 4) + (k >> 1));
+        }
       });
   }
   vm_wait<0>();   // the tail's clamped re-loads land before the workgroup's LDS is released
@@ -557,6 +578,10 @@ int gemm_tile(const bf16_t* X, const bf16_t* W, bf16_t* Y, const bf16_t* bias, i
     if (silu_gu) gemm_tile256_h4_kernel<kEpiSilu><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
     else if (bias) gemm_tile256_h4_kernel<kEpiBias><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
     else gemm_tile256_h4_kernel<kEpiStore><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+  } else if (variant == 4 && off32) {   // h4 with W-fragment MFMA groups (timing)
+    if (silu_gu) gemm_tile256_h4_kernel<kEpiSilu, 16, true><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+    else if (bias) gemm_tile256_h4_kernel<kEpiBias, 16, true><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+    else gemm_tile256_h4_kernel<kEpiStore, 16, true><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
   } else if (variant == 2 || (variant == 0 && M > 256)) {
     // 8-wave ping-pong, two barrier segments per K-tile (the round-3 default; 2-8 % behind
     // variant 1 on the prefill shapes, profiles/gemm_tile_h4_vs_ph2_m32k.jsonl); also the
