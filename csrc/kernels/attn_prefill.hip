@@ -405,7 +405,11 @@ __device__ __forceinline__ s16x4 ds_read_tr16(const char* p) {
 // share) followed by its own slen keys; its query rows are its own tokens, at positions
 // seq_pfx[seq] + row. Prefix keys are visible to every row; a last, partial prefix tile is
 // masked past the prefix length.
-template <int G>
+// OPT bit 0: the next tile's K/V loads are issued after this tile's S MFMAs (they are in
+// flight during softmax + P.V instead of holding registers across the S MFMAs); bit 1:
+// deferred rescale — a row keeps its running max until a tile raises it by more than 8
+// (log2 units, so P <= 256 in fp32 / bf16), skipping the O / l rescale otherwise.
+template <int G, int OPT = 0>
 __global__ void __launch_bounds__(512) attn_prefill_mfma32_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     bf16_t* __restrict__ o, const int* __restrict__ cu_seqlens, const int* __restrict__ work_seq,
@@ -491,8 +495,11 @@ __global__ void __launch_bounds__(512) attn_prefill_mfma32_kernel(
     __syncthreads();  // previous tile fully consumed
     store_tile();
     __syncthreads();
-    if (kt + 1 < ntiles) load_tile(kt + 1);   // in flight during this tile's MFMAs
-    if (!active || kb >= wend) continue;      // wave-uniform: no visible key for this wave
+    if (!(OPT & 1) && kt + 1 < ntiles) load_tile(kt + 1);   // in flight during this tile's MFMAs
+    if (!active || kb >= wend) {   // wave-uniform: no visible key for this wave
+      if ((OPT & 1) && kt + 1 < ntiles) load_tile(kt + 1);
+      continue;
+    }
 
     // ---- S^T = K Q^T (two 32-key blocks) ----
     f32x16 sacc[2];
@@ -507,6 +514,7 @@ __global__ void __launch_bounds__(512) attn_prefill_mfma32_kernel(
         sacc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(ka), as_bf8(qb[s]), sacc[b], 0, 0, 0);
       }
     }
+    if ((OPT & 1) && kt + 1 < ntiles) load_tile(kt + 1);   // in flight during softmax + P.V
     // ---- online softmax: register i of block b is key kb + 32b + (i&3) + 8(i>>2) + 4h ----
     const bool ptile = kb < 0;
     const int pend = pl - kt * BK;   // prefix tile: its keys below pend are prefix keys
@@ -525,9 +533,14 @@ __global__ void __launch_bounds__(512) attn_prefill_mfma32_kernel(
         mx = fmaxf(mx, sv);
       }
     mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
-    const float mnew = fmaxf(mrow, mx);
+    float mnew = fmaxf(mrow, mx);
+    bool rescale = true;
+    if constexpr ((OPT & 2) != 0) {
+      rescale = mrow == -INFINITY || mnew > mrow + 8.f;
+      if (!rescale) mnew = mrow;
+    }
     const float msafe = (mnew == -INFINITY) ? 0.f : mnew;
-    const float alpha = exp2f(mrow - msafe);
+    const float alpha = rescale ? exp2f(mrow - msafe) : 1.f;
     mrow = mnew;
     float rs = 0.f;
     u16x8 pb[2][2];
@@ -544,10 +557,12 @@ __global__ void __launch_bounds__(512) attn_prefill_mfma32_kernel(
         pb[b][s] = __builtin_bit_cast(u16x8, __builtin_convertvector(p, bf16x8_t));
       }
     lpart = lpart * alpha + rs;
+    if (rescale) {
 #pragma unroll
-    for (int dd = 0; dd < 4; ++dd)
+      for (int dd = 0; dd < 4; ++dd)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) oacc[dd][i] *= alpha;
+        for (int i = 0; i < 16; ++i) oacc[dd][i] *= alpha;
+    }
 
     // ---- O^T += V^T P^T: B element j of half h is key 32b + 16s + 8(j>>2) + 4h + (j&3) ----
 #pragma unroll
@@ -587,6 +602,7 @@ __global__ void __launch_bounds__(512) attn_prefill_mfma32_kernel(
 // 2 = GQA-grouped 16-row waves (G = Hq / Hkv in {1, 2, 4, 8}), 3 = GQA-grouped
 // swapped 32x32 (32-row waves, any G <= 8: 8 / G row blocks per item); else -1.
 int attn_prefill_block_q(int Hq, int Hkv, int variant) {
+  if (variant == 4 || variant == 5) variant = 3;   // v3 schedule options (attn_prefill)
   if (variant == 1) return 64;
   if (Hkv <= 0 || Hq % Hkv != 0) return -1;
   const int G = Hq / Hkv;
@@ -603,6 +619,8 @@ int attn_prefill(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, c
   if (head_dim != 128) return -1;
   if (Hq % Hkv != 0) return -3;
   if (attn_prefill_block_q(Hq, Hkv, variant) < 0) return -4;
+  const int opt = variant == 4 ? 1 : variant == 5 ? 3 : 0;   // 4, 5: v3 with load / rescale options
+  if (variant >= 4) variant = 3;
   if (seq_pfx != nullptr && (variant != 3 || pk == nullptr || pv == nullptr)) return -5;   // v3 only
   const float sl2 = scale * 1.4426950408889634f;
   const int G = Hq / Hkv;
@@ -612,8 +630,18 @@ int attn_prefill(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, c
   } else {
     dim3 grid(num_work, Hkv);
 #define OAMD_PF(KERN, GG) KERN<GG><<<grid, 512, 0, stream>>>(q, k, v, o, cu_seqlens, work_seq, work_q0, Hq, Hkv, sl2)
-#define OAMD_PF3(GG) \
-  attn_prefill_mfma32_kernel<GG><<<grid, 512, 0, stream>>>(q, k, v, o, cu_seqlens, work_seq, work_q0, Hq, Hkv, sl2, pk, pv, seq_pfx)
+#define OAMD_PF3(GG)                                                                                         \
+  do {                                                                                                       \
+    if (opt == 1)                                                                                            \
+      attn_prefill_mfma32_kernel<GG, 1><<<grid, 512, 0, stream>>>(q, k, v, o, cu_seqlens, work_seq, work_q0, \
+                                                                   Hq, Hkv, sl2, pk, pv, seq_pfx);           \
+    else if (opt == 3)                                                                                       \
+      attn_prefill_mfma32_kernel<GG, 3><<<grid, 512, 0, stream>>>(q, k, v, o, cu_seqlens, work_seq, work_q0, \
+                                                                   Hq, Hkv, sl2, pk, pv, seq_pfx);           \
+    else                                                                                                     \
+      attn_prefill_mfma32_kernel<GG, 0><<<grid, 512, 0, stream>>>(q, k, v, o, cu_seqlens, work_seq, work_q0, \
+                                                                   Hq, Hkv, sl2, pk, pv, seq_pfx);           \
+  } while (0)
 #define OAMD_PF_G(KERN)            \
   switch (G) {                     \
     case 1: OAMD_PF(KERN, 1); break; \

@@ -74,7 +74,7 @@ def test_rope_kv_and_cache(Hq, Hkv):
 
 @pytest.mark.parametrize("lens", [[1], [17, 64, 130], [300, 5, 64]])
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 8), (16, 2), (8, 4), (64, 8), (24, 8), (28, 4), (10, 2), (12, 2)])
-@pytest.mark.parametrize("variant", [3, 2, 1])
+@pytest.mark.parametrize("variant", [3, 2, 1, 4, 5])
 def test_attn_prefill(lens, Hq, Hkv, variant):
     if variant == 2 and Hq // Hkv not in (1, 2, 4, 8):
         pytest.skip("v2 takes GQA groups 1, 2, 4, 8 only")
@@ -92,13 +92,20 @@ def test_attn_prefill(lens, Hq, Hkv, variant):
     torch.testing.assert_close(o.cpu().float(), o_r.float(), atol=2e-2, rtol=3e-2)
 
 
-def test_attn_prefill_large_scores():
-    """Spike one key so the running max jumps mid-sequence (forces the rescale path)."""
+@pytest.mark.parametrize("variant", [None, 5])
+def test_attn_prefill_large_scores(variant):
+    """Spike one key so the running max jumps mid-sequence (forces the rescale path; variant
+    5 defers a rescale until the max rises by more than 2^8)."""
     torch.manual_seed(3)
     lens, Hq, Hkv, D = [256], 8, 8, 128
     q, k, v = _rand(256, Hq, D), _rand(256, Hkv, D), _rand(256, Hkv, D)
     k[200] = (q[220].float() * 6).to(torch.bfloat16)[: Hkv]
-    o = ops.attn_prefill(q, k, v, lens, 1 / math.sqrt(D))
+    work = None
+    if variant is not None:
+        ws, wq = ops.prefill_work_list(lens, ops.prefill_block_q(Hq, Hkv, variant))
+        it = lambda x: torch.tensor(x, dtype=torch.int32, device=DEV)  # noqa: E731
+        work = (it([0, 256]), it(ws), it(wq), variant)
+    o = ops.attn_prefill(q, k, v, lens, 1 / math.sqrt(D), work=work)
     o_r = ref.attn_prefill(q.cpu(), k.cpu(), v.cpu(), [0, 256], 1 / math.sqrt(D))
     torch.testing.assert_close(o.cpu().float(), o_r.float(), atol=3e-2, rtol=3e-2)
 

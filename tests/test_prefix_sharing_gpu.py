@@ -14,9 +14,10 @@ from operator_amd.ops import reference
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("var", [3, 4, 5])
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (28, 4)])
-def test_prefill_attention_with_prefix_matches_fp32(Hq, Hkv):
-    """attn_prefill variant 3 with pk / pv / seq_pfx == fp32 attention over [prefix ++ own]
+def test_prefill_attention_with_prefix_matches_fp32(Hq, Hkv, var):
+    """attn_prefill variant 3 (and its schedule options 4, 5) with pk / pv / seq_pfx == fp32 attention over [prefix ++ own]
     keys (prefix 0 - 192 keys per sequence, partial last prefix tiles included; own
     lengths around the 32-row blocks)."""
     torch.manual_seed(3)
@@ -30,8 +31,6 @@ def test_prefill_attention_with_prefix_matches_fp32(Hq, Hkv):
     cu = [0]
     for n in own:
         cu.append(cu[-1] + n)
-    var = ops.prefill_variant(Hq, Hkv)
-    assert var == 3
     ws, wq = ops.prefill_work_list(own, ops.prefill_block_q(Hq, Hkv, var))
     i32 = lambda x: torch.tensor(x, dtype=torch.int32, device="cuda")  # noqa: E731
     work = (i32(cu), i32(ws), i32(wq), var)

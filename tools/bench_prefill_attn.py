@@ -24,6 +24,7 @@ ap.add_argument("--hq", type=int, default=32)
 ap.add_argument("--hkv", type=int, default=8)
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--out", default=None)
+ap.add_argument("--variants", default="1,2,3", help="attn_prefill variants (4, 5: v3 schedule options)")
 a = ap.parse_args()
 
 dev = "cuda:0"
@@ -63,7 +64,7 @@ for shape in a.shapes.split(","):
     it = lambda x: torch.tensor(x, dtype=torch.int32, device=dev)  # noqa: E731
     o = torch.empty_like(q)
     outs = {}
-    for var in (1, 2, 3):
+    for var in tuple(int(x) for x in a.variants.split(",")):
         ws, wq = ops.prefill_work_list(lens, ops.prefill_block_q(a.hq, a.hkv, var))
         work = (it(cu), it(ws), it(wq), var)
         ms = timed(lambda: ops.attn_prefill(q, k, v, lens, scale, out=o, work=work), a.iters)
