@@ -80,7 +80,7 @@ def main():
         t1, t2 = 0.0, min(warm)
         stage = {"analyze_" + k: round(v, 4) for k, v in eng.last_timing.items()}
         lz, mat = [], []
-        for _ in range(3):   # lazy: compact per-doc events only; then materialize every result
+        for _ in range(3):   # lazy: events + context windows; then materialize every result object
             u1 = time.perf_counter()
             lres = eng.analyze(docs, lazy=True)
             u2 = time.perf_counter()
