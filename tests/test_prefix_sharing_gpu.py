@@ -14,7 +14,7 @@ from operator_amd.ops import reference
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("var", [3, 4, 5])
+@pytest.mark.parametrize("var", [3, 4, 5, 6, 7])
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (28, 4)])
 def test_prefill_attention_with_prefix_matches_fp32(Hq, Hkv, var):
     """attn_prefill variant 3 (and its schedule options 4, 5) with pk / pv / seq_pfx == fp32 attention over [prefix ++ own]
