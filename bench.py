@@ -74,6 +74,8 @@ def parse_args():
                          "others as child processes")
     ap.add_argument("--shard-index", type=int, default=None, help=argparse.SUPPRESS)  # internal: child shard
     ap.add_argument("--multi-step", type=int, default=8, help="decode steps per graph window (engine.multi_step)")
+    ap.add_argument("--admit-wait-ms", type=float, default=None,
+                    help="idle engine: gather arrivals this long before a partial prefill (engine.admit_wait_ms)")
     ap.add_argument("--sink-concurrency", type=int, default=16,
                     help="operator.sink_concurrency: analyses writing results at once (0 = unbounded); a bound "
                          "keeps a finished wave's 256 result writers from starving the next wave's ramp "
@@ -226,6 +228,7 @@ def main() -> int:
             "engine.kv_cache_gb": kv, "engine.kv_dtype": a.kv_dtype, "engine.use_graphs": not a.no_graphs,
             "engine.ignore_eos": True,
             "engine.multi_step": a.multi_step, "engine.page_size": a.page_size,
+            **({} if a.admit_wait_ms is None else {"engine.admit_wait_ms": a.admit_wait_ms}),
             "engine.prefix_sharing": not a.no_prefix_sharing,
             "engine.seed": 0, "health.enabled": False, "operator.workers": 2 * a.batch + 16, "operator.io_workers": 16,
             "operator.sink_concurrency": a.sink_concurrency,

@@ -4,8 +4,8 @@ hipGraph-captured decode steps.
 * Admission reserves the pages a request can ever need (prompt + max_tokens),
   so a running request is never preempted; with 288 GB of HBM per GPU the
   reservation costs nothing in practice (Llama-3-8B: ~1.5M tokens of KV).
-* Prefill runs eagerly over a packed multi-sequence batch (variable shapes,
-  GEMM-dominated, launch overhead negligible).
+* Prefill runs over a packed multi-sequence batch, replayed from a captured graph of
+  the smallest token bucket that holds it (``_PrefillGraph``; eager on the CPU).
 * Decode steps for a batch padded to a bucket size (1, 2, 4, ... max_batch)
   are captured once per bucket as a hipGraph (torch.cuda.CUDAGraph) and
   replayed: embedding -> 32 x (norm, QKV GEMM, rope+KV write, paged attention,
@@ -85,7 +85,7 @@ class EngineStats:
     graph_replays: int = 0
     prefill_graph_replays: int = 0
     prefill_padded_tokens: int = 0   # bucket padding computed by prefill-graph replays
-    prefill_eager: int = 0           # prefill batches no graph bucket fit (<= 15 % padding)
+    prefill_eager: int = 0           # prefill batches run eagerly (no graphs, or above every bucket)
     prefix_hits: int = 0             # requests whose prompt started with the shared prefix
     prefix_tokens: int = 0           # ... prompt tokens they did not prefill
     prefix_builds: int = 0           # shared prefixes computed
@@ -113,6 +113,22 @@ class _Window:
     event: object
 
 
+def _prefill_bucket_sizes(max_tokens: int) -> list[int]:
+    """Prefill graph buckets: every 512 tokens up to 4096, then steps of 1/4 of the
+    power of two below (5k, 6k, 7k, 8k, 10k, ...), capped at ``max_tokens`` (always a
+    bucket). A batch cut at bucket T (LLMEngine._prefill_cap) holds more than T minus
+    one request, so it replays a graph padded by at most ~20 %; with power-of-two
+    buckets and a 15 % padding rule, the batches cut at 2-4k tokens missed their bucket
+    and ran eagerly (57 of 231 batches in the round-4 20-wave driver-shaped run, each
+    ~400 launches under the operator threads' GIL contention)."""
+    out, t = set(), 512
+    while t < max_tokens:
+        out.add(t)
+        t += 512 if t < 4096 else (1 << (t.bit_length() - 1)) // 4
+    out.add(max_tokens)
+    return sorted(out)
+
+
 def _buckets(max_batch: int) -> list[int]:
     b, out = 1, []
     while b < max_batch:
@@ -134,29 +150,37 @@ class _BucketState:
     def __init__(self, eng: "LLMEngine", bp: int):
         dev = eng.device
         self.bp = bp
-        self.ids = torch.zeros(bp, dtype=torch.long, device=dev)
-        self.pos = torch.zeros(bp, dtype=torch.long, device=dev)
-        self.bt = torch.zeros(bp, eng.max_pages, dtype=torch.int32, device=dev)
-        self.ctx = torch.zeros(bp, dtype=torch.int32, device=dev)
-        self.temp = torch.zeros(bp, dtype=torch.float32, device=dev)
-        self.seeds = torch.zeros(bp, dtype=torch.long, device=dev)
+        # the per-row state ``load`` rewrites lives in one byte buffer (one H2D copy per
+        # batch-composition change instead of six)
+        mp = eng.max_pages
+        self._spec = (("ids", (bp,), torch.long), ("pos", (bp,), torch.long), ("seeds", (bp,), torch.long),
+                      ("ctx", (bp,), torch.int32), ("temp", (bp,), torch.float32), ("bt", (bp, mp), torch.int32))
+        self._nbytes = sum(int(np.prod(s)) * torch.empty((), dtype=dt).element_size() for _, s, dt in self._spec)
+        self._buf = torch.zeros(self._nbytes, dtype=torch.uint8, device=dev)
+        for n, t in self._views(self._buf).items():
+            setattr(self, n, t)
         self.hist = torch.zeros(bp, eng.multi_step, dtype=torch.long, device=dev)
         self.step = torch.zeros(1, dtype=torch.long, device=dev)
         self.slots = torch.zeros(bp, dtype=torch.long, device=dev)   # per step: cache slot of each row's token
         self.spos = torch.zeros(bp, dtype=torch.long, device=dev)    # per step: sampler stream position
 
+    def _views(self, buf: torch.Tensor) -> dict:
+        out, off = {}, 0
+        for n, shape, dt in self._spec:   # 8-byte fields first, then 4-byte: every view aligned
+            nb = int(np.prod(shape)) * torch.empty((), dtype=dt).element_size()
+            out[n] = buf[off:off + nb].view(dt).view(shape)
+            off += nb
+        return out
+
     def load(self, reqs: list[GenRequest], max_pages: int) -> None:
         """Write the per-row state of ``reqs`` (rows beyond are padding). Built in numpy
         (one pass over the rows, no per-element tensor indexing: ~0.3 ms instead of
         ~10 ms for 256 rows at every batch-composition change) and copied in once."""
-        bp = self.bp
         n = len(reqs)
-        ids = np.zeros(bp, dtype=np.int64)
-        pos = np.zeros(bp, dtype=np.int64)
-        ctx = np.zeros(bp, dtype=np.int32)
-        bt = np.zeros((bp, max_pages), dtype=np.int32)
-        temp = np.zeros(bp, dtype=np.float32)
-        seeds = np.zeros(bp, dtype=np.int64)
+        host = torch.zeros(self._nbytes, dtype=torch.uint8)
+        v = {k: t.numpy() for k, t in self._views(host).items()}
+        ids, pos, ctx, bt, temp, seeds = v["ids"], v["pos"], v["ctx"], v["bt"], v["temp"], v["seeds"]
+        assert bt.shape[1] == max_pages
         if n:
             lens = np.fromiter((r.length for r in reqs), dtype=np.int64, count=n)
             ids[:n] = np.fromiter((r.output[-1] for r in reqs), dtype=np.int64, count=n)
@@ -166,11 +190,8 @@ class _BucketState:
             seeds[:n] = np.fromiter((r.seed for r in reqs), dtype=np.int64, count=n)
             for i, r in enumerate(reqs):
                 bt[i, :len(r.pages)] = r.pages
-        nb = self.ids.is_cuda
-        for dst, src in ((self.ids, ids), (self.pos, pos), (self.ctx, ctx), (self.bt, bt), (self.temp, temp),
-                         (self.seeds, seeds)):
-            t = torch.from_numpy(src)
-            dst.copy_(t.pin_memory() if nb else t, non_blocking=nb)
+        nb = self._buf.is_cuda
+        self._buf.copy_(host.pin_memory() if nb else host, non_blocking=nb)
 
 
 @contextlib.contextmanager
@@ -271,21 +292,39 @@ class _PrefillGraph:
         self.eng, self.T, self.S, self.variant = eng, T, S, variant
         self.W = T // block_q + S               # work items: sum ceil(len / bq) <= T / bq + S
         i64, i32 = torch.long, torch.int32
-        self.dev = {n: torch.zeros(k, dtype=dt, device=dev) for n, k, dt in (
-            ("ids", T, i64), ("pos", T, i64), ("slots", T, i64), ("last", S, i64), ("seeds", S, i64),
-            ("spos", S, i64), ("cu", S + 1, i32), ("ws", self.W, i32), ("wq", self.W, i32),
-            ("temp", S, torch.float32), ("pfx", S, i32))}
+        # every input is a view into ONE byte buffer, so a launch is one H2D copy (the
+        # eleven separate copies it replaced each needed the GIL between them: with the
+        # operator's threads holding it at a wave start, up to ~1.7 ms of GPU idle each,
+        # profiles/bench_r4_flagship_idle.jsonl "copyBuffer -> copyBuffer")
+        spec = (("ids", T, i64), ("pos", T, i64), ("slots", T, i64), ("last", S, i64), ("seeds", S, i64),
+                ("spos", S, i64), ("cu", S + 1, i32), ("ws", self.W, i32), ("wq", self.W, i32),
+                ("temp", S, torch.float32), ("pfx", S, i32))
+        self._layout, off = [], 0
+        for n, k, dt in spec:
+            isz = torch.empty((), dtype=dt).element_size()
+            self._layout.append((n, off, k, dt))
+            off += (k * isz + 15) // 16 * 16
+        self._nbytes = off
+        self._dbuf = torch.zeros(off, dtype=torch.uint8, device=dev)
+        self.dev = self._views(self._dbuf)
         # two pinned input sets + sampled-token buffers, used alternately: a launch
         # returns without waiting for the GPU, so the engine can queue the next
         # prefill batch before reading this one's tokens (LLMEngine._prefill); a set is
         # rewritten only after the event of its previous launch (two launches ago)
-        self.hosts = [{n: torch.zeros_like(t, device="cpu").pin_memory() for n, t in self.dev.items()}
-                      for _ in range(2)]
+        self._hbufs = [torch.zeros(off, dtype=torch.uint8).pin_memory() for _ in range(2)]
+        self.hosts = [self._views(b) for b in self._hbufs]
         self.outs = [torch.zeros(S, dtype=i64).pin_memory() for _ in range(2)]
         self.events: list = [None, None]
         self._i = 0
         self.graph: torch.cuda.CUDAGraph | None = None
         self.tok: torch.Tensor | None = None
+
+    def _views(self, buf: torch.Tensor) -> dict:
+        out = {}
+        for n, off, k, dt in self._layout:
+            isz = torch.empty((), dtype=dt).element_size()
+            out[n] = buf[off:off + k * isz].view(dt)
+        return out
 
     def _run(self) -> None:
         e, d = self.eng, self.dev
@@ -326,8 +365,7 @@ class _PrefillGraph:
             v = h[name].numpy()
             v[:len(arr)] = arr
             v[len(arr):] = fill
-        for name in h:
-            self.dev[name].copy_(h[name], non_blocking=True)
+        self._dbuf.copy_(self._hbufs[i], non_blocking=True)
         _launch_graph(self.graph, 1, self.eng.device)
         out = self.outs[i]
         out[:b].copy_(self.tok[:b], non_blocking=True)
@@ -383,11 +421,10 @@ class LLMEngine:
         # requests. Not part of step() itself, which stays deterministic for TP.
         self.admit_wait_s = admit_wait_s
         # graph-captured prefill buckets (tokens): the largest is max_prefill_tokens; a
-        # batch runs in the smallest bucket >= its tokens when that pads it by <= 15 %,
-        # eagerly otherwise
+        # batch runs in the smallest bucket >= its tokens (_prefill_bucket_sizes: spaced
+        # so the padding stays below one typical request / 20 %)
         self.prefill_graphs = use_graphs and model.device.type == "cuda" and prefill_graphs
-        self.prefill_buckets = sorted({max_prefill_tokens} | {1024 << i for i in range(8)
-                                                              if (1024 << i) < max_prefill_tokens})
+        self.prefill_buckets = _prefill_bucket_sizes(max_prefill_tokens)
         self._prefill_g: dict[int, _PrefillGraph] = {}
         self._prefill_pool = None
         self.device = model.device
@@ -657,15 +694,23 @@ class LLMEngine:
     def _admittable(self) -> bool:
         return bool(self.waiting) and self._rows() < self.max_batch
 
+    # a queue that pads its graph bucket by at most this many tokens is prefilled whole;
+    # a larger pad (only above 4k tokens, where buckets are 1/4 octave apart) is cut at
+    # the bucket below and the rest follows in the next batch
+    PREFILL_MAX_PAD = 1024
+
     def _prefill_cap(self) -> int:
         """Token budget of the next prefill batch: a full batch (max_prefill_tokens)
-        when that many prompt tokens wait, else the largest graph bucket the queue
-        fills (>= 1024 tokens), so a partial batch replays a full bucket instead of
-        padding a larger one or running eagerly; the rest follows in the next batch."""
+        when that many prompt tokens wait; else everything queued when its graph bucket
+        pads it by <= PREFILL_MAX_PAD tokens, else the largest bucket the queue fills (a
+        batch padded by less than one request; the rest is queued behind it)."""
         # the admitted queue only (never a TP leader's not-yet-broadcast submissions):
         # every rank must cut the same batch
         q = LLMEngine.queued_prompt_tokens(self)
         if q >= self.max_prefill_tokens or not self.prefill_graphs:
+            return self.max_prefill_tokens
+        up = next(b for b in self.prefill_buckets if b >= q)
+        if up - q <= self.PREFILL_MAX_PAD:
             return self.max_prefill_tokens
         fit = [b for b in self.prefill_buckets if b <= q]
         return fit[-1] if fit else self.max_prefill_tokens
@@ -791,12 +836,12 @@ class LLMEngine:
 
     def _prefill_graph_for(self, tokens: int, seqs: int) -> _PrefillGraph | None:
         """Graph bucket for a prefill of ``tokens`` tokens: the smallest bucket that
-        holds it, if the padding is <= 15 % (else None: run eagerly)."""
+        holds it (None: run eagerly)."""
         if not self.prefill_graphs or seqs > self.max_batch:
             return None
         for T in self.prefill_buckets:
             if T >= tokens:
-                return self._prefill_graph(T) if tokens >= 0.85 * T else None
+                return self._prefill_graph(T)
         return None
 
     def _state(self, bp: int) -> _BucketState:

@@ -379,12 +379,16 @@ class MatchEngine:
             return None
         _, first_t, seg, text = r
         n = len(q_doc)
-        q = torch.tensor(np.stack([np.asarray(q_doc, np.int64), np.asarray(q_off, np.int64),
-                                   np.asarray(q_k, np.int64)], 1)).to(self.device, non_blocking=True)
-        lens = torch.tensor([len(d) for d in docs], dtype=torch.int64).to(self.device, non_blocking=True)
-        base = first_t[:-1] * seg
-        out = torch.empty(n, 4, dtype=torch.int64, device=self.device)
+        # every input is made on the scan stream, where the kernel runs: the engine thread's
+        # stream (the LLM's decode graphs, tens of ms deep) would let the kernel read the
+        # query / length / base buffers before their copies land (a memory fault in the
+        # flagship pipeline)
         with self._on_stream():
+            q = torch.tensor(np.stack([np.asarray(q_doc, np.int64), np.asarray(q_off, np.int64),
+                                       np.asarray(q_k, np.int64)], 1)).to(self.device, non_blocking=True)
+            lens = torch.tensor([len(d) for d in docs], dtype=torch.int64).to(self.device, non_blocking=True)
+            base = first_t[:-1] * seg
+            out = torch.empty(n, 4, dtype=torch.int64, device=self.device)
             kernels().context_spans(text, base, lens, q, out)
             spans = out.cpu().numpy()
         return patterns().contexts_from_spans(docs, q_doc, spans)

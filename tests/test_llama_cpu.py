@@ -328,3 +328,18 @@ def test_tile_out_ok_rejects_outputs_gemm_tile_cannot_write():
     assert not ops.tile_out_ok(base[:, 1:129])                                        # base 2 B off
     assert not ops.tile_out_ok(base.t())                                               # column stride
     assert not ops.tile_out_ok(torch.empty(64, 128, dtype=torch.float32))
+
+
+def test_prefill_bucket_sizes_bound_padding():
+    """Prefill graph buckets: 512-token steps to 4096, then quarter-octave steps, capped
+    at max_prefill_tokens; any batch <= the cap fits a bucket padded by < 512 tokens or
+    <= 20 % (so no batch cut at a bucket runs eagerly)."""
+    from operator_amd.engine.llm import _prefill_bucket_sizes
+
+    b = _prefill_bucket_sizes(32768)
+    assert b[:8] == [512 * i for i in range(1, 9)] and b[-1] == 32768
+    assert b == sorted(set(b))
+    for t in range(1, 32769, 97):
+        T = next(x for x in b if x >= t)
+        assert T - t < 512 or (T - t) <= 0.2 * T
+    assert _prefill_bucket_sizes(1000) == [512, 1000]

@@ -236,7 +236,7 @@ def test_weight_cache_maps_shard_onto_the_gpu(tmp_path, wd):
 def test_graph_prefill_equals_eager_prefill():
     """A prefill replayed from a captured bucket graph (tokens padded to the bucket,
     padding slots -1, padding attention items -1) writes the same KV cache and samples
-    the same tokens as the eager prefill; a batch too small for any bucket runs eagerly."""
+    the same tokens as the eager prefill; a 3-token batch replays the smallest (512) bucket."""
     cfg = get_config("tiny-gqa4")
     m = LlamaModel(cfg, device="cuda").init_random(seed=7)
     lens = [400, 350, 30, 170]          # 950 tokens: bucket 1024 (7 % padding)
@@ -256,9 +256,10 @@ def test_graph_prefill_equals_eager_prefill():
             eng.step()
         outs.append([r.output for r in reqs])
         replays.append(eng.stats.prefill_graph_replays)
-        small = [GenRequest([5, 6, 7], max_tokens=2, ignore_eos=True)]   # 3 tokens: eager
+        small = [GenRequest([5, 6, 7], max_tokens=2, ignore_eos=True)]   # 3 tokens: bucket 512
         eng.generate(small)
-        assert eng.stats.prefill_graph_replays == replays[-1]
+        assert eng.stats.prefill_graph_replays == replays[-1] + pg
+        assert eng.stats.prefill_eager == (0 if pg else 2)
     assert replays == [0, 1]
     assert outs[0] == outs[1]
     assert torch.equal(caches[0], caches[1])

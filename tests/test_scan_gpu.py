@@ -232,6 +232,23 @@ def test_context_spans_equal_host_contexts():
         assert a["metadata"]["totalLines"] == b["metadata"]["totalLines"]
 
 
+def test_context_windows_while_default_stream_is_busy():
+    """The flagship runs the LLM's decode graphs on the default stream while the match
+    engine scans on its own: the GPU context windows (lazy analyze) must not read their
+    query / length buffers before those land (they are made on the scan stream)."""
+    ps = synthetic_library(200, seed=3)
+    bdocs = LogFactory(n_patterns=200, seed=9).batch(48, 8 * 1024, n_failures=3, seed=5)[0]
+    eng = MatchEngine(ps, device="cuda", seg_bytes=1024, profile_bytes=0)
+    host = [r.to_obj() for r in MatchEngine(ps, device="cpu").analyze(bdocs)]
+    for _ in range(3):
+        torch.cuda._sleep(300_000_000)   # the default stream stays busy for ~0.1 s
+        got = eng.analyze(bdocs, lazy=True)
+        for i, b in enumerate(host):
+            a = got[i].to_obj()
+            assert [e["context"] for e in a["events"]] == [e["context"] for e in b["events"]]
+    torch.cuda.synchronize()
+
+
 def test_scan_match_overflow_regrows():
     small = MatchEngine(PatternSet.from_dicts([{"id": "e", "primary_pattern": {"literal": "e"}}]), device="cuda",
                         seg_bytes=256, match_cap=64, profile_bytes=0)

@@ -137,6 +137,14 @@ def run_sharded(shards: int, failures: int, workdir: str, timeout_s: float = 600
         from concurrent.futures import ThreadPoolExecutor
 
         st = failed_pod("x", finished_at="2025-08-29T10:00:00Z")["status"]
+
+        def cpu_s(pid):   # user + system CPU seconds of a process (Linux /proc)
+            try:
+                f = open(f"/proc/{pid}/stat").read().rsplit(")", 1)[1].split()
+                return (int(f[11]) + int(f[12])) / os.sysconf("SC_CLK_TCK")
+            except OSError:
+                return float("nan")
+        c0 = cpu_s(srv.pid)
         t0 = time.perf_counter()
         with ThreadPoolExecutor(16) as ex:
             list(ex.map(lambda n: kube.patch_status(PODS, n, "default", st), names))
@@ -155,6 +163,7 @@ def run_sharded(shards: int, failures: int, workdir: str, timeout_s: float = 600
             if n_done >= failures:
                 break
         elapsed = time.perf_counter() - t0
+        srv_cpu = cpu_s(srv.pid) - c0
         time.sleep(2.0)   # let the last Events land before counting them
         per_pod = Counter(e.get("regarding", {}).get("name") for e in kube.list(EVENTS, "default")
                           if e.get("reason") == "PodmortemAnalysisComplete"
@@ -162,6 +171,9 @@ def run_sharded(shards: int, failures: int, workdir: str, timeout_s: float = 600
         return {"topology": f"shard-per-gpu x{shards} on one REST API server (stub log-parser + echo explainer)",
                 "failures": failures, "analysed": n_done, "analyses_per_s": round(failures / elapsed, 1),
                 "inject_s": round(t_inj, 2), "elapsed_s": round(elapsed, 2),
+                # the API server's CPU time over the run: its ms per analysis bound the rate one
+                # server process can sustain (1000 / ms analyses/s)
+                "apiserver_cpu_s": round(srv_cpu, 2), "apiserver_cpu_ms_per_analysis": round(1e3 * srv_cpu / failures, 2),
                 "complete_events_per_pod": dict(Counter(per_pod.get(n, 0) for n in names))}
     finally:
         if op is not None:
