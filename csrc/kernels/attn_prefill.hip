@@ -405,22 +405,23 @@ __device__ __forceinline__ s16x4 ds_read_tr16(const char* p) {
 // share) followed by its own slen keys; its query rows are its own tokens, at positions
 // seq_pfx[seq] + row. Prefix keys are visible to every row; a last, partial prefix tile is
 // masked past the prefix length.
-// OPT bit 0: the next tile's K/V loads are issued after this tile's S MFMAs (they are in
-// flight during softmax + P.V instead of holding registers across the S MFMAs); bit 1:
-// deferred rescale — a row keeps its running max until a tile raises it by more than 8
-// (log2 units, so P <= 256 in fp32 / bf16), skipping the O / l rescale otherwise; bit 2:
-// two LDS tile buffers — tile kt + 1 is stored into the idle buffer after tile kt's
-// MFMAs and one barrier per tile replaces two.
-template <int G, int OPT = 0>
+// Schedule: the next tile's K/V loads are issued after this tile's S MFMAs (they are in
+// flight during softmax + P.V instead of holding registers across the S MFMAs), and the
+// rescale is deferred — a row keeps its running max until a tile raises it by more than 8
+// (log2 units, so P <= 256 in fp32 / bf16), skipping the O / l rescale otherwise. Measured
+// against the plain schedule on MI355X (profiles/prefill_attn_v3_schedule_variants.jsonl):
+// 16x1024 0.290 vs 0.326 ms, 4x4096 0.857 vs 0.963 ms; the late loads alone, and two LDS
+// tile buffers with one barrier per tile (with or without the deferred rescale), were
+// slower than this pair and were removed.
+template <int G>
 __global__ void __launch_bounds__(512) attn_prefill_mfma32_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     bf16_t* __restrict__ o, const int* __restrict__ cu_seqlens, const int* __restrict__ work_seq,
     const int* __restrict__ work_q0, int Hq, int Hkv, float scale_log2, const bf16_t* __restrict__ pk,
     const bf16_t* __restrict__ pv, const int* __restrict__ seq_pfx) {
   constexpr int D = 128, BK = 64, RG = 8 / G, BQ = 32 * RG;
-  constexpr int NB = (OPT & 4) ? 2 : 1;   // LDS tile buffers
-  __shared__ __attribute__((aligned(16))) char Ks[NB * BK * 256];
-  __shared__ __attribute__((aligned(16))) char Vs[NB * BK * 256];
+  __shared__ __attribute__((aligned(16))) char Ks[BK * 256];
+  __shared__ __attribute__((aligned(16))) char Vs[BK * 256];
 
   const int wi = blockIdx.x, kvh = blockIdx.y;
   const int seq = work_seq[wi];
@@ -482,44 +483,26 @@ __global__ void __launch_bounds__(512) attn_prefill_mfma32_kernel(
       }
     }
   };
-  auto store_tile = [&](int buf) {
+  auto store_tile = [&]() {
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
       const int c = tid + r * 512;
       const int key = c >> 4, ch = c & 15;
-      *reinterpret_cast<u16x8*>(Ks + buf * (BK * 256) + k_img(key, ch)) = kr[r];
-      *reinterpret_cast<u16x8*>(Vs + buf * (BK * 256) + v_img(key, ch)) = vr[r];
+      *reinterpret_cast<u16x8*>(Ks + k_img(key, ch)) = kr[r];
+      *reinterpret_cast<u16x8*>(Vs + v_img(key, ch)) = vr[r];
     }
   };
 
   load_tile(0);
-  if constexpr (NB == 2) {   // tile 0 staged, tile 1 in flight
-    store_tile(0);
-    if (ntiles > 1) load_tile(1);
-    __syncthreads();
-  }
   for (int kt = 0; kt < ntiles; ++kt) {
     const int kb = (kt - npt) * BK;   // own-key coordinates (negative: a prefix tile)
-    const char* Kc = Ks + (NB == 2 ? (kt & 1) * (BK * 256) : 0);
-    const char* Vc = Vs + (NB == 2 ? (kt & 1) * (BK * 256) : 0);
-    if constexpr (NB == 1) {
-      __syncthreads();  // previous tile fully consumed
-      store_tile(0);
-      __syncthreads();
-      if (!(OPT & 1) && kt + 1 < ntiles) load_tile(kt + 1);   // in flight during this tile's MFMAs
-    }
-    // NB == 2: the idle buffer takes tile kt + 1 once this tile's MFMAs are issued, then
-    // tile kt + 2 goes in flight; one barrier per tile
-    auto next = [&]() {
-      if constexpr (NB == 2) {
-        if (kt + 1 < ntiles) store_tile((kt + 1) & 1);
-        if (kt + 2 < ntiles) load_tile(kt + 2);
-        __syncthreads();
-      }
-    };
+    const char* Kc = Ks;
+    const char* Vc = Vs;
+    __syncthreads();  // previous tile fully consumed
+    store_tile();
+    __syncthreads();
     if (!active || kb >= wend) {   // wave-uniform: no visible key for this wave
-      if (NB == 1 && (OPT & 1) && kt + 1 < ntiles) load_tile(kt + 1);
-      next();
+      if (kt + 1 < ntiles) load_tile(kt + 1);
       continue;
     }
 
@@ -536,7 +519,7 @@ __global__ void __launch_bounds__(512) attn_prefill_mfma32_kernel(
         sacc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(ka), as_bf8(qb[s]), sacc[b], 0, 0, 0);
       }
     }
-    if (NB == 1 && (OPT & 1) && kt + 1 < ntiles) load_tile(kt + 1);   // in flight during softmax + P.V
+    if (kt + 1 < ntiles) load_tile(kt + 1);   // in flight during softmax + P.V
     // ---- online softmax: register i of block b is key kb + 32b + (i&3) + 8(i>>2) + 4h ----
     const bool ptile = kb < 0;
     const int pend = pl - kt * BK;   // prefix tile: its keys below pend are prefix keys
@@ -556,11 +539,8 @@ __global__ void __launch_bounds__(512) attn_prefill_mfma32_kernel(
       }
     mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
     float mnew = fmaxf(mrow, mx);
-    bool rescale = true;
-    if constexpr ((OPT & 2) != 0) {
-      rescale = mrow == -INFINITY || mnew > mrow + 8.f;
-      if (!rescale) mnew = mrow;
-    }
+    const bool rescale = mrow == -INFINITY || mnew > mrow + 8.f;   // deferred rescale
+    if (!rescale) mnew = mrow;
     const float msafe = (mnew == -INFINITY) ? 0.f : mnew;
     const float alpha = rescale ? exp2f(mrow - msafe) : 1.f;
     mrow = mnew;
@@ -602,7 +582,6 @@ __global__ void __launch_bounds__(512) attn_prefill_mfma32_kernel(
                                                             as_bf8(pb[b][s]), oacc[dd], 0, 0, 0);
         }
       }
-    next();
   }
   if (!active) return;
   const float lsum = lpart + __shfl_xor(lpart, 32, kWave);
@@ -625,7 +604,6 @@ __global__ void __launch_bounds__(512) attn_prefill_mfma32_kernel(
 // 2 = GQA-grouped 16-row waves (G = Hq / Hkv in {1, 2, 4, 8}), 3 = GQA-grouped
 // swapped 32x32 (32-row waves, any G <= 8: 8 / G row blocks per item); else -1.
 int attn_prefill_block_q(int Hq, int Hkv, int variant) {
-  if (variant >= 4 && variant <= 7) variant = 3;   // v3 schedule options (attn_prefill)
   if (variant == 1) return 64;
   if (Hkv <= 0 || Hq % Hkv != 0) return -1;
   const int G = Hq / Hkv;
@@ -642,9 +620,6 @@ int attn_prefill(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, c
   if (head_dim != 128) return -1;
   if (Hq % Hkv != 0) return -3;
   if (attn_prefill_block_q(Hq, Hkv, variant) < 0) return -4;
-  // 4 - 7: v3 with the OPT schedule bits 1 / 3 / 4 / 6 (late loads, deferred rescale, LDS double buffer)
-  const int opt = variant == 4 ? 1 : variant == 5 ? 3 : variant == 6 ? 4 : variant == 7 ? 6 : 0;
-  if (variant >= 4 && variant <= 7) variant = 3;
   if (seq_pfx != nullptr && (variant != 3 || pk == nullptr || pv == nullptr)) return -5;   // v3 only
   const float sl2 = scale * 1.4426950408889634f;
   const int G = Hq / Hkv;
@@ -654,24 +629,9 @@ int attn_prefill(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, c
   } else {
     dim3 grid(num_work, Hkv);
 #define OAMD_PF(KERN, GG) KERN<GG><<<grid, 512, 0, stream>>>(q, k, v, o, cu_seqlens, work_seq, work_q0, Hq, Hkv, sl2)
-#define OAMD_PF3(GG)                                                                                         \
-  do {                                                                                                       \
-    if (opt == 1)                                                                                            \
-      attn_prefill_mfma32_kernel<GG, 1><<<grid, 512, 0, stream>>>(q, k, v, o, cu_seqlens, work_seq, work_q0, \
-                                                                   Hq, Hkv, sl2, pk, pv, seq_pfx);           \
-    else if (opt == 3)                                                                                       \
-      attn_prefill_mfma32_kernel<GG, 3><<<grid, 512, 0, stream>>>(q, k, v, o, cu_seqlens, work_seq, work_q0, \
-                                                                   Hq, Hkv, sl2, pk, pv, seq_pfx);           \
-    else if (opt == 4)                                                                                       \
-      attn_prefill_mfma32_kernel<GG, 4><<<grid, 512, 0, stream>>>(q, k, v, o, cu_seqlens, work_seq, work_q0, \
-                                                                   Hq, Hkv, sl2, pk, pv, seq_pfx);           \
-    else if (opt == 6)                                                                                       \
-      attn_prefill_mfma32_kernel<GG, 6><<<grid, 512, 0, stream>>>(q, k, v, o, cu_seqlens, work_seq, work_q0, \
-                                                                   Hq, Hkv, sl2, pk, pv, seq_pfx);           \
-    else                                                                                                     \
-      attn_prefill_mfma32_kernel<GG, 0><<<grid, 512, 0, stream>>>(q, k, v, o, cu_seqlens, work_seq, work_q0, \
-                                                                   Hq, Hkv, sl2, pk, pv, seq_pfx);           \
-  } while (0)
+#define OAMD_PF3(GG)                                                                                          \
+  attn_prefill_mfma32_kernel<GG><<<grid, 512, 0, stream>>>(q, k, v, o, cu_seqlens, work_seq, work_q0, Hq, Hkv, sl2, \
+                                                           pk, pv, seq_pfx)
 #define OAMD_PF_G(KERN)            \
   switch (G) {                     \
     case 1: OAMD_PF(KERN, 1); break; \

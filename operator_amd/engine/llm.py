@@ -111,6 +111,7 @@ class _Window:
     k: int
     host: torch.Tensor
     event: object
+    s0: int = 0           # hist column of the window's first step (columns wrap mod multi_step)
 
 
 def _prefill_bucket_sizes(max_tokens: int) -> list[int]:
@@ -153,14 +154,19 @@ class _BucketState:
         # the per-row state ``load`` rewrites lives in one byte buffer (one H2D copy per
         # batch-composition change instead of six)
         mp = eng.max_pages
-        self._spec = (("ids", (bp,), torch.long), ("pos", (bp,), torch.long), ("seeds", (bp,), torch.long),
-                      ("ctx", (bp,), torch.int32), ("temp", (bp,), torch.float32), ("bt", (bp, mp), torch.int32))
+        self._spec = (("step", (1,), torch.long), ("ids", (bp,), torch.long), ("pos", (bp,), torch.long),
+                      ("seeds", (bp,), torch.long), ("ctx", (bp,), torch.int32), ("temp", (bp,), torch.float32),
+                      ("bt", (bp, mp), torch.int32))
         self._nbytes = sum(int(np.prod(s)) * torch.empty((), dtype=dt).element_size() for _, s, dt in self._spec)
         self._buf = torch.zeros(self._nbytes, dtype=torch.uint8, device=dev)
         for n, t in self._views(self._buf).items():
             setattr(self, n, t)
         self.hist = torch.zeros(bp, eng.multi_step, dtype=torch.long, device=dev)
-        self.step = torch.zeros(1, dtype=torch.long, device=dev)
+        # steps replayed since the last load: the device counter (``step``, bumped by every
+        # replay; hist column = step % multi_step) mirrored on the host, so a window needs
+        # no kernel to reset it (the one-element fill it replaced sat ~1 ms behind the previous
+        # window's token copy on the GPU at every window boundary, round-4 flagship trace)
+        self.step_host = 0
         self.slots = torch.zeros(bp, dtype=torch.long, device=dev)   # per step: cache slot of each row's token
         self.spos = torch.zeros(bp, dtype=torch.long, device=dev)    # per step: sampler stream position
 
@@ -191,7 +197,8 @@ class _BucketState:
             for i, r in enumerate(reqs):
                 bt[i, :len(r.pages)] = r.pages
         nb = self._buf.is_cuda
-        self._buf.copy_(host.pin_memory() if nb else host, non_blocking=nb)
+        self._buf.copy_(host.pin_memory() if nb else host, non_blocking=nb)   # step = 0
+        self.step_host = 0
 
 
 @contextlib.contextmanager
@@ -478,7 +485,7 @@ class LLMEngine:
         # shared prompt prefix: the GPU path needs the v3 prefill attention kernel; TP
         # engines replay the leader's steps and keep it off
         self.prefix_sharing = prefix_sharing and (
-            self.device.type != "cuda" or 3 <= ops.prefill_variant(model.hq, model.hkv) <= 7)
+            self.device.type != "cuda" or ops.prefill_variant(model.hq, model.hkv) == 3)
         self._pfx: _SharedPrefix | None = None
         self._pfx_seen: deque = deque()
         self._pfx_count: dict = {}
@@ -886,7 +893,8 @@ class LLMEngine:
             reqs = list(self.running)
             st.load(reqs, self.max_pages)
             self._active = st
-        st.step.zero_()
+        s0 = st.step_host % self.multi_step
+        st.step_host += k
         with trace_range(f"decode[{bp}x{k}]"):
             if self.use_graphs and g.graph is not None:
                 # the whole window from C++ with the GIL released: ROCm feeds a graph's
@@ -902,21 +910,25 @@ class LLMEngine:
         if self._host_bufs is not None:
             self._hb ^= 1
             host = self._host_bufs[self._hb]
-            host[:B, :k].copy_(st.hist[:B, :k], non_blocking=True)
+            host[:B].copy_(st.hist[:B], non_blocking=True)
             ev = torch.cuda.Event()
             ev.record()
         else:
             host, ev = st.hist, None
         self.stats.graph_replays += k if self.use_graphs else 0
         self.stats.decode_windows += 1
-        return _Window(st, reqs, B, k, host, ev)
+        return _Window(st, reqs, B, k, host, ev, s0)
 
     def _consume(self, win: _Window) -> None:
         if win.event is not None:
             t_w = time.perf_counter()
             win.event.synchronize()
             self.stats.decode_wait_s += time.perf_counter() - t_w
-        toks = win.host[:win.B, :win.k].tolist()
+        ms = self.multi_step
+        if win.s0 + win.k <= ms:
+            toks = win.host[:win.B, win.s0:win.s0 + win.k].tolist()
+        else:   # the window's columns wrap
+            toks = win.host[:win.B].numpy()[:, [(win.s0 + i) % ms for i in range(win.k)]].tolist()
         for r, row in zip(win.reqs, toks):
             if r.done:   # finished (EOS / cancel) in an earlier window: discard
                 continue

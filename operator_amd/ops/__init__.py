@@ -172,7 +172,7 @@ def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, cos: torch.Tensor, sin: torch.
 
 # v3 schedule options (csrc/kernels/attn_prefill.hip OPT bits): l = K/V loads after the
 # S MFMAs, r = deferred rescale, d = two LDS tile buffers (one barrier per tile)
-_PREFILL_VARIANTS = {"v1": 1, "v2": 2, "v3": 3, "v3l": 4, "v3lr": 5, "v3d": 6, "v3dr": 7}
+_PREFILL_VARIANTS = {"v1": 1, "v2": 2, "v3": 3}
 
 
 def prefill_variant(Hq: int, Hkv: int) -> int:
@@ -237,7 +237,7 @@ def attn_prefill(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, seq_lens: li
     # work = (cu_seqlens, work_seq, work_q0, variant); the work list must be cut at that variant's block_q
     var = work[3] if len(work) > 3 else 1
     if prefix is not None:
-        if not 3 <= var <= 7:
+        if var != 3:
             raise ValueError("a shared prefix needs attn_prefill variant 3")
         kernels().attn_prefill(q, k, v, o, work[0], work[1], work[2], scale, var, prefix[0], prefix[1], prefix[2])
     else:

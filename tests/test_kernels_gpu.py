@@ -74,7 +74,7 @@ def test_rope_kv_and_cache(Hq, Hkv):
 
 @pytest.mark.parametrize("lens", [[1], [17, 64, 130], [300, 5, 64]])
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 8), (16, 2), (8, 4), (64, 8), (24, 8), (28, 4), (10, 2), (12, 2)])
-@pytest.mark.parametrize("variant", [3, 2, 1, 4, 5, 6, 7])
+@pytest.mark.parametrize("variant", [3, 2, 1])
 def test_attn_prefill(lens, Hq, Hkv, variant):
     if variant == 2 and Hq // Hkv not in (1, 2, 4, 8):
         pytest.skip("v2 takes GQA groups 1, 2, 4, 8 only")

@@ -343,3 +343,24 @@ def test_prefill_bucket_sizes_bound_padding():
         T = next(x for x in b if x >= t)
         assert T - t < 512 or (T - t) <= 0.2 * T
     assert _prefill_bucket_sizes(1000) == [512, 1000]
+
+
+def test_decode_window_columns_wrap():
+    """A decode window's tokens sit in hist columns (s0 + i) % multi_step (the device step
+    counter is not reset per window); _consume reads them in step order across the wrap."""
+    import torch
+
+    from operator_amd.engine.llm import GenRequest, LLMEngine, _Window
+
+    eng = LLMEngine.__new__(LLMEngine)
+    eng.multi_step, eng.eos, eng.token_hook = 8, set(), None
+
+    class _S:
+        decode_tokens = 0
+    eng.stats = _S()
+    reqs = [GenRequest([1], ignore_eos=True), GenRequest([1], ignore_eos=True)]
+    host = torch.arange(16).reshape(2, 8)            # row r, column c -> 8 r + c
+    eng._consume(_Window(None, reqs, 2, 4, host, None, 6))
+    assert reqs[0].output == [6, 7, 0, 1] and reqs[1].output == [14, 15, 8, 9]
+    eng._consume(_Window(None, reqs, 2, 2, host, None, 2))
+    assert reqs[0].output[-2:] == [2, 3]
