@@ -92,10 +92,10 @@ def test_attn_prefill(lens, Hq, Hkv, variant):
     torch.testing.assert_close(o.cpu().float(), o_r.float(), atol=2e-2, rtol=3e-2)
 
 
-@pytest.mark.parametrize("variant", [None, 5, 7])
+@pytest.mark.parametrize("variant", [None, 3])
 def test_attn_prefill_large_scores(variant):
-    """Spike one key so the running max jumps mid-sequence (forces the rescale path; variant
-    5 defers a rescale until the max rises by more than 2^8)."""
+    """Spike one key so the running max jumps mid-sequence (forces the rescale path; v3
+    defers a rescale until the max rises by more than 2^8)."""
     torch.manual_seed(3)
     lens, Hq, Hkv, D = [256], 8, 8, 128
     q, k, v = _rand(256, Hq, D), _rand(256, Hkv, D), _rand(256, Hkv, D)
