@@ -203,7 +203,8 @@ class FakeKube:
         self._last_rv = rv
         ev = None
         for w in list(self._watches):
-            if w.res == res and (w.namespace is None or w.namespace == obj["metadata"].get("namespace")):
+            if (w.res is res or w.res == res) and (w.namespace is None
+                                                   or w.namespace == obj["metadata"].get("namespace")):
                 if ev is None:
                     ev = _Event(typ, obj)
                 w.push(typ, obj, ev)
