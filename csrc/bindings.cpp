@@ -459,7 +459,7 @@ void attn_prefill(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
   const bf16_t *pkp = nullptr, *pvp = nullptr;
   const int* pfx = nullptr;
   if (seq_pfx.has_value()) {
-    TORCH_CHECK(pk.has_value() && pv.has_value() && variant == 3, "a prefix needs pk, pv and variant 3");
+    TORCH_CHECK(pk.has_value() && pv.has_value() && (variant == 3 || variant == 4), "a prefix needs pk, pv and variant 3 / 4");
     for (const auto* t : {&*pk, &*pv}) { CHECK_DEV(*t); CHECK_BF16(*t); CHECK_CONTIG(*t); }
     TORCH_CHECK(pk->dim() == 3 && pv->sizes() == pk->sizes() && pk->size(1) == k.size(1) && pk->size(2) == 128,
                 "pk / pv [prefix, Hkv, 128]");

@@ -1,8 +1,9 @@
 // Causal flash attention for prefill, variable-length packed sequences, GQA,
-// on MFMA. Three variants share the work-list contract
+// on MFMA. Four variants share the work-list contract
 // (attn_prefill_block_q): v1 per-query-head (below), v2 GQA-grouped 16-row waves
 // with a software-pipelined K/V tile, v3 GQA-grouped swapped-operand 32x32 MFMA
-// waves (S^T = K Q^T, P stays in registers as the next MFMA's B operand).
+// waves (S^T = K Q^T, P stays in registers as the next MFMA's B operand) in 8-wave
+// workgroups, v4 the same waves in 4-wave workgroups (two per CU; GQA groups <= 4).
 //
 // v1 work item = (64-row query block of one sequence, query head). 4 waves; each
 // wave owns 16 query rows. Per 64-key tile:
@@ -413,13 +414,18 @@ __device__ __forceinline__ s16x4 ds_read_tr16(const char* p) {
 // 16x1024 0.290 vs 0.326 ms, 4x4096 0.857 vs 0.963 ms; the late loads alone, and two LDS
 // tile buffers with one barrier per tile (with or without the deferred rescale), were
 // slower than this pair and were removed.
-template <int G>
-__global__ void __launch_bounds__(512) attn_prefill_mfma32_kernel(
+// NW: waves per workgroup. 8 (one work item = 8 waves of (head, 32-row block)) holds a CU
+// alone at 239 VGPRs (2 waves per SIMD), so every barrier of its K/V tile loop idles the
+// CU; NW = 4 (G <= 4) halves the work item and puts two workgroups on each CU.
+template <int G, int NW = 8>
+__global__ void __launch_bounds__(NW * 64, 2) attn_prefill_mfma32_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     bf16_t* __restrict__ o, const int* __restrict__ cu_seqlens, const int* __restrict__ work_seq,
     const int* __restrict__ work_q0, int Hq, int Hkv, float scale_log2, const bf16_t* __restrict__ pk,
     const bf16_t* __restrict__ pv, const int* __restrict__ seq_pfx) {
-  constexpr int D = 128, BK = 64, RG = 8 / G, BQ = 32 * RG;
+  constexpr int D = 128, BK = 64, RG = NW / G, BQ = 32 * RG;
+  constexpr int NT = NW * 64, NC = BK * 16 / NT;   // threads; 16-B K (and V) chunks each stages per tile
+  static_assert(RG >= 1, "a workgroup needs a row block per head");
   __shared__ __attribute__((aligned(16))) char Ks[BK * 256];
   __shared__ __attribute__((aligned(16))) char Vs[BK * 256];
 
@@ -434,7 +440,7 @@ __global__ void __launch_bounds__(512) attn_prefill_mfma32_kernel(
   const int hq = kvh * G + (w % G);
   const int rbase = q0 + 32 * (w / G);  // this wave's first query row
   const int qrow = rbase + r32;          // this lane's query row (C column)
-  // G = 3, 5, 6, 7: only G x RG of the 8 waves have a (head, row block); the rest
+  // G = 3, 5, 6, 7: only G x RG of the NW waves have a (head, row block); the rest
   // stage K/V tiles with the others and compute nothing
   const bool wave_used = w < G * RG;
 
@@ -463,11 +469,11 @@ __global__ void __launch_bounds__(512) attn_prefill_mfma32_kernel(
   const int gi = lane & 15, g = lane >> 4;
   const int trq = gi >> 2, trp = gi & 3;
 
-  u16x8 kr[2], vr[2];
+  u16x8 kr[NC], vr[NC];
   auto load_tile = [&](int kt) {   // key tile kt: a prefix tile (kt < npt) or own tile kt - npt
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const int c = tid + r * 512;
+    for (int r = 0; r < NC; ++r) {
+      const int c = tid + r * NT;
       const int key = c >> 4, ch = c & 15;
       kr[r] = vr[r] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
       if (kt < npt) {
@@ -485,8 +491,8 @@ __global__ void __launch_bounds__(512) attn_prefill_mfma32_kernel(
   };
   auto store_tile = [&]() {
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const int c = tid + r * 512;
+    for (int r = 0; r < NC; ++r) {
+      const int c = tid + r * NT;
       const int key = c >> 4, ch = c & 15;
       *reinterpret_cast<u16x8*>(Ks + k_img(key, ch)) = kr[r];
       *reinterpret_cast<u16x8*>(Vs + v_img(key, ch)) = vr[r];
@@ -609,6 +615,7 @@ int attn_prefill_block_q(int Hq, int Hkv, int variant) {
   const int G = Hq / Hkv;
   if (variant == 2 && (G == 1 || G == 2 || G == 4 || G == 8)) return 16 * (8 / G);
   if (variant == 3 && G >= 1 && G <= 8) return 32 * (8 / G);
+  if (variant == 4 && G >= 1 && G <= 4) return 32 * (4 / G);   // v3 in 4-wave workgroups
   return -1;
 }
 
@@ -620,7 +627,7 @@ int attn_prefill(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, c
   if (head_dim != 128) return -1;
   if (Hq % Hkv != 0) return -3;
   if (attn_prefill_block_q(Hq, Hkv, variant) < 0) return -4;
-  if (seq_pfx != nullptr && (variant != 3 || pk == nullptr || pv == nullptr)) return -5;   // v3 only
+  if (seq_pfx != nullptr && (variant < 3 || pk == nullptr || pv == nullptr)) return -5;   // v3 / v4 only
   const float sl2 = scale * 1.4426950408889634f;
   const int G = Hq / Hkv;
   if (variant == 1) {
@@ -632,6 +639,9 @@ int attn_prefill(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, c
 #define OAMD_PF3(GG)                                                                                          \
   attn_prefill_mfma32_kernel<GG><<<grid, 512, 0, stream>>>(q, k, v, o, cu_seqlens, work_seq, work_q0, Hq, Hkv, sl2, \
                                                            pk, pv, seq_pfx)
+#define OAMD_PF4(GG)                                                                                          \
+  attn_prefill_mfma32_kernel<GG, 4><<<grid, 256, 0, stream>>>(q, k, v, o, cu_seqlens, work_seq, work_q0, Hq, Hkv,  \
+                                                              sl2, pk, pv, seq_pfx)
 #define OAMD_PF_G(KERN)            \
   switch (G) {                     \
     case 1: OAMD_PF(KERN, 1); break; \
@@ -641,6 +651,13 @@ int attn_prefill(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, c
   }
     if (variant == 2) {
       OAMD_PF_G(attn_prefill_gqa_kernel)
+    } else if (variant == 4) {
+      switch (G) {
+        case 1: OAMD_PF4(1); break;
+        case 2: OAMD_PF4(2); break;
+        case 3: OAMD_PF4(3); break;
+        default: OAMD_PF4(4); break;
+      }
     } else {
       switch (G) {  // groups of Llama-3.2-3B (3), Qwen2.5-32B (5), Qwen2.5-7B (7)
         case 1: OAMD_PF3(1); break;
@@ -653,6 +670,7 @@ int attn_prefill(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, c
         default: OAMD_PF3(8); break;
       }
     }
+#undef OAMD_PF4
 #undef OAMD_PF3
 #undef OAMD_PF_G
 #undef OAMD_PF

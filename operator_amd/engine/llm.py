@@ -485,7 +485,7 @@ class LLMEngine:
         # shared prompt prefix: the GPU path needs the v3 prefill attention kernel; TP
         # engines replay the leader's steps and keep it off
         self.prefix_sharing = prefix_sharing and (
-            self.device.type != "cuda" or ops.prefill_variant(model.hq, model.hkv) == 3)
+            self.device.type != "cuda" or ops.prefill_variant(model.hq, model.hkv) in (3, 4))
         self._pfx: _SharedPrefix | None = None
         self._pfx_seen: deque = deque()
         self._pfx_count: dict = {}

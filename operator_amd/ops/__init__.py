@@ -172,28 +172,33 @@ def rope_kv(qkv: torch.Tensor, pos: torch.Tensor, cos: torch.Tensor, sin: torch.
 
 # v3 schedule options (csrc/kernels/attn_prefill.hip OPT bits): l = K/V loads after the
 # S MFMAs, r = deferred rescale, d = two LDS tile buffers (one barrier per tile)
-_PREFILL_VARIANTS = {"v1": 1, "v2": 2, "v3": 3}
+_PREFILL_VARIANTS = {"v1": 1, "v2": 2, "v3": 3, "v4": 4}
 
 
 def prefill_variant(Hq: int, Hkv: int) -> int:
     """attn_prefill kernel variant: 1 = per-query-head (any G), 2 = GQA-grouped 16-row waves
-    (G = Hq / Hkv in 1, 2, 4, 8), 3 = GQA-grouped swapped-operand 32x32 MFMA waves (G <= 8).
-    OAMD_PREFILL_ATTN=v1|v2|v3 overrides the default (v3); a grouped variant that cannot
-    take G falls back to v3, then v1."""
+    (G = Hq / Hkv in 1, 2, 4, 8), 3 = GQA-grouped swapped-operand 32x32 MFMA waves in 8-wave
+    workgroups (G <= 8), 4 = the same waves in 4-wave workgroups, two per CU (G <= 4;
+    profiles/prefill_attn_v3_vs_v4.jsonl: 6-9 % faster at 16x1024 and mixed lengths, equal at
+    4x4096). Default: v4 where G <= 4, else v3. OAMD_PREFILL_ATTN=v1|v2|v3|v4 overrides it; a
+    grouped variant that cannot take G falls back to v3, then v1."""
     G = Hq // Hkv if Hkv and Hq % Hkv == 0 else 0
-    want = _PREFILL_VARIANTS.get(os.environ.get("OAMD_PREFILL_ATTN", "v3"), 3)
+    want = _PREFILL_VARIANTS.get(os.environ.get("OAMD_PREFILL_ATTN", ""), 4 if 1 <= G <= 4 else 3)
     if want == 2 and G not in (1, 2, 4, 8):
+        want = 3
+    if want == 4 and G > 4:
         want = 3
     return want if 1 <= G <= 8 else 1
 
 
 def prefill_block_q(Hq: int, Hkv: int, variant: int | None = None) -> int:
-    """Query rows per attn_prefill work item: 64 (v1), 16 x (8 / G) (v2), 32 x (8 / G) (v3)."""
+    """Query rows per attn_prefill work item: 64 (v1), 16 x (8 / G) (v2), 32 x (8 / G) (v3),
+    32 x (4 / G) (v4)."""
     v = prefill_variant(Hq, Hkv) if variant is None else variant
     if v == 1:
         return 64
     G = Hq // Hkv
-    return (16 if v == 2 else 32) * (8 // G)
+    return (16 if v == 2 else 32) * ((4 if v == 4 else 8) // G)
 
 
 def prefill_work_list(seq_lens: list[int], block_q: int = 64) -> tuple[list[int], list[int]]:
@@ -237,8 +242,8 @@ def attn_prefill(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, seq_lens: li
     # work = (cu_seqlens, work_seq, work_q0, variant); the work list must be cut at that variant's block_q
     var = work[3] if len(work) > 3 else 1
     if prefix is not None:
-        if var != 3:
-            raise ValueError("a shared prefix needs attn_prefill variant 3")
+        if var not in (3, 4):
+            raise ValueError("a shared prefix needs attn_prefill variant 3 or 4")
         kernels().attn_prefill(q, k, v, o, work[0], work[1], work[2], scale, var, prefix[0], prefix[1], prefix[2])
     else:
         kernels().attn_prefill(q, k, v, o, work[0], work[1], work[2], scale, var)

@@ -74,10 +74,12 @@ def test_rope_kv_and_cache(Hq, Hkv):
 
 @pytest.mark.parametrize("lens", [[1], [17, 64, 130], [300, 5, 64]])
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 8), (16, 2), (8, 4), (64, 8), (24, 8), (28, 4), (10, 2), (12, 2)])
-@pytest.mark.parametrize("variant", [3, 2, 1])
+@pytest.mark.parametrize("variant", [3, 2, 1, 4])
 def test_attn_prefill(lens, Hq, Hkv, variant):
     if variant == 2 and Hq // Hkv not in (1, 2, 4, 8):
         pytest.skip("v2 takes GQA groups 1, 2, 4, 8 only")
+    if variant == 4 and Hq // Hkv > 4:
+        pytest.skip("v4 (4-wave workgroups) takes GQA groups <= 4")
     torch.manual_seed(2)
     T, D = sum(lens), 128
     q, k, v = _rand(T, Hq, D), _rand(T, Hkv, D), _rand(T, Hkv, D)
@@ -92,7 +94,7 @@ def test_attn_prefill(lens, Hq, Hkv, variant):
     torch.testing.assert_close(o.cpu().float(), o_r.float(), atol=2e-2, rtol=3e-2)
 
 
-@pytest.mark.parametrize("variant", [None, 3])
+@pytest.mark.parametrize("variant", [None, 3, 4])
 def test_attn_prefill_large_scores(variant):
     """Spike one key so the running max jumps mid-sequence (forces the rescale path; v3
     defers a rescale until the max rises by more than 2^8)."""

@@ -5,5 +5,5 @@ timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout
 tail -3 gpurun_out/gpu_tests.log
 timeout -k 10 400 python -u bench.py --steps ${STEPS:-3} --warmup 2 > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail -20 gpurun_out/bench.err; exit 1; }
 tail -c 1500 gpurun_out/bench.json
-timeout -k 10 300 python -u tools/bench_prefill_attn.py --variants 3 --shapes 16x1024,4x4096,mixed > gpurun_out/pattn.jsonl 2> gpurun_out/pattn.err
+timeout -k 10 300 python -u tools/bench_prefill_attn.py --variants 3,4 --shapes 16x1024,4x4096,mixed > gpurun_out/pattn.jsonl 2> gpurun_out/pattn.err
 cat gpurun_out/pattn.jsonl
