@@ -19,7 +19,6 @@ loop thread that owns the GPU (LLMEngine.step).
 from __future__ import annotations
 
 import hashlib
-import os
 import sys
 import threading
 import time
@@ -233,9 +232,6 @@ class ExplainEngine:
         self._stream = hasattr(tokenizer, "byte_table") and tokenizer.byte_table() is not None
         if self._stream:
             llm.token_hook = self._feed
-        # OAMD_BATCH_ADMIT=0: the batcher only tokenizes and each caller submits its own
-        # request (the previous hand-off, kept for A/B measurements)
-        self._batch_admit = os.environ.get("OAMD_BATCH_ADMIT", "1") != "0"
         self.prompts = PromptBatcher(self._batch_build)
         self.prompts.start()
         if start_loop:
@@ -302,7 +298,7 @@ class ExplainEngine:
 
     def _batch_build(self, items: list[tuple[AnalysisResult, AIProviderConfig]]) -> list:
         ids = self.build_prompts(items)
-        return self._admit_many(items, ids) if self._batch_admit else ids
+        return self._admit_many(items, ids)
 
     def _admit_many(self, items: list[tuple[AnalysisResult, AIProviderConfig]],
                     prompts: list[list[int]]) -> list[_Pending | AIResponse | BaseException]:
@@ -335,8 +331,6 @@ class ExplainEngine:
         (except a failure to admit a single coalesced item, raised as before)."""
         if len(items) == 1 and self.prompts.is_alive():   # one caller of many: coalesced with the others
             pend = [self.prompts.build(*items[0])]
-            if not self._batch_admit:
-                pend = self._admit_many(items, pend)
         else:
             pend = self._admit_many(items, self.build_prompts(items))
         if len(pend) == 1 and isinstance(pend[0], BaseException):
