@@ -391,9 +391,12 @@ __global__ void __launch_bounds__(512) attn_prefill_gqa_kernel(
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x8 __attribute__((ext_vector_type(8)));
 
-// K tile image: 256-B rows, chunk ch of row r at 16 * (ch ^ (r & 15)) -> the
-// ds_read_b128 of 16 consecutive rows at one chunk hits 16 distinct chunk slots.
-__device__ __forceinline__ int k_img(int r, int ch) { return 256 * r + 16 * (ch ^ (r & 15)); }
+// K tile image: rows padded to 272 B (kRowK), chunk ch of row r at 272 r + 16 ch -> the
+// ds_read_b128 of 16 consecutive rows at one chunk hits 16 distinct bank groups, and a
+// lane's reads of one tile are its row base plus compile-time offsets (no per-read
+// address arithmetic, unlike an XOR swizzle).
+constexpr int kRowK = 272;
+__device__ __forceinline__ int k_img(int r, int ch) { return kRowK * r + 16 * ch; }
 // V tile image (§5.5 T10 image (b)): conflict-free for the 32x32x16 transposed reads.
 __device__ __forceinline__ int v_img(int r, int ch) { return 256 * r + 16 * (ch ^ (((r & 3) << 2) | ((r >> 2) & 3))); }
 
@@ -426,7 +429,7 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_prefill_mfma32_kernel(
   constexpr int D = 128, BK = 64, RG = NW / G, BQ = 32 * RG;
   constexpr int NT = NW * 64, NC = BK * 16 / NT;   // threads; 16-B K (and V) chunks each stages per tile
   static_assert(RG >= 1, "a workgroup needs a row block per head");
-  __shared__ __attribute__((aligned(16))) char Ks[BK * 256];
+  __shared__ __attribute__((aligned(16))) char Ks[BK * kRowK];
   __shared__ __attribute__((aligned(16))) char Vs[BK * 256];
 
   const int wi = blockIdx.x, kvh = blockIdx.y;
