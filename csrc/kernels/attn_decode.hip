@@ -442,12 +442,40 @@ __global__ void __launch_bounds__(1024) attn_decode_combine_q8_kernel(
     int max_tokens, int chunk) {
   constexpr int D = 128;
   constexpr int NT = 1024;
+  constexpr int kMaxStats = 2048;   // Hq x splits per row staged in LDS (host-checked)
   __shared__ float red[NT / 64];
+  // per (head, split): the split's running max, then its combine weight; per head: the row sum.
+  // Loaded by all threads at once (one round trip) instead of a dependent load per split in
+  // every element's loop (two chains of `splits` L2 round trips per element).
+  __shared__ float wst[kMaxStats];
+  __shared__ float lst[kMaxStats];
   const int b = blockIdx.x, tid = threadIdx.x;
   const int len = min(seq_lens[b], max_tokens);
   const int per = len > 0 ? split_len(len, num_splits, chunk) : 1;
   const int ns = len > 0 ? (len + per - 1) / per : 1;
+  const bool split = !(len <= 0 || ns == 1 || num_splits == 1);
   const int n = Hq * D;
+  if (split) {
+    for (int i = tid; i < Hq * ns; i += NT) {
+      const int h = i / ns, sp = i - h * ns;
+      const float* ml = ml_part + (((int64_t)b * Hq + h) * num_splits + sp) * 2;
+      wst[i] = ml[0];
+      lst[i] = ml[1];
+    }
+    __syncthreads();
+    if (tid < Hq) {   // the same order and arithmetic as attn_decode_combine_kernel
+      float M = -INFINITY;
+      for (int sp = 0; sp < ns; ++sp) M = fmaxf(M, wst[tid * ns + sp]);
+      float L = 0.f;
+      for (int sp = 0; sp < ns; ++sp) {
+        const float wgt = exp2f(wst[tid * ns + sp] - M);
+        L += wgt * lst[tid * ns + sp];
+        wst[tid * ns + sp] = wgt;
+      }
+      lst[tid * ns] = L;
+    }
+    __syncthreads();
+  }
   float v[MAXV];
   float amax = 0.f;
 #pragma unroll
@@ -457,18 +485,23 @@ __global__ void __launch_bounds__(1024) attn_decode_combine_q8_kernel(
     if (e < n) {
       const int h = e / D, d = e % D;
       const int64_t bh = (int64_t)b * Hq + h;
-      if (len <= 0 || ns == 1 || num_splits == 1) {
+      if (!split) {
         v[i] = bf2f(out[bh * D + d]);
       } else {
-        const float* ml = ml_part + bh * num_splits * 2;
-        float M = -INFINITY;
-        for (int s = 0; s < ns; ++s) M = fmaxf(M, ml[2 * s]);
-        float L = 0.f, o = 0.f;
-        for (int s = 0; s < ns; ++s) {
-          const float wgt = exp2f(ml[2 * s] - M);
-          L += wgt * ml[2 * s + 1];
-          o += wgt * o_part[(bh * num_splits + s) * D + d];
+        const float* op = o_part + bh * num_splits * D + d;
+        const float* wg = wst + h * ns;
+        float o = 0.f;
+        int sp = 0;
+        for (; sp + 4 <= ns; sp += 4) {   // four independent loads in flight
+          const float x0 = op[(int64_t)sp * D], x1 = op[(int64_t)(sp + 1) * D];
+          const float x2 = op[(int64_t)(sp + 2) * D], x3 = op[(int64_t)(sp + 3) * D];
+          o += wg[sp] * x0;
+          o += wg[sp + 1] * x1;
+          o += wg[sp + 2] * x2;
+          o += wg[sp + 3] * x3;
         }
+        for (; sp < ns; ++sp) o += wg[sp] * op[(int64_t)sp * D];
+        const float L = lst[h * ns];
         v[i] = bf2f(f2bf(L > 0.f ? o / L : 0.f));
       }
       amax = fmaxf(amax, fabsf(v[i]));
@@ -554,6 +587,7 @@ int attn_decode(const bf16_t* q, const void* k_cache, const void* v_cache, bool 
   OAMD_LAUNCH_CHECK();
   if (q8 != nullptr) {   // combine (if split) + per-token e4m3fn rows for the fp8 o-projection
     const int n = Hq * 128;
+    if (Hq * num_splits > 2048) return -7;   // attn_decode_combine_q8_kernel's LDS statistics
     if (n <= 1024)
       attn_decode_combine_q8_kernel<1><<<B, 1024, 0, stream>>>(o_part, ml_part, seq_lens, out, q8, sx, Hq, num_splits,
                                                                max_pages * page_size, chunk);
