@@ -147,7 +147,9 @@ __global__ void __launch_bounds__(f8::kWaves * 64, 1)
 // projection's input quantization in one kernel.
 // P (SILU only): the gate|up rows are S fp32 split-K slabs [S, M, 2K] instead of bf16 `x`;
 // they are summed in slab order and bf16-rounded first (== splitk_reduce_fp32 then SILU).
-template <int MAXV, bool SILU>
+// SC (SILU with slabs): compile-time slab count, so every slab load of an element is issued
+// before the first add (0: runtime S, one slab per loop trip).
+template <int MAXV, bool SILU, int SC = 0>
 __global__ void __launch_bounds__(256) quantize_rows_reg_kernel(const bf16_t* __restrict__ x, uint8_t* __restrict__ q,
                                                                 float* __restrict__ sx, int K, int64_t ld,
                                                                 const float* __restrict__ P, int S) {
@@ -169,12 +171,31 @@ __global__ void __launch_bounds__(256) quantize_rows_reg_kernel(const bf16_t* __
           const float* pr = P + m * 2 * K + c;
           f32x4 g0 = *reinterpret_cast<const f32x4*>(pr), g1 = *reinterpret_cast<const f32x4*>(pr + 4);
           f32x4 u0 = *reinterpret_cast<const f32x4*>(pr + 64), u1 = *reinterpret_cast<const f32x4*>(pr + 68);
-          for (int s = 1; s < S; ++s) {
-            const float* ps = pr + s * MN;
-            g0 += *reinterpret_cast<const f32x4*>(ps);
-            g1 += *reinterpret_cast<const f32x4*>(ps + 4);
-            u0 += *reinterpret_cast<const f32x4*>(ps + 64);
-            u1 += *reinterpret_cast<const f32x4*>(ps + 68);
+          if constexpr (SC > 1) {
+            f32x4 sl[SC - 1][4];
+#pragma unroll
+            for (int s = 1; s < SC; ++s) {
+              const float* ps = pr + s * MN;
+              sl[s - 1][0] = *reinterpret_cast<const f32x4*>(ps);
+              sl[s - 1][1] = *reinterpret_cast<const f32x4*>(ps + 4);
+              sl[s - 1][2] = *reinterpret_cast<const f32x4*>(ps + 64);
+              sl[s - 1][3] = *reinterpret_cast<const f32x4*>(ps + 68);
+            }
+#pragma unroll
+            for (int s = 1; s < SC; ++s) {   // slab order, as splitk_reduce_fp32
+              g0 += sl[s - 1][0];
+              g1 += sl[s - 1][1];
+              u0 += sl[s - 1][2];
+              u1 += sl[s - 1][3];
+            }
+          } else if constexpr (SC == 0) {
+            for (int s = 1; s < S; ++s) {
+              const float* ps = pr + s * MN;
+              g0 += *reinterpret_cast<const f32x4*>(ps);
+              g1 += *reinterpret_cast<const f32x4*>(ps + 4);
+              u0 += *reinterpret_cast<const f32x4*>(ps + 64);
+              u1 += *reinterpret_cast<const f32x4*>(ps + 68);
+            }
           }
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
@@ -274,10 +295,20 @@ int silu_quantize_fp8(const bf16_t* gu, const float* P, int S, uint8_t* q, float
   if (M == 0) return 0;
   if (inter % 64 != 0 || (gu == nullptr) == (P == nullptr) || S < 1) return -1;
   const int nv = inter / 8;
-  if (nv <= 256 * 2) quantize_rows_reg_kernel<2, true><<<M, 256, 0, stream>>>(gu, q, sx, inter, ld, P, S);
-  else if (nv <= 256 * 4) quantize_rows_reg_kernel<4, true><<<M, 256, 0, stream>>>(gu, q, sx, inter, ld, P, S);
-  else if (nv <= 256 * 8) quantize_rows_reg_kernel<8, true><<<M, 256, 0, stream>>>(gu, q, sx, inter, ld, P, S);
+  const int sc = P == nullptr ? 1 : S;
+#define OAMD_SQ(MV)                                                                                       \
+  switch (sc) {                                                                                           \
+    case 1: quantize_rows_reg_kernel<MV, true, 1><<<M, 256, 0, stream>>>(gu, q, sx, inter, ld, P, S); break; \
+    case 2: quantize_rows_reg_kernel<MV, true, 2><<<M, 256, 0, stream>>>(gu, q, sx, inter, ld, P, S); break; \
+    case 4: quantize_rows_reg_kernel<MV, true, 4><<<M, 256, 0, stream>>>(gu, q, sx, inter, ld, P, S); break; \
+    case 8: quantize_rows_reg_kernel<MV, true, 8><<<M, 256, 0, stream>>>(gu, q, sx, inter, ld, P, S); break; \
+    default: quantize_rows_reg_kernel<MV, true, 0><<<M, 256, 0, stream>>>(gu, q, sx, inter, ld, P, S); break; \
+  }
+  if (nv <= 256 * 2) { OAMD_SQ(2) }
+  else if (nv <= 256 * 4) { OAMD_SQ(4) }
+  else if (nv <= 256 * 8) { OAMD_SQ(8) }
   else return -2;
+#undef OAMD_SQ
   OAMD_LAUNCH_CHECK();
   return 0;
 }

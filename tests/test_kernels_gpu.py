@@ -282,10 +282,12 @@ def test_silu_quantize_fp8_matches_unfused(inter):
     assert (got == want).float().mean() > 0.99
 
 
-def test_silu_quantize_fp8_from_splitk_slabs():
-    """SplitK gate|up slabs -> summed + bf16-rounded in-kernel == reduce then fused kernel."""
+@pytest.mark.parametrize("S", [2, 3, 4, 8])
+def test_silu_quantize_fp8_from_splitk_slabs(S):
+    """SplitK gate|up slabs -> summed + bf16-rounded in-kernel == reduce then fused kernel
+    (S = 2, 4, 8: compile-time slab counts, every load issued first; 3: the runtime loop)."""
     torch.manual_seed(11)
-    S, M, inter = 4, 23, 3584
+    M, inter = 23, 3584
     P = torch.randn(S, M, 2 * inter, device="cuda") / 2
     a = P[0].clone()
     for k in range(1, S):
