@@ -216,9 +216,27 @@ __global__ void __launch_bounds__(car::kThreads) oneshot_ar_rmsnorm_kernel(
     if constexpr (SLABS) {
       const float* pv = slabs + v * 8;
       f32x4 a0 = *reinterpret_cast<const f32x4*>(pv), a1 = *reinterpret_cast<const f32x4*>(pv + 4);
-      for (int s = 1; s < S; ++s) {
-        a0 += *reinterpret_cast<const f32x4*>(pv + s * MN);
-        a1 += *reinterpret_cast<const f32x4*>(pv + s * MN + 4);
+      if (S == 2) {   // the usual decode split: both slabs' loads in flight together
+        const f32x4 b0 = *reinterpret_cast<const f32x4*>(pv + MN), b1 = *reinterpret_cast<const f32x4*>(pv + MN + 4);
+        a0 += b0;
+        a1 += b1;
+      } else if (S == 4) {
+        f32x4 b[3][2];
+#pragma unroll
+        for (int s = 1; s < 4; ++s) {
+          b[s - 1][0] = *reinterpret_cast<const f32x4*>(pv + s * MN);
+          b[s - 1][1] = *reinterpret_cast<const f32x4*>(pv + s * MN + 4);
+        }
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {   // slab order
+          a0 += b[s][0];
+          a1 += b[s][1];
+        }
+      } else {
+        for (int s = 1; s < S; ++s) {
+          a0 += *reinterpret_cast<const f32x4*>(pv + s * MN);
+          a1 += *reinterpret_cast<const f32x4*>(pv + s * MN + 4);
+        }
       }
       x = make_uint4(pack_bf2(a0[0], a0[1]), pack_bf2(a0[2], a0[3]), pack_bf2(a1[0], a1[1]), pack_bf2(a1[2], a1[3]));
     } else {

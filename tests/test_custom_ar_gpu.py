@@ -81,29 +81,29 @@ def _worker(rank: int, world: int, port: int, q) -> None:
             assert torch.equal(h, h_ref), (rows, hidden, (h.float() - h_ref.float()).abs().max())
             torch.testing.assert_close(y.float(), y_ref.float(), atol=1e-2, rtol=1e-2)
             # split-K slabs in (summed in slab order, bf16-rounded) and e4m3fn rows out
-            S = 4
-            ps = [(_inputs(50 + r, S * rows * hidden, torch.float32, call) / S).view(S, rows, hidden)
-                  for r in range(world)]
-            ts = []
-            for pr in ps:
-                a = pr[0].clone()
-                for k in range(1, S):
-                    a += pr[k]
-                ts.append(a.to(torch.bfloat16))
-            ssum = sum(x.float() for x in ts).to(torch.bfloat16).to(dev)
-            y_ref, h_ref = _rmsnorm_fp32(ssum, wv, 1e-5, h0)
-            h = h0.clone()
-            slabs = ops.SplitK(ps[rank].reshape(-1).to(dev), S, rows, hidden)
-            q8, sx = grp.all_reduce_rmsnorm(slabs, wv, 1e-5, residual=h, quant=True)
-            torch.cuda.synchronize()
-            assert torch.equal(h, h_ref), ("slabs", rows, hidden, (h.float() - h_ref.float()).abs().max())
-            # the e4m3fn rows: per-row scale max|y| / 448 of the fp32-formula y, then round
-            amax = y_ref.float().abs().amax(-1)
-            s_ref = torch.where(amax > 0, amax / 448.0, torch.ones_like(amax))
-            q_ref = (y_ref.float() / s_ref[:, None]).clamp(-448, 448).to(torch.float8_e4m3fn)
-            torch.testing.assert_close(sx, s_ref, rtol=2e-2, atol=0)
-            deq, deq_ref = q8.float() * sx[:, None], q_ref.float() * s_ref[:, None]
-            torch.testing.assert_close(deq, deq_ref, atol=3e-2 * float(deq_ref.abs().max()), rtol=0.07)
+            for S in (2, 3, 4):   # two- and four-slab paths load every slab together; 3: the loop
+                ps = [(_inputs(50 + r, S * rows * hidden, torch.float32, call) / S).view(S, rows, hidden)
+                      for r in range(world)]
+                ts = []
+                for pr in ps:
+                    a = pr[0].clone()
+                    for k in range(1, S):
+                        a += pr[k]
+                    ts.append(a.to(torch.bfloat16))
+                ssum = sum(x.float() for x in ts).to(torch.bfloat16).to(dev)
+                y_ref, h_ref = _rmsnorm_fp32(ssum, wv, 1e-5, h0)
+                h = h0.clone()
+                slabs = ops.SplitK(ps[rank].reshape(-1).to(dev), S, rows, hidden)
+                q8, sx = grp.all_reduce_rmsnorm(slabs, wv, 1e-5, residual=h, quant=True)
+                torch.cuda.synchronize()
+                assert torch.equal(h, h_ref), ("slabs", rows, hidden, (h.float() - h_ref.float()).abs().max())
+                # the e4m3fn rows: per-row scale max|y| / 448 of the fp32-formula y, then round
+                amax = y_ref.float().abs().amax(-1)
+                s_ref = torch.where(amax > 0, amax / 448.0, torch.ones_like(amax))
+                q_ref = (y_ref.float() / s_ref[:, None]).clamp(-448, 448).to(torch.float8_e4m3fn)
+                torch.testing.assert_close(sx, s_ref, rtol=2e-2, atol=0)
+                deq, deq_ref = q8.float() * sx[:, None], q_ref.float() * s_ref[:, None]
+                torch.testing.assert_close(deq, deq_ref, atol=3e-2 * float(deq_ref.abs().max()), rtol=0.07)
             t = xs[rank].reshape(-1).to(dev)
             grp.all_reduce_(t)                      # a plain call in between
             torch.cuda.synchronize()
