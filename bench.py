@@ -271,7 +271,7 @@ def main() -> int:
     from operator_amd.engine.pool import PoolExplainService, PoolMatchService
     from operator_amd.engine.service import LocalExplainService, LocalMatchService
     from operator_amd.kube.fake import FakeKube, failed_pod, running_pod
-    from operator_amd.kube.resources import AIPROVIDERS, PODMORTEMS, PODS
+    from operator_amd.kube.resources import AIPROVIDERS, EVENTS, PODMORTEMS, PODS
     from operator_amd.utils.tracing import mark, trace_range
 
     s = settings(dev, a.max_batch, int(os.environ.get("OAMD_BENCH_WORLD", world)) if child else world)
@@ -570,6 +570,29 @@ def main() -> int:
         for o, n in r["outcomes"].items():
             counter["outcomes"][o] = counter["outcomes"].get(o, 0) + n
 
+    # whole-job outcomes (every rank's analyses) and, with one API server, its own record of
+    # them: every bench pod must carry exactly one PodmortemAnalysisComplete Event (each
+    # failure analysed once, by exactly one operator shard). Untimed: after the timed pass.
+    job_outcomes = dict(counter["outcomes"])
+    if world > 1:
+        allo: list = [None] * world
+        dist.all_gather_object(allo, counter["outcomes"])
+        job_outcomes = {}
+        for d in allo:
+            for o, n in d.items():
+                job_outcomes[o] = job_outcomes.get(o, 0) + n
+    audit = None
+    if a.mode == "pipeline" and (rank == 0 or not rest):
+        per_pod: dict[str, int] = {}
+        for ev in fk.list(EVENTS, "default"):
+            reg = ev.get("regarding") or {}
+            if ev.get("reason") == "PodmortemAnalysisComplete" and reg.get("kind") == "Pod" \
+                    and reg.get("name", "").startswith("app-r"):
+                per_pod[reg["name"]] = per_pod.get(reg["name"], 0) + 1
+        counts = list(per_pod.values())
+        audit = {"pods_with_complete_event": len(per_pod), "max_complete_events_per_pod": max(counts, default=0),
+                 "expected_pods": a.batch * waves * (world if rest else 1)}   # inproc: this process's shard
+
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev if info.backend == "nccl" else "cpu")
     p50_local = statistics.median(lat) if lat else float("nan")
     p50 = torch.tensor([p50_local], dtype=torch.float64, device=el.device)
@@ -625,6 +648,9 @@ def main() -> int:
                    "decode_windows_ahead": stats1.get("decode_windows_ahead", 0) - stats0.get("decode_windows_ahead", 0),
                    "no_pipeline": stats1.get("no_pipeline", {}),
                    "decode_tok_s_per_gpu": round(dtoks / elapsed, 1), "outcomes": counter["outcomes"],
+                   "outcomes_all_ranks": job_outcomes,
+                   # the API server's Events (rest: the one server every rank used; warmup waves included)
+                   "apiserver_audit": audit,
                    "dfa_states": stats1["dfa_states"], "timed_monotonic_ns": [mono0, mono1],
                    "rccl_world": dist.get_world_size() if dist.is_initialized() else 1,
                    "dist_backend": info.backend,

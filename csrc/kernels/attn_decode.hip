@@ -536,6 +536,8 @@ int attn_decode(const bf16_t* q, const void* k_cache, const void* v_cache, bool 
   if (page_size < 16 || (page_size & (page_size - 1)) != 0) return -2;
   if (max_pages > kMaxPagesLds) return -4;
   if (num_splits < 1) return -5;
+  // validate every launch of this call before the first one: nothing is enqueued on a bad shape
+  if (q8 != nullptr && Hq * 128 > 8192) return -6;
   int log2p = 0;
   while ((1 << log2p) < page_size) ++log2p;
   const int G = Hq / Hkv;
@@ -587,18 +589,26 @@ int attn_decode(const bf16_t* q, const void* k_cache, const void* v_cache, bool 
   OAMD_LAUNCH_CHECK();
   if (q8 != nullptr) {   // combine (if split) + per-token e4m3fn rows for the fp8 o-projection
     const int n = Hq * 128;
-    if (Hq * num_splits > 2048) return -7;   // attn_decode_combine_q8_kernel's LDS statistics
+    int q8_splits = num_splits;
+    if (num_splits > 1 && Hq * num_splits > 2048) {
+      // more (head, split) statistics than attn_decode_combine_q8_kernel stages in LDS (e.g. a
+      // 64-head model at 64 splits): combine into `out` with the plain kernel first, then
+      // quantize those bf16 rows (num_splits = 1 makes the q8 kernel read `out`) -- the same
+      // bf16 values, one extra pass over the row
+      attn_decode_combine_kernel<<<B * Hq, 128, 0, stream>>>(o_part, ml_part, seq_lens, out, Hq, num_splits,
+                                                             max_pages * page_size, chunk);
+      OAMD_LAUNCH_CHECK();
+      q8_splits = 1;
+    }
     if (n <= 1024)
-      attn_decode_combine_q8_kernel<1><<<B, 1024, 0, stream>>>(o_part, ml_part, seq_lens, out, q8, sx, Hq, num_splits,
+      attn_decode_combine_q8_kernel<1><<<B, 1024, 0, stream>>>(o_part, ml_part, seq_lens, out, q8, sx, Hq, q8_splits,
                                                                max_pages * page_size, chunk);
     else if (n <= 4096)
       attn_decode_combine_q8_kernel<4><<<B, 1024, 0, stream>>>(o_part, ml_part, seq_lens, out, q8, sx, Hq,
-                                                               num_splits, max_pages * page_size, chunk);
-    else if (n <= 8192)
-      attn_decode_combine_q8_kernel<8><<<B, 1024, 0, stream>>>(o_part, ml_part, seq_lens, out, q8, sx, Hq,
-                                                               num_splits, max_pages * page_size, chunk);
+                                                               q8_splits, max_pages * page_size, chunk);
     else
-      return -6;
+      attn_decode_combine_q8_kernel<8><<<B, 1024, 0, stream>>>(o_part, ml_part, seq_lens, out, q8, sx, Hq,
+                                                               q8_splits, max_pages * page_size, chunk);
     OAMD_LAUNCH_CHECK();
     return 0;
   }

@@ -38,7 +38,9 @@ __device__ __forceinline__ void st_granule(uint64_t* p, uint64_t v) {
 
 }  // namespace
 
-// state: [0] = tile counter (low 32 bits) + 1 pad word, [2 .. 2 + tiles) = tile granules
+// state: [0] = tile counter (low 32 bits), [1] = error word (non-zero: a look-back gave up
+// and this launch's prefix is wrong -- the host reruns the batch on the CPU path),
+// [2 .. 2 + tiles) = tile granules
 __global__ void __launch_bounds__(kLpThreads) line_prefix_kernel(const uint32_t* __restrict__ cnt, int64_t n,
                                                                  int64_t* __restrict__ excl,
                                                                  uint64_t* __restrict__ state) {
@@ -85,7 +87,10 @@ __global__ void __launch_bounds__(kLpThreads) line_prefix_kernel(const uint32_t*
         const uint64_t g = ld_granule(gran + j);   // every lane reads the same word
         const uint64_t st = g & ~kValMask;
         if (st == 0) {
-          if (++spins > kSpinMax) break;   // bounded: a stalled predecessor cannot hang the GPU
+          if (++spins > kSpinMax) {   // bounded: a stalled predecessor cannot hang the GPU;
+            if (lane == 0) st_granule(state + 1, 1ull);   // flag the launch, never a silent prefix
+            break;
+          }
           __builtin_amdgcn_s_sleep(1);
           continue;
         }

@@ -616,14 +616,31 @@ class LLMEngine:
         fb = ForwardBatch(torch.tensor(best, dtype=torch.long, device=dev), torch.arange(n, device=dev), slots, True,
                           torch.tensor([n - 1], dtype=torch.long, device=dev), seq_lens=[n], prefill_work=work,
                           kv_sink=sink)
-        with trace_range(f"prefix[{n}]"):
-            self.model.forward(fb, self.kv)
+        try:
+            with trace_range(f"prefix[{n}]"):
+                self.model.forward(fb, self.kv)
+        except BaseException:
+            # the pages belong to no request yet: _fail_all would never see them
+            self.kv.allocator.release(pages)
+            raise
         if cur is not None:
             cur.retired = True
             if cur.users == 0:
                 self.kv.allocator.release(cur.pages)
         self._pfx = _SharedPrefix(best, pages)
         self.stats.prefix_builds += 1
+
+    def _drop_idle_prefix(self) -> bool:
+        """Release the shared prefix's pages when no request holds them (admission would
+        otherwise turn a request away, or stall, for pages only the idle prefix occupies).
+        It is rebuilt once its prompts come back."""
+        cur = self._pfx
+        if cur is None or cur.users > 0:
+            return False
+        cur.retired = True
+        self.kv.allocator.release(cur.pages)
+        self._pfx = None
+        return True
 
     def has_work(self) -> bool:
         return bool(self.waiting or self.running or self._pf is not None)
@@ -741,6 +758,8 @@ class LLMEngine:
                 if out and toks + own > cap:
                     break
                 need = self.kv.pages_needed(len(r.prompt) + r.max_tokens) - (len(pf.pages) if shared else 0)
+                if need > self.kv.allocator.free and not shared and self._drop_idle_prefix():
+                    pf = None   # its pages were what stood in the way
                 if need > self.kv.allocator.free:
                     if not rows and not out:
                         r.error = "KV cache too small for request"

@@ -23,6 +23,7 @@ from __future__ import annotations
 
 import contextlib
 import gc
+import logging
 import os
 import threading
 import time
@@ -38,6 +39,8 @@ from operator_amd.patterns import oracle
 from operator_amd.patterns.compiler import CompiledPatterns, compile_patterns
 from operator_amd.patterns.schema import SEVERITIES, SEVERITY_RANK, PatternSet
 
+log = logging.getLogger(__name__)
+
 
 @dataclass
 class ScanStats:
@@ -47,6 +50,7 @@ class ScanStats:
     verified_hits: int = 0
     scan_ms: float = 0.0
     host_ms: float = 0.0
+    gpu_fallbacks: int = 0   # batches rescanned on the host after a GPU look-back timeout
 
 
 class LazyResults(Sequence):
@@ -354,6 +358,14 @@ class MatchEngine:
             C.line_prefix(seg_nl[:n_segs], excl, lp_state)
             C.scan_fixup(self._matches, self._count, excl[:n_segs], first_t, seg, seg_nl[n_segs:2 * n_segs])
             cnt = int(self._count.item())
+            if int(lp_state[1].item()) != 0:
+                # a line_prefix look-back hit its spin bound: the line numbers of this launch
+                # are wrong, so the batch is recomputed on the host path instead
+                log.warning("line_prefix look-back timed out; rescanning %d docs on the CPU path", len(docs))
+                self.stats.gpu_fallbacks += 1
+                self._resident = None
+                self._doc_newlines = None
+                return self.scan_cpu(docs)
             if cnt <= self._matches.shape[0]:
                 break
             self.match_cap = int(cnt * 1.25) + 1024  # overflow: grow and rescan (rare)

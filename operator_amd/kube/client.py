@@ -150,7 +150,10 @@ class _Pool:
     request costs ~0.25 ms of client CPU here against ~1.2 ms through httpx, and an
     operator shard issues ~11 API calls per analysis under its GIL (watch streams stay on
     httpx). A request that fails on a REUSED connection the server had already closed is
-    sent again once on a fresh one (nothing was processed for it)."""
+    sent again once on a fresh one when it failed before reaching the server (any method),
+    or when the reply was lost and the method is idempotent (GET/HEAD/PUT/DELETE/OPTIONS)."""
+
+    IDEMPOTENT = frozenset({"GET", "HEAD", "PUT", "DELETE", "OPTIONS"})
 
     def __init__(self, server: str, headers: dict, timeout_s: float, ca=None, cert=None):
         import ssl
@@ -197,12 +200,25 @@ class _Pool:
                 conn = self._new()
             try:
                 conn.request(method, self.prefix + path, body=body, headers=h)
-                r = conn.getresponse()
-                data = r.read()
-            except (http.client.RemoteDisconnected, ConnectionResetError, BrokenPipeError,
-                    http.client.CannotSendRequest):
+            except (ConnectionResetError, BrokenPipeError, http.client.CannotSendRequest):
+                # failed while SENDING on a connection the server had closed: the request
+                # never reached it, so any method may be sent again on a fresh connection
                 conn.close()
                 if reused and attempt == 0:
+                    continue
+                raise
+            except BaseException:
+                conn.close()
+                raise
+            try:
+                r = conn.getresponse()
+                data = r.read()
+            except (http.client.RemoteDisconnected, ConnectionResetError, BrokenPipeError):
+                # sent, then the connection dropped: the server may have processed it. Only
+                # idempotent methods are resent (a POST/PATCH twice could duplicate an Event
+                # or repeat a non-idempotent write)
+                conn.close()
+                if reused and attempt == 0 and method.upper() in self.IDEMPOTENT:
                     continue
                 raise
             except BaseException:

@@ -462,9 +462,12 @@ def test_rope_kv_writes_fp8_cache():
     assert torch.equal(vc.cpu().view(torch.uint8), exact.view(torch.uint8))
 
 
-@pytest.mark.parametrize("Hq,Hkv,splits,variant", [(8, 1, 8, 0), (8, 1, 1, 0), (32, 8, 4, 0), (64, 8, 2, 2)])
+@pytest.mark.parametrize("Hq,Hkv,splits,variant", [(8, 1, 8, 0), (8, 1, 1, 0), (32, 8, 4, 0), (64, 8, 2, 2),
+                                                   (64, 8, 64, 0), (40, 8, 64, 0)])
 def test_attn_decode_fused_quant_matches_quantized_output(Hq, Hkv, splits, variant):
-    """quant=True: the split-combine kernel's e4m3fn rows == quantize_fp8 of the bf16 output."""
+    """quant=True: the split-combine kernel's e4m3fn rows == quantize_fp8 of the bf16 output.
+    Hq x splits > 2048 (70B / Qwen2.5-32B heads at 64 splits) overflows the fused kernel's LDS
+    statistics and takes the combine-then-quantize path."""
     torch.manual_seed(21)
     B, D, page = 6, 128, 16
     lens = torch.tensor([1, 17, 300, 64, 129, 511], dtype=torch.int32)

@@ -305,3 +305,82 @@ def test_shard_per_gpu_env_and_jittered_retrier():
     ds = [r.delay(0.1) for _ in range(200)]
     assert 0.05 <= min(ds) < 0.07 and 0.13 < max(ds) <= 0.15
     assert Retrier(5, 0.1).delay(0.4) == 0.4
+
+
+def _drop_second_request_server():
+    """HTTP/1.1 server: answers the first request of every connection (keep-alive) and
+    drops the connection after READING the second one, unanswered -- the server may have
+    acted on it. Returns (port, seen list of methods, stop)."""
+    import socket
+    import threading
+
+    seen: list[str] = []
+    srv = socket.socket()
+    srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+    srv.bind(("127.0.0.1", 0))
+    srv.listen(8)
+    stop = threading.Event()
+
+    def read_req(f):
+        line = f.readline()
+        if not line:
+            return None
+        n = 0
+        while True:
+            h = f.readline()
+            if h in (b"\r\n", b"\n", b""):
+                break
+            k, _, v = h.decode().partition(":")
+            if k.strip().lower() == "content-length":
+                n = int(v)
+        if n:
+            f.read(n)
+        return line.split()[0].decode()
+
+    def conn_loop(c):
+        with c, c.makefile("rb") as f:
+            m = read_req(f)
+            if m is None:
+                return
+            seen.append(m)
+            c.sendall(b"HTTP/1.1 200 OK\r\nContent-Type: application/json\r\nContent-Length: 2\r\n\r\n{}")
+            m = read_req(f)
+            if m is not None:
+                seen.append(m)   # processed, then the reply is lost
+
+    def accept_loop():
+        srv.settimeout(0.2)
+        while not stop.is_set():
+            try:
+                c, _ = srv.accept()
+            except OSError:
+                continue
+            threading.Thread(target=conn_loop, args=(c,), daemon=True).start()
+
+    threading.Thread(target=accept_loop, daemon=True).start()
+    return srv.getsockname()[1], seen, lambda: (stop.set(), srv.close())
+
+
+def test_pool_resends_only_idempotent_requests_after_a_lost_reply():
+    """A request sent on a reused connection whose reply is lost is resent once for GET
+    (idempotent), never for POST (the server may already have created the object)."""
+    import http.client
+
+    from operator_amd.kube.client import _Pool
+
+    port, seen, stop = _drop_second_request_server()
+    try:
+        p = _Pool(f"http://127.0.0.1:{port}", {}, 5.0)
+        assert p.request("GET", "/a")[0] == 200
+        assert p.request("GET", "/a")[0] == 200          # lost reply on the reused conn -> resent
+        assert seen == ["GET", "GET", "GET"]
+        p.close()
+        seen.clear()
+        p = _Pool(f"http://127.0.0.1:{port}", {}, 5.0)
+        assert p.request("POST", "/e", b"{}")[0] == 200
+        with pytest.raises((http.client.RemoteDisconnected, ConnectionResetError)):
+            p.request("POST", "/e", b"{}")
+        assert seen == ["POST", "POST"]                  # not sent a third time
+        p.close()
+    finally:
+        stop()

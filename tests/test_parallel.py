@@ -176,3 +176,35 @@ def test_bench_two_ranks_gloo(shards, apiserver):
     assert out["config"]["operator_shards_per_gpu"] == shards
     assert out["detail"]["outcomes"] == {"ai-complete": 6 * shards} and out["value"] > 0
     assert out["config"]["apiserver"].startswith("one REST API server" if apiserver == "auto" else "in-process")
+
+
+def test_bench_eight_ranks_gloo_one_apiserver():
+    """The N = 8 launch exactly as the driver starts it (torch.distributed.run, 8 ranks,
+    127.0.0.1 rendezvous), on the CPU tier: rank 0 starts ONE REST API server and
+    broadcasts its URL, every rank is one operator shard against it, the world is checked
+    against --gpus, and every failure of every rank is analysed exactly once."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
+           "--gpus", "8", "--steps", "1", "--warmup", "1", "--model", "tiny", "--batch", "3",
+           "--max-tokens", "4", "--prompt-tokens", "128", "--log-kb", "4", "--patterns", "40"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd=root, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 8 and out["config"]["parallelism"] == "dp8" and out["config"]["global_batch"] == 24
+    assert out["detail"]["rccl_world"] == 8 and len(out["detail"]["per_rank_elapsed_s"]) == 8
+    assert out["config"]["apiserver"].startswith("one REST API server")
+    assert out["detail"]["outcomes"] == {"ai-complete": 3}              # rank 0's own timed wave
+    assert out["detail"]["outcomes_all_ranks"] == {"ai-complete": 24}   # 8 ranks x 3 failures
+    # the one API server's record: every pod of every rank (warmup waves too) has exactly one
+    # PodmortemAnalysisComplete Event -- each failure analysed once, by one operator shard
+    audit = out["detail"]["apiserver_audit"]
+    assert audit == {"pods_with_complete_event": 48, "max_complete_events_per_pod": 1, "expected_pods": 48}
+    assert out["value"] > 0

@@ -87,3 +87,55 @@ def test_engine_prefix_replaced_only_when_unused():
     eng2.generate([GenRequest(list(range(200, 240)), max_tokens=2, temperature=0.0, ignore_eos=True)
                    for _ in range(4)])
     assert eng2.stats.prefix_builds == 0 and eng2.prefix_pages == 0
+
+
+def test_prefix_build_failure_releases_its_pages():
+    """A forward that raises while the shared prefix is computed returns the prefix's
+    pages (they belong to no request yet, so nothing else would free them); the engine
+    then carries on and builds the prefix once the forward works again."""
+    cfg = get_config("tiny-gqa4")
+    m = LlamaModel(cfg, device="cpu", dtype=torch.float32).init_random(seed=13)
+    kv, eng = _engine(m, cfg, True)
+    head = list(range(100, 140))
+    real = m.forward
+
+    def boom(fb, cache):
+        if fb.kv_sink is not None:
+            raise RuntimeError("injected prefix forward failure")
+        return real(fb, cache)
+
+    m.forward = boom
+    reqs = [GenRequest(head + [i + 1], max_tokens=2, temperature=0.0, ignore_eos=True) for i in range(4)]
+    for r in reqs:
+        eng.submit(r)
+    raised = False
+    try:
+        for _ in range(100):
+            eng.step()
+    except RuntimeError:
+        raised = True
+    assert raised and eng._pfx is None
+    held = sum(len(r.pages) for r in reqs)   # admitted requests (running or mid-prefill)
+    assert kv.allocator.free + held == kv.num_pages   # nothing leaked by the failed build
+    m.forward = real
+    while any(not r.done for r in reqs):
+        eng.step()
+    assert kv.allocator.free + eng.prefix_pages == kv.num_pages
+
+
+def test_idle_prefix_gives_way_to_admission():
+    """When a request's pages do not fit only because an idle shared prefix (no users)
+    holds them, the prefix is dropped and the request admitted, not refused."""
+    cfg = get_config("tiny-gqa4")
+    m = LlamaModel(cfg, device="cpu", dtype=torch.float32).init_random(seed=14)
+    kv = PagedKVCache(cfg.layers, 12, cfg.kv_heads, cfg.head_dim, page_size=16, device="cpu", dtype=torch.float32)
+    eng = LLMEngine(m, kv, max_batch=2, max_context=256, use_graphs=False, prefix_sharing=True)
+    head = list(range(100, 140))
+    eng.generate([GenRequest(head + [i + 1], max_tokens=2, temperature=0.0, ignore_eos=True) for i in range(4)])
+    assert eng.prefix_pages == 2
+    # 12 pages, 2 held by the idle prefix: a request needing 11 fits only without it
+    big = GenRequest(list(range(500, 500 + 160)), max_tokens=16, temperature=0.0, ignore_eos=True)
+    assert kv.pages_needed(len(big.prompt) + big.max_tokens) == 11
+    eng.generate([big])
+    assert big.error is None and len(big.output) == 16
+    assert eng.prefix_pages == 0 and kv.allocator.free == kv.num_pages

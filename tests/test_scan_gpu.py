@@ -154,6 +154,7 @@ def test_line_prefix_equals_cumsum_and_replays():
         for _ in range(2):
             C.line_prefix(cnt, excl, st)
             assert torch.equal(excl.cpu(), ref), n
+            assert int(st[1]) == 0, n   # error word: no look-back gave up
         first = torch.tensor(sorted({0, n} | set(torch.randint(0, n + 1, (5,), generator=g).tolist())),
                              dtype=torch.int64)
         dn = torch.empty(len(first) - 1, dtype=torch.int64, device="cuda")

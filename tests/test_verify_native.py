@@ -53,26 +53,43 @@ def test_unsupported_constructs_fall_back_to_re(rx):
 
 _atoms = st.sampled_from([b"a", b"b", b"x", b"0", b".", b"\\d", b"\\w", b"\\s", b"[a-c]", b"[^ab]", b"[0-9x]",
                           b"\\b", b"^", b"$", b"A", b"-"])
+_quants = st.sampled_from([b"", b"*", b"+", b"?", b"{1,3}", b"*?", b"{2}"])
+
+
+@st.composite
+def _flat(draw):
+    """1-3 unquantified atoms: the body of a quantified group."""
+    return b"".join(draw(_atoms) for _ in range(draw(st.integers(1, 3))))
 
 
 @st.composite
 def _regex(draw, depth=0):
+    """Random regex in the verifier's subset, shaped so Python ``re`` (the oracle, a
+    backtracking matcher) stays polynomial: a quantified group holds only a flat run of
+    atoms -- never a nested quantifier or an alternation, the shapes that backtrack
+    exponentially (e.g. ``(.|[^ab])*A``) -- while unquantified groups may nest and
+    alternate freely."""
     parts = []
     for _ in range(draw(st.integers(1, 4))):
         kind = draw(st.integers(0, 6 if depth < 2 else 2))
+        q = b""
         if kind <= 2:
             a = draw(_atoms)
+            if a not in (b"\\b", b"^", b"$"):
+                q = draw(_quants)
         elif kind == 3:
             a = b"(" + draw(_regex(depth + 1)) + b"|" + draw(_regex(depth + 1)) + b")"
-        else:
+        elif kind == 4:
             a = b"(" + draw(_regex(depth + 1)) + b")"
-        if a not in (b"\\b", b"^", b"$"):
-            a += draw(st.sampled_from([b"", b"*", b"+", b"?", b"{1,3}", b"*?", b"{2}"]))
-        parts.append(a)
+        else:
+            a = b"(" + draw(_flat()) + b")"
+            q = draw(_quants)
+        parts.append(a + q)
     return b"".join(parts)
 
 
-@settings(max_examples=300, deadline=None)
+# derandomize: the same 300 examples every run, so the CPU tier's runtime is fixed
+@settings(max_examples=300, deadline=None, derandomize=True)
 @given(_regex(), st.lists(st.binary(min_size=0, max_size=24).map(lambda b: bytes(x % 128 for x in b if x != 10)),
                           min_size=1, max_size=12), st.booleans())
 def test_nfa_property_random_regexes(rx, lines, icase):

@@ -1,0 +1,188 @@
+// Per-CU ingest ceilings of the M = 256 decode GEMM (gate|up shape: X [256, 4096] bf16,
+// L2-resident; W [28672, 4096] bf16 streamed cold from HBM). Not production code: a
+// diagnostic that times the pieces of gemm_pp's K-loop in isolation on one MI355X --
+// LDS-DMA of the X and/or W regions only (no MFMA), MFMA on LDS only (no loads), and both
+// -- so the decode GEMM's limiter can be read off directly.
+//   hipcc --offload-arch=gfx950 -O3 -o ingest ingest.hip && ./ingest
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <vector>
+#include <algorithm>
+
+#define CK(x)                                                                        \
+  do {                                                                               \
+    hipError_t e_ = (x);                                                             \
+    if (e_ != hipSuccess) {                                                          \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_));      \
+      return 1;                                                                      \
+    }                                                                                \
+  } while (0)
+
+typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+
+constexpr int kRegion = 16384;  // 128 rows x 64 k bf16
+
+template <int N>
+__device__ __forceinline__ void vmw() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// NX X regions (128 token rows each) + NW W regions (128 weight rows each) per K-tile,
+// NBUF K-tiles of LDS ring; LOADS / MFMA switch the two halves of the work on and off.
+template <int NBUF, int NX, int NW, bool LOADS, bool MFMA, bool NT>
+__global__ void __launch_bounds__(512) ingest_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W,
+                                                     int K, float* __restrict__ sink) {
+  constexpr int NR = NX + NW;
+  constexpr int BUF = NR * kRegion;
+  __shared__ __attribute__((aligned(1024))) char lds[NBUF * BUF];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n0 = blockIdx.x * 128 * (NW > 0 ? NW : 1);
+  const int T = K / 64;
+  const int lrow = lane >> 3, lslot = lane & 7;
+  const uint16_t* src[4][2];   // fixed size: a template-sized array here drops the launch stub (hipcc 7.2)
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = 8 * (w + 8 * i) + lrow;
+      const int chunk = lslot ^ ((row >> 1) & 7);
+      if (r < NX) src[r][i] = X + (int64_t)(r * 128 + row) * K + chunk * 8;
+      else src[r][i] = W + (int64_t)(n0 + (r - NX) * 128 + row) * K + chunk * 8;
+    }
+  auto issue = [&](int buf, int kt) {
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      char* dst = lds + buf * BUF + r * kRegion;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        if (NT && r >= NX)
+          __builtin_amdgcn_global_load_lds(src[r][i] + kt * 64, (__attribute__((address_space(3))) void*)(dst + (w + 8 * i) * 1024), 16, 0, 2);
+        else
+          __builtin_amdgcn_global_load_lds(src[r][i] + kt * 64, (__attribute__((address_space(3))) void*)(dst + (w + 8 * i) * 1024), 16, 0, 0);
+      }
+    }
+  };
+  const int l15 = lane & 15, lq = lane >> 4, sw = (l15 >> 1) & 7;
+  const int g = w >> 2, wc = w & 3;
+  f32x4 acc[NX > 0 ? NX : 1][4][2];
+#pragma unroll
+  for (int h = 0; h < (NX > 0 ? NX : 1); ++h)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[h][b][0] = acc[h][b][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](const char* cur) {
+    u16x8 xf[NX > 0 ? NX : 1][4][2], wf[2][2];
+#pragma unroll
+    for (int h = 0; h < (NX > 0 ? NX : 1); ++h)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+          xf[h][b][s] = *reinterpret_cast<const u16x8*>(cur + h * kRegion + (g * 64 + b * 16 + l15) * 128 +
+                                                       (((4 * s + lq) ^ sw) << 4));
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        wf[e][s] = *reinterpret_cast<const u16x8*>(cur + NX * kRegion + (e * 64 + wc * 16 + l15) * 128 +
+                                                  (((4 * s + lq) ^ sw) << 4));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int h = 0; h < (NX > 0 ? NX : 1); ++h)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+          for (int e = 0; e < 2; ++e)
+            acc[h][b][e] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, wf[e][s]),
+                                                                   __builtin_bit_cast(bf16x8_t, xf[h][b][s]),
+                                                                   acc[h][b][e], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  if (LOADS) {
+#pragma unroll
+    for (int p = 0; p < NBUF - 1; ++p)
+      if (p < T) issue(p, p);
+  }
+  for (int t = 0; t < T; ++t) {
+    if (LOADS) {
+      if (t + NBUF - 2 < T) vmw<(NBUF - 2) * NR * 2>(); else vmw<0>();
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (LOADS && t + NBUF - 1 < T) issue((t + NBUF - 1) % NBUF, t + NBUF - 1);
+    if (MFMA) compute(lds + (t % NBUF) * BUF);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int h = 0; h < (NX > 0 ? NX : 1); ++h)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) s += acc[h][b][0][0] + acc[h][b][1][3];
+  if (!MFMA) s = reinterpret_cast<const float*>(lds)[tid];
+  sink[blockIdx.x * 512 + tid] = s;
+}
+
+template <int NBUF, int NX, int NW, bool LOADS, bool MFMA, bool NT>
+int run(const char* name, int grid, const uint16_t* X, const std::vector<uint16_t*>& Ws, int K, float* sink) {
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  auto launch = [&](int i) {
+    ingest_kernel<NBUF, NX, NW, LOADS, MFMA, NT><<<grid, 512>>>(X, Ws[i % Ws.size()], K, sink);
+  };
+  for (int i = 0; i < 6; ++i) launch(i);
+  CK(hipDeviceSynchronize());
+  const int iters = 30;
+  std::vector<float> ts;
+  for (int rep = 0; rep < 5; ++rep) {
+    CK(hipEventRecord(a));
+    for (int i = 0; i < iters; ++i) launch(i);
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    ts.push_back(ms * 1000.f / iters);
+  }
+  std::sort(ts.begin(), ts.end());
+  const double us = ts[2];
+  const double bytes_per_wg = (double)(NX + NW) * kRegion * (K / 64);
+  printf("{\"variant\": \"%s\", \"grid\": %d, \"nbuf\": %d, \"x_regions\": %d, \"w_regions\": %d, \"loads\": %d, "
+         "\"mfma\": %d, \"nt\": %d, \"us\": %.2f, \"ingest_gb_s_per_cu\": %.1f, \"w_tb_s\": %.2f}\n",
+         name, grid, NBUF, NX, NW, (int)LOADS, (int)MFMA, (int)NT, us, LOADS ? bytes_per_wg / us / 1e3 : 0.0,
+         LOADS && NW ? (double)grid * NW * kRegion * (K / 64) / us / 1e6 : 0.0);
+  fflush(stdout);
+  return 0;
+}
+
+int main() {
+  const int K = 4096, N = 28672, M = 256;
+  uint16_t* X;
+  CK(hipMalloc(&X, (size_t)M * K * 2));
+  CK(hipMemset(X, 0x3c, (size_t)M * K * 2));
+  std::vector<uint16_t*> Ws(3);
+  for (auto& w : Ws) {
+    CK(hipMalloc(&w, (size_t)N * K * 2));
+    CK(hipMemset(w, 0x3b, (size_t)N * K * 2));
+  }
+  float* sink;
+  CK(hipMalloc(&sink, 512 * 512 * 4));
+  // the gate|up tile of gemm_pp (2 X regions + 1 W region per K-tile, 3-deep ring), 224 workgroups
+  run<3, 2, 1, true, false, true>("loads_x2w1", 224, X, Ws, K, sink);
+  run<3, 0, 1, true, false, true>("loads_w1", 224, X, Ws, K, sink);
+  run<3, 2, 0, true, false, true>("loads_x2", 224, X, Ws, K, sink);
+  run<3, 2, 1, false, true, true>("mfma_only", 224, X, Ws, K, sink);
+  run<3, 2, 1, true, true, true>("loads_x2w1+mfma", 224, X, Ws, K, sink);
+  run<3, 2, 1, true, true, false>("loads_x2w1+mfma_default_policy", 224, X, Ws, K, sink);
+  run<2, 2, 1, true, false, true>("loads_x2w1_nbuf2", 224, X, Ws, K, sink);
+  // 2 W regions (BN = 256) per X read: half the X ingest per weight byte, 112 workgroups
+  run<2, 2, 2, true, false, true>("loads_x2w2_nbuf2", 112, X, Ws, K, sink);
+  // every CU: W-only stream at 256 workgroups (28672 / 112 rows would be the even split)
+  run<3, 0, 1, true, false, true>("loads_w1_g256", 224, X, Ws, K, sink);
+  return 0;
+}

@@ -8,6 +8,7 @@ import re
 ap = argparse.ArgumentParser()
 ap.add_argument("csv")
 ap.add_argument("--match", default="oamd", help="substring filter on the kernel name")
+ap.add_argument("--grid", action="store_true", help="key kernels by name AND grid size (one template, many shapes)")
 a = ap.parse_args()
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 dur = collections.defaultdict(dict)
@@ -16,6 +17,8 @@ for r in csv.DictReader(open(a.csv)):
     if not re.search(a.match, name):
         continue
     short = re.sub(r"\(.*", "", name)[:80]
+    if a.grid:
+        short += f" grid={r.get('Grid_Size') or r.get('Grid_Size_X', '?')}"
     agg[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
     dur[short][r["Dispatch_Id"]] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
 for k, cs in agg.items():
