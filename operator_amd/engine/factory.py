@@ -50,7 +50,7 @@ def build_llm(s: Settings, device: str | torch.device | None = None, tp=None):
                       k_scale=e.kv_scale, v_scale=e.kv_scale)
     kw = dict(max_batch=e.max_batch, max_prefill_tokens=e.max_prefill_tokens, max_context=e.max_context,
               use_graphs=e.use_graphs, multi_step=e.multi_step, admit_wait_s=e.admit_wait_ms / 1e3,
-              prefill_graphs=e.prefill_graphs, prefix_sharing=e.prefix_sharing and (tp is None or tp.world == 1))
+              prefill_graphs=e.prefill_graphs, prefix_sharing=e.prefix_sharing)
     if tp is not None and tp.world > 1:   # one replica over the TP group: lock-stepped engines
         from operator_amd.engine.tp import TPLLMEngine, control_group
 

@@ -162,3 +162,74 @@ def test_bench_tp_simulate_runs_one_rank_shard():
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][0])
     assert out["simulated_tp"] == 8 and out["tp"] == 8 and out["decode_tok_s"] > 0 and out["weight_floor_ms"] > 0
+
+
+SHARED_HEAD = list(range(100, 140))
+
+
+def _shared_reqs():
+    from operator_amd.engine.llm import GenRequest
+
+    return [GenRequest(SHARED_HEAD + list(range(3 + i, 10 + 2 * i)), max_tokens=6, temperature=0.0, ignore_eos=True)
+            for i in range(6)]
+
+
+def _tp_prefix_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from operator_amd.engine.tp import TPLLMEngine, control_group
+    from operator_amd.models.config import get_config
+    from operator_amd.models.kv_cache import PagedKVCache
+    from operator_amd.models.llama import LlamaModel
+    from operator_amd.parallel.comm import init_from_env, split_groups
+
+    init_from_env(backend="gloo")
+    tp, _ = split_groups(world)
+    cfg = get_config("tiny-tp8")
+    m = LlamaModel(cfg, device="cpu", tp=tp, dtype=torch.float32).init_random(seed=22)
+    kv = PagedKVCache(cfg.layers, 96, m.hkv, cfg.head_dim, 16, device="cpu", dtype=torch.float32)
+    eng = TPLLMEngine(m, kv, tp_group=tp, ctrl_group=control_group(tp), max_batch=2, max_context=256,
+                      use_graphs=False, prefix_sharing=True)
+    if tp.rank == 0:
+        reqs = _shared_reqs()
+        for r in reqs:
+            eng.submit(r)
+        while any(not r.done for r in reqs):
+            eng.step()
+        eng.close()
+        torch.save({"out": [r.output for r in reqs], "builds": eng.stats.prefix_builds,
+                    "hits": eng.stats.prefix_hits}, os.path.join(out_dir, "tp_pfx.pt"))
+    else:
+        eng.follow()
+        torch.save({"builds": eng.stats.prefix_builds, "hits": eng.stats.prefix_hits},
+                   os.path.join(out_dir, f"tp_pfx_{tp.rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_tp_prefix_sharing_matches_tp1(tmp_path):
+    """Shared prompt-prefix pages under TP = 4: the prefix is built at the same step on
+    every rank (admission replays the leader's submissions deterministically), the
+    followers share it exactly as the leader does, and greedy outputs equal a TP = 1
+    engine with sharing."""
+    from operator_amd.engine.llm import LLMEngine
+    from operator_amd.models.config import get_config
+    from operator_amd.models.kv_cache import PagedKVCache
+    from operator_amd.models.llama import LlamaModel
+
+    world = 4
+    mp.start_processes(_tp_prefix_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    got = torch.load(tmp_path / "tp_pfx.pt", weights_only=True)
+    assert got["builds"] == 1 and got["hits"] >= 3
+    for r in range(1, world):
+        f = torch.load(tmp_path / f"tp_pfx_{r}.pt", weights_only=True)
+        assert (f["builds"], f["hits"]) == (got["builds"], got["hits"])
+    cfg = get_config("tiny-tp8")
+    m = LlamaModel(cfg, device="cpu", dtype=torch.float32).init_random(seed=22)
+    kv = PagedKVCache(cfg.layers, 96, cfg.kv_heads, cfg.head_dim, 16, device="cpu", dtype=torch.float32)
+    eng = LLMEngine(m, kv, max_batch=2, max_context=256, use_graphs=False, prefix_sharing=True)
+    reqs = _shared_reqs()
+    eng.generate(reqs)
+    assert got["out"] == [r.output for r in reqs]
