@@ -45,17 +45,38 @@ struct ScanStream {
   bool active;
 };
 
-__device__ __forceinline__ void emit_matches(uint32_t state, uint32_t seg, uint32_t off, uint32_t nl,
-                                             const uint32_t* __restrict__ out_off,
-                                             const uint32_t* __restrict__ out_ids, MatchRec* __restrict__ matches,
-                                             uint32_t* __restrict__ count, uint32_t cap) {
-  const uint32_t b = out_off[state], e = out_off[state + 1];
-  for (uint32_t k = b; k < e; ++k) {
-    const uint32_t idx = atomicAdd(count, 1u);
-    if (idx < cap) {
-      MatchRec r;
-      r.x = seg; r.y = out_ids[k]; r.z = off; r.w = nl;
-      matches[idx] = r;
+// Append the output patterns of `state` for every lane with `emit` set: one atomicAdd on
+// the global counter per wave and round (ballot + popcount; the leader lane adds the
+// round's total, each lane's slot is its rank among the wave's emitting lanes), not one
+// per match -- a pattern that hits every line of a noisy log would otherwise serialise
+// its whole wave on the counter. Rounds = the largest output set among the wave's lanes
+// (usually 1). Correct under a partial EXEC mask: only active lanes take part.
+__device__ __forceinline__ void emit_matches_wave(bool emit, uint32_t state, uint32_t seg, uint32_t off, uint32_t nl,
+                                                  const uint32_t* __restrict__ out_off,
+                                                  const uint32_t* __restrict__ out_ids,
+                                                  MatchRec* __restrict__ matches, uint32_t* __restrict__ count,
+                                                  uint32_t cap) {
+  uint32_t k = 0, e = 0;
+  if (emit) {
+    k = out_off[state];
+    e = out_off[state + 1];
+  }
+  const int lane = threadIdx.x & 63;
+  for (;; ++k) {
+    const bool has = k < e;
+    const uint64_t m = __ballot(has);
+    if (m == 0) break;
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(count, static_cast<uint32_t>(__popcll(m)));
+    base = __shfl(base, leader, 64);
+    if (has) {
+      const uint32_t idx = base + static_cast<uint32_t>(__popcll(m & ((1ull << lane) - 1ull)));
+      if (idx < cap) {
+        MatchRec r;
+        r.x = seg; r.y = out_ids[k]; r.z = off; r.w = nl;
+        matches[idx] = r;
+      }
     }
   }
 }
@@ -129,8 +150,12 @@ __global__ void __launch_bounds__(kScanThreads) ac_scan_kernel(
             st[1].s = eb & 0x7fffu;
             if (own) {
               const uint32_t off = static_cast<uint32_t>(c * 64 + j * 16 + wd * 4 + by);
-              if (ea & 0x8000u) emit_matches(st[0].s, st[0].seg, off, st[0].nl, out_off, out_ids, matches, count, cap);
-              if (eb & 0x8000u) emit_matches(st[1].s, st[1].seg, off, st[1].nl, out_off, out_ids, matches, count, cap);
+              if (__ballot((ea & 0x8000u) != 0))
+                emit_matches_wave((ea & 0x8000u) != 0, st[0].s, st[0].seg, off, st[0].nl, out_off, out_ids, matches,
+                                  count, cap);
+              if (__ballot((eb & 0x8000u) != 0))
+                emit_matches_wave((eb & 0x8000u) != 0, st[1].s, st[1].seg, off, st[1].nl, out_off, out_ids, matches,
+                                  count, cap);
               st[0].nl += (ba == 10u);
               st[1].nl += (bb == 10u);
             }
@@ -280,11 +305,10 @@ __global__ void __launch_bounds__(NT) ac_scan_wide_kernel(
           if (sk >= Hs) e = tg[(sk << log2C) | cls[b]];
         }
         if (__ballot(own && (e & 0x8000u))) {
-          if (own && (e & 0x8000u)) {
-            const uint64_t p = static_cast<uint64_t>(at + 4 * d + by);
-            emit_matches(e & 0x7fffu, static_cast<uint32_t>(p >> seg_shift), static_cast<uint32_t>(p) & seg_mask,
-                         nl_now | ((mid >> k & 1u) << 31), out_off, out_ids, matches, count, cap);
-          }
+          const uint64_t p = static_cast<uint64_t>(at + 4 * d + by);
+          emit_matches_wave(own && (e & 0x8000u), e & 0x7fffu, static_cast<uint32_t>(p >> seg_shift),
+                            static_cast<uint32_t>(p) & seg_mask, nl_now | ((mid >> k & 1u) << 31), out_off, out_ids,
+                            matches, count, cap);
         }
         nl_now += (own && b == 10u);
         s = e;

@@ -41,6 +41,23 @@ from operator_amd.patterns.schema import SEVERITIES, SEVERITY_RANK, PatternSet
 
 log = logging.getLogger(__name__)
 
+_EVENT_FIELDS = frozenset(AnalysisEvent.model_fields)
+_SUMMARY_FIELDS = frozenset(AnalysisSummary.model_fields)
+_RESULT_FIELDS = frozenset(AnalysisResult.model_fields)
+_set_dict = object.__setattr__
+
+
+def _mk(cls, d: dict, fields: frozenset):
+    """A pydantic model from a COMPLETE dict of already-typed field values (the same
+    object KModel.fast builds when every field is given: fields set = all of them, no
+    extras), with the least Python per object."""
+    m = cls.__new__(cls)
+    _set_dict(m, "__dict__", d)
+    _set_dict(m, "__pydantic_fields_set__", set(fields))
+    _set_dict(m, "__pydantic_extra__", {})
+    _set_dict(m, "__pydantic_private__", None)
+    return m
+
 
 @dataclass
 class ScanStats:
@@ -201,6 +218,7 @@ class MatchEngine:
         self._verify = np.asarray(self.cp.matcher_verify + [False], dtype=bool)
         self._init_verifier()
         self._mp_cache: dict[int, MatchedPattern] = {}
+        self._pinfo: list | None = None   # per-pattern (severity rank, MatchedPattern, remediation)
         self.last_timing: dict[str, float] = {}   # stage split of the last analyze() (host seconds)
         if self.device.type == "cuda" and self.cp.factors:
             self._upload_dfa()
@@ -641,33 +659,45 @@ class MatchEngine:
                 id=p.id, name=p.name, severity=p.severity, category=p.category or None, library=p.library or None)
         return mp
 
+    def _pattern_info(self) -> list:
+        """Per pattern, built once: (severity rank, MatchedPattern, remediation or None)."""
+        if self._pinfo is None:
+            self._pinfo = [(p.severity_rank, self._matched(i), p.remediation or None)
+                           for i, p in enumerate(self.cp.patset.patterns)]
+        return self._pinfo
+
     def _result(self, doc: bytes, ev: list[oracle.Event], ctxs: list, pod, ms: float,
                 newlines: int | None = None, analysis_id: str | None = None) -> AnalysisResult:
-        pats = self.cp.patset.patterns
-        dist = {s: 0 for s in SEVERITIES}
+        # the hot host loop of a scan batch (4096 results for BASELINE config 2): per-pattern
+        # constants looked up once (_pattern_info), severities counted by rank, and every
+        # model built by _mk from a complete field dict (all fields given, so no defaults /
+        # factories to merge)
+        info = self._pattern_info()
+        counts = [0, 0, 0, 0, 0]
         sig = 0
         hi = -1
+        thr = self.significance
         for e in ev:
-            p = pats[e.pattern]
-            dist[p.severity] += 1
-            hi = max(hi, p.severity_rank)
-            if e.score >= self.significance:
+            r = info[e.pattern][0]
+            counts[r] += 1
+            if r > hi:
+                hi = r
+            if e.score >= thr:
                 sig += 1
         events = []
         for e, (ctx, line) in zip(ev[: self.max_events], ctxs):
-            p = pats[e.pattern]
-            # KModel.fast: these are the engine's own, already-typed values (validation was
-            # ~2/3 of the host time per result, model_construct's field walk most of the rest)
-            events.append(AnalysisEvent.fast(
-                line_number=e.line + 1, matched_pattern=self._matched(e.pattern),
-                score=round(e.score, 6), context=ctx, matched_line=line,
-                remediation=p.remediation or None))
-        summary = AnalysisSummary.fast(highest_severity=SEVERITIES[hi] if hi >= 0 else None,
-                                                  significant_events=sig, total_events=len(ev),
-                                                  severity_distribution={k: v for k, v in dist.items() if v})
-        return AnalysisResult.fast(
-            analysis_id=analysis_id or str(uuid.uuid4()), pod_name=pod[0], pod_namespace=pod[1], events=events, summary=summary,
-            metadata={"engine": "gpu-ac" if self.device.type == "cuda" else "cpu-oracle",
-                      "patternsChecked": len(pats),
-                      "totalLines": (doc.count(b"\n") if newlines is None else newlines) + 1,
-                      "bytes": len(doc), "processingTimeMs": round(ms, 3)})
+            _, mp, rem = info[e.pattern]
+            events.append(_mk(AnalysisEvent, {"line_number": e.line + 1, "matched_pattern": mp,
+                                              "score": round(e.score, 6), "context": ctx, "matched_line": line,
+                                              "remediation": rem}, _EVENT_FIELDS))
+        summary = _mk(AnalysisSummary, {"highest_severity": SEVERITIES[hi] if hi >= 0 else None,
+                                        "significant_events": sig, "total_events": len(ev),
+                                        "severity_distribution": {SEVERITIES[i]: c for i, c in enumerate(counts) if c}},
+                      _SUMMARY_FIELDS)
+        return _mk(AnalysisResult, {
+            "analysis_id": analysis_id or str(uuid.uuid4()), "pod_name": pod[0], "pod_namespace": pod[1],
+            "events": events, "summary": summary,
+            "metadata": {"engine": "gpu-ac" if self.device.type == "cuda" else "cpu-oracle",
+                         "patternsChecked": len(info),
+                         "totalLines": (doc.count(b"\n") if newlines is None else newlines) + 1,
+                         "bytes": len(doc), "processingTimeMs": round(ms, 3)}}, _RESULT_FIELDS)

@@ -255,3 +255,22 @@ def test_scan_match_overflow_regrows():
                         seg_bytes=256, match_cap=64, profile_bytes=0)
     assert small.scan_gpu([b"eee\n" * 500]).shape[0] == 1500 and small.match_cap >= 1500
     assert small.scan_gpu([b"eee\n" * 500]).shape[0] == 1500
+
+
+def test_noisy_log_every_line_matches_equals_cpu_scan():
+    """A pattern that hits every line of a noisy log (and one whose output set holds
+    several patterns: "ERROR" ends both "ERROR" and "RROR"): the wave-aggregated match
+    append (one counter atomic per wave and round) gives exactly the CPU scan's records."""
+    ps = PatternSet.from_dicts([
+        {"id": "err", "primary_pattern": {"literal": "ERROR"}},
+        {"id": "rror", "primary_pattern": {"literal": "RROR"}},
+        {"id": "ror", "primary_pattern": {"literal": "ROR"}},
+        {"id": "id", "primary_pattern": {"literal": "req-"}},
+    ])
+    eng = MatchEngine(ps, device="cuda", seg_bytes=1024)
+    docs = [b"".join(b"2025-08-29 ERROR req-%d failed\n" % i for i in range(40000)),
+            b"ERRORERRORERROR\n" * 3000, b"", b"no match here\n" * 100]
+    gpu = eng.scan_gpu(docs)
+    cpu = eng.scan_cpu(docs)
+    assert gpu.shape[0] == cpu.shape[0] > 4 * 40000
+    assert _rows(gpu) == _rows(cpu)
