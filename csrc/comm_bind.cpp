@@ -1,4 +1,4 @@
-// Binding for the one-shot IPC all-reduce (csrc/kernels/allreduce.hip):
+// Binding for the one-shot / two-shot IPC all-reduce (csrc/kernels/allreduce.hip):
 // operator_amd._C.CustomAllReduce. The handle exchange itself happens in
 // Python over the process group (operator_amd/parallel/custom_ar.py); this
 // object owns the local fine-grained buffer and the opened peer mappings.
@@ -49,7 +49,9 @@ class CustomAllReduce {
     opened_ = true;
   }
 
-  void all_reduce(const at::Tensor& in, at::Tensor& out) {
+  // proto: 0 one-shot, 1 two-shot (reduce-scatter + all-gather), 2 one-shot with the original
+  // system-fence hand-off (A/B)
+  void all_reduce(const at::Tensor& in, at::Tensor& out, int64_t proto) {
     TORCH_CHECK(opened_ || world_ == 1, "CustomAllReduce: open() the peer handles first");
     TORCH_CHECK(in.is_cuda() && out.is_cuda() && in.device().index() == device_, "tensors must be on this device");
     TORCH_CHECK(in.is_contiguous() && out.is_contiguous(), "tensors must be contiguous");
@@ -60,8 +62,9 @@ class CustomAllReduce {
     const c10::hip::HIPGuardMasqueradingAsCUDA g(in.device());
     const int rc = oamd::car_all_reduce(in.data_ptr(), out.data_ptr(), bytes, in.scalar_type() == at::kBFloat16,
                                         (int)rank_, (int)world_, bases_.data(), (size_t)cap_, (int)blocks_,
-                                        herr_dev_, timeout_s_, c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream());
-    TORCH_CHECK(rc == 0, "one-shot all-reduce launch failed rc=", rc);
+                                        herr_dev_, timeout_s_, (int)proto,
+                                        c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream());
+    TORCH_CHECK(rc == 0, "IPC all-reduce launch failed rc=", rc);
   }
 
   // residual += all_reduce(in) (bf16-rounded); y = rmsnorm(residual) * w — one launch.
@@ -69,7 +72,7 @@ class CustomAllReduce {
   // q8/sx given: y is also emitted as per-row e4m3fn for the next fp8 GEMM.
   void all_reduce_rmsnorm(const c10::optional<at::Tensor>& in, at::Tensor& residual, const at::Tensor& w,
                           at::Tensor& y, double eps, const c10::optional<at::Tensor>& slabs, int64_t splits,
-                          const c10::optional<at::Tensor>& q8, const c10::optional<at::Tensor>& sx) {
+                          const c10::optional<at::Tensor>& q8, const c10::optional<at::Tensor>& sx, int64_t proto) {
     TORCH_CHECK(opened_ || world_ == 1, "CustomAllReduce: open() the peer handles first");
     TORCH_CHECK(in.has_value() != slabs.has_value(), "exactly one of in / slabs");
     TORCH_CHECK(q8.has_value() == sx.has_value(), "q8 and sx together");
@@ -113,8 +116,8 @@ class CustomAllReduce {
         ip, sp, (int)splits, reinterpret_cast<oamd::bf16_t*>(residual.data_ptr()),
         reinterpret_cast<const oamd::bf16_t*>(w.data_ptr()), reinterpret_cast<oamd::bf16_t*>(y.data_ptr()), qp, xp,
         (int)rows, (int)hidden, (float)eps, (int)rank_, (int)world_, bases_.data(), (size_t)cap_, (int)blocks_,
-        herr_dev_, timeout_s_, c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream());
-    TORCH_CHECK(rc == 0, "one-shot all-reduce + rmsnorm launch failed rc=", rc);
+        herr_dev_, timeout_s_, (int)proto, c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream());
+    TORCH_CHECK(rc == 0, "IPC all-reduce + rmsnorm launch failed rc=", rc);
   }
 
   // Host read of the mapped error word: no device synchronisation, so the engine
@@ -165,10 +168,12 @@ void register_comm_bindings(pybind11::module_& m) {
            pybind11::arg("timeout_s") = 2.0)
       .def("handle", &CustomAllReduce::handle)
       .def("open", &CustomAllReduce::open)
-      .def("all_reduce", &CustomAllReduce::all_reduce)
+      .def("all_reduce", &CustomAllReduce::all_reduce, pybind11::arg("in"), pybind11::arg("out"),
+           pybind11::arg("proto") = 0)
       .def("all_reduce_rmsnorm", &CustomAllReduce::all_reduce_rmsnorm, pybind11::arg("in"), pybind11::arg("residual"),
            pybind11::arg("w"), pybind11::arg("y"), pybind11::arg("eps"), pybind11::arg("slabs") = pybind11::none(),
-           pybind11::arg("splits") = 1, pybind11::arg("q8") = pybind11::none(), pybind11::arg("sx") = pybind11::none())
+           pybind11::arg("splits") = 1, pybind11::arg("q8") = pybind11::none(), pybind11::arg("sx") = pybind11::none(),
+           pybind11::arg("proto") = 0)
       .def("error", &CustomAllReduce::error)
       .def("reset", &CustomAllReduce::reset)
       .def("close", &CustomAllReduce::close)

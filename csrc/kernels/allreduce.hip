@@ -1,37 +1,56 @@
-// One-shot all-reduce over peer-mapped HBM.
+// One-shot and two-shot all-reduce over peer-mapped HBM.
 //
 // Tensor-parallel decode all-reduces are small (M x hidden x 2 B: 16 KB per
-// token at 70B) and latency-bound. A ring all-reduce over xGMI takes
-// 2 (n - 1) dependent link hops; here every rank PUSHES its whole input into
-// a per-source slot of every peer's receive buffer (one hop over the direct
-// point-to-point link to each peer; the 7 links of an MI355X run in
-// parallel), raises a per-block flag in each peer, waits for the flags of all
-// peers and reduces the n slots from its OWN HBM. One kernel, one fabric hop.
+// token at 70B) and latency-bound; a ring all-reduce over xGMI takes 2 (n - 1)
+// dependent link hops. Two protocols, both one kernel, no host per call:
 //
-// Memory: each rank owns one fine-grained (uncached) allocation, exported
-// with hipIpcGetMemHandle and opened by every peer:
-//   [0, 2 KB)        flags[kMaxBlocks][kMaxRanks]  u32, written by peers
-//   [8 KB, 8 KB+256) rounds[kMaxBlocks]            u32, this rank's per-block call counter
-//   [12 KB]          err                           u32, set when a wait times out
-//   [64 KB, ...)     recv[2][world][cap]           parity-double-buffered slots
-// Ordering (cdna_hip_programming.md Guideline 16, at SYSTEM scope because the
-// producer is another device): data stores -> __threadfence_system ->
-// barrier -> release store of the flag into the peer; the consumer's acquire
-// load of its flag invalidates its caches before it reads the slots.
-// Round numbers are per block and kept on the device, so a call is a pure
-// kernel launch (capturable into a hipGraph) and ranks never exchange host
-// state per call. Parity buffers make slot reuse safe: a peer can be at most
-// one round ahead (it needs this rank's flag of round r+1 to finish r+1, and
-// that flag is raised only after this rank finished reading round r).
-// Every wait is bounded (wall clock, ~2 s by default): a missing peer sets
-// `err` and the kernel drains instead of spinning forever. A timed-out block
-// never leaves a partial sum behind: it writes NaN over its output slice, and
-// the error is STICKY — every later call sees `err` at entry, poisons its whole
-// output and touches no peer — because after a timeout the per-block round
-// counters of the ranks no longer agree, so the parity-buffer reuse invariant
-// above is gone. The error is mirrored into a host-mapped word, so the engine
-// polls it after each decode window with a plain host read (no device sync)
-// and fails the TP replica; the pool respawns it with fresh buffers.
+//  * ONE-SHOT: every rank PUSHES its whole input into a per-source slot of every
+//    peer's receive buffer (one hop over the direct point-to-point link to each
+//    peer; the 7 links of an MI355X run in parallel), raises a per-block flag in
+//    each peer, waits for the flags of all peers and reduces the n slots from its
+//    OWN HBM. Out of each rank: (n - 1) x S bytes. For small messages.
+//  * TWO-SHOT (reduce-scatter + all-gather over the same buffers): each block's
+//    range is cut into n pieces, piece q owned by rank q. A rank pushes piece q of
+//    its input into rank q's slot, waits, reduces ITS piece (the same fp32 sum in
+//    rank order as one-shot, so results are bit-identical), pushes the reduced piece
+//    into every rank's gather buffer, waits, and reads the whole range back. Out of
+//    each rank: 2 (n - 1) / n x S bytes -- at the 70B B=256 decode all-reduce (4 MB,
+//    world 8) 7 MB instead of one-shot's 28 MB. For large messages; the crossover
+//    is a config key (parallel/custom_ar.py), unmeasured until an 8-GPU node exists.
+//
+// Memory: each rank owns one fine-grained (uncached) allocation, exported with
+// hipIpcGetMemHandle and opened by every peer:
+//   [0, 2 KB)        flags[kMaxBlocks][kMaxRanks]     u32 (one-shot; two-shot scatter phase)
+//   [2 KB, 4 KB)     gflags[kMaxBlocks][kMaxRanks]    u32 (two-shot gather phase)
+//   [8 KB, 8 KB+256) rounds[kMaxBlocks]               u32, this rank's per-block call counter
+//   [12 KB]          err                              u32, set when a wait times out
+//   [64 KB, ...)     recv[2][world][cap]              parity-double-buffered slots
+//   then             gather[2][cap]                   two-shot reduced pieces
+// Hand-off (system scope: the producer is another device). Every slot and flag
+// access is a system-coherent (sc0 sc1) buffer access, which bypasses the GPU
+// caches whatever the page's cache type, so no cache maintenance is needed:
+// data stores -> each storing wave's s_waitcnt vmcnt(0) (the stores are complete
+// at the destination) -> block barrier -> sc0 sc1 flag store; the consumer polls
+// its flag with sc0 sc1 loads, barriers, and reads the slots with sc0 sc1 loads.
+// The previous protocol (__threadfence_system + release / acquire at system
+// scope: an L2 write-back and invalidate per block and call, ~15.7 us per fused
+// call even at world 1 in the TP=8 simulation) is kept as the "fence" protocol
+// (OAMD_CAR_PROTOCOL=fence) for A/B.
+// Round numbers are per block and kept on the device, so a call is a pure kernel
+// launch (capturable into a hipGraph) and ranks never exchange host state per
+// call. Every call of either kind advances every block's round by one. Parity
+// buffers make slot reuse safe: a peer can be at most one round ahead (it needs
+// this rank's flag of round r+1 to finish r+1, raised only after this rank
+// finished reading round r; the two-shot gather buffer likewise, through the
+// scatter flags of round r+1). Every wait is bounded (wall clock, ~2 s by
+// default): a missing peer sets `err` and the kernel drains instead of spinning
+// forever. A timed-out block never leaves a partial sum behind: it writes NaN over
+// its output slice, and the error is STICKY -- every later call sees `err` at
+// entry, poisons its whole output and touches no peer -- because after a timeout
+// the per-block round counters of the ranks no longer agree. The error is
+// mirrored into a host-mapped word, so the engine polls it after each decode
+// window with a plain host read (no device sync) and fails the TP replica; the
+// pool respawns it with fresh buffers.
 #include <cstring>
 
 #include "common.h"
@@ -44,6 +63,7 @@ constexpr int kMaxRanks = 8;
 constexpr int kMaxBlocks = 64;
 constexpr int kThreads = 512;
 constexpr size_t kFlagsOff = 0;
+constexpr size_t kGFlagsOff = 2 << 10;
 constexpr size_t kRoundsOff = 8 << 10;
 constexpr size_t kErrOff = 12 << 10;
 constexpr size_t kDataOff = 64 << 10;
@@ -53,6 +73,70 @@ constexpr uint64_t kDefaultTimeoutTicks = 200000000ull;  // wall_clock64 runs at
 struct CarPeers {
   char* base[car::kMaxRanks];
 };
+
+namespace car {
+constexpr int kSys = 17;   // buffer-op cache policy sc0 | sc1: system coherent, bypasses every GPU cache
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(char* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ void st16(__amdgpu_buffer_rsrc_t r, int64_t off, uint4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, r, (int)off, 0, kSys);
+}
+__device__ __forceinline__ uint4 ld16(__amdgpu_buffer_rsrc_t r, int64_t off) {
+  const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, kSys);
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
+// byte offsets inside a rank's buffer
+__device__ __forceinline__ int64_t slot_off(int par, int W, int src, int64_t capvec, int64_t v) {
+  return (int64_t)kDataOff + (((int64_t)par * W + src) * capvec + v) * 16;
+}
+__device__ __forceinline__ int64_t gather_off(int par, int W, int64_t capvec, int64_t v) {
+  return (int64_t)kDataOff + ((2 * (int64_t)W + par) * capvec + v) * 16;
+}
+
+// Raise this block's flag (value `round`) in every rank for phase `flags_off`, after
+// every store the block made: LIGHT = each wave waits for its own sc0 sc1 stores to
+// complete, then the barrier, then an sc0 sc1 flag store; otherwise the system-scope
+// fence + release store of the original protocol.
+template <int W, bool LIGHT>
+__device__ __forceinline__ void publish(const CarPeers& peers, size_t flags_off, int b, int rank, uint32_t round,
+                                        int tid) {
+  if (LIGHT) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  } else {
+    __threadfence_system();
+    __syncthreads();
+  }
+  if (tid < W) {
+    uint32_t* f = reinterpret_cast<uint32_t*>(peers.base[tid] + flags_off) + b * kMaxRanks + rank;
+    if (LIGHT) __hip_atomic_store(f, round, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else __hip_atomic_store(f, round, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// Wait (bounded) until every rank raised this block's flag of phase `flags_off` to
+// `round`; ends with a block barrier. Sets *s_err on a timeout.
+template <int W, bool LIGHT>
+__device__ __forceinline__ void wait_all(char* mine, size_t flags_off, int b, uint32_t round, uint64_t timeout_ticks,
+                                         int tid, uint32_t* s_err) {
+  if (tid < W) {
+    uint32_t* f = reinterpret_cast<uint32_t*>(mine + flags_off) + b * kMaxRanks + tid;
+    const uint64_t t0 = (uint64_t)wall_clock64();
+    while ((LIGHT ? __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                  : __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM)) < round) {
+      __builtin_amdgcn_s_sleep(2);
+      if ((uint64_t)wall_clock64() - t0 > timeout_ticks) {
+        *s_err = 1;
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+}  // namespace car
 
 __device__ __forceinline__ void acc8(float* a, uint4 v, bool is_bf16) {
   if (is_bf16) {
@@ -70,6 +154,12 @@ __device__ __forceinline__ void acc8(float* a, uint4 v, bool is_bf16) {
   }
 }
 
+__device__ __forceinline__ uint4 pack8(const float* a, bool is_bf16) {
+  if (is_bf16)
+    return make_uint4(pack_bf2(a[0], a[1]), pack_bf2(a[2], a[3]), pack_bf2(a[4], a[5]), pack_bf2(a[6], a[7]));
+  return make_uint4(__float_as_uint(a[0]), __float_as_uint(a[1]), __float_as_uint(a[2]), __float_as_uint(a[3]));
+}
+
 // NaN over out[v0, v1): a failed call must never look like a valid sum.
 template <bool BF16>
 __device__ __forceinline__ void poison(uint4* __restrict__ out, int64_t v0, int64_t v1, int tid) {
@@ -77,100 +167,119 @@ __device__ __forceinline__ void poison(uint4* __restrict__ out, int64_t v0, int6
   for (int64_t v = v0 + tid; v < v1; v += car::kThreads) out[v] = make_uint4(nan, nan, nan, nan);
 }
 
-// One 16-B vector = 8 bf16 or 4 fp32 elements.
-template <int W, bool BF16>
-__global__ void __launch_bounds__(car::kThreads) oneshot_allreduce_kernel(const uint4* __restrict__ in,
-                                                                          uint4* __restrict__ out, int64_t nvec,
-                                                                          int64_t capvec, int rank, CarPeers peers,
-                                                                          uint32_t* herr, uint64_t timeout_ticks) {
+// The sum over the W receive slots of vector v, fp32 in rank order (both protocols).
+template <int W>
+__device__ __forceinline__ void sum_slots(float* a, __amdgpu_buffer_rsrc_t rm, int par, int64_t capvec, int64_t v,
+                                          bool is_bf16) {
+  uint4 x[W];
+#pragma unroll
+  for (int p = 0; p < W; ++p) x[p] = car::ld16(rm, car::slot_off(par, W, p, capvec, v));
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a[i] = 0.f;
+#pragma unroll
+  for (int p = 0; p < W; ++p) acc8(a, x[p], is_bf16);
+}
+
+// Call prologue shared by every kernel: this block's round, and whether an earlier
+// call left the sticky error.
+struct CarCall {
+  uint32_t round;
+  int par;
+  bool failed;
+};
+__device__ __forceinline__ CarCall car_begin(char* mine, int b, int tid, uint32_t* s_round, uint32_t* s_err) {
+  uint32_t* rounds = reinterpret_cast<uint32_t*>(mine + car::kRoundsOff);
+  uint32_t* err = reinterpret_cast<uint32_t*>(mine + car::kErrOff);
+  if (tid == 0) {
+    *s_round = rounds[b] + 1;
+    *s_err = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __syncthreads();
+  return CarCall{*s_round, static_cast<int>(*s_round & 1), *s_err != 0};
+}
+__device__ __forceinline__ void car_fail(char* mine, int b, int tid, uint32_t round, uint32_t* herr) {
+  if (tid == 0) {
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(mine + car::kErrOff), 1u, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    if (herr != nullptr) __hip_atomic_store(herr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    reinterpret_cast<uint32_t*>(mine + car::kRoundsOff)[b] = round;
+  }
+}
+__device__ __forceinline__ void car_end(char* mine, int b, int tid, uint32_t round) {
+  if (tid == 0) reinterpret_cast<uint32_t*>(mine + car::kRoundsOff)[b] = round;
+}
+
+// Plain all-reduce, one 16-B vector = 8 bf16 or 4 fp32 elements. TWO: two-shot.
+template <int W, bool BF16, bool TWO, bool LIGHT>
+__global__ void __launch_bounds__(car::kThreads) allreduce_kernel(const uint4* __restrict__ in,
+                                                                  uint4* __restrict__ out, int64_t nvec,
+                                                                  int64_t capvec, int rank, CarPeers peers,
+                                                                  uint32_t* herr, uint64_t timeout_ticks) {
   __shared__ uint32_t s_round;
   __shared__ uint32_t s_err;
   const int b = blockIdx.x, tid = threadIdx.x;
   char* mine = peers.base[rank];
-  uint32_t* rounds = reinterpret_cast<uint32_t*>(mine + car::kRoundsOff);
-  uint32_t* err = reinterpret_cast<uint32_t*>(mine + car::kErrOff);
-  if (tid == 0) {
-    s_round = rounds[b] + 1;
-    s_err = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  __syncthreads();
-  const uint32_t round = s_round;
-  const int par = round & 1;
+  const CarCall c = car_begin(mine, b, tid, &s_round, &s_err);
   const int64_t per = (nvec + gridDim.x - 1) / gridDim.x;
   const int64_t v0 = min(nvec, per * b), v1 = min(nvec, v0 + per);
-  if (s_err) {   // sticky: an earlier call timed out, the ranks are out of step
+  if (c.failed) {   // sticky: an earlier call timed out, the ranks are out of step
     poison<BF16>(out, v0, v1, tid);
     return;
   }
-
-  // ---- push: my slice of `in` into slot [par][rank] of every rank (me included)
-  for (int64_t v = v0 + tid; v < v1; v += car::kThreads) {
-    const uint4 x = in[v];
+  __amdgpu_buffer_rsrc_t rs[W];
 #pragma unroll
-    for (int p = 0; p < W; ++p) {
-      uint4* dst = reinterpret_cast<uint4*>(peers.base[p] + car::kDataOff) + ((int64_t)par * W + rank) * capvec;
-      dst[v] = x;
-    }
+  for (int p = 0; p < W; ++p) rs[p] = car::rsrc(peers.base[p]);
+  const __amdgpu_buffer_rsrc_t rm = car::rsrc(mine);
+  const int64_t pq = (v1 - v0 + W - 1) / W;   // two-shot piece per owner
+  // ---- push: one-shot: the whole range into slot [par][rank] of every rank;
+  //      two-shot: piece q into rank q's slot [par][rank]
+#pragma unroll
+  for (int p = 0; p < W; ++p) {
+    const int64_t a = TWO ? min(v1, v0 + p * pq) : v0, e = TWO ? min(v1, a + pq) : v1;
+    for (int64_t v = a + tid; v < e; v += car::kThreads) car::st16(rs[p], car::slot_off(c.par, W, rank, capvec, v), in[v]);
   }
-  __threadfence_system();
-  __syncthreads();
-  if (tid < W) {
-    uint32_t* f = reinterpret_cast<uint32_t*>(peers.base[tid] + car::kFlagsOff) + b * car::kMaxRanks + rank;
-    __hip_atomic_store(f, round, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  // ---- wait for every peer's slice of this block (bounded)
-  if (tid < W) {
-    uint32_t* f = reinterpret_cast<uint32_t*>(mine + car::kFlagsOff) + b * car::kMaxRanks + tid;
-    const uint64_t t0 = (uint64_t)wall_clock64();
-    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < round) {
-      __builtin_amdgcn_s_sleep(2);
-      if ((uint64_t)wall_clock64() - t0 > timeout_ticks) {
-        s_err = 1;
-        break;
-      }
-    }
-  }
-  __syncthreads();
+  car::publish<W, LIGHT>(peers, car::kFlagsOff, b, rank, c.round, tid);
+  car::wait_all<W, LIGHT>(mine, car::kFlagsOff, b, c.round, timeout_ticks, tid, &s_err);
   if (s_err) {
-    if (tid == 0) {
-      __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      if (herr != nullptr) __hip_atomic_store(herr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      rounds[b] = round;
-    }
+    car_fail(mine, b, tid, c.round, herr);
     poison<BF16>(out, v0, v1, tid);
     return;
   }
-  // ---- reduce the W slots from local HBM, fp32 accumulation in rank order
-  const uint4* slots = reinterpret_cast<const uint4*>(mine + car::kDataOff) + (int64_t)par * W * capvec;
-  for (int64_t v = v0 + tid; v < v1; v += car::kThreads) {
-    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    uint4 x[W];
-#pragma unroll
-    for (int p = 0; p < W; ++p) x[p] = slots[(int64_t)p * capvec + v];
-#pragma unroll
-    for (int p = 0; p < W; ++p) acc8(a, x[p], BF16);
-    uint4 o;
-    if (BF16) {
-      o.x = pack_bf2(a[0], a[1]);
-      o.y = pack_bf2(a[2], a[3]);
-      o.z = pack_bf2(a[4], a[5]);
-      o.w = pack_bf2(a[6], a[7]);
-    } else {
-      o.x = __float_as_uint(a[0]);
-      o.y = __float_as_uint(a[1]);
-      o.z = __float_as_uint(a[2]);
-      o.w = __float_as_uint(a[3]);
+  if constexpr (!TWO) {
+    for (int64_t v = v0 + tid; v < v1; v += car::kThreads) {
+      float a[8];
+      sum_slots<W>(a, rm, c.par, capvec, v, BF16);
+      out[v] = pack8(a, BF16);
     }
-    out[v] = o;
+  } else {
+    // reduce this rank's piece, hand it to every rank's gather buffer
+    const int64_t a0 = min(v1, v0 + rank * pq), e0 = min(v1, a0 + pq);
+    for (int64_t v = a0 + tid; v < e0; v += car::kThreads) {
+      float a[8];
+      sum_slots<W>(a, rm, c.par, capvec, v, BF16);
+      const uint4 o = pack8(a, BF16);
+#pragma unroll
+      for (int p = 0; p < W; ++p) car::st16(rs[p], car::gather_off(c.par, W, capvec, v), o);
+    }
+    car::publish<W, LIGHT>(peers, car::kGFlagsOff, b, rank, c.round, tid);
+    car::wait_all<W, LIGHT>(mine, car::kGFlagsOff, b, c.round, timeout_ticks, tid, &s_err);
+    if (s_err) {
+      car_fail(mine, b, tid, c.round, herr);
+      poison<BF16>(out, v0, v1, tid);
+      return;
+    }
+    for (int64_t v = v0 + tid; v < v1; v += car::kThreads) out[v] = car::ld16(rm, car::gather_off(c.par, W, capvec, v));
   }
-  if (tid == 0) rounds[b] = round;
+  car_end(mine, b, tid, c.round);
 }
 
 // Fused TP block epilogue: h = h + bf16(sum over ranks of in); y = RMSNorm(h) * w.
-// Row-partitioned (block b owns rows [r0, r1)), so after the one-hop push and the
-// per-block flag wait each block holds whole rows and normalises them in place:
-// the all-reduce's output never round-trips through HBM before the norm, and one
-// launch replaces two (the fusion that makes TP=8 pay).
+// Row-partitioned (block b owns rows [r0, r1)), so after the all-reduce each block
+// holds whole rows and normalises them in place: the all-reduce's output never
+// round-trips through HBM before the norm, and one launch replaces two (SURVEY.md
+// §7.4 item 6: the fusion that makes TP=8 pay). TWO: the block's rows go through the
+// two-shot protocol (reduce-scatter of pieces, all-gather of their sums) instead of
+// one-shot; the sums are bit-identical.
 // Numerics are those of all-reduce + rmsnorm_kernel: the sum is rounded to bf16,
 // the residual add is rounded to bf16, the normalised value is rounded before w.
 // SLABS: the input is S fp32 split-K slabs [S, rows, hidden] of the producing GEMM,
@@ -178,8 +287,8 @@ __global__ void __launch_bounds__(car::kThreads) oneshot_allreduce_kernel(const 
 // (bit-identical to splitk_reduce_fp32 + the bf16 path, one kernel fewer).
 // Q8: also emit the normalised rows as per-row e4m3fn (q8, sx) for the next fp8 GEMM,
 // bit-identical to quantize_fp8(y) — the activation quantization kernel disappears.
-template <int W, int MAXV, bool SLABS, bool Q8>
-__global__ void __launch_bounds__(car::kThreads) oneshot_ar_rmsnorm_kernel(
+template <int W, int MAXV, bool SLABS, bool Q8, bool TWO, bool LIGHT>
+__global__ void __launch_bounds__(car::kThreads) ar_rmsnorm_kernel(
     const uint4* __restrict__ in, const float* __restrict__ slabs, int S, bf16_t* __restrict__ residual,
     const bf16_t* __restrict__ w, bf16_t* __restrict__ y, uint8_t* __restrict__ q8, float* __restrict__ sx,
     int rows, int hidden, float eps, int64_t capvec, int rank, CarPeers peers, uint32_t* herr,
@@ -190,29 +299,27 @@ __global__ void __launch_bounds__(car::kThreads) oneshot_ar_rmsnorm_kernel(
   __shared__ float mscratch[car::kThreads / 64];
   const int b = blockIdx.x, tid = threadIdx.x;
   char* mine = peers.base[rank];
-  uint32_t* rounds = reinterpret_cast<uint32_t*>(mine + car::kRoundsOff);
-  uint32_t* err = reinterpret_cast<uint32_t*>(mine + car::kErrOff);
-  if (tid == 0) {
-    s_round = rounds[b] + 1;
-    s_err = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  __syncthreads();
-  const uint32_t round = s_round;
-  const int par = round & 1;
+  const CarCall c = car_begin(mine, b, tid, &s_round, &s_err);
   const int nvr = hidden >> 3;
   const int per = (rows + gridDim.x - 1) / gridDim.x;
   const int r0 = min(rows, per * b), r1 = min(rows, r0 + per);
   const int64_t v0 = (int64_t)r0 * nvr, v1 = (int64_t)r1 * nvr;
   uint4* y4 = reinterpret_cast<uint4*>(y);
-  if (s_err) {
+  auto fail_out = [&]() {
     poison<true>(y4, v0, v1, tid);
     if constexpr (Q8)
       for (int r = r0 + tid; r < r1; r += car::kThreads) sx[r] = __builtin_nanf("");
+  };
+  if (c.failed) {
+    fail_out();
     return;
   }
+  __amdgpu_buffer_rsrc_t rs[W];
+#pragma unroll
+  for (int p = 0; p < W; ++p) rs[p] = car::rsrc(peers.base[p]);
+  const __amdgpu_buffer_rsrc_t rm = car::rsrc(mine);
   const int64_t MN = (int64_t)rows * hidden;
-  for (int64_t v = v0 + tid; v < v1; v += car::kThreads) {
-    uint4 x;
+  auto load_x = [&](int64_t v) -> uint4 {
     if constexpr (SLABS) {
       const float* pv = slabs + v * 8;
       f32x4 a0 = *reinterpret_cast<const f32x4*>(pv), a1 = *reinterpret_cast<const f32x4*>(pv + 4);
@@ -221,16 +328,16 @@ __global__ void __launch_bounds__(car::kThreads) oneshot_ar_rmsnorm_kernel(
         a0 += b0;
         a1 += b1;
       } else if (S == 4) {
-        f32x4 b[3][2];
+        f32x4 bb[3][2];
 #pragma unroll
         for (int s = 1; s < 4; ++s) {
-          b[s - 1][0] = *reinterpret_cast<const f32x4*>(pv + s * MN);
-          b[s - 1][1] = *reinterpret_cast<const f32x4*>(pv + s * MN + 4);
+          bb[s - 1][0] = *reinterpret_cast<const f32x4*>(pv + s * MN);
+          bb[s - 1][1] = *reinterpret_cast<const f32x4*>(pv + s * MN + 4);
         }
 #pragma unroll
         for (int s = 0; s < 3; ++s) {   // slab order
-          a0 += b[s][0];
-          a1 += b[s][1];
+          a0 += bb[s][0];
+          a1 += bb[s][1];
         }
       } else {
         for (int s = 1; s < S; ++s) {
@@ -238,46 +345,42 @@ __global__ void __launch_bounds__(car::kThreads) oneshot_ar_rmsnorm_kernel(
           a1 += *reinterpret_cast<const f32x4*>(pv + s * MN + 4);
         }
       }
-      x = make_uint4(pack_bf2(a0[0], a0[1]), pack_bf2(a0[2], a0[3]), pack_bf2(a1[0], a1[1]), pack_bf2(a1[2], a1[3]));
+      return make_uint4(pack_bf2(a0[0], a0[1]), pack_bf2(a0[2], a0[3]), pack_bf2(a1[0], a1[1]),
+                        pack_bf2(a1[2], a1[3]));
     } else {
-      x = in[v];
+      return in[v];
     }
+  };
+  const int64_t pq = (v1 - v0 + W - 1) / W;
 #pragma unroll
-    for (int p = 0; p < W; ++p) {
-      uint4* dst = reinterpret_cast<uint4*>(peers.base[p] + car::kDataOff) + ((int64_t)par * W + rank) * capvec;
-      dst[v] = x;
-    }
+  for (int p = 0; p < W; ++p) {
+    const int64_t a = TWO ? min(v1, v0 + p * pq) : v0, e = TWO ? min(v1, a + pq) : v1;
+    for (int64_t v = a + tid; v < e; v += car::kThreads) car::st16(rs[p], car::slot_off(c.par, W, rank, capvec, v), load_x(v));
   }
-  __threadfence_system();
-  __syncthreads();
-  if (tid < W) {
-    uint32_t* f = reinterpret_cast<uint32_t*>(peers.base[tid] + car::kFlagsOff) + b * car::kMaxRanks + rank;
-    __hip_atomic_store(f, round, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  if (tid < W) {
-    uint32_t* f = reinterpret_cast<uint32_t*>(mine + car::kFlagsOff) + b * car::kMaxRanks + tid;
-    const uint64_t t0 = (uint64_t)wall_clock64();
-    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < round) {
-      __builtin_amdgcn_s_sleep(2);
-      if ((uint64_t)wall_clock64() - t0 > timeout_ticks) {
-        s_err = 1;
-        break;
-      }
-    }
-  }
-  __syncthreads();
+  car::publish<W, LIGHT>(peers, car::kFlagsOff, b, rank, c.round, tid);
+  car::wait_all<W, LIGHT>(mine, car::kFlagsOff, b, c.round, timeout_ticks, tid, &s_err);
   if (s_err) {
-    if (tid == 0) {
-      __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      if (herr != nullptr) __hip_atomic_store(herr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      rounds[b] = round;
-    }
-    poison<true>(y4, v0, v1, tid);
-    if constexpr (Q8)
-      for (int r = r0 + tid; r < r1; r += car::kThreads) sx[r] = __builtin_nanf("");
+    car_fail(mine, b, tid, c.round, herr);
+    fail_out();
     return;
   }
-  const uint4* slots = reinterpret_cast<const uint4*>(mine + car::kDataOff) + (int64_t)par * W * capvec;
+  if constexpr (TWO) {
+    const int64_t a0 = min(v1, v0 + rank * pq), e0 = min(v1, a0 + pq);
+    for (int64_t v = a0 + tid; v < e0; v += car::kThreads) {
+      float a[8];
+      sum_slots<W>(a, rm, c.par, capvec, v, true);
+      const uint4 o = pack8(a, true);
+#pragma unroll
+      for (int p = 0; p < W; ++p) car::st16(rs[p], car::gather_off(c.par, W, capvec, v), o);
+    }
+    car::publish<W, LIGHT>(peers, car::kGFlagsOff, b, rank, c.round, tid);
+    car::wait_all<W, LIGHT>(mine, car::kGFlagsOff, b, c.round, timeout_ticks, tid, &s_err);
+    if (s_err) {
+      car_fail(mine, b, tid, c.round, herr);
+      fail_out();
+      return;
+    }
+  }
   const u16x8* w8 = reinterpret_cast<const u16x8*>(w);
   for (int r = r0; r < r1; ++r) {
     u16x8* hr = reinterpret_cast<u16x8*>(residual + (int64_t)r * hidden);
@@ -289,17 +392,22 @@ __global__ void __launch_bounds__(car::kThreads) oneshot_ar_rmsnorm_kernel(
       const int vi = tid + i * car::kThreads;
       if (vi < nvr) {
         const int64_t g = (int64_t)r * nvr + vi;
-        float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        uint4 x[W];
+        float a[8];
+        if constexpr (TWO) {   // the gathered bf16 sums
+          const uint4 x = car::ld16(rm, car::gather_off(c.par, W, capvec, g));
 #pragma unroll
-        for (int p = 0; p < W; ++p) x[p] = slots[(int64_t)p * capvec + g];
+          for (int j = 0; j < 8; ++j) a[j] = 0.f;
+          acc8(a, x, true);
+        } else {
+          sum_slots<W>(a, rm, c.par, capvec, g, true);
 #pragma unroll
-        for (int p = 0; p < W; ++p) acc8(a, x[p], true);
+          for (int j = 0; j < 8; ++j) a[j] = bf2f(f2bf(a[j]));
+        }
         const u16x8 hv = hr[vi];
         u16x8 s;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          s[j] = f2bf(bf2f(f2bf(a[j])) + bf2f(hv[j]));
+          s[j] = f2bf(a[j] + bf2f(hv[j]));
           v[i][j] = bf2f(s[j]);
           ss += v[i][j] * v[i][j];
         }
@@ -307,7 +415,7 @@ __global__ void __launch_bounds__(car::kThreads) oneshot_ar_rmsnorm_kernel(
       }
     }
     const float tot = block_sum<car::kThreads>(ss, scratch);
-    const float rs = rsqrtf(tot / static_cast<float>(hidden) + eps);
+    const float rs_ = rsqrtf(tot / static_cast<float>(hidden) + eps);
 #pragma unroll
     for (int i = 0; i < MAXV; ++i) {
       const int vi = tid + i * car::kThreads;
@@ -315,7 +423,7 @@ __global__ void __launch_bounds__(car::kThreads) oneshot_ar_rmsnorm_kernel(
         const u16x8 wv = w8[vi];
         u16x8 o;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = f2bf(bf2f(f2bf(v[i][j] * rs)) * bf2f(wv[j]));
+        for (int j = 0; j < 8; ++j) o[j] = f2bf(bf2f(f2bf(v[i][j] * rs_)) * bf2f(wv[j]));
         yr[vi] = o;
         if constexpr (Q8) {
 #pragma unroll
@@ -355,12 +463,13 @@ __global__ void __launch_bounds__(car::kThreads) oneshot_ar_rmsnorm_kernel(
       }
     }
   }
-  if (tid == 0) rounds[b] = round;
+  car_end(mine, b, tid, c.round);
 }
 
 // ------------------------------------------------------------------ host side
 
-size_t car_buffer_bytes(size_t cap_bytes, int world) { return car::kDataOff + 2 * (size_t)world * cap_bytes; }
+// receive slots [2][world][cap] + the two-shot gather buffer [2][cap]
+size_t car_buffer_bytes(size_t cap_bytes, int world) { return car::kDataOff + 2 * ((size_t)world + 1) * cap_bytes; }
 
 int car_alloc(size_t cap_bytes, int world, void** base, void* handle_out) {
   if (world < 1 || world > car::kMaxRanks || cap_bytes % 16 != 0) return -1;
@@ -411,26 +520,33 @@ int car_reset(void* base, uint32_t* host) {
   return (int)e;
 }
 
+// proto: kCarOneShot / kCarTwoShot (sc0 sc1 hand-off) or kCarOneShotFence (the original
+// system-scope fence protocol, for A/B). A two-shot call at world 1 runs one-shot.
 int car_all_reduce(const void* in, void* out, int64_t bytes, bool bf16, int rank, int world, void* const* bases,
-                   size_t cap_bytes, int blocks, uint32_t* herr_dev, double timeout_s, hipStream_t stream) {
+                   size_t cap_bytes, int blocks, uint32_t* herr_dev, double timeout_s, int proto,
+                   hipStream_t stream) {
   if (world < 1 || world > car::kMaxRanks || rank < 0 || rank >= world) return -1;
   if (bytes % 16 != 0 || (size_t)bytes > cap_bytes || cap_bytes % 16 != 0) return -2;
   if (blocks < 1 || blocks > car::kMaxBlocks) return -3;
   if ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15) return -4;
+  if (proto < kCarOneShot || proto > kCarOneShotFence) return -6;
+  if (world == 1 && proto == kCarTwoShot) proto = kCarOneShot;
   CarPeers peers{};
   for (int p = 0; p < world; ++p) peers.base[p] = static_cast<char*>(bases[p]);
   const int64_t nvec = bytes / 16, capvec = cap_bytes / 16;
   const uint4* i4 = static_cast<const uint4*>(in);
   uint4* o4 = static_cast<uint4*>(out);
   const uint64_t ticks = timeout_s > 0 ? (uint64_t)(timeout_s * 1e8) : car::kDefaultTimeoutTicks;
-#define OAMD_CAR(W)                                                                                               \
-  case W:                                                                                                         \
-    if (bf16)                                                                                                     \
-      oneshot_allreduce_kernel<W, true>                                                                           \
-          <<<blocks, car::kThreads, 0, stream>>>(i4, o4, nvec, capvec, rank, peers, herr_dev, ticks);             \
-    else                                                                                                          \
-      oneshot_allreduce_kernel<W, false>                                                                          \
-          <<<blocks, car::kThreads, 0, stream>>>(i4, o4, nvec, capvec, rank, peers, herr_dev, ticks);             \
+#define OAMD_CARP(W, B, T, L) \
+  allreduce_kernel<W, B, T, L><<<blocks, car::kThreads, 0, stream>>>(i4, o4, nvec, capvec, rank, peers, herr_dev, ticks)
+#define OAMD_CARD(W, B)                                    \
+  if (proto == kCarTwoShot) OAMD_CARP(W, B, (W > 1), true); \
+  else if (proto == kCarOneShot) OAMD_CARP(W, B, false, true); \
+  else OAMD_CARP(W, B, false, false);
+#define OAMD_CAR(W)                 \
+  case W:                           \
+    if (bf16) { OAMD_CARD(W, true) } \
+    else { OAMD_CARD(W, false) }     \
     break;
   switch (world) {
     OAMD_CAR(1)
@@ -444,18 +560,16 @@ int car_all_reduce(const void* in, void* out, int64_t bytes, bool bf16, int rank
     default: return -1;
   }
 #undef OAMD_CAR
+#undef OAMD_CARD
+#undef OAMD_CARP
   OAMD_LAUNCH_CHECK();
   return 0;
 }
 
-}  // namespace oamd
-
-namespace oamd {
-
 int car_all_reduce_rmsnorm(const void* in, const float* slabs, int S, bf16_t* residual, const bf16_t* w, bf16_t* y,
                            uint8_t* q8, float* sx, int rows, int hidden, float eps, int rank, int world,
                            void* const* bases, size_t cap_bytes, int blocks, uint32_t* herr_dev, double timeout_s,
-                           hipStream_t stream) {
+                           int proto, hipStream_t stream) {
   if ((slabs == nullptr) == (in == nullptr) || (slabs != nullptr && S < 1)) return -5;
   if ((q8 == nullptr) != (sx == nullptr)) return -5;
   if (world < 1 || world > car::kMaxRanks || rank < 0 || rank >= world) return -1;
@@ -465,6 +579,8 @@ int car_all_reduce_rmsnorm(const void* in, const float* slabs, int S, bf16_t* re
   if ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(slabs) | reinterpret_cast<uintptr_t>(residual) |
        reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(y) | reinterpret_cast<uintptr_t>(q8)) & 15)
     return -4;
+  if (proto < kCarOneShot || proto > kCarOneShotFence) return -6;
+  if (world == 1 && proto == kCarTwoShot) proto = kCarOneShot;
   CarPeers peers{};
   for (int p = 0; p < world; ++p) peers.base[p] = static_cast<char*>(bases[p]);
   const int64_t capvec = cap_bytes / 16;
@@ -472,23 +588,27 @@ int car_all_reduce_rmsnorm(const void* in, const float* slabs, int S, bf16_t* re
   const uint64_t ticks = timeout_s > 0 ? (uint64_t)(timeout_s * 1e8) : car::kDefaultTimeoutTicks;
   const bool big = hidden > car::kThreads * 8 * 2;
   const int mode = (slabs != nullptr ? 1 : 0) | (q8 != nullptr ? 2 : 0);
-#define OAMD_CARK(W, MV, SL, Q)                                                                               \
-  oneshot_ar_rmsnorm_kernel<W, MV, SL, Q><<<blocks, car::kThreads, 0, stream>>>(                              \
+#define OAMD_CARK(W, MV, SL, Q, T, L)                                                                          \
+  ar_rmsnorm_kernel<W, MV, SL, Q, T, L><<<blocks, car::kThreads, 0, stream>>>(                                 \
       i4, slabs, S, residual, w, y, q8, sx, rows, hidden, eps, capvec, rank, peers, herr_dev, ticks)
-#define OAMD_CARM(W, MV)                                                                                      \
-  switch (mode) {                                                                                             \
-    case 0: OAMD_CARK(W, MV, false, false); break;                                                            \
-    case 1: OAMD_CARK(W, MV, true, false); break;                                                             \
-    case 2: OAMD_CARK(W, MV, false, true); break;                                                             \
-    default: OAMD_CARK(W, MV, true, true); break;                                                             \
+#define OAMD_CARP(W, MV, SL, Q)                                                                                \
+  if (proto == kCarTwoShot) OAMD_CARK(W, MV, SL, Q, (W > 1), true);                                            \
+  else if (proto == kCarOneShot) OAMD_CARK(W, MV, SL, Q, false, true);                                         \
+  else OAMD_CARK(W, MV, SL, Q, false, false);
+#define OAMD_CARM(W, MV)                                                                                       \
+  switch (mode) {                                                                                              \
+    case 0: { OAMD_CARP(W, MV, false, false) } break;                                                          \
+    case 1: { OAMD_CARP(W, MV, true, false) } break;                                                           \
+    case 2: { OAMD_CARP(W, MV, false, true) } break;                                                           \
+    default: { OAMD_CARP(W, MV, true, true) } break;                                                           \
   }
-#define OAMD_CARN(W)                                                                                          \
-  case W:                                                                                                     \
-    if (big) {                                                                                                \
-      OAMD_CARM(W, 4)                                                                                         \
-    } else {                                                                                                  \
-      OAMD_CARM(W, 2)                                                                                         \
-    }                                                                                                         \
+#define OAMD_CARN(W)                                                                                           \
+  case W:                                                                                                      \
+    if (big) {                                                                                                 \
+      OAMD_CARM(W, 4)                                                                                          \
+    } else {                                                                                                   \
+      OAMD_CARM(W, 2)                                                                                          \
+    }                                                                                                          \
     break;
   switch (world) {
     OAMD_CARN(1)
@@ -503,6 +623,7 @@ int car_all_reduce_rmsnorm(const void* in, const float* slabs, int S, bf16_t* re
   }
 #undef OAMD_CARM
 #undef OAMD_CARK
+#undef OAMD_CARP
 #undef OAMD_CARN
   OAMD_LAUNCH_CHECK();
   return 0;

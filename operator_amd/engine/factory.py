@@ -37,7 +37,7 @@ def build_llm(s: Settings, device: str | torch.device | None = None, tp=None):
     dtype = getattr(torch, e.dtype)
     if tp is not None and tp.world > 1 and dev.type == "cuda" and e.oneshot_allreduce_mb > 0 \
             and getattr(tp, "oneshot", None) is None:
-        tp.enable_oneshot(dev, int(e.oneshot_allreduce_mb * (1 << 20)))
+        tp.enable_oneshot(dev, int(e.oneshot_allreduce_mb * (1 << 20)), int(e.oneshot_max_kb * 1024))
     model = LlamaModel(cfg, device=dev, tp=tp, dtype=dtype, weight_dtype=e.weight_dtype)
     weight_cache.load_or_build(model, e.weight_cache_dir, e.model_path, e.seed)
     # KV cache: the compute dtype, or OCP fp8 (e4m3fn, per-tensor scales) with engine.kv_dtype=fp8

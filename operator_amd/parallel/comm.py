@@ -103,21 +103,23 @@ class Group:
         g.pg, g.rank, g.world, g.ranks = None, 0, 1, [0]
         return g
 
-    def enable_oneshot(self, device, max_bytes: int | None = None) -> bool:
-        """Route small GPU all-reduces through the one-shot IPC kernel (custom_ar.py).
-        Collective over the group; returns False (RCCL stays in use) on world 1 or CPU."""
+    def enable_oneshot(self, device, max_bytes: int | None = None, oneshot_max_bytes: int | None = None) -> bool:
+        """Route GPU all-reduces up to ``max_bytes`` through the IPC kernels (custom_ar.py):
+        one-shot up to ``oneshot_max_bytes``, two-shot above. Collective over the group;
+        returns False (RCCL stays in use) on world 1 or CPU."""
         if self.world <= 1 or torch.device(device).type != "cuda":
             return False
-        from .custom_ar import DEFAULT_MAX_BYTES, OneShotAllReduce
+        from .custom_ar import DEFAULT_MAX_BYTES, DEFAULT_ONESHOT_MAX_BYTES, OneShotAllReduce
 
-        self.oneshot = OneShotAllReduce(self, device, max_bytes or DEFAULT_MAX_BYTES)
+        self.oneshot = OneShotAllReduce(self, device, max_bytes or DEFAULT_MAX_BYTES,
+                                        oneshot_max_bytes=oneshot_max_bytes or DEFAULT_ONESHOT_MAX_BYTES)
         return True
 
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
         if self.world > 1:
             car = getattr(self, "oneshot", None)
             if car is not None and car.fits(t):
-                COLLECTIVES.add("all_reduce", "oneshot", _nbytes(t))
+                COLLECTIVES.add("all_reduce", "ipc", _nbytes(t))
                 return car.all_reduce_(t)
             t0 = time.perf_counter()
             dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.pg)
@@ -137,7 +139,7 @@ class Group:
         if self.world > 1:
             car = getattr(self, "oneshot", None)
             if car is not None and car.fits_rows(t) and residual.is_contiguous():
-                COLLECTIVES.add("all_reduce_rmsnorm", "oneshot", 2 * t.shape[0] * t.shape[1])
+                COLLECTIVES.add("all_reduce_rmsnorm", "ipc", 2 * t.shape[0] * t.shape[1])
                 return car.all_reduce_rmsnorm_(t, residual, w, eps, quant=quant)
             if isinstance(t, ops.SplitK):
                 t = t.materialize()

@@ -38,8 +38,9 @@ def _rmsnorm_fp32(x: torch.Tensor, w: torch.Tensor, eps: float, residual: torch.
     return (y.float() * w.float()).to(torch.bfloat16), h
 
 
-def _worker(rank: int, world: int, port: int, q) -> None:
+def _worker(rank: int, world: int, port: int, q, protocol: str = "auto") -> None:
     try:
+        os.environ["OAMD_CAR_PROTOCOL"] = protocol
         import torch.distributed as dist
 
         from operator_amd.parallel.comm import Group
@@ -139,7 +140,11 @@ def _worker(rank: int, world: int, port: int, q) -> None:
         q.put((rank, "error", traceback.format_exc()))
 
 
-def test_oneshot_allreduce_two_ranks_one_gpu():
+@pytest.mark.parametrize("protocol", ["auto", "oneshot", "twoshot", "fence"])
+def test_oneshot_allreduce_two_ranks_one_gpu(protocol):
+    """Every protocol (auto: one-shot up to 512 KB, two-shot above; each forced; the
+    original system-fence one-shot) gives the exact fp32-in-rank-order sums, fused
+    epilogues included, interleaved on the same per-block round counters."""
     import torch.multiprocessing as mp
 
     if not torch.cuda.is_available():
@@ -150,7 +155,7 @@ def test_oneshot_allreduce_two_ranks_one_gpu():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, protocol)) for r in range(2)]
     for p in procs:
         p.start()
     res = []
@@ -167,10 +172,11 @@ def test_oneshot_allreduce_two_ranks_one_gpu():
     assert all(r[2] >= 30 for r in res), res
 
 
-def _missing_peer_worker(rank: int, world: int, port: int, q) -> None:
+def _missing_peer_worker(rank: int, world: int, port: int, q, protocol: str = "oneshot") -> None:
     """Rank 1 skips one all-reduce: rank 0 must time out with an error and NaN output,
     never return its own partial sum; after that the error is sticky on both ranks."""
     try:
+        os.environ["OAMD_CAR_PROTOCOL"] = protocol
         import time
 
         import torch.distributed as dist
@@ -211,11 +217,12 @@ def _missing_peer_worker(rank: int, world: int, port: int, q) -> None:
             out["sticky_s"] = time.perf_counter() - t0
         dist.barrier()
         if rank == 1:
-            # rank 0 pushed its slice before it timed out, so rank 1's call of that round
-            # still completes with the true sum ...
+            # one-shot: rank 0 pushed its slice before it timed out, so rank 1's call of that
+            # round still completes with the true sum ...
             y = car.all_reduce(x)
             torch.cuda.synchronize()
             out["late_ok"] = torch.equal(y.cpu(), torch.full((n,), 3.0, dtype=torch.bfloat16)) and not car.failed
+            out["late_nan"] = bool(torch.isnan(y.float()).all())
             y = car.all_reduce(x)           # ... but rank 0 now pushes nothing: timeout, NaN
             torch.cuda.synchronize()
             out["all_nan"] = bool(torch.isnan(y.float()).all())
@@ -230,7 +237,11 @@ def _missing_peer_worker(rank: int, world: int, port: int, q) -> None:
         q.put((rank, "error", traceback.format_exc()))
 
 
-def test_oneshot_allreduce_missing_peer_fails_loudly():
+@pytest.mark.parametrize("protocol", ["oneshot", "twoshot"])
+def test_oneshot_allreduce_missing_peer_fails_loudly(protocol):
+    """One-shot: rank 1's late call still completes (rank 0 pushed before timing out),
+    its next one times out. Two-shot: rank 0 never reaches the all-gather phase, so rank
+    1's late call already times out. Either way: NaN, never a partial sum, and sticky."""
     import torch.multiprocessing as mp
 
     if not torch.cuda.is_available():
@@ -238,7 +249,7 @@ def test_oneshot_allreduce_missing_peer_fails_loudly():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_missing_peer_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_missing_peer_worker, args=(r, 2, port, q, protocol)) for r in range(2)]
     for p in procs:
         p.start()
     res = {}
@@ -257,4 +268,7 @@ def test_oneshot_allreduce_missing_peer_fails_loudly():
     assert r0["failed"] and r0["raised"] and r0["all_nan"], r0
     assert 0.15 < r0["wait_s"] < 5.0, r0
     assert r0["sticky_nan"] and r0["sticky_s"] < 0.1, r0
-    assert r1["late_ok"] and r1["failed"] and r1["all_nan"], r1
+    if protocol == "oneshot":
+        assert r1["late_ok"] and r1["failed"] and r1["all_nan"], r1
+    else:   # rank 0 never published its gather piece: the late call already fails
+        assert not r1["late_ok"] and r1["late_nan"] and r1["failed"] and r1["all_nan"], r1

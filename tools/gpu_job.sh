@@ -22,7 +22,7 @@ for job in "$@"; do
   echo "== job $job ($(date +%T))"
   case $job in
     tests)          pytest_gpu gpu_tests.log tests -m gpu ;;
-    tests-changed)  pytest_gpu gpu_tests_changed.log tests/test_kernels_gpu.py tests/test_scan_gpu.py \
+    tests-changed)  pytest_gpu gpu_tests_changed.log tests/test_kernels_gpu.py tests/test_scan_gpu.py tests/test_custom_ar_gpu.py \
                       tests/test_prefix_sharing_gpu.py -m gpu ;;
     smoke)          timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)          timeout -k 10 900 python -u bench.py ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err
