@@ -54,10 +54,18 @@ __device__ __forceinline__ uint2 pack4(f32x4 v) { return make_uint2(pack_bf2(v[0
 }  // namespace
 
 // XH: 128-token halves per tile (1 or 2). Regions per buffer: [X half 0][W][X half 1].
-// ONE (XH == 2): the K-tile in ONE barrier segment per wave group (both X halves' 32
-// MFMAs behind one pair of barriers, all three regions of tile t+2 issued together) —
-// the XH == 1 schedule with a second X fragment set, half the barriers of two phases.
-template <int XH, int EPI, bool NT, bool ONE = false>
+// SCHED (XH == 2):
+//   0: ping-pong, two barrier segments per K-tile (one per X half);
+//   1 (ONE): ping-pong, the K-tile in ONE barrier segment per wave group (both X halves'
+//      32 MFMAs behind one pair of barriers, all three regions of tile t+2 issued together);
+//   2 (LOCKSTEP): no wave groups: per K-tile every wave waits for tile t, ONE barrier,
+//      issues tile t+2's three regions, then reads its 20 fragments and runs 32 MFMAs.
+//      Measured on the gate|up shape with the kernel's loop in isolation
+//      (tools/microbench/ingest.hip, profiles/decode_gemm_ingest_gate_up.jsonl): loads
+//      alone 55.1 us, MFMA alone 44.9 us, both 60.6 us -- against 72 us for schedule 0:
+//      with 2 waves per SIMD the MFMA of one wave covers the other's fragment reads
+//      without the second barrier set of the ping-pong.
+template <int XH, int EPI, bool NT, int SCHED = 0>
 __global__ void __launch_bounds__(512) gemm_pp_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
                                                       bf16_t* __restrict__ Y, float* __restrict__ P, int M, int N,
                                                       int K) {
@@ -170,6 +178,32 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const bf16_t* __restrict__
     __builtin_amdgcn_sched_barrier(0);
   };
 
+  constexpr bool ONE = SCHED == 1;
+  if constexpr (SCHED == 2) {
+    static_assert(XH == 2, "lock-step schedule: 256-token tiles");
+#pragma unroll
+    for (int r = 0; r < NR; ++r) issue(r, 0, 0);
+    if (T > 1) {
+#pragma unroll
+      for (int r = 0; r < NR; ++r) issue(r, 1, 1);
+    }
+    for (int t = 0; t < T; ++t) {
+      // tile t landed (tile t+1 may stay in flight); every wave's reads of tile t-1 were
+      // retired before its MFMAs, so after the barrier buffer (t+2) % 3 is free
+      if (t + 1 < T) vmw<GL * NR>(); else vmw<0>();
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (t + 2 < T) {
+#pragma unroll
+        for (int r = 0; r < NR; ++r) issue(r, (t + 2) % kNBuf, t + 2);
+      }
+      const char* cur = lds + (t % kNBuf) * BUF;
+      read_x(cur);
+      read_w(cur + kRegion);
+      read_x2(cur + 2 * kRegion);
+      mfma_q2(acc[0], acc[XH - 1]);
+    }
+  } else {
   // prologue: K-tiles 0 and 1 in flight; tile 0's first phase regions (X0, W) retired
 #pragma unroll
   for (int r = 0; r < NR; ++r) issue(r, 0, 0);
@@ -238,6 +272,7 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const bf16_t* __restrict__
     }
   }
   if (g == 0) seg();
+  }
 
 #pragma unroll
   for (int h = 0; h < XH; ++h)
@@ -270,9 +305,10 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const bf16_t* __restrict__
 }
 
 int gemm_pp(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, int N, int K, int S, int bm, bool silu_gu,
-            bool nt, hipStream_t stream, bool one_seg) {
+            bool nt, hipStream_t stream, int sched) {
   if (M < 1 || N % 128 != 0 || S < 1 || S > 32 || K % (kBK * S) != 0) return -1;
   if (bm != 128 && bm != 256) return -2;
+  if (sched < 0 || sched > 2 || (sched > 0 && bm != 256)) return -6;
   if (silu_gu && S != 1) return -3;
   if (S > 1 && P == nullptr) return -4;
   if (S == 1 && Y == nullptr) return -5;
@@ -283,11 +319,15 @@ int gemm_pp(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, int N,
   if (epi == kSilu) OAMD_PP(XH, kSilu, NTB); \
   else if (epi == kPartial) OAMD_PP(XH, kPartial, NTB); \
   else OAMD_PP(XH, kStore, NTB)
-#define OAMD_PP1(E) gemm_pp_kernel<2, E, true, true><<<grid, 512, 0, stream>>>(X, W, Y, P, M, N, K)
-  if (bm == 256 && one_seg) {   // one barrier segment per K-tile (nt weights)
-    if (epi == kSilu) OAMD_PP1(kSilu);
-    else if (epi == kPartial) OAMD_PP1(kPartial);
-    else OAMD_PP1(kStore);
+#define OAMD_PP1(E, SC) gemm_pp_kernel<2, E, true, SC><<<grid, 512, 0, stream>>>(X, W, Y, P, M, N, K)
+  if (sched == 1) {   // one barrier segment per K-tile (nt weights)
+    if (epi == kSilu) OAMD_PP1(kSilu, 1);
+    else if (epi == kPartial) OAMD_PP1(kPartial, 1);
+    else OAMD_PP1(kStore, 1);
+  } else if (sched == 2) {   // lock-step (nt weights)
+    if (epi == kSilu) OAMD_PP1(kSilu, 2);
+    else if (epi == kPartial) OAMD_PP1(kPartial, 2);
+    else OAMD_PP1(kStore, 2);
   } else if (bm == 256) {
     if (nt) { OAMD_PP_E(2, true); } else { OAMD_PP_E(2, false); }
   } else {

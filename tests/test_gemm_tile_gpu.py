@@ -136,10 +136,16 @@ def test_gemm_pp_decode(M, N, K):
                 ops.kernels().gemm_pp(x, w, None, P, S, bm, False, True)
                 torch.cuda.synchronize()
                 _close(P[:S * M * N].view(S, M, N).sum(0), r)
-            if bm == 256:   # one barrier segment per K-tile
-                y = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
-                ops.kernels().gemm_pp(x, w, y, P if S > 1 else None, S, bm, False, True, True)
-                _close(y, r)
+            if bm == 256:   # one barrier segment per K-tile (1), lock-step (2)
+                for sched in (1, 2):
+                    y = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+                    ops.kernels().gemm_pp(x, w, y, P if S > 1 else None, S, bm, False, True, sched)
+                    _close(y, r)
+                    if S > 1:
+                        P.fill_(float("nan"))
+                        ops.kernels().gemm_pp(x, w, None, P, S, bm, False, True, sched)
+                        torch.cuda.synchronize()
+                        _close(P[:S * M * N].view(S, M, N).sum(0), r)
 
 
 @pytest.mark.parametrize("M", [3, 128, 256])
@@ -153,7 +159,7 @@ def test_gemm_pp_silu(M):
     gg = (x.float() @ g.float().t()).to(torch.bfloat16)
     uu = (x.float() @ u.float().t()).to(torch.bfloat16)
     r = ref.silu_mul(torch.cat([gg, uu], 1), None)
-    for bm, one in ((128, False), (256, False), (256, True)):
+    for bm, sched in ((128, 0), (256, 0), (256, 1), (256, 2)):
         y = torch.empty(M, inter, dtype=torch.bfloat16, device=DEV)
-        ops.kernels().gemm_pp(x, wgu, y, None, 1, bm, True, True, one)
+        ops.kernels().gemm_pp(x, wgu, y, None, 1, bm, True, True, sched)
         _close(y, r, 3e-2)

@@ -29,6 +29,7 @@ for job in "$@"; do
                     cat gpurun_out/bench.json ;;
     ingest)         hipcc --offload-arch=gfx950 -O3 -std=c++17 -o /tmp/ingest tools/microbench/ingest.hip
                     timeout -k 10 120 /tmp/ingest | tee gpurun_out/ingest.jsonl ;;
+    decode-sched)   timeout -k 10 600 python -u tools/bench_decode_sched.py ${DS_ARGS:-} | tee gpurun_out/decode_sched.jsonl ;;
     decode-gemm)    timeout -k 10 300 python -u tools/bench_decode_gemm.py ${DG_ARGS:-} | tee gpurun_out/decode_gemm.jsonl ;;
     decode-pmc)     for i in 0 1 2; do
                       timeout -s KILL 240 rocprofv3 --pmc ${PMC_PASSES[$i]} --kernel-include-regex \
@@ -44,6 +45,13 @@ for job in "$@"; do
     tp8)            timeout -k 10 600 python -u tools/bench_tp.py --simulate-tp 8 --model llama3-70b --weights fp8 \
                       --batch 64 --prompt 1024 --gen 48 ${TP_ARGS:-} > gpurun_out/tp8.json 2> gpurun_out/tp8.err
                     tail -3 gpurun_out/tp8.json ;;
+    tp8-trace)      rm -rf gpurun_out/prof_tp8
+                    timeout -k 10 600 rocprofv3 --kernel-trace -d gpurun_out/prof_tp8 -o run --output-format csv \
+                      -- python3 tools/bench_tp.py --simulate-tp 8 --model llama3-70b --weights fp8 --batch 64 \
+                      --prompt 1024 --gen 48 ${TP_ARGS:-} > gpurun_out/tp8_trace.json 2> gpurun_out/tp8_trace.err
+                    python3 tools/trace_summary.py gpurun_out/prof_tp8/run_kernel_trace.csv \
+                      --out gpurun_out/tp8_trace_by_shape.txt --top 60 --delete
+                    tail -2 gpurun_out/tp8_trace.json; head -30 gpurun_out/tp8_trace_by_shape.txt ;;
     tp8-car)        for nb in 32 64; do   # one-shot AR+RMSNorm workgroup count
                       OAMD_CAR_BLOCKS=$nb timeout -k 10 300 python -u tools/bench_tp.py --simulate-tp 8 --model llama3-70b \
                         --weights fp8 --batch 64 --prompt 1024 --gen 48 > gpurun_out/tp_car$nb.log 2>&1 \
