@@ -10,7 +10,7 @@ from operator_amd.ops import reference as ref
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-VARIANTS = (0, 1, 2, 3, 4)   # gemm_tile schedules: auto (default = 1), 4-wave two-buffer four-phase, 8-wave 2-segment, 8-wave 4-segment, 4-wave with W-fragment MFMA groups
+VARIANTS = (0, 1, 2, 3, 4, 5)   # gemm_tile schedules: auto (default = 1), 4-wave two-buffer four-phase, 8-wave 2-segment, 8-wave 4-segment, 4-wave with W-fragment MFMA groups, 4-wave on 32x32x16 MFMAs
 
 
 def _rand(*shape, scale=1.0):
