@@ -137,7 +137,7 @@ def test_gemm_pp_decode(M, N, K):
                 torch.cuda.synchronize()
                 _close(P[:S * M * N].view(S, M, N).sum(0), r)
             if bm == 256:   # one barrier segment per K-tile (1), lock-step (2), wave-specialised loaders (3-5)
-                for sched in (1, 2, 3, 4, 5):
+                for sched in (1, 2, 3, 4, 5, 6, 7, 8):
                     y = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
                     ops.kernels().gemm_pp(x, w, y, P if S > 1 else None, S, bm, False, True, sched)
                     _close(y, r)
@@ -159,7 +159,7 @@ def test_gemm_pp_silu(M):
     gg = (x.float() @ g.float().t()).to(torch.bfloat16)
     uu = (x.float() @ u.float().t()).to(torch.bfloat16)
     r = ref.silu_mul(torch.cat([gg, uu], 1), None)
-    for bm, sched in ((128, 0), (256, 0), (256, 1), (256, 2), (256, 3), (256, 4), (256, 5)):
+    for bm, sched in ((128, 0), (256, 0), (256, 1), (256, 2), (256, 3), (256, 4), (256, 5), (256, 6), (256, 7), (256, 8)):
         y = torch.empty(M, inter, dtype=torch.bfloat16, device=DEV)
         ops.kernels().gemm_pp(x, wgu, y, None, 1, bm, True, True, sched)
         _close(y, r, 3e-2)

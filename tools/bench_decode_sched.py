@@ -43,7 +43,7 @@ def main() -> int:
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--shapes", default="qkv,o,down,gate_up+silu")
-    ap.add_argument("--scheds", default="0,1,2,3,4,5")
+    ap.add_argument("--scheds", default="0,2,4,6,7,8")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     M = a.m
