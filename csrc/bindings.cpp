@@ -247,7 +247,7 @@ void gemm_tile(const at::Tensor& x, const at::Tensor& w, const c10::optional<at:
 }
 
 void gemm_pp(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& y_opt,
-             const c10::optional<at::Tensor>& p, int64_t splits, int64_t bm, bool silu_gu, bool nt, int64_t sched) {
+             const c10::optional<at::Tensor>& p, int64_t splits, int64_t bm, bool silu_gu, bool nt, bool one_seg) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && w.size(1) == x.size(1), "x [M,K], w [N,K]");
   const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
@@ -273,7 +273,7 @@ void gemm_pp(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::T
   TORCH_CHECK(M * K < (1LL << 40) && N * K < (1LL << 40), "gemm too large");
   const c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   RC(oamd::gemm_pp(ptr<bf16_t>(x), ptr<bf16_t>(w), yp, pp, (int)M, (int)N, (int)K, (int)splits, (int)bm, silu_gu, nt,
-                   cur_stream(), (int)sched));
+                   cur_stream(), one_seg));
 }
 
 void gemm_skinny(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& y_opt,
@@ -549,7 +549,7 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("splits") = 1, pybind11::arg("partial") = pybind11::none());
   m.def("gemm_pp", &gemm_pp, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"),
         pybind11::arg("p") = pybind11::none(), pybind11::arg("splits") = 1, pybind11::arg("bm") = 256,
-        pybind11::arg("silu_gu") = false, pybind11::arg("nt") = true, pybind11::arg("sched") = 0);
+        pybind11::arg("silu_gu") = false, pybind11::arg("nt") = true, pybind11::arg("one_seg") = false);
   m.def("gemm_skinny", &gemm_skinny, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"),
         pybind11::arg("p") = pybind11::none(), pybind11::arg("splits") = 1, pybind11::arg("silu_gu") = false);
   m.def("attn_prefill", &attn_prefill, pybind11::arg("q"), pybind11::arg("k"), pybind11::arg("v"),

@@ -525,204 +525,6 @@ __global__ void __launch_bounds__(256) gemm_tile256_h4_kernel(const bf16_t* __re
   }
 }
 
-// 32x32x16 bf16 MFMA with the accumulator tied in AGPRs (16 per lane).
-__device__ __forceinline__ void mfma32_tied(f32x16& acc, const u16x8& a, const u16x8& b) {
-  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
-}
-
-// Variant 5: h4 on v_mfma_f32_32x32x16_bf16 (cdna_hip_programming.md §5.4 rule 28: build
-// both MFMA shapes at the same output tile per wave, keep the faster by wall). The same
-// 256 x 256 tile, 4 waves of 128 x 128 outputs, LDS image, DMA order, waits and barriers as
-// h4; the wave tile is 4 x 4 fragments of 32 x 32 (16 tied AGPRs each, 256 in all), half the
-// MFMA instructions (64 per K-tile, 32 cycles each) for the same operand bytes. Fragments
-// (A = W, B = X, so a lane holds 4 consecutive OUTPUT FEATURES of one token per register
-// quad): X fragment i = tokens wm*128 + 32 i + lane%32, W fragment j (f = j / 2, type = j % 2)
-// = rows f*128 + type*64 + wn*32 + lane%32 (gate / up of the same features in j = 2f, 2f+1);
-// k-substep s of k-half h reads chunk 4h + 2s + lane/32 of the row (the h4 source swizzle is
-// conflict-free for this pattern too: each 16-lane ds_read_b128 group covers 16 distinct
-// (row parity, slot) pairs). Phases per K-tile t (buffer t & 1), 16 MFMAs each:
-//   1. (k-half 0, s 0) from A; read k-half 1 of tile t into B (16 reads)   lgkmcnt + barrier
-//   2. (k-half 0, s 1) from A; 8 W pieces of tile t+2 into buffer t & 1    vmcnt(16) + barrier
-//   3. (k-half 1, s 0) from B; 8 X pieces of tile t+2; W of tile t+1 k-half 0 into A
-//                                                                          vmcnt(16) + barrier
-//   4. (k-half 1, s 1) from B; X of tile t+1 k-half 0 into A
-template <int EPI, int AUX = 16>
-__global__ void __launch_bounds__(256) gemm_tile256_h4m32_kernel(const bf16_t* __restrict__ X,
-                                                                 const bf16_t* __restrict__ W, bf16_t* __restrict__ Y,
-                                                                 const bf16_t* __restrict__ bias, int M, int N, int K,
-                                                                 int ldy) {
-  constexpr int kHalf = 32768;
-  constexpr int kTile = 2 * kHalf;
-  __shared__ __attribute__((aligned(1024))) char lds[2 * kTile];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = w >> 1, wn = w & 1;
-
-  const int mt = (M + kT - 1) / kT, nt = (N + kT - 1) / kT;
-  const int nwg = mt * nt;
-  const int lid = xcd_remap(blockIdx.x, nwg);
-  const int gsz = kGroupM * nt;
-  const int first_m = (lid / gsz) * kGroupM;
-  const int gm = min(mt - first_m, kGroupM);
-  const int tm = first_m + (lid % gsz) % gm;
-  const int tn = (lid % gsz) / gm;
-  const int m0 = tm * kT, n0 = tn * kT;
-
-  const int lrow = lane >> 3, lslot = lane & 7;
-  uint32_t xo[8], wo[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const int row = 8 * (w + 4 * q) + lrow;
-    const int chunk = lslot ^ ((row >> 1) & 7);
-    xo[q] = ((uint32_t)min(m0 + row, M - 1) * (uint32_t)K + chunk * 8) * 2u;
-    wo[q] = ((uint32_t)min(n0 + row, N - 1) * (uint32_t)K + chunk * 8) * 2u;
-  }
-  const auto xr = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)((uint32_t)M * (uint32_t)K * 2u), 0x00020000);
-  const auto wr = __builtin_amdgcn_make_buffer_rsrc((void*)W, (short)0, (int)((uint32_t)N * (uint32_t)K * 2u), 0x00020000);
-  const int T = K / kBK;
-  auto dma_x = [&](int kt, int buf, int q) {
-    char* dst = lds + buf * kTile + (w + 4 * q) * 1024;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)dst, 16, (int)xo[q],
-                                             min(kt, T - 1) * (kBK * 2), 0, AUX);
-  };
-  auto dma_w = [&](int kt, int buf, int q) {
-    char* dst = lds + buf * kTile + kHalf + (w + 4 * q) * 1024;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (__attribute__((address_space(3))) void*)dst, 16, (int)wo[q],
-                                             min(kt, T - 1) * (kBK * 2), 0, AUX);
-  };
-
-  const int l31 = lane & 31, lh = lane >> 5, sw = (l31 >> 1) & 7;
-  const int xrow = (wm * 128 + l31) * 128, wrow = (wn * 32 + l31) * 128;
-  // chunk slot of k-half h, substep s
-  auto slot = [&](int h, int s) { return ((4 * h + 2 * s + lh) ^ sw) << 4; };
-  auto rdx = [&](int buf, int h, int s, u16x8& dst, int i) {
-    dst = *reinterpret_cast<const u16x8*>(lds + buf * kTile + xrow + i * 4096 + slot(h, s));
-  };
-  auto rdw = [&](int buf, int h, int s, u16x8& dst, int j) {
-    const int r = (j >> 1) * 128 + (j & 1) * 64;
-    dst = *reinterpret_cast<const u16x8*>(lds + buf * kTile + kHalf + wrow + r * 128 + slot(h, s));
-  };
-
-  f32x16 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-  u16x8 xa[2][4], wa[2][4], xb[2][4], wb[2][4];
-  // 16 MFMAs of one substep, op(k) after MFMA k (k = 0..15) when EVERY, else after odd ones
-  auto phase = [&](const u16x8 (&xf)[4], const u16x8 (&wf)[4], auto op) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        mfma32_tied(acc[i][j], wf[j], xf[i]);
-        __builtin_amdgcn_sched_barrier(0);
-        op(4 * i + j);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-  };
-
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) asm volatile("" : "+a"(acc[i][j]));
-  asm volatile("s_nop 4");
-
-#pragma unroll
-  for (int tt = 0; tt < 2; ++tt) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) dma_w(tt, tt, q);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) dma_x(tt, tt, q);
-  }
-  vm_wait<16>();
-  seg_barrier();
-#pragma unroll
-  for (int s = 0; s < 2; ++s)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      rdx(0, 0, s, xa[s][i], i);
-      rdw(0, 0, s, wa[s][i], i);
-    }
-
-  for (int t = 0; t < T; ++t) {
-    const int b = t & 1, nb = b ^ 1;
-    // 1: k-half 0, substep 0; read k-half 1 of tile t (16 fragments, one per MFMA)
-    phase(xa[0], wa[0], [&](int k) {
-      const int s = k >> 3, i = (k >> 1) & 3;
-      if (k & 1) rdw(b, 1, s, wb[s][i], i);
-      else rdx(b, 1, s, xb[s][i], i);
-    });
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    seg_barrier();
-    // 2: k-half 0, substep 1; W pieces of tile t+2 into buffer b
-    phase(xa[1], wa[1], [&](int k) {
-      if (k & 1) dma_w(t + 2, b, k >> 1);
-    });
-    vm_wait<16>();
-    seg_barrier();
-    // 3: k-half 1, substep 0; X pieces of tile t+2; W of tile t+1, k-half 0
-    phase(xb[0], wb[0], [&](int k) {
-      if (k & 1) rdw(nb, 0, k >> 3, wa[k >> 3][(k >> 1) & 3], (k >> 1) & 3);
-      else dma_x(t + 2, b, k >> 1);
-    });
-    vm_wait<16>();
-    seg_barrier();
-    // 4: k-half 1, substep 1; X of tile t+1, k-half 0
-    phase(xb[1], wb[1], [&](int k) {
-      if (k & 1) rdx(nb, 0, k >> 3, xa[k >> 3][(k >> 1) & 3], (k >> 1) & 3);
-    });
-  }
-  vm_wait<0>();
-  asm volatile("s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
-
-  // lane: token m0 + wm*128 + 32 i + lane%32; register quad q of fragment j: features
-  // 8 q + 4 (lane / 32) .. + 3 of the fragment's 32 rows
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int tok = m0 + wm * 128 + i * 32 + l31;
-    if (tok >= M) continue;
-    bf16_t* yrow = Y + (int64_t)tok * ldy;
-#pragma unroll
-    for (int f = 0; f < 2; ++f)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int fo = wn * 32 + 8 * q + 4 * lh;   // feature offset inside the 64-row gate / up block
-        if constexpr (EPI == kEpiSilu) {
-          const int col = (n0 >> 1) + f * 64 + fo;
-          if (2 * col >= N) continue;
-          f32x4 o;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float gg = bf2f(f2bf(acc[i][2 * f][4 * q + r]));
-            const float uu = bf2f(f2bf(acc[i][2 * f + 1][4 * q + r]));
-            o[r] = bf2f(f2bf(gg / (1.f + __expf(-gg)))) * uu;
-          }
-          *reinterpret_cast<uint2*>(yrow + col) = pack4(o);
-        } else {
-#pragma unroll
-          for (int ty = 0; ty < 2; ++ty) {
-            const int col = n0 + f * 128 + ty * 64 + fo;
-            if (col >= N) continue;
-            f32x4 v;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = acc[i][2 * f + ty][4 * q + r];
-            if constexpr (EPI == kEpiBias) {
-              const uint2 bb = *reinterpret_cast<const uint2*>(bias + col);
-              v[0] += __uint_as_float(bb.x << 16);
-              v[1] += __uint_as_float(bb.x & 0xffff0000u);
-              v[2] += __uint_as_float(bb.y << 16);
-              v[3] += __uint_as_float(bb.y & 0xffff0000u);
-            }
-            *reinterpret_cast<uint2*>(yrow + col) = pack4(v);
-          }
-        }
-      }
-  }
-}
-
 // y[m, f] = SwiGLU of the split-K sums of the interleaved gate|up slabs (64-feature
 // blocks): g = bf16(sum_s P[s][m][128 b + j]), u = bf16(sum_s P[s][m][128 b + 64 + j]),
 // y = bf16(bf16(silu(g)) * u) — the numerics of the fused epilogue. 4 features per thread.
@@ -776,10 +578,6 @@ int gemm_tile(const bf16_t* X, const bf16_t* W, bf16_t* Y, const bf16_t* bias, i
     if (silu_gu) gemm_tile256_h4_kernel<kEpiSilu><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
     else if (bias) gemm_tile256_h4_kernel<kEpiBias><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
     else gemm_tile256_h4_kernel<kEpiStore><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-  } else if (variant == 5 && off32) {   // h4 on 32x32x16 MFMAs
-    if (silu_gu) gemm_tile256_h4m32_kernel<kEpiSilu><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-    else if (bias) gemm_tile256_h4m32_kernel<kEpiBias><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-    else gemm_tile256_h4m32_kernel<kEpiStore><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
   } else if (variant == 4 && off32) {   // h4 with W-fragment MFMA groups (timing)
     if (silu_gu) gemm_tile256_h4_kernel<kEpiSilu, 16, true><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
     else if (bias) gemm_tile256_h4_kernel<kEpiBias, 16, true><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);

@@ -66,7 +66,7 @@ def main():
                     C.gemm_tile(x, w, y, None, silu, 0, S, P if S > 1 else None)
                 return f
 
-            def pp(S, bm, nt, one=0):
+            def pp(S, bm, nt, one=False):
                 def f():
                     w = ws[it["i"] % len(ws)]
                     it["i"] += 1
@@ -84,8 +84,7 @@ def main():
                         for nt in (True, False):
                             cands[f"pp_bm{bm}_s{S}{'_nt' if nt else ''}"] = pp(S, bm, nt)
                         if bm == 256:
-                            cands[f"pp_bm256_s{S}_one"] = pp(S, bm, True, 1)
-                            cands[f"pp_bm256_s{S}_ls"] = pp(S, bm, True, 2)
+                            cands[f"pp_bm256_s{S}_one"] = pp(S, bm, True, True)
             t = {k: [] for k in cands}
             for _ in range(a.rounds):
                 for k, f in cands.items():

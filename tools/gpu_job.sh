@@ -29,7 +29,6 @@ for job in "$@"; do
                     cat gpurun_out/bench.json ;;
     ingest)         hipcc --offload-arch=gfx950 -O3 -std=c++17 -o /tmp/ingest tools/microbench/ingest.hip
                     timeout -k 10 120 /tmp/ingest | tee gpurun_out/ingest.jsonl ;;
-    decode-sched)   timeout -k 10 600 python -u tools/bench_decode_sched.py ${DS_ARGS:-} | tee gpurun_out/decode_sched.jsonl ;;
     decode-gemm)    timeout -k 10 300 python -u tools/bench_decode_gemm.py ${DG_ARGS:-} | tee gpurun_out/decode_gemm.jsonl ;;
     decode-pmc)     for i in 0 1 2; do
                       timeout -s KILL 240 rocprofv3 --pmc ${PMC_PASSES[$i]} --kernel-include-regex \

@@ -315,15 +315,26 @@ int run(const char* name, int grid, const uint16_t* X, const std::vector<uint16_
   return 0;
 }
 
+// uniform-ish random bf16 in [-1, 1) from a hash (constant operands inflate MFMA clocks:
+// cdna_hip_programming.md §5.4 rule 25)
+__global__ void fill_random(uint16_t* p, size_t n, uint32_t seed, float scale) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+    h ^= h >> 15; h *= 2246822519u; h ^= h >> 13;
+    const float f = ((h & 0xffffff) / 16777216.f * 2.f - 1.f) * scale;
+    p[i] = (uint16_t)(__float_as_uint(f) >> 16);
+  }
+}
+
 int main() {
   const int K = 4096, N = 28672, M = 256;
   uint16_t* X;
   CK(hipMalloc(&X, (size_t)M * K * 2));
-  CK(hipMemset(X, 0x3c, (size_t)M * K * 2));
+  fill_random<<<1024, 256>>>(X, (size_t)M * K, 1u, 1.f);
   std::vector<uint16_t*> Ws(3);
   for (auto& w : Ws) {
     CK(hipMalloc(&w, (size_t)N * K * 2));
-    CK(hipMemset(w, 0x3b, (size_t)N * K * 2));
+    fill_random<<<4096, 256>>>(w, (size_t)N * K, 7u, 0.05f);
   }
   float* sink;
   CK(hipMalloc(&sink, 512 * 512 * 4));
