@@ -44,7 +44,7 @@ int gemm_tile(const bf16_t* X, const bf16_t* W, bf16_t* Y, const bf16_t* bias, i
 // (128 / 256), 128-column tiles (N % 128 == 0), S-way split-K slabs P (S > 1; reduced into Y unless Y is
 // nullptr); silu_gu: fused SwiGLU (S == 1), Y [M, N/2]; nt: non-temporal weight loads.
 int gemm_pp(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, int N, int K, int S, int bm, bool silu_gu,
-            bool nt, hipStream_t stream, bool one_seg = false);   // sched: 0 ping-pong, 1 one segment, 2 lock-step, 3-5 wave-specialised loaders, 6-8 pipelined fragment reads (8: lock-step loaders)
+            bool nt, hipStream_t stream, bool one_seg = false);
 // Y[M, N] = bf16(sum_s P[s][M][N]) (fp32 split-K slabs).
 int splitk_reduce(const float* P, bf16_t* Y, int64_t MN, int S, hipStream_t stream);
 // Skinny-M decode GEMM (M <= 32, gemm_skinny.hip): N % 16 == 0, K % (128 S) == 0; S-way split-K slabs P
