@@ -357,6 +357,21 @@ __global__ void __launch_bounds__(car::kThreads) ar_rmsnorm_kernel(
     const int64_t a = TWO ? min(v1, v0 + p * pq) : v0, e = TWO ? min(v1, a + pq) : v1;
     for (int64_t v = a + tid; v < e; v += car::kThreads) car::st16(rs[p], car::slot_off(c.par, W, rank, capvec, v), load_x(v));
   }
+  // the first row's residual and weight vectors, loaded while the hand-off is in flight
+  // (they do not depend on it): one memory round trip off the critical path
+  const u16x8* w8 = reinterpret_cast<const u16x8*>(w);
+  u16x8 h_pre[MAXV], w_pre[MAXV];
+  if (r0 < r1) {
+    const u16x8* hr0 = reinterpret_cast<const u16x8*>(residual + (int64_t)r0 * hidden);
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      const int vi = tid + i * car::kThreads;
+      if (vi < nvr) {
+        h_pre[i] = hr0[vi];
+        w_pre[i] = w8[vi];
+      }
+    }
+  }
   car::publish<W, LIGHT>(peers, car::kFlagsOff, b, rank, c.round, tid);
   car::wait_all<W, LIGHT>(mine, car::kFlagsOff, b, c.round, timeout_ticks, tid, &s_err);
   if (s_err) {
@@ -381,7 +396,6 @@ __global__ void __launch_bounds__(car::kThreads) ar_rmsnorm_kernel(
       return;
     }
   }
-  const u16x8* w8 = reinterpret_cast<const u16x8*>(w);
   for (int r = r0; r < r1; ++r) {
     u16x8* hr = reinterpret_cast<u16x8*>(residual + (int64_t)r * hidden);
     u16x8* yr = reinterpret_cast<u16x8*>(y + (int64_t)r * hidden);
@@ -403,7 +417,7 @@ __global__ void __launch_bounds__(car::kThreads) ar_rmsnorm_kernel(
 #pragma unroll
           for (int j = 0; j < 8; ++j) a[j] = bf2f(f2bf(a[j]));
         }
-        const u16x8 hv = hr[vi];
+        const u16x8 hv = r == r0 ? h_pre[i] : hr[vi];
         u16x8 s;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -420,7 +434,7 @@ __global__ void __launch_bounds__(car::kThreads) ar_rmsnorm_kernel(
     for (int i = 0; i < MAXV; ++i) {
       const int vi = tid + i * car::kThreads;
       if (vi < nvr) {
-        const u16x8 wv = w8[vi];
+        const u16x8 wv = w_pre[i];   // the same weight vector for every row
         u16x8 o;
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = f2bf(bf2f(f2bf(v[i][j] * rs_)) * bf2f(wv[j]));

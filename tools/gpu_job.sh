@@ -73,6 +73,14 @@ for job in "$@"; do
                       2> gpurun_out/bench_power.err || { kill $mon; tail -5 gpurun_out/bench_power.err; exit 1; }
                     kill $mon || true
                     tail -c 300 gpurun_out/bench_power.json ;;
+    blas-names)     # which hipBLASLt kernels F.linear runs on the prefill shapes (tile, MFMA, schedule in the name)
+                    rm -rf gpurun_out/prof_blas
+                    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_blas -o run --output-format csv \
+                      -- python3 tools/gemm_tile_variants.py --variants 1 --m 32768 --n 4096 --k 14336 --rounds 2 \
+                      > gpurun_out/blas_names.log 2>&1
+                    python3 -c "import csv,collections;c=collections.Counter(r['Kernel_Name'][:200] for r in csv.DictReader(open('gpurun_out/prof_blas/run_kernel_trace.csv')));[print(n,k) for k,n in c.most_common(8)]" \
+                      | tee gpurun_out/blas_kernel_names.txt
+                    rm -f gpurun_out/prof_blas/run_kernel_trace.csv ;;
     gemm-tile)      timeout -k 10 300 python -u tools/gemm_tile_variants.py ${GTV_ARGS:-} | tee gpurun_out/gtv.jsonl ;;
     pmc-gemm-tile)  bash tools/pmc_gemm_tile.sh "${PMC_VARIANTS:-1 2 blas}"
                     cat gpurun_out/pmc_summary.txt ;;
