@@ -46,7 +46,7 @@ PROTO_ONESHOT, PROTO_TWOSHOT, PROTO_FENCE = 0, 1, 2   # csrc/kernels/kernels.h k
 _FORCED = {"oneshot": PROTO_ONESHOT, "twoshot": PROTO_TWOSHOT, "fence": PROTO_FENCE}
 # workgroups of every one-shot call (fixed per group: each block keeps its own round
 # counter and data-slot parity, so every call of a group must use the same count)
-DEFAULT_BLOCKS = int(os.environ.get("OAMD_CAR_BLOCKS", "32"))
+DEFAULT_BLOCKS = int(os.environ.get("OAMD_CAR_BLOCKS", "64"))   # 64 vs 32: 7.15 vs 7.63 ms TP8-sim step (profiles/tp8_car_blocks_r5.jsonl)
 
 
 class OneShotAllReduce:
