@@ -274,3 +274,44 @@ def test_noisy_log_every_line_matches_equals_cpu_scan():
     cpu = eng.scan_cpu(docs)
     assert gpu.shape[0] == cpu.shape[0] > 4 * 40000
     assert _rows(gpu) == _rows(cpu)
+
+
+@pytest.mark.parametrize("lazy", [False, True])
+def test_pipelined_analyze_equals_one_batch(lazy):
+    """A large batch is analysed in sub-batches (MatchEngine._analyze_pipelined: the next
+    sub-batch's pack + H2D + scan on a worker thread in the other buffer set, while the
+    host verifies, scores and builds the previous one): every result equals the
+    one-batch analyze and the host path, and three back-to-back calls reuse both
+    buffer sets."""
+    ps = synthetic_library(300, seed=4)
+    docs = LogFactory(n_patterns=300, seed=11).batch(61, 24 * 1024, n_failures=3, seed=3)[0]
+    docs[7] = b""                      # an empty doc inside a sub-batch
+    one = MatchEngine(ps, device="cuda", seg_bytes=1024, profile_bytes=0)
+    one.PIPE_SUB_BYTES = 0
+    pipe = MatchEngine(ps, device="cuda", seg_bytes=1024, profile_bytes=0)
+    pipe.PIPE_MIN_BYTES = 1
+    pipe.PIPE_SUB_BYTES = 200 * 1024   # ~7 sub-batches
+    subs = pipe._sub_batches(docs)
+    assert subs is not None and len(subs) >= 5
+    assert subs[0][0] == 0 and subs[-1][1] == len(docs) and all(a[1] == b[0] for a, b in zip(subs, subs[1:]))
+    pods = [(f"pod-{i}", "ns") for i in range(len(docs))]
+
+    def strip(o):
+        o = dict(o)
+        o.pop("analysisId", None)
+        o.pop("analysis_id", None)
+        m = dict(o.get("metadata", {}))
+        m.pop("processingTimeMs", None)
+        m.pop("engine", None)
+        o["metadata"] = m
+        return o
+
+    want = [strip(r.to_obj()) for r in one.analyze(docs, pods)]
+    host = [strip(r.to_obj()) for r in MatchEngine(ps, device="cpu").analyze(docs, pods)]
+    assert want == host
+    for _ in range(3):
+        got = pipe.analyze(docs, pods, lazy=lazy)
+        assert len(got) == len(docs)
+        assert [strip(got[i].to_obj()) for i in range(len(docs))] == want
+        assert pipe.last_timing["subs"] == len(subs)
+    torch.cuda.synchronize()

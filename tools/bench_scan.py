@@ -53,6 +53,8 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--arms", default="bfs,profiled")
     ap.add_argument("--pack-sweep", action="store_true")
+    ap.add_argument("--pipe-sweep", default="0,128,256,400,640",
+                    help="MatchEngine.PIPE_SUB_BYTES values (MB; 0 = one batch) timed after the main arm")
     a = ap.parse_args()
     ps = synthetic_library(a.patterns)
     t0 = time.perf_counter()
@@ -74,6 +76,7 @@ def main():
         first_s = t2 - t1
         warm = []
         for _ in range(3):   # steady state: best of three more calls (the first loads the score tables)
+            del res          # the previous call's result objects are freed outside the timed call
             u1 = time.perf_counter()
             res = eng.analyze(docs)
             warm.append(time.perf_counter() - u1)
@@ -81,6 +84,7 @@ def main():
         stage = {"analyze_" + k: round(v, 4) for k, v in eng.last_timing.items()}
         lz, mat = [], []
         for _ in range(3):   # lazy: events + context windows; then materialize every result object
+            lres = None
             u1 = time.perf_counter()
             lres = eng.analyze(docs, lazy=True)
             u2 = time.perf_counter()
@@ -108,6 +112,22 @@ def main():
                         best = min(best, time.perf_counter() - u1)
                     print(json.dumps({"bench": "scan_pack", "chunk_mb": chunk_mb, "threads": th,
                                       "analyze_s": round(best, 4)}), flush=True)
+        pipe = {}
+        sub0 = eng.PIPE_SUB_BYTES
+        sweep = [int(x) for x in a.pipe_sweep.split(",") if x]
+        for _ in range(5):   # round-robin over the settings: host-state drift hits every one alike
+            for mb in sweep:
+                eng.PIPE_SUB_BYTES = mb << 20
+                r = None
+                u1 = time.perf_counter()
+                r = eng.analyze(docs)
+                dt = time.perf_counter() - u1
+                cur = pipe.setdefault(str(mb), {"analyze_s": 1e9})
+                if dt < cur["analyze_s"]:
+                    pipe[str(mb)] = {"analyze_s": round(dt, 4),
+                                     "timing": {k: round(v, 4) for k, v in eng.last_timing.items()}}
+                del r
+        eng.PIPE_SUB_BYTES = sub0
         print(json.dumps({"bench": "scan", "arm": arm, "bytes": total, "padded_bytes": tot_pad,
                           "patterns": a.patterns, "states": eng.dfa_states, "hot_states": eng.hot_states,
                           "hot_coverage": eng.hot_coverage, "kernel_ms": round(ms, 3),
@@ -115,7 +135,7 @@ def main():
                           "same_matches_as_first_arm": same, "analyze_s": round(t2 - t1, 4),
                           "analyze_first_call_s": round(first_s, 3), "analyze_GBps": round(total / (t2 - t1) / 1e9, 1),
                           "analyses_per_s": round(len(res) / (t2 - t1), 1), "gen_s": round(gen_s, 1),
-                          "stages_best_of_3": stage}), flush=True)
+                          "stages_best_of_3": stage, "pipe_sub_mb_sweep": pipe}), flush=True)
         del eng
 
 
