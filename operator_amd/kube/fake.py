@@ -35,6 +35,18 @@ from operator_amd.utils.timefmt import instant_str
 from .resources import (ALL, PODS, ApiError, Resource, WatchClosed, match_fields, match_selector, parse_selector)
 
 
+_KEYS: dict[int, tuple[Resource, str]] = {}
+
+
+def _res_key(res: Resource) -> str:
+    """Store key of a resource, computed once per Resource object (every verb needs it;
+    the dataclass property + f-string per call showed in the API server's profile)."""
+    e = _KEYS.get(id(res))
+    if e is None or e[0] is not res:
+        e = _KEYS[id(res)] = (res, f"{res.api_version}/{res.plural}")
+    return e[1]
+
+
 def _jcopy(o: Any) -> Any:
     """Deep copy of a JSON value (dicts, lists, scalars): what copy.deepcopy does for
     API objects, without its memo bookkeeping (several times faster; API objects
@@ -180,9 +192,7 @@ class FakeKube:
             self.calls.append((verb, res.plural, ns, name))
 
     # ------------------------------------------------------------------ helpers
-    @staticmethod
-    def _key(res: Resource) -> str:
-        return f"{res.api_version}/{res.plural}"
+    _key = staticmethod(_res_key)
 
     def _kind(self, key: str) -> dict:
         """Per-resource index {(ns, name): obj} over the same objects as ``_objs``."""
@@ -252,7 +262,10 @@ class FakeKube:
                 out.append(o)
         return [_jcopy(o) for o in out] if copy else out
 
-    def create(self, res: Resource, obj: dict, namespace: str | None = None, *, copy: bool = True) -> dict:
+    def create(self, res: Resource, obj: dict, namespace: str | None = None, *, copy: bool = True,
+               owned: bool = False) -> dict:
+        """``owned``: the caller hands ``obj`` over (a freshly decoded request body, the REST
+        server) -- it is stored as is instead of deep-copied first."""
         ns = namespace or obj.get("metadata", {}).get("namespace") or ("default" if res.namespaced else "")
         name = obj.get("metadata", {}).get("name")
         self._log_call("create", res, ns, name)
@@ -266,7 +279,7 @@ class FakeKube:
             k = (self._key(res), ns if res.namespaced else "", name)
             if k in self._objs:
                 raise ApiError(409, f"{res.plural} {name} already exists", "AlreadyExists")
-            o = _jcopy(obj)
+            o = obj if owned else _jcopy(obj)
             md = o.setdefault("metadata", {})
             md["name"] = name
             if res.namespaced:

@@ -18,10 +18,13 @@ from __future__ import annotations
 import json
 import socketserver
 import threading
-from urllib.parse import parse_qs, urlparse
+from urllib.parse import parse_qsl
 
 from .fake import FakeKube
 from .resources import ALL, ApiError, Resource, WatchClosed
+
+
+_BY_PATH = {(r.group, r.version, r.plural): r for r in ALL}
 
 
 def _route(path: str) -> tuple[Resource, str | None, str | None, str | None] | None:
@@ -37,11 +40,11 @@ def _route(path: str) -> tuple[Resource, str | None, str | None, str | None] | N
     ns = None
     if len(rest) >= 2 and rest[0] == "namespaces" and len(rest) > 2:
         ns, rest = rest[1], rest[2:]
+    if not rest:
+        return None
     plural, name, sub = rest[0], (rest[1] if len(rest) > 1 else None), (rest[2] if len(rest) > 2 else None)
-    for r in ALL:
-        if r.group == group and r.version == version and r.plural == plural:
-            return r, ns, name, sub
-    return None
+    r = _BY_PATH.get((group, version, plural))
+    return None if r is None else (r, ns, name, sub)
 
 
 _REASONS = {200: b"OK", 201: b"Created", 400: b"Bad Request", 403: b"Forbidden", 404: b"Not Found",
@@ -124,9 +127,12 @@ class FakeKubeServer:
         """Serve one unary request into ``c`` (``respond`` / ``json``); a watch request
         is returned as (resource, namespace, resourceVersion) for the caller to stream."""
         fk = self.fk
-        u = urlparse(target)
-        q = {k: v[0] for k, v in parse_qs(u.query).items()}
-        rt = _route(u.path)
+        path, _, query = target.partition("?")
+        q = {}
+        if query:
+            for k, v in parse_qsl(query.partition("#")[0]):
+                q.setdefault(k, v)   # the first value of a repeated key, as parse_qs()[k][0]
+        rt = _route(path.partition("#")[0])
         if rt is None:
             return c.json(404, {"message": "not found", "reason": "NotFound", "code": 404})
         res, ns, name, sub = rt
@@ -153,7 +159,7 @@ class FakeKubeServer:
                     raise ApiError(404, f"{res.plural} {name} not found", "NotFound")
                 return c.json(200, o)
             if method == "POST":
-                return c.json(201, fk.create(res, body(), ns, copy=False))
+                return c.json(201, fk.create(res, body(), ns, copy=False, owned=True))
             if method == "PUT":
                 if sub == "status":
                     return c.json(200, fk.replace_status(res, body(), ns, copy=False))
