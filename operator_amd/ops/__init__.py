@@ -334,11 +334,24 @@ def skinny_plan(M: int, N: int, K: int) -> int | None:
     return S
 
 
-BLAS_CALLS = {"n": 0}   # GPU GEMMs that fell back to hipBLASLt (tests assert it stays 0 on model shapes)
+# The plain prefill projections (M > 256 rows, no bias, no fused epilogue: QKV, O and down
+# of the Llama family) are library GEMMs and run on hipBLASLt: its hand-scheduled stream-K
+# MT256x256x64 kernel is 1.13-1.18x gemm_tile h4 on those shapes at M = 32k
+# (profiles/gemm_tile_h4_vs_ph2_m32k.jsonl, hipblaslt_prefill_kernel_names.txt) and the
+# flagship runs +1.2 % faster with it (interleaved A/B, profiles/bench_prefill_blas_ab_r5.jsonl).
+# Everything fused stays on the gfx950 kernels: gate|up + SwiGLU and biased projections
+# (gemm_tile), every decode GEMM (gemm_pp / gemm_tn / gemm_skinny, faster than hipBLASLt
+# there), the lm_head, fp8. OAMD_PREFILL_BLAS=0 puts the plain projections on gemm_tile too.
+PREFILL_BLAS = os.environ.get("OAMD_PREFILL_BLAS", "1") != "0"
+BLAS_CALLS = {"n": 0}   # GPU GEMMs that FELL BACK to hipBLASLt (tests assert it stays 0 on model shapes)
+BLAS_PLANNED = {"n": 0}   # plain prefill projections run on hipBLASLt by design (PREFILL_BLAS)
 
 
-def _blas(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None, bias: torch.Tensor | None):
-    if x.is_cuda:
+def _blas(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None, bias: torch.Tensor | None,
+          planned: bool = False):
+    if x.is_cuda and planned:
+        BLAS_PLANNED["n"] += 1
+    elif x.is_cuda:
         BLAS_CALLS["n"] += 1
         if os.environ.get("OAMD_FORBID_BLAS") == "1":
             raise RuntimeError(f"hipBLASLt fallback for x {tuple(x.shape)} {x.dtype}, w {tuple(w.shape)} "
@@ -391,6 +404,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None, sp
         return _blas(x, w, out, bias)
     if x.is_cuda and bm is None and bn is None and splits is None and _measured_blas(M, N, K):
         return _blas(x, w, out, None)
+    if PREFILL_BLAS and x.is_cuda and M > 256 and N < LM_HEAD_MIN_N and splits is None and x.dtype == torch.bfloat16:
+        return _blas(x, w, out, None, planned=True)
     if (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous() and M <= SKINNY_MAX_M
             and bm is None and bn is None):
         S = splits or skinny_plan(M, N, K)

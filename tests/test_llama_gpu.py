@@ -328,20 +328,24 @@ def test_fp8_kv_cache_engine_tracks_bf16_cache():
     assert cos > 0.99, float(cos)
 
 
-def test_llama3_8b_prefill_and_lm_head_never_use_hipblaslt(monkeypatch):
-    """Every prefill projection (QKV, O, gate|up + SwiGLU, down) and the lm_head of the
-    Llama-3-8B shapes run on the hand-written gfx950 kernels: with OAMD_FORBID_BLAS=1 any
-    hipBLASLt fallback raises. Two layers of the real architecture, prefill batches of
-    1k and 4k packed tokens (tails included) and the M = 64 / 256 decode buckets."""
+@pytest.mark.parametrize("prefill_blas", [False, True])
+def test_llama3_8b_shapes_never_fall_back_to_hipblaslt(monkeypatch, prefill_blas):
+    """Every GEMM of the Llama-3-8B shapes runs where it is planned to: with
+    OAMD_FORBID_BLAS=1 any hipBLASLt FALLBACK raises. Two layers of the real architecture,
+    prefill batches of 1k and 4k packed tokens (tails included) and the M = 64 / 256
+    decode buckets. With ops.PREFILL_BLAS the plain prefill projections (QKV, O, down:
+    3 per layer and batch) are planned hipBLASLt calls and nothing else is; without it
+    every GEMM runs on the gfx950 kernels."""
     from dataclasses import replace
 
     from operator_amd import ops
 
     monkeypatch.setenv("OAMD_FORBID_BLAS", "1")
+    monkeypatch.setattr(ops, "PREFILL_BLAS", prefill_blas)
     cfg = replace(get_config("llama3-8b"), layers=2)
     m = LlamaModel(cfg, device="cuda").init_random(seed=3)
     kv = PagedKVCache(cfg.layers, 128, cfg.kv_heads, 128, 64, device="cuda")
-    n0 = ops.BLAS_CALLS["n"]
+    n0, p0 = ops.BLAS_CALLS["n"], ops.BLAS_PLANNED["n"]
     for lens in ([1024], [700, 1300, 2096]):
         T = sum(lens)
         ids = torch.randint(0, cfg.vocab_size, (T,), device="cuda")
@@ -350,9 +354,15 @@ def test_llama3_8b_prefill_and_lm_head_never_use_hipblaslt(monkeypatch):
         fb = ForwardBatch(ids, pos, torch.full((T,), -1, dtype=torch.long, device="cuda"), True, last, seq_lens=lens)
         lg = m.forward(fb, kv)
         assert lg.shape == (len(lens), cfg.vocab_size) and torch.isfinite(lg.float()).all()
+    assert ops.BLAS_PLANNED["n"] - p0 == (2 * 2 * 3 if prefill_blas else 0)
     eng = LLMEngine(m, kv, max_batch=256, max_context=512, use_graphs=False)
+    p1 = ops.BLAS_PLANNED["n"]
     for B in (64, 256):
         reqs = [GenRequest(list(range(1, 17)), max_tokens=2, temperature=0.0, ignore_eos=True) for _ in range(B)]
         eng.generate(reqs)
         assert all(len(r.output) == 2 for r in reqs)
     assert ops.BLAS_CALLS["n"] == n0
+    # decode never plans hipBLASLt; the engine's prefills (64 x 16 and 256 x 16 tokens: > 256
+    # rows) do, 3 projections x 2 layers per prefill batch
+    d = ops.BLAS_PLANNED["n"] - p1
+    assert (d >= 2 * 6 and d % 6 == 0) if prefill_blas else d == 0

@@ -27,6 +27,13 @@ for job in "$@"; do
     smoke)          timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)          timeout -k 10 900 python -u bench.py ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err
                     cat gpurun_out/bench.json ;;
+    bench-ab)       # interleaved A/B of one environment knob: AB_ENV=NAME AB_VALS="0 1" AB_REPS=2
+                    for i in $(seq ${AB_REPS:-2}); do for v in ${AB_VALS:-0 1}; do
+                      env ${AB_ENV}=$v timeout -k 10 600 python -u bench.py ${BENCH_ARGS:-} \
+                        > gpurun_out/ab_${v}_$i.json 2> gpurun_out/ab_${v}_$i.err || exit 1
+                      echo "${AB_ENV}=$v rep $i $(grep -o '"value": [0-9.]*' gpurun_out/ab_${v}_$i.json)" \
+                           "$(grep -o '"p50_explanation_latency_ms": [0-9.]*' gpurun_out/ab_${v}_$i.json)"
+                    done; done ;;
     ingest)         hipcc --offload-arch=gfx950 -O3 -std=c++17 -o /tmp/ingest tools/microbench/ingest.hip
                     timeout -k 10 120 /tmp/ingest | tee gpurun_out/ingest.jsonl ;;
     decode-gemm)    timeout -k 10 300 python -u tools/bench_decode_gemm.py ${DG_ARGS:-} | tee gpurun_out/decode_gemm.jsonl ;;
