@@ -524,7 +524,9 @@ def decode_splits(max_context: int, batch: int = 1, kv_heads: int = 8) -> int:
     want = -(-DECODE_TARGET_BLOCKS // max(1, batch * kv_heads))
     cap = -(-max(1, int(max_context)) // DECODE_MIN_SPLIT_TOKENS)
     ns = max(1, min(want, cap, 256))
-    return 1 << (ns - 1).bit_length()
+    # the power of two at or BELOW: splits of 256-512 tokens, not 128-256 (B = 64, one kv-head,
+    # ctx 1100: 4 splits 15.2 us vs 8 splits 19.9 us with the combine, profiles/attn_decode_tp8_splits_r5.jsonl)
+    return 1 << (ns.bit_length() - 1)
 
 
 def decode_workspace(B: int, Hq: int, num_splits: int, device, D: int = 128):
