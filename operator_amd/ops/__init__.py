@@ -25,7 +25,9 @@ __all__ = [
 # never split a sequence into pieces shorter than this / split only while B x Hkv
 # decode-attention workgroups < this (env overrides for tuning runs)
 DECODE_MIN_SPLIT_TOKENS = int(os.environ.get("OAMD_DECODE_MIN_SPLIT", "256"))
-DECODE_TARGET_BLOCKS = int(os.environ.get("OAMD_DECODE_TARGET_BLOCKS", "512"))
+# one workgroup per CU: the best split count at every measured (B, group, ctx) of
+# profiles/attn_decode_splits_sweep_r5.jsonl lands at B x Hkv x splits ~ 256
+DECODE_TARGET_BLOCKS = int(os.environ.get("OAMD_DECODE_TARGET_BLOCKS", "256"))
 
 
 class SplitK:
