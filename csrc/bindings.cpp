@@ -402,7 +402,10 @@ void attn_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tenso
                  const at::Tensor& block_tables, const at::Tensor& seq_lens, at::Tensor& out,
                  at::Tensor& o_part, at::Tensor& ml_part, int64_t num_splits, double scale, int64_t variant,
                  double k_scale, double v_scale, const c10::optional<at::Tensor>& q8,
-                 const c10::optional<at::Tensor>& sx) {
+                 const c10::optional<at::Tensor>& sx, const c10::optional<at::Tensor>& rope_x, int64_t rope_splits,
+                 const c10::optional<at::Tensor>& pos, const c10::optional<at::Tensor>& cos_t,
+                 const c10::optional<at::Tensor>& sin_t, const c10::optional<at::Tensor>& slots,
+                 const c10::optional<at::Tensor>& bias) {
   CHECK_DEV(q); CHECK_BF16(q); CHECK_CONTIG(q); CHECK_BF16(out); CHECK_CONTIG(out);
   const bool fp8 = kv_is_fp8(k_cache);
   TORCH_CHECK(fp8 ? kv_is_fp8(v_cache) : (k_cache.scalar_type() == at::kBFloat16 &&
@@ -436,11 +439,50 @@ void attn_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tenso
     q8p = static_cast<uint8_t*>(q8->data_ptr());
     sxp = sx->data_ptr<float>();
   }
+  // rope_x: the decode step's RoPE + KV write folded in (q unused, a shape carrier): the QKV
+  // projection as `rope_splits` fp32 split-K slabs [S, B, (Hq+2Hkv)D] or bf16 rows [B, (Hq+2Hkv)D]
+  oamd::DecRope rp{};
+  const oamd::DecRope* rpp = nullptr;
+  if (rope_x.has_value()) {
+    TORCH_CHECK(pos.has_value() && cos_t.has_value() && sin_t.has_value() && slots.has_value(),
+                "fused RoPE needs pos, cos, sin and slots");
+    const int64_t ncol = (Hq + 2 * Hkv) * D;
+    CHECK_DEV(*rope_x); CHECK_CONTIG(*rope_x);
+    if (rope_x->scalar_type() == at::kFloat) {
+      TORCH_CHECK(rope_splits >= 1 && rope_x->numel() >= rope_splits * B * ncol, "fused RoPE: slabs too small");
+      rp.xp = rope_x->data_ptr<float>();
+      rp.S = (int)rope_splits;
+      rp.slab = B * ncol;
+    } else {
+      CHECK_BF16(*rope_x);
+      TORCH_CHECK(rope_x->dim() == 2 && rope_x->size(0) == B && rope_x->size(1) == ncol, "fused RoPE: qkv [B, ncol]");
+      rp.row = ptr<bf16_t>(*rope_x);
+      rp.row_stride = rope_x->stride(0);
+      rp.S = 1;
+    }
+    CHECK_DT(*pos, at::kLong); CHECK_CONTIG(*pos); CHECK_DT(*slots, at::kLong); CHECK_CONTIG(*slots);
+    TORCH_CHECK(pos->numel() == B && slots->numel() == B, "fused RoPE: pos / slots [B]");
+    CHECK_DT(*cos_t, at::kFloat); CHECK_DT(*sin_t, at::kFloat); CHECK_CONTIG(*cos_t); CHECK_CONTIG(*sin_t);
+    TORCH_CHECK(cos_t->dim() == 2 && cos_t->size(1) == D / 2 && sin_t->sizes() == cos_t->sizes(), "cos/sin [max_pos, 64]");
+    if (bias.has_value()) {
+      CHECK_BF16(*bias); CHECK_CONTIG(*bias);
+      TORCH_CHECK(bias->numel() == ncol, "fused RoPE: bias [(Hq+2Hkv)D]");
+      rp.bias = ptr<bf16_t>(*bias);
+    }
+    rp.pos = pos->data_ptr<int64_t>();
+    rp.slots = slots->data_ptr<int64_t>();
+    rp.cos_t = cos_t->data_ptr<float>();
+    rp.sin_t = sin_t->data_ptr<float>();
+    rp.max_pos = cos_t->size(0);
+    rp.k_inv = (float)(1.0 / k_scale);
+    rp.v_inv = (float)(1.0 / v_scale);
+    rpp = &rp;
+  }
   const c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
   RC(oamd::attn_decode(ptr<bf16_t>(q), k_cache.data_ptr(), v_cache.data_ptr(), fp8, (float)k_scale, (float)v_scale,
                        ptr<int>(block_tables), ptr<int>(seq_lens), ptr<bf16_t>(out), ptr<float>(o_part),
                        ptr<float>(ml_part), (int)B, (int)Hq, (int)Hkv, (int)D, (int)page, (int)block_tables.size(1),
-                       (int)num_splits, (float)scale, (int)variant, cur_stream(), q8p, sxp));
+                       (int)num_splits, (float)scale, (int)variant, cur_stream(), q8p, sxp, rpp));
 }
 
 // pk / pv / seq_pfx: a shared prompt prefix (kernels.h attn_prefill, variant 3): seq_pfx[s] prefix
@@ -530,7 +572,10 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("block_tables"), pybind11::arg("seq_lens"), pybind11::arg("out"), pybind11::arg("o_part"),
         pybind11::arg("ml_part"), pybind11::arg("num_splits"), pybind11::arg("scale"), pybind11::arg("variant") = 0,
         pybind11::arg("k_scale") = 1.0, pybind11::arg("v_scale") = 1.0, pybind11::arg("q8") = pybind11::none(),
-        pybind11::arg("sx") = pybind11::none());
+        pybind11::arg("sx") = pybind11::none(), pybind11::arg("rope_x") = pybind11::none(),
+        pybind11::arg("rope_splits") = 1, pybind11::arg("pos") = pybind11::none(), pybind11::arg("cos") = pybind11::none(),
+        pybind11::arg("sin") = pybind11::none(), pybind11::arg("slots") = pybind11::none(),
+        pybind11::arg("bias") = pybind11::none());
   m.def("decode_slots", &decode_slots);
   m.def("decode_advance", &decode_advance);
   m.def("quantize_fp8", &quantize_fp8);

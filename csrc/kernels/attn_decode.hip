@@ -114,19 +114,87 @@ __device__ __forceinline__ int split_len(int len, int num_splits, int chunk) {
   return (per + chunk - 1) / chunk * chunk;
 }
 
+// 4 bf16 values (packed) -> 4 cache elements (bf16: as is; fp8: e4m3(x * inv), saturated)
+template <typename KV>
+struct Put4;
+template <>
+struct Put4<bf16_t> {
+  static __device__ __forceinline__ void put(bf16_t* dst, uint2 v, float) { *reinterpret_cast<uint2*>(dst) = v; }
+};
+template <>
+struct Put4<uint8_t> {
+  static __device__ __forceinline__ void put(uint8_t* dst, uint2 v, float inv) {
+    auto f = [&](uint32_t w, bool hi) {
+      return fminf(fmaxf(__uint_as_float(hi ? (w & 0xffff0000u) : (w << 16)) * inv, -448.f), 448.f);
+    };
+    int o = 0;
+    o = __builtin_amdgcn_cvt_pk_fp8_f32(f(v.x, false), f(v.x, true), o, false);
+    o = __builtin_amdgcn_cvt_pk_fp8_f32(f(v.y, false), f(v.y, true), o, true);
+    *reinterpret_cast<int*>(dst) = o;
+  }
+};
+
+// Row b, columns col..col+3 of the QKV projection as rope_kv sees them: bf16(sum of the S
+// fp32 slabs in slab order (+ bias)), or the bf16 row (+ bias, then rounded). SC: slab
+// count known at compile time (1, 4, 8: every slab load issued before the first add) or
+// 9 (runtime S).
+template <int SC>
+__device__ __forceinline__ f32x4 qkv4(const DecRope& r, int b, int ncol, int col) {
+  f32x4 a;
+  if (r.xp != nullptr) {
+    const float* p = r.xp + (int64_t)b * ncol + col;
+    a = *reinterpret_cast<const f32x4*>(p);
+    if constexpr (SC > 1 && SC <= 8) {
+      f32x4 t[SC - 1];
+#pragma unroll
+      for (int k = 1; k < SC; ++k) t[k - 1] = *reinterpret_cast<const f32x4*>(p + k * r.slab);
+#pragma unroll
+      for (int k = 1; k < SC; ++k) a += t[k - 1];
+    } else if constexpr (SC == 9) {
+      for (int k = 1; k < r.S; ++k) a += *reinterpret_cast<const f32x4*>(p + k * r.slab);
+    }
+  } else {
+    const uint2 u = *reinterpret_cast<const uint2*>(r.row + (int64_t)b * r.row_stride + col);
+    a = f32x4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+              __uint_as_float(u.y & 0xffff0000u)};
+  }
+  if (r.bias != nullptr) {
+    const uint2 u = *reinterpret_cast<const uint2*>(r.bias + col);
+    a += f32x4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+               __uint_as_float(u.y & 0xffff0000u)};
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) a[j] = bf2f(f2bf(a[j]));
+  return a;
+}
+
+// rotate-half RoPE of 4 (x1, x2 = x1's dims + 64) pairs -> packed bf16 (rope_pair: rope_kv's numerics)
+__device__ __forceinline__ void rope4(const f32x4& x1, const f32x4& x2, const float* cr, const float* sr, uint2& o1,
+                                      uint2& o2) {
+  const f32x4 c = *reinterpret_cast<const f32x4*>(cr), sn = *reinterpret_cast<const f32x4*>(sr);
+  float r1[4], r2[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) rope_pair(x1[j], x2[j], c[j], sn[j], r1[j], r2[j]);
+  o1 = make_uint2(pack_bf2(r1[0], r1[1]), pack_bf2(r1[2], r1[3]));
+  o2 = make_uint2(pack_bf2(r2[0], r2[1]), pack_bf2(r2[2], r2[3]));
+}
+
 template <typename KV, int NT>
 struct KVRegs {
   typename KVT<KV>::frag k[NT][4];   // K tile i: token 16i + l15, dims 32*lg + 8*ks
   typename KVT<KV>::frag v[4 * NT];  // token 4*it + lg, dims 8*l15
 };
 
-template <int G, int NT, typename KV = bf16_t>
+// FR (fused RoPE, DecRope): 0 = q comes rotated from rope_kv; else q is rotated here from
+// the QKV projection (FR = its slab class for qkv4: 1, 4, 8, 9) and the workgroup whose
+// split ends the sequence writes the decode token's K / V into the cache first.
+template <int G, int NT, typename KV = bf16_t, int FR = 0>
 __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2)
     attn_decode_kernel(const bf16_t* __restrict__ q, const KV* __restrict__ kc, const KV* __restrict__ vc,
                        const int* __restrict__ block_tables, const int* __restrict__ seq_lens,
                        bf16_t* __restrict__ out, float* __restrict__ o_part, float* __restrict__ ml_part, int Hkv,
                        int page_size, int log2_page, int max_pages, int num_splits, float scale_log2,
-                       float v_scale, int head_minor) {
+                       float v_scale, int head_minor, DecRope rp) {
   using T = KVT<KV>;
   constexpr int D = 128;
   constexpr int TW = 16 * NT;  // tokens per wave per chunk
@@ -180,7 +248,7 @@ __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2)
   const int* btb = block_tables + (int64_t)b * max_pages + page0;
   const int pid0 = tid < npg ? btb[tid] : 0;   // issued before any K/V load (vmcnt is in order)
   u16x8 qv[4];
-  if (w == 0) {
+  if (FR == 0 && w == 0) {
     const int hq = kvh * G + (l15 < G ? l15 : 0);
     const bf16_t* qp = q + ((int64_t)b * Hq + hq) * D + 32 * lg;
 #pragma unroll
@@ -239,11 +307,74 @@ __global__ void __launch_bounds__(256, (NT == 1 && G <= 4) ? 3 : 2)
   for (int i = tid + 256; i < npg; i += 256) pg_lds[i] = btb[i];   // > 256 pages: rare
   // q as the MFMA B operand (column = head, zero past G), staged once in LDS and read per
   // k-step (16 VGPRs fewer per lane than q in registers)
-  if (w == 0) {
+  bool kv_new = false;
+  if constexpr (FR == 0) {
+    if (w == 0) {
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) q_lds[ks][lane] = l15 < G ? qv[ks] : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      for (int ks = 0; ks < 4; ++ks) q_lds[ks][lane] = l15 < G ? qv[ks] : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  } else {
+    // rope_kv's decode work, while the first two chunks are in flight. q: thread (head h,
+    // quad) rotates dims 4 quad.. and 4 quad + 64.. of head kvh*G + h into its q_lds slots
+    // (dim d of head h: q_lds[(d % 32) / 8][16 (d / 32) + h], element d % 8)
+    const int ncol = (Hq + 2 * Hkv) * D;
+    int64_t p = rp.pos[b];
+    p = p < 0 ? 0 : (p >= rp.max_pos ? rp.max_pos - 1 : p);
+    const float* cr = rp.cos_t + p * (D / 2);
+    const float* sr = rp.sin_t + p * (D / 2);
+    uint16_t* ql = reinterpret_cast<uint16_t*>(&q_lds[0][0]);
+    auto qidx = [&](int d, int h) { return ((((d & 31) >> 3) * 64 + (d >> 5) * 16 + h) << 3) + (d & 7); };
+    if ((lane & 15) >= G) q_lds[w][lane] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};   // 4 waves x 64 = every slot
+    if (tid < G * 16) {
+      const int h = tid >> 4, d0 = (tid & 15) * 4;
+      const int col = (kvh * G + h) * D + d0;
+      const f32x4 x1 = qkv4<FR>(rp, b, ncol, col), x2 = qkv4<FR>(rp, b, ncol, col + D / 2);
+      uint2 o1, o2;
+      rope4(x1, x2, cr + d0, sr + d0, o1, o2);
+      *reinterpret_cast<uint2*>(ql + qidx(d0, h)) = o1;
+      *reinterpret_cast<uint2*>(ql + qidx(d0 + D / 2, h)) = o2;
+    }
+    // the decode token (position len - 1) belongs to the split that ends the sequence: its
+    // workgroup writes the token's rotated K and its V for head kvh (wave 2: lanes 0-15 K
+    // pairs, 16-47 V quads) and drains the stores before the barrier below
+    const int64_t slot = rp.slots[b];
+    kv_new = end == len && slot >= 0;
+    if (kv_new && w == 2 && lane < 48) {
+      const int64_t page = slot >> log2_page, off = slot & (page_size - 1);
+      KV* kdst = const_cast<KV*>(kc) + (page * Hkv * page_size + (off & ~15)) * D + (int64_t)kvh * page_size * D;
+      KV* vdst = const_cast<KV*>(vc) + (page * Hkv * page_size + off) * D + (int64_t)kvh * page_size * D;
+      const int t16 = static_cast<int>(off & 15);
+      // tiled K (rope_kv): [ks][lg][token][8 dims], d = 32 lg + 8 ks + j
+      auto kofs = [&](int d) { return ((((d & 31) >> 3) * 4 + (d >> 5)) * 16 + t16) * 8 + (d & 7); };
+      if (lane < 16) {
+        const int d0 = lane * 4, col = (Hq + kvh) * D + d0;
+        const f32x4 x1 = qkv4<FR>(rp, b, ncol, col), x2 = qkv4<FR>(rp, b, ncol, col + D / 2);
+        uint2 o1, o2;
+        rope4(x1, x2, cr + d0, sr + d0, o1, o2);
+        Put4<KV>::put(kdst + kofs(d0), o1, rp.k_inv);
+        Put4<KV>::put(kdst + kofs(d0 + D / 2), o2, rp.k_inv);
+      } else {
+        const int d0 = (lane - 16) * 4, col = (Hq + Hkv + kvh) * D + d0;
+        const f32x4 v = qkv4<FR>(rp, b, ncol, col);
+        Put4<KV>::put(vdst + d0, make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])), rp.v_inv);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
   }
   __syncthreads();
+  if constexpr (FR != 0) {
+    // the token's chunk (or a chunk of clamped copies of it) already requested above read the
+    // slot before it was written: request it again, now that the stores have landed
+    if (kv_new && nch <= 2) {
+      if (nch == 1) {
+        load_k(ra, 0, tile_lds);
+        load_v(ra, 0, tile_lds);
+      } else {
+        load_k(rb, 1, tile_lds);
+        load_v(rb, 1, tile_lds);
+      }
+    }
+  }
 
   // Online softmax per (head, token group): lane (l15, lg) of the S = K Q^T tile holds head
   // l15 of tokens 4lg..4lg+3 of every 16-token tile, and the P.V lanes (dims 8 l15.., lg)
@@ -530,12 +661,16 @@ __global__ void __launch_bounds__(1024) attn_decode_combine_q8_kernel(
 int attn_decode(const bf16_t* q, const void* k_cache, const void* v_cache, bool fp8, float k_scale, float v_scale,
                 const int* block_tables, const int* seq_lens, bf16_t* out, float* o_part, float* ml_part, int B,
                 int Hq, int Hkv, int head_dim, int page_size, int max_pages, int num_splits, float scale, int variant,
-                hipStream_t stream, uint8_t* q8, float* sx) {
+                hipStream_t stream, uint8_t* q8, float* sx, const DecRope* rope) {
   if (B == 0) return 0;
   if (head_dim != 128) return -1;
   if (page_size < 16 || (page_size & (page_size - 1)) != 0) return -2;
   if (max_pages > kMaxPagesLds) return -4;
   if (num_splits < 1) return -5;
+  if (rope != nullptr && (rope->pos == nullptr || rope->slots == nullptr || rope->cos_t == nullptr ||
+                          rope->sin_t == nullptr || rope->max_pos < 1 ||
+                          (rope->xp == nullptr ? rope->row == nullptr : rope->S < 1)))
+    return -8;
   // validate every launch of this call before the first one: nothing is enqueued on a bad shape
   if (q8 != nullptr && Hq * 128 > 8192) return -6;
   int log2p = 0;
@@ -548,12 +683,30 @@ int attn_decode(const bf16_t* q, const void* k_cache, const void* v_cache, bool 
   // Bit 2: the old dispatch order (below).
   int chunk = 0;
   dim3 grid(B * num_splits, Hkv, 1);
+  DecRope rp{};
+  int fr = 0;
+  if (rope != nullptr) {
+    rp = *rope;
+    fr = rp.xp == nullptr ? 1 : (rp.S == 1 || rp.S == 4 || rp.S == 8) ? rp.S : 9;
+  }
+#define OAMD_DEC_K(GG, NTT, KVT_, FRR)                                                                    \
+  attn_decode_kernel<GG, NTT, KVT_, FRR><<<grid, 256, 0, stream>>>(                                       \
+      q, static_cast<const KVT_*>(k_cache), static_cast<const KVT_*>(v_cache), block_tables, seq_lens,   \
+      out, o_part, ml_part, Hkv, page_size, log2p, max_pages, num_splits, scale_log2, v_scale, hm, rp)
 #define OAMD_DEC(GG, NTT, KVT_)                                                                           \
   do {                                                                                                    \
-    attn_decode_kernel<GG, NTT, KVT_><<<grid, 256, 0, stream>>>(                                         \
-        q, static_cast<const KVT_*>(k_cache), static_cast<const KVT_*>(v_cache), block_tables, seq_lens, \
-        out, o_part, ml_part, Hkv, page_size, log2p, max_pages, num_splits, scale_log2, v_scale, hm);      \
-    chunk = 64 * NTT;                                                                                     \
+    if (fr == 0) {                                                                                        \
+      OAMD_DEC_K(GG, NTT, KVT_, 0);                                                                       \
+      chunk = 64 * NTT;                                                                                   \
+    } else {   /* fused RoPE: the NT = 1 schedule */                                                     \
+      switch (fr) {                                                                                       \
+        case 1: OAMD_DEC_K(GG, 1, KVT_, 1); break;                                                        \
+        case 4: OAMD_DEC_K(GG, 1, KVT_, 4); break;                                                        \
+        case 8: OAMD_DEC_K(GG, 1, KVT_, 8); break;                                                        \
+        default: OAMD_DEC_K(GG, 1, KVT_, 9); break;                                                       \
+      }                                                                                                   \
+      chunk = 64;                                                                                         \
+    }                                                                                                     \
   } while (0)
   const bool nt2 = (variant & 3) == 2;
   // kv-heads of one sequence dispatched back to back (default; tools/bench_attn.py at B = 256:
@@ -586,6 +739,7 @@ int attn_decode(const bf16_t* q, const void* k_cache, const void* v_cache, bool 
     }
   }
 #undef OAMD_DEC
+#undef OAMD_DEC_K
   OAMD_LAUNCH_CHECK();
   if (q8 != nullptr) {   // combine (if split) + per-token e4m3fn rows for the fp8 o-projection
     const int n = Hq * 128;

@@ -36,6 +36,13 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
 }
 
 // Pack two floats into two bf16 (lo in the low half).
+// rotate-half RoPE of one (x[d], x[d + D/2]) pair with explicit FMAs: one numerics for
+// rope_kv and the RoPE folded into decode attention (no compiler-chosen contraction)
+__device__ __forceinline__ void rope_pair(float a, float b, float c, float s, float& o1, float& o2) {
+  o1 = __builtin_fmaf(a, c, -(b * s));
+  o2 = __builtin_fmaf(b, c, a * s);
+}
+
 __device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
   return static_cast<uint32_t>(f2bf(lo)) | (static_cast<uint32_t>(f2bf(hi)) << 16);
 }

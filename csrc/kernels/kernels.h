@@ -71,11 +71,32 @@ int score_events(const int64_t* keys, const int* hit_doc, const int* doc_ptr, in
                  const double* conf, const int* severity, int num_matchers, double significance, double* ev_score,
                  int* ev_pat, int* ev_line, int* order, int* summary, hipStream_t stream);
 
+// The decode step's RoPE + KV-cache write folded into decode attention (rope_kv's decode
+// work): q is rotated from the QKV projection inside every workgroup, and the workgroup
+// holding a sequence's last token writes that token's rotated K and its V into the cache.
+// Row b of the projection is bf16(sum of S fp32 split-K slabs [S][rows][ncol] (+ bias)) or
+// a bf16 row (+ bias), ncol = (Hq + 2 Hkv) * 128 -- the numerics of rope_kv.
+struct DecRope {
+  const float* xp;          // split-K slabs, or nullptr
+  const bf16_t* row;        // bf16 rows [rows][row_stride] when xp == nullptr
+  int64_t row_stride;
+  int S;                    // slab count (xp)
+  int64_t slab;             // elements per slab = rows * ncol
+  const bf16_t* bias;       // [(Hq + 2 Hkv) * 128] or nullptr
+  const int64_t* pos;       // [rows] positions of the decode tokens
+  const float* cos_t;       // [max_pos][64]
+  const float* sin_t;
+  int64_t max_pos;
+  const int64_t* slots;     // [rows] cache slot of the decode token (< 0: none)
+  float k_inv, v_inv;       // fp8 cache: 1 / k_scale, 1 / v_scale
+};
+
 // k_cache / v_cache: bf16, or (fp8) OCP e4m3fn bytes holding x / k_scale, x / v_scale
+// rope != nullptr: q is unused; see DecRope
 int attn_decode(const bf16_t* q, const void* k_cache, const void* v_cache, bool fp8, float k_scale, float v_scale,
                 const int* block_tables, const int* seq_lens, bf16_t* out, float* o_part, float* ml_part, int B,
                 int Hq, int Hkv, int head_dim, int page_size, int max_pages, int num_splits, float scale, int variant,
-                hipStream_t stream, uint8_t* q8 = nullptr, float* sx = nullptr);
+                hipStream_t stream, uint8_t* q8 = nullptr, float* sx = nullptr, const DecRope* rope = nullptr);
 // (q8, sx non-null: the output rows are also emitted as per-token e4m3fn [B, Hq*128] + fp32 scales,
 // == quantize_fp8_rows(out); `out` then holds valid bf16 only for rows of a single split.)
 // Causal prefill attention; the work list holds one item per attn_prefill_block_q(Hq, Hkv, variant)

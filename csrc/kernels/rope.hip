@@ -147,9 +147,10 @@ __global__ void __launch_bounds__(kRopeItems) rope_kv_kernel(
       for (int j = 0; j < 8; ++j) {
         const float c = j < 4 ? c0[j & 3] : c1[j & 3];
         const float s = j < 4 ? s0[j & 3] : s1[j & 3];
-        const float a = bf2f(x1[j]), b = bf2f(x2[j]);
-        o1[j] = f2bf(a * c - b * s);
-        o2[j] = f2bf(b * c + a * s);
+        float r1, r2;
+        rope_pair(bf2f(x1[j]), bf2f(x2[j]), c, s, r1, r2);
+        o1[j] = f2bf(r1);
+        o2[j] = f2bf(r2);
       }
       if (h < Hq) {
         bf16_t* dst = q_out + ((int64_t)t * Hq + h) * D;

@@ -268,10 +268,10 @@ class LlamaModel:
                     pre = (fb.prefix[0][i], fb.prefix[1][i], fb.prefix[2], fb.prefix[3])
                 o = ops.attn_prefill(q, k, v, fb.seq_lens, self.scale, work=fb.prefill_work, prefix=pre)
             else:
-                q, _, _ = ops.rope_kv(qkv, fb.positions, self.cos, self.sin, self.hq, self.hkv, kc, vc, fb.slots,
-                                      want_kv=False, bias=bias, k_scale=kv.k_scale, v_scale=kv.v_scale)
-                o = ops.attn_decode(q, kc, vc, fb.block_tables, fb.context_lens, self.scale, fb.num_splits,
-                                    workspace=ws, k_scale=kv.k_scale, v_scale=kv.v_scale, quant=q8)
+                # RoPE + the decode token's KV write run inside the attention kernel
+                o = ops.attn_decode_rope(qkv, fb.positions, self.cos, self.sin, self.hq, kc, vc, fb.slots,
+                                         fb.block_tables, fb.context_lens, self.scale, fb.num_splits, workspace=ws,
+                                         bias=bias, k_scale=kv.k_scale, v_scale=kv.v_scale, quant=q8)
             a = self._lin(o if isinstance(o, tuple) else o.view(T, self.hq * c.head_dim), lw.wo, lw.so, defer=True)
             x = self.tp.all_reduce_rmsnorm(a, lw.mlp_norm, c.rms_eps, residual=h, quant=q8)   # fused under TP
             if lw.sgu is None:

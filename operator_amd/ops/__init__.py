@@ -16,7 +16,7 @@ from . import reference
 from ._native import kernels, native_available, patterns
 
 __all__ = [
-    "rmsnorm", "silu_mul", "embedding", "rope_kv", "attn_prefill", "attn_decode", "sample",
+    "rmsnorm", "silu_mul", "embedding", "rope_kv", "attn_prefill", "attn_decode", "attn_decode_rope", "sample",
     "kernels", "patterns", "native_available", "reference", "prefill_work_list", "prefill_block_q", "prefill_variant", "decode_splits",
     "decode_workspace", "linear", "gemm_splits", "gemm_plan", "gate_up_silu", "interleave_gate_up",
     "quantize_fp8", "silu_quantize_fp8", "linear_fp8", "fp8_plan", "SplitK", "linear_tile", "tile_ok", "BLAS_CALLS",
@@ -563,6 +563,47 @@ def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, b
         sx = torch.empty(B, dtype=torch.float32, device=q.device)
     kernels().attn_decode(q, k_cache, v_cache, block_tables, seq_lens, o, workspace[0], workspace[1],
                           num_splits, scale, variant, k_scale, v_scale, q8, sx)
+    return (q8, sx) if quant else o
+
+
+# decode RoPE + KV-cache write folded into decode attention (OAMD_FUSED_ROPE=0: rope_kv, then attn_decode),
+# for batches of at most FUSED_ROPE_MAX_SEQ_HEADS (sequence, kv-head) pairs: there attention is
+# latency-bound and the fold removes a launch (TP=8 70B fp8 B=64: 6.85 -> 6.64 ms/step); at the
+# 8B flagship's 256 x 8 pairs attention streams HBM and every workgroup would pay the fold's
+# slab reads and store drain up front (-1.3 % analyses/s, profiles/fused_decode_rope_ab_r5.jsonl)
+FUSED_DECODE_ROPE = os.environ.get("OAMD_FUSED_ROPE", "1") != "0"
+FUSED_ROPE_MAX_SEQ_HEADS = int(os.environ.get("OAMD_FUSED_ROPE_MAX", "256"))
+
+
+def attn_decode_rope(qkv, pos: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, Hq: int, k_cache: torch.Tensor,
+                     v_cache: torch.Tensor, slots: torch.Tensor, block_tables: torch.Tensor, seq_lens: torch.Tensor,
+                     scale: float, num_splits: int, workspace: tuple[torch.Tensor, torch.Tensor] | None = None,
+                     bias: torch.Tensor | None = None, k_scale: float = 1.0, v_scale: float = 1.0,
+                     quant: bool = False, variant: int = 0):
+    """One decode step's ``rope_kv`` (want_kv=False) + ``attn_decode`` as ONE kernel: every
+    attention workgroup rotates its q from the QKV projection (``qkv``: bf16 rows or the
+    GEMM's :class:`SplitK` slabs, + the Qwen2 bias), and the workgroup holding each
+    sequence's last token writes that token's rotated K and its V into the cache before
+    reading it (csrc/kernels/attn_decode.hip, ``DecRope``). Same numerics as the two
+    kernels; one launch and the q round trip fewer per layer."""
+    Hkv = k_cache.shape[1]
+    if not (qkv.is_cuda and FUSED_DECODE_ROPE and qkv.shape[0] * Hkv <= FUSED_ROPE_MAX_SEQ_HEADS):
+        q, _, _ = rope_kv(qkv, pos, cos, sin, Hq, Hkv, k_cache, v_cache, slots, want_kv=False, bias=bias,
+                          k_scale=k_scale, v_scale=v_scale)
+        return attn_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, num_splits, workspace=workspace,
+                           variant=variant, k_scale=k_scale, v_scale=v_scale, quant=quant)
+    B = qkv.shape[0]
+    D = cos.shape[1] * 2
+    o = torch.empty(B, Hq, D, dtype=torch.bfloat16, device=qkv.device)
+    if workspace is None:
+        workspace = decode_workspace(B, Hq, num_splits, qkv.device)
+    q8 = sx = None
+    if quant:
+        q8 = torch.empty(B, Hq * D, dtype=torch.float8_e4m3fn, device=qkv.device)
+        sx = torch.empty(B, dtype=torch.float32, device=qkv.device)
+    rx, S = (qkv.p, qkv.S) if isinstance(qkv, SplitK) else (qkv, 1)
+    kernels().attn_decode(o, k_cache, v_cache, block_tables, seq_lens, o, workspace[0], workspace[1], num_splits,
+                          scale, variant, k_scale, v_scale, q8, sx, rx, S, pos, cos, sin, slots, bias)
     return (q8, sx) if quant else o
 
 

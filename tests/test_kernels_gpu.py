@@ -509,3 +509,70 @@ def test_decode_step_bookkeeping_kernels_match_torch():
         want_hist[:, step0 % ms] = tok
         assert torch.equal(ids, tok) and torch.equal(hist, want_hist)
         assert torch.equal(p2, pos + act.long()) and torch.equal(c2, ctx + act.int()) and st.item() == step0 + 1
+
+
+@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (28, 4)])
+@pytest.mark.parametrize("splits_qkv", [1, 2, 4, 8])
+@pytest.mark.parametrize("fp8", [False, True])
+def test_attn_decode_rope_equals_rope_kv_then_attn(Hq, Hkv, splits_qkv, fp8):
+    """The decode RoPE + KV write folded into decode attention (ops.attn_decode_rope) is
+    bit-identical to rope_kv then attn_decode: the same cache bytes for the new token and
+    the same output rows (and e4m3fn rows with quant), for every split schedule. The new
+    token's slot holds NaN before the call, so a workgroup reading it before its own write
+    (the chunk requested in the prologue, or a clamped copy of the token) poisons the row.
+    Contexts 1 / 17 / 64 / 65 / 130 / 700 cover the one- and two-chunk reload paths; qkv
+    as bf16 rows (1), runtime (2) and compiled (4, 8) slab counts; a Qwen2-style bias."""
+    torch.manual_seed(21)
+    lens, P, D = [1, 17, 64, 65, 130, 700, 0], 16, 128
+    B = len(lens)
+    maxp = (max(lens) + P - 1) // P + 1
+    pages = B * maxp + 3
+    ncol = (Hq + 2 * Hkv) * D
+    k_scale, v_scale = (0.5, 2.0) if fp8 else (1.0, 1.0)
+    kf, vf = torch.randn(pages, Hkv, P, D, device=DEV), torch.randn(pages, Hkv, P, D, device=DEV)
+    if fp8:
+        kc0, vc0 = ref.kv_store(kf, torch.float8_e4m3fn, k_scale), ref.kv_store(vf, torch.float8_e4m3fn, v_scale)
+    else:
+        kc0, vc0 = kf.to(torch.bfloat16), vf.to(torch.bfloat16)
+    bt = torch.randperm(pages, device=DEV)[: B * maxp].reshape(B, maxp).int()
+    sl = torch.tensor(lens, dtype=torch.int32, device=DEV)
+    pos = torch.tensor([max(n - 1, 0) for n in lens], dtype=torch.long, device=DEV)
+    slots = torch.tensor([int(bt[b, (n - 1) // P]) * P + (n - 1) % P if n > 0 else -1 for b, n in enumerate(lens)],
+                         dtype=torch.long, device=DEV)
+    # the new tokens' slots start as NaN (whatever a freed page held)
+    for b, n in enumerate(lens):
+        if n > 0:
+            pg, off = int(bt[b, (n - 1) // P]), (n - 1) % P
+            kc0.view(torch.uint8)[pg, :, off] = 0x7F if fp8 else 0
+            vc0.view(torch.uint8)[pg, :, off] = 0x7F if fp8 else 0
+            if not fp8:
+                kc0[pg, :, off] = float("nan")
+                vc0[pg, :, off] = float("nan")
+    theta = 500000.0
+    inv = 1.0 / theta ** (torch.arange(0, D, 2, device=DEV).float() / D)
+    ang = torch.arange(4096, device=DEV).float()[:, None] * inv[None]
+    cos, sin = ang.cos().contiguous(), ang.sin().contiguous()
+    bias = (torch.randn(ncol, device=DEV) * 0.1).to(torch.bfloat16) if Hq == 28 else None
+    if splits_qkv == 1:
+        qkv = (torch.randn(B, ncol, device=DEV)).to(torch.bfloat16)
+    else:
+        qkv = ops.SplitK(torch.randn(splits_qkv * B * ncol, device=DEV) * 0.5, splits_qkv, B, ncol)
+    scale = 1 / math.sqrt(D)
+    for ns in (1, 2, 4):
+        for quant in ((False, True) if Hq * D <= 8192 else (False,)):
+            kc_a, vc_a, kc_b, vc_b = kc0.clone(), vc0.clone(), kc0.clone(), vc0.clone()
+            q, _, _ = ops.rope_kv(qkv, pos, cos, sin, Hq, Hkv, kc_a, vc_a, slots, want_kv=False, bias=bias,
+                                  k_scale=k_scale, v_scale=v_scale)
+            want = ops.attn_decode(q, kc_a, vc_a, bt, sl, scale, ns, k_scale=k_scale, v_scale=v_scale, quant=quant)
+            got = ops.attn_decode_rope(qkv, pos, cos, sin, Hq, kc_b, vc_b, slots, bt, sl, scale, ns, bias=bias,
+                                       k_scale=k_scale, v_scale=v_scale, quant=quant)
+            torch.cuda.synchronize()
+            assert torch.equal(kc_a.view(torch.uint8), kc_b.view(torch.uint8))
+            assert torch.equal(vc_a.view(torch.uint8), vc_b.view(torch.uint8))
+            if quant:
+                assert torch.equal(got[0].view(torch.uint8), want[0].view(torch.uint8))
+                assert torch.equal(got[1], want[1])
+            else:
+                live = sl.cpu() > 0
+                assert torch.isfinite(got.float()[live.to(DEV)]).all()
+                assert torch.equal(got.view(torch.int16)[live.to(DEV)], want.view(torch.int16)[live.to(DEV)])
