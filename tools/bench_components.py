@@ -29,7 +29,7 @@ def bench_llm(model_name, batches, ctx, prompt_len, max_context):
         t0 = time.perf_counter()
         for r in reqs:
             eng.submit(r)
-        while eng.waiting:
+        while eng.waiting or eng._pf is not None:   # admitted + the pipelined prefill finished
             eng.step()
         torch.cuda.synchronize()
         t1 = time.perf_counter()
