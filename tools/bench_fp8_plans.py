@@ -25,13 +25,14 @@ def main():
     ap.add_argument("--m", type=int, default=64)
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--shapes", default=",".join(SHAPES))
+    ap.add_argument("--hot", action="store_true", help="one weight copy (L2/MALL-resident): isolates the cold-HBM cost")
     a = ap.parse_args()
     torch.manual_seed(0)
     dev = "cuda"
     M = a.m
     for name in a.shapes.split(","):
         N, K = SHAPES[name]
-        copies = max(2, (640 << 20) // (N * K))
+        copies = 1 if a.hot else max(2, (640 << 20) // (N * K))
         ws = [ops.quantize_fp8(torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.02) for _ in range(copies)]
         x = ops.quantize_fp8(torch.randn(M, K, device=dev, dtype=torch.bfloat16))
         ref = (x[0].float() * x[1][:, None]) @ (ws[0][0].float() * ws[0][1][:, None]).t()
