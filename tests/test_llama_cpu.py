@@ -364,3 +364,16 @@ def test_decode_window_columns_wrap():
     assert reqs[0].output == [6, 7, 0, 1] and reqs[1].output == [14, 15, 8, 9]
     eng._consume(_Window(None, reqs, 2, 2, host, None, 2))
     assert reqs[0].output[-2:] == [2, 3]
+
+
+def test_decode_buckets_skip_the_skinny_row_counts():
+    """9-64 decode rows share the 64-row bucket (llm.SKIP_BUCKETS: the 16 / 32-row buckets
+    would put the bf16 GEMMs on gemm_skinny); an engine whose max_batch is one of them
+    keeps it as its largest bucket."""
+    from operator_amd.engine.llm import _buckets
+
+    assert _buckets(256) == [1, 2, 4, 8, 64, 128, 256]
+    assert _buckets(64) == [1, 2, 4, 8, 64]
+    assert _buckets(32) == [1, 2, 4, 8, 32]
+    assert _buckets(16) == [1, 2, 4, 8, 16]
+    assert _buckets(48) == [1, 2, 4, 8, 48]

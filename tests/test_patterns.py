@@ -187,3 +187,24 @@ def test_log_factory_injects_signatures_of_the_scanned_library_for_any_seed():
                                                                                   seed=seed + 7)
         for r, t in zip(eng.analyze(docs), truth):
             assert set(t) <= {e.matched_pattern.id for e in r.events}, (seed, t)
+
+
+def test_pipelined_analyze_sub_batches_cover_the_batch_in_order():
+    """MatchEngine._sub_batches (the GPU analyze pipeline's split): doc-aligned, contiguous,
+    non-empty, about PIPE_SUB_BYTES each, None below PIPE_MIN_BYTES or with the pipeline
+    off (the split logic itself touches no GPU: the device is only compared)."""
+    import torch
+
+    eng = MatchEngine(catalog_library(), device="cpu")
+    assert eng._sub_batches([b"x" * 10] * 4) is None            # CPU engine: never split
+    eng.device = torch.device("cuda")
+    eng.PIPE_MIN_BYTES, eng.PIPE_SUB_BYTES = 1000, 300
+    docs = [b"a" * n for n in (100, 250, 40, 0, 600, 10, 10, 200, 90)]
+    subs = eng._sub_batches(docs)
+    assert subs[0][0] == 0 and subs[-1][1] == len(docs)
+    assert all(lo < hi for lo, hi in subs) and all(a[1] == b[0] for a, b in zip(subs, subs[1:]))
+    total = sum(map(len, docs))
+    assert len(subs) <= -(-total // eng.PIPE_SUB_BYTES)
+    assert eng._sub_batches(docs[:2]) is None                  # below PIPE_MIN_BYTES
+    eng.PIPE_SUB_BYTES = 0
+    assert eng._sub_batches(docs) is None                      # pipeline off
