@@ -85,6 +85,9 @@ def parse_args():
                          "operator shard talks to over HTTP, each rank owning the pods that hash to it "
                          "(`run --shard-per-gpu`); inproc: an in-memory FakeKube inside the rank process; "
                          "auto: rest when --gpus > 1")
+    ap.add_argument("--handoff", choices=["generated", "explained"], default="generated",
+                    help="pipelined waves: wave w+1 fails when wave w's explanations are generated (the "
+                         "engine's finish hook) or once every pipeline thread has its explanation back")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--cpu", action="store_true",
                     help="CPU rehearsal (gloo, tiny models): allows --gpus N > 1 on a host without N GPUs")
@@ -369,6 +372,30 @@ def main() -> int:
                 explained["n"] += 1
                 exp_cv.notify_all()
 
+        # The hand-off between pipelined waves is the moment a wave's explanations are
+        # GENERATED: with the engine in this process, its finish hook (the batch's texts
+        # detokenized) counts them, instead of each of the 256 pipeline threads after it
+        # has woken up and built its response (~50 ms later at the end of a wave, under
+        # the GIL). Pool engines: counted by the explainer wrapper as before.
+        generated = {"n": 0, "on": False}
+        if llm is not None and a.handoff == "generated":
+            inner_hook = llm.finish_hook
+
+            def finish_hook(reqs) -> None:
+                if inner_hook is not None:
+                    inner_hook(reqs)
+                with exp_cv:
+                    generated["n"] += len(reqs)
+                    if generated["n"] >= generated.get("want", 0):
+                        exp_cv.notify_all()
+
+            llm.finish_hook = finish_hook
+            generated["on"] = True
+        non_ai = {"n": 0}   # failures that never reached the explainer (count toward a hand-off too)
+
+        def handed() -> int:
+            return (generated["n"] + non_ai["n"]) if generated["on"] else explained["n"]
+
         class CountingExplainer:
             """Counts generated explanations: the hand-off point between pipelined waves."""
 
@@ -399,6 +426,8 @@ def main() -> int:
         def on_done(monitor, pod, outcome):
             name = pod["metadata"]["name"]
             if outcome not in ("ai-complete", "ai-failed"):   # never reached the explainer
+                with exp_cv:
+                    non_ai["n"] += 1
                 count_explained()
             with lock:
                 lat.append(time.perf_counter() - t_inject.get(name, time.perf_counter()))
@@ -468,12 +497,13 @@ def main() -> int:
             with lock:
                 counter["n"], counter["target"] = 0, a.batch * len(ws)
                 done_ev.clear()
-            base = explained["n"]
+            base = handed()
             for j, w in enumerate(ws):
                 inject(w)
                 if j + 1 < len(ws):
                     with exp_cv:
-                        exp_cv.wait_for(lambda: explained["n"] >= base + (j + 1) * a.batch)
+                        generated["want"] = base + (j + 1) * a.batch
+                        exp_cv.wait_for(lambda: handed() >= base + (j + 1) * a.batch)
                     mark(f"handoff[{w}]")
             done_ev.wait()
             op.drain(600)
@@ -628,7 +658,8 @@ def main() -> int:
                    "kv_page_tokens": a.page_size, "shared_prompt_prefix": not a.no_prefix_sharing,
                    "apiserver": ("one REST API server process, rank r = operator shard r (run --shard-per-gpu)"
                                  if rest else "in-process FakeKube per rank"),
-                   "waves": "serial" if (a.serial_waves or a.mode != "pipeline") else "pipelined"},
+                   "waves": "serial" if (a.serial_waves or a.mode != "pipeline") else "pipelined",
+                   "wave_handoff": a.handoff},
         "detail": {"init_s": round(init_s, 1), "prefill_tokens_per_gpu": ptoks, "decode_tokens_per_gpu": dtoks,
                    # workload check: every failure carries three signatures of the scanned library, so
                    # this stays ~885 whatever the rank / shard layout (README "Correction"); it counts
