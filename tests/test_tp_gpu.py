@@ -1,0 +1,122 @@
+"""Tensor parallelism on the GPU kernels: TP = 2 as two ranks on the one MI355X of the
+box (cuda:0), the decode all-reduces through the IPC kernels between them (the fused
+all-reduce + residual + RMSNorm, and with fp8 weights its e4m3fn epilogue), gloo only
+for the handle exchange (RCCL refuses two ranks on one device). The sharded model's
+prefill logits and one paged decode step (the decode RoPE folded into attention, the
+per-rank kv-head shard) track the TP = 1 model run on the same kernels. The CPU tier
+pins TP = 4 / 8 to TP = 1 exactly in fp32 (tests/test_tp_scale.py); here bf16 / fp8 and
+a different reduction order allow a relative difference (SURVEY.md §4.2 "Distributed")."""
+import os
+import socket
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+LENS = [200, 90, 33]   # 323 prefill rows: the planned hipBLASLt projections too
+P, PER = 16, 16
+
+
+def _cfg():
+    from operator_amd.models.config import LlamaConfig
+
+    return LlamaConfig(name="tp-gpu", vocab_size=4096, hidden=2048, intermediate=4096, layers=2, heads=16,
+                       kv_heads=8, max_position=4096, bos_id=4000, eos_ids=(4001,))
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(m, hkv: int):
+    """Prefill LENS, then one decode step: (last-token prefill logits, decode logits), the
+    rank's vocab shard, on the CPU."""
+    from operator_amd.models.kv_cache import PagedKVCache
+    from operator_amd.models.llama import ForwardBatch
+
+    B, dev = len(LENS), "cuda"
+    kv = PagedKVCache(m.cfg.layers, B * PER, hkv, 128, P, device=dev)
+    bt = torch.arange(B * PER, dtype=torch.int32).reshape(B, PER)
+    ids = [torch.randint(0, m.cfg.vocab_size, (L,), generator=torch.Generator().manual_seed(i))
+           for i, L in enumerate(LENS)]
+    pos = torch.cat([torch.arange(L) for L in LENS])
+    slots = torch.cat([bt[i, torch.arange(L) // P].long() * P + torch.arange(L) % P for i, L in enumerate(LENS)])
+    last = torch.tensor(LENS).cumsum(0) - 1
+    fb = ForwardBatch(torch.cat(ids).to(dev), pos.to(dev), slots.to(dev), True, last.to(dev), seq_lens=LENS)
+    pre = m.forward(fb, kv).float().cpu()
+    nxt = torch.tensor([int(x[-1]) for x in ids])
+    dpos = torch.tensor(LENS)
+    dslots = torch.stack([bt[i, L // P].long() * P + L % P for i, L in enumerate(LENS)])
+    fb = ForwardBatch(nxt.to(dev), dpos.to(dev), dslots.to(dev), False, None, block_tables=bt.to(dev),
+                      context_lens=(dpos + 1).int().to(dev), num_splits=1)
+    dec = m.forward(fb, kv).float().cpu()
+    torch.cuda.synchronize()
+    return pre, dec
+
+
+def _worker(rank: int, world: int, port: int, wdt: str, q) -> None:
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                          LOCAL_RANK="0")
+        import torch.distributed as dist
+
+        from operator_amd.models.llama import LlamaModel
+        from operator_amd.parallel.comm import init_from_env, split_groups
+
+        init_from_env(backend="gloo")
+        torch.cuda.set_device(0)
+        tp, _ = split_groups(world)
+        assert tp.enable_oneshot(torch.device("cuda", 0))
+        m = LlamaModel(_cfg(), device="cuda", tp=tp, weight_dtype=wdt).init_random(seed=7)
+        pre, dec = _run(m, m.hkv)
+        tp.oneshot.check()
+        dist.barrier()
+        tp.oneshot.close()
+        dist.destroy_process_group()
+        q.put((rank, "ok", pre.numpy(), dec.numpy()))   # by value: the child exits before the get
+    except BaseException:  # noqa: BLE001
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc(), None))
+
+
+@pytest.mark.parametrize("wdt", ["bfloat16", "fp8"])
+def test_tp2_on_one_gpu_tracks_tp1(wdt):
+    import torch.multiprocessing as mp
+
+    from operator_amd.models.llama import LlamaModel
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, wdt, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    try:
+        for _ in range(world):
+            rank, status, a, b = q.get(timeout=300)
+            assert status == "ok", a
+            got[rank] = (torch.from_numpy(a), torch.from_numpy(b))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    pre = torch.cat([got[r][0] for r in range(world)], dim=1)   # vocab shards in rank order
+    dec = torch.cat([got[r][1] for r in range(world)], dim=1)
+    m1 = LlamaModel(_cfg(), device="cuda", weight_dtype=wdt).init_random(seed=7)
+    pre1, dec1 = _run(m1, m1.hkv)
+    tol = 0.05 if wdt == "bfloat16" else 0.12   # fp8: per-shard channel scales of the row-parallel weights
+    for got_, want in ((pre, pre1), (dec, dec1)):
+        assert got_.shape == want.shape
+        err = float((got_ - want).abs().max() / want.abs().max())
+        assert err < tol, err
+    # the decode step's greedy token agrees for rows whose top-2 logits are not a near tie
+    top2 = dec1.topk(2, dim=1).values
+    clear = (top2[:, 0] - top2[:, 1]) > 0.05 * dec1.abs().max()
+    assert torch.equal(dec.argmax(1)[clear], dec1.argmax(1)[clear])
