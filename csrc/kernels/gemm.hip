@@ -95,10 +95,13 @@ __global__ void __launch_bounds__(kWaves * 64, NS == 2 ? 2 : 1) gemm_tn_kernel(c
       const int wn_ = n0 + row - BM;
       // tiled W ([N/64][K/64][64][64]): each 8-row x 128-B piece of a stage is one
       // contiguous 1 KB of HBM instead of 8 separate 128-B row segments
-      const bf16_t* wsrc = w_tiled ? W + ((int64_t)(wn_ >> 6) * (K >> 6) + (k0 >> 6)) * 4096 + (wn_ & 63) * 64 + chunk * 8
+      const bf16_t* wsrc = (w_tiled & 1) ? W + ((int64_t)(wn_ >> 6) * (K >> 6) + (k0 >> 6)) * 4096 + (wn_ & 63) * 64 + chunk * 8
                                    : W + (int64_t)wn_ * K + k0 + chunk * 8;
       const bf16_t* src = (row < BM) ? X + (int64_t)row * K + k0 + chunk * 8 : wsrc;
-      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(sbase + q * 1024), 16, 0, 0);
+      if ((w_tiled & 2) && row >= BM)   // wave-uniform (8-row pieces): weights stream non-temporal
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(sbase + q * 1024), 16, 0, 2);
+      else
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(sbase + q * 1024), 16, 0, 0);
     }
   };
   auto issue = [&](int t, int buf) {
@@ -237,8 +240,10 @@ int splitk_reduce(const float* P, bf16_t* Y, int64_t MN, int S, hipStream_t stre
 
 int gemm_decode(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, int N, int K, int S, int BN,
                 int BM, bool silu_gu, bool w_tiled_b, int stages, hipStream_t stream) {
-  const int w_tiled = w_tiled_b ? 1 : 0;
-  if (w_tiled && (N % 64 != 0 || K % 64 != 0)) return -6;
+  // bit 0: tiled W layout; bit 1: W streams with the non-temporal policy (OAMD_BF16_WNT)
+  static const int wnt = [] { const char* e = getenv("OAMD_BF16_WNT"); return e && e[0] == '0' ? 0 : 2; }();
+  const int w_tiled = (w_tiled_b ? 1 : 0) | wnt;
+  if (w_tiled_b && (N % 64 != 0 || K % 64 != 0)) return -6;
   if ((BM != 64 && BM != 128 && BM != 256) || M % BM != 0) return -1;
   if (silu_gu) {  // fused SwiGLU: one K slice, 128-column tiles of 64 gate + 64 up rows
     if (BN != 128 || S != 1 || N % 128 != 0 || K % kBK != 0) return -5;

@@ -57,7 +57,7 @@ template <int BM, int BN, bool PARTIAL>
 __global__ void __launch_bounds__(f8::kWaves * 64, 1)
     gemm_fp8_kernel(const uint8_t* __restrict__ X, const uint8_t* __restrict__ W, const float* __restrict__ sx,
                     const float* __restrict__ sw, bf16_t* __restrict__ Y, float* __restrict__ P, int M, int N, int K,
-                    int S) {
+                    int S, int wnt) {
   using C = f8::Cfg<BM, BN>;
   __shared__ __attribute__((aligned(1024))) char lds[C::LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -77,7 +77,10 @@ __global__ void __launch_bounds__(f8::kWaves * 64, 1)
       const int chunk = f8::swz(row, lslot);
       const uint8_t* src = (row < BM) ? X + (int64_t)min(m0 + row, M - 1) * K + k0 + chunk * 16
                                       : W + (int64_t)(n0 + row - BM) * K + k0 + chunk * 16;
-      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(sbase + q * 1024), 16, 0, 0);
+      if (wnt && row >= BM)   // wave-uniform (8-row pieces): weights stream non-temporal
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(sbase + q * 1024), 16, 0, 2);
+      else
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(sbase + q * 1024), 16, 0, 0);
     }
   };
 
@@ -332,9 +335,11 @@ int gemm_fp8(const uint8_t* X, const uint8_t* W, const float* sx, const float* s
   if (S < 1 || 8 % S != 0 || K % (f8::kBK * S) != 0) return -3;
   if (S > 1 && P == nullptr) return -4;
   const dim3 grid((N / BN) * S, (M + BM - 1) / BM);
-#define OAMD_G8(BMM, BNN)                                                                                          \
-  if (S > 1) gemm_fp8_kernel<BMM, BNN, true><<<grid, f8::kWaves * 64, 0, stream>>>(X, W, sx, sw, Y, P, M, N, K, S); \
-  else gemm_fp8_kernel<BMM, BNN, false><<<grid, f8::kWaves * 64, 0, stream>>>(X, W, sx, sw, Y, P, M, N, K, S)
+  static const int wnt = [] { const char* e = getenv("OAMD_FP8_WNT"); return e && e[0] == '0' ? 0 : 1; }();
+#define OAMD_G8(BMM, BNN)                                                                                     \
+  if (S > 1)                                                                                                  \
+    gemm_fp8_kernel<BMM, BNN, true><<<grid, f8::kWaves * 64, 0, stream>>>(X, W, sx, sw, Y, P, M, N, K, S, wnt); \
+  else gemm_fp8_kernel<BMM, BNN, false><<<grid, f8::kWaves * 64, 0, stream>>>(X, W, sx, sw, Y, P, M, N, K, S, wnt)
 #define OAMD_G8M(BMM) \
   if (BN == 64) { OAMD_G8(BMM, 64); } else { OAMD_G8(BMM, 128); }
   switch (BM) {
