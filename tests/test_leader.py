@@ -118,10 +118,14 @@ def test_stalled_renewal_stops_leading_within_deadline():
     a = LeaderElector(slow, "l", "ns", identity="a", lease_duration_s=1.5, renew_deadline_s=0.8, retry_period_s=0.1,
                       on_started_leading=lambda: events.append(("a", "start", time.monotonic())),
                       on_stopped_leading=lambda: events.append(("a", "stop", time.monotonic()))).start()
-    b = LeaderElector(fk, "l", "ns", identity="b", lease_duration_s=1.5, renew_deadline_s=0.8, retry_period_s=0.1,
-                      on_started_leading=lambda: events.append(("b", "start", time.monotonic()))).start()
+    b = None
     try:
         wait_for(lambda: a.leading)
+        # the standby starts once a holds the lease: started together, b could win the
+        # first acquisition and a would never lead (a race, not the behaviour under test)
+        b = LeaderElector(fk, "l", "ns", identity="b", lease_duration_s=1.5, renew_deadline_s=0.8,
+                          retry_period_s=0.1,
+                          on_started_leading=lambda: events.append(("b", "start", time.monotonic()))).start()
         time.sleep(0.3)
         assert not b.leading
         t_stall = time.monotonic()
@@ -136,7 +140,8 @@ def test_stalled_renewal_stops_leading_within_deadline():
         assert start_b > stop_t    # never two leaders at once
     finally:
         slow.stall_s = 0.0
-        b.stop()
+        if b is not None:
+            b.stop()
         a.stop(timeout=1)
 
 

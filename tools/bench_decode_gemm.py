@@ -47,6 +47,8 @@ def main() -> int:
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--shapes", default="qkv,o,down,gate_up+silu")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--tile", action="store_true",
+                    help="also time the 256x256-tile kernel (gemm_tile) with split-K S = 1, 2, 4, 8, 16")
     a = ap.parse_args()
     M = a.m
     rows = []
@@ -75,6 +77,23 @@ def main() -> int:
             norm = lambda r: ops.rmsnorm(r, nw, 1e-5, residual=res, out=yn)  # noqa: E731
             cands["table"] = lambda: ops.linear(x, nxt(), defer_reduce=True)
             cands["table+norm"] = lambda: norm(ops.linear(x, nxt(), defer_reduce=True))
+        if a.tile:
+            C = ops.kernels()
+            P = torch.empty(16 * M * N, dtype=torch.float32, device="cuda")
+            for S in (1, 2, 4, 8, 16):
+                if K % (64 * S):
+                    continue
+                if silu:
+                    y2 = torch.empty(M, N // 2, dtype=torch.bfloat16, device="cuda")
+                    cands[f"tile_s{S}"] = (lambda S=S, y2=y2: C.gemm_tile(x, nxt(), y2, None, True, 0, S,
+                                                                         P if S > 1 else None))
+                elif S == 1:
+                    y1 = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+                    cands["tile_s1+norm"] = lambda y1=y1: (C.gemm_tile(x, nxt(), y1, None, False, 0, 1, None),
+                                                           norm(y1))
+                else:
+                    cands[f"tile_s{S}+norm"] = (lambda S=S: (C.gemm_tile(x, nxt(), None, None, False, 0, S, P),
+                                                             norm(ops.SplitK(P, S, M, N))))
         times = {k: [] for k in cands}
         for _ in range(a.rounds):
             for k, fn in cands.items():
