@@ -492,8 +492,9 @@ class LLMEngine:
         if self.device.type == "cuda":
             self._host_bufs = [torch.empty(max_batch, self.multi_step, dtype=torch.long, pin_memory=True)
                                for _ in range(2)]
-        # shared prompt prefix: the GPU path needs the v3 prefill attention kernel; TP
-        # engines replay the leader's steps and keep it off
+        # shared prompt prefix: the GPU path needs the v3 / v4 prefill attention kernel; TP
+        # followers replay the leader's admissions, so every rank builds the same prefix at
+        # the same step (tests/test_tp_scale.py::test_tp_prefix_sharing_matches_tp1)
         self.prefix_sharing = prefix_sharing and (
             self.device.type != "cuda" or ops.prefill_variant(model.hq, model.hkv) in (3, 4))
         self._pfx: _SharedPrefix | None = None
