@@ -79,6 +79,7 @@ class FakeWatch:
 
     def __init__(self, fk: "FakeKube", res: Resource, namespace: str | None, sink=None):
         self.fk, self.res, self.namespace = fk, res, namespace
+        self.rkey = _res_key(res)   # events match by key (the REST server builds a Resource per request)
         self.q: queue.Queue = queue.Queue()
         # sink(item): deliver events / end / failure markers somewhere else than self.q
         # (the asyncio REST server feeds its watch coroutines this way)
@@ -209,12 +210,13 @@ class FakeKube:
         rv = int(obj["metadata"]["resourceVersion"])
         # stored objects are never mutated after they are stored (every update stores a
         # new dict), so the history can hold them by reference
-        self._history.append((rv, self._key(res), typ, obj))
+        k = self._key(res)
+        self._history.append((rv, k, typ, obj))
         self._last_rv = rv
         ev = None
+        ns = obj["metadata"].get("namespace")
         for w in list(self._watches):
-            if (w.res is res or w.res == res) and (w.namespace is None
-                                                   or w.namespace == obj["metadata"].get("namespace")):
+            if w.rkey == k and (w.namespace is None or w.namespace == ns):
                 if ev is None:
                     ev = _Event(typ, obj)
                 w.push(typ, obj, ev)

@@ -12,6 +12,7 @@ queued events. An 8-shard plumbing run is bound by this process (tools/bench_plu
 from __future__ import annotations
 
 import asyncio
+import os
 import json
 import threading
 
@@ -52,7 +53,22 @@ class AsyncFakeKubeServer:
         self._server = self.loop.run_until_complete(
             asyncio.start_server(self._client, host, port, backlog=1024, limit=1 << 20))
         self.url = f"http://{host}:{self._server.sockets[0].getsockname()[1]}"
-        self._t = threading.Thread(target=self.loop.run_forever, name="fakekube-aio", daemon=True)
+        self._t = threading.Thread(target=self._run, name="fakekube-aio", daemon=True)
+
+    def _run(self) -> None:
+        prof_path = os.environ.get("OAMD_APISERVER_PROFILE")   # cProfile of the serving loop (tools)
+        if not prof_path:
+            self.loop.run_forever()
+            return
+        import cProfile
+
+        prof = cProfile.Profile()
+        prof.enable()
+        try:
+            self.loop.run_forever()
+        finally:
+            prof.disable()
+            prof.dump_stats(prof_path)
 
     def start(self) -> "AsyncFakeKubeServer":
         self._t.start()

@@ -203,9 +203,20 @@ def test_cli_run_with_two_shards_starts_and_stops_both(tmp_path):
     import time as _t
     import urllib.request
 
-    with socket.socket() as sk:
-        sk.bind(("127.0.0.1", 0))
-        port = sk.getsockname()[1]
+    import random
+
+    # two consecutive free ports below the ephemeral range (port + 1 of an ephemeral port
+    # can be any outgoing connection's, and shard 1 then never binds)
+    rng = random.Random()
+    for _ in range(200):
+        port = rng.randrange(20000, 32000)
+        try:
+            with socket.socket() as a, socket.socket() as b:
+                a.bind(("127.0.0.1", port))
+                b.bind(("127.0.0.1", port + 1))
+            break
+        except OSError:
+            continue
     env = dict(os.environ, PODMORTEM_LOG_LEVEL="WARNING")
     p = subprocess.Popen([sys.executable, "-m", "operator_amd", "run", "--fake", "--shards", "2",
                           "--set", f"health.port={port}", "--set", "health.host=127.0.0.1",
