@@ -1,5 +1,5 @@
-"""Tensor parallelism on the GPU kernels: TP = 2 as two ranks on the one MI355X of the
-box (cuda:0), the decode all-reduces through the IPC kernels between them (the fused
+"""Tensor parallelism on the GPU kernels: TP = 2 and 4 as ranks sharing the one MI355X of
+the box (cuda:0), the decode all-reduces through the IPC kernels between them (the fused
 all-reduce + residual + RMSNorm, and with fp8 weights its e4m3fn epilogue), gloo only
 for the handle exchange (RCCL refuses two ranks on one device). The sharded model's
 prefill logits and one paged decode step (the decode RoPE folded into attention, the
@@ -83,13 +83,12 @@ def _worker(rank: int, world: int, port: int, wdt: str, q) -> None:
         q.put((rank, "error", traceback.format_exc(), None))
 
 
-@pytest.mark.parametrize("wdt", ["bfloat16", "fp8"])
-def test_tp2_on_one_gpu_tracks_tp1(wdt):
+@pytest.mark.parametrize("wdt,world", [("bfloat16", 2), ("fp8", 2), ("bfloat16", 4)])
+def test_tp_on_one_gpu_tracks_tp1(wdt, world):
     import torch.multiprocessing as mp
 
     from operator_amd.models.llama import LlamaModel
 
-    world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
