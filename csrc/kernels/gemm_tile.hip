@@ -323,12 +323,11 @@ __device__ __forceinline__ void mfma_tied(f32x4& acc, const u16x8& a, const u16x
 // COLS: the MFMA groups run over W fragments (A operand fixed for 8 MFMAs, as hipBLASLt's
 // MT256x256x64 loop does) instead of X fragments; every group then needs all 8 X fragments,
 // so the X pieces / fragments of the next tile come first (phases 2-3) and W last.
-// kEpiPartial: split-K over blockIdx.y (K / gridDim.y per block), fp32 slab P[y][M][N].
 template <int EPI, int AUX = 16, bool COLS = false>
 __global__ void __launch_bounds__(256) gemm_tile256_h4_kernel(const bf16_t* __restrict__ X,
                                                               const bf16_t* __restrict__ W, bf16_t* __restrict__ Y,
                                                               const bf16_t* __restrict__ bias, int M, int N, int K,
-                                                              int ldy, float* __restrict__ P = nullptr) {
+                                                              int ldy) {
   constexpr int kHalf = 32768;       // one operand of a tile: 256 rows x 128 B
   constexpr int kTile = 2 * kHalf;   // X then W
   __shared__ __attribute__((aligned(1024))) char lds[2 * kTile];
@@ -349,18 +348,17 @@ __global__ void __launch_bounds__(256) gemm_tile256_h4_kernel(const bf16_t* __re
   // DMA piece q (0..7) of an operand for wave w = rows 8 (w + 4q) .. +7; lane l -> row + l/8,
   // LDS slot l % 8, source chunk slot ^ ((row >> 1) & 7). 32-bit byte offsets (launcher checks)
   const int lrow = lane >> 3, lslot = lane & 7;
-  const uint32_t kbase = (uint32_t)blockIdx.y * (uint32_t)(K / gridDim.y);   // split-K slice (kEpiPartial)
   uint32_t xo[8], wo[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const int row = 8 * (w + 4 * q) + lrow;
     const int chunk = lslot ^ ((row >> 1) & 7);
-    xo[q] = ((uint32_t)min(m0 + row, M - 1) * (uint32_t)K + kbase + chunk * 8) * 2u;
-    wo[q] = ((uint32_t)min(n0 + row, N - 1) * (uint32_t)K + kbase + chunk * 8) * 2u;
+    xo[q] = ((uint32_t)min(m0 + row, M - 1) * (uint32_t)K + chunk * 8) * 2u;
+    wo[q] = ((uint32_t)min(n0 + row, N - 1) * (uint32_t)K + chunk * 8) * 2u;
   }
   const auto xr = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)((uint32_t)M * (uint32_t)K * 2u), 0x00020000);
   const auto wr = __builtin_amdgcn_make_buffer_rsrc((void*)W, (short)0, (int)((uint32_t)N * (uint32_t)K * 2u), 0x00020000);
-  const int T = K / (int)gridDim.y / kBK;
+  const int T = K / kBK;
   auto dma_x = [&](int kt, int buf, int q) {
     char* dst = lds + buf * kTile + (w + 4 * q) * 1024;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)dst, 16, (int)xo[q],
@@ -494,14 +492,7 @@ __global__ void __launch_bounds__(256) gemm_tile256_h4_kernel(const bf16_t* __re
     for (int f = 0; f < 2; ++f)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        if constexpr (EPI == kEpiPartial) {
-          float* prow = P + ((int64_t)blockIdx.y * M + tok) * N;
-#pragma unroll
-          for (int ty = 0; ty < 2; ++ty) {
-            const int col = n0 + f * 128 + ty * 64 + wn * 32 + j * 16 + 4 * lq;
-            if (col < N) *reinterpret_cast<f32x4*>(prow + col) = acc[i][f * 4 + ty * 2 + j];
-          }
-        } else if constexpr (EPI == kEpiSilu) {
+        if constexpr (EPI == kEpiSilu) {
           const int col = (n0 >> 1) + f * 64 + wn * 32 + j * 16 + 4 * lq;
           if (2 * col >= N) continue;
           const f32x4 gt = acc[i][f * 4 + j], up = acc[i][f * 4 + 2 + j];
@@ -569,12 +560,8 @@ int gemm_tile(const bf16_t* X, const bf16_t* W, bf16_t* Y, const bf16_t* bias, i
   if (S < 1 || S > 64 || K % (kBK * S) != 0 || (S > 1 && (P == nullptr || bias != nullptr))) return -5;
   if (Y == nullptr && (S == 1 || silu_gu)) return -6;
   const int nwg = ((M + kT - 1) / kT) * ((N + kT - 1) / kT);
-  const bool off32 = (int64_t)M * K * 2 < (1LL << 32) && (int64_t)N * K * 2 < (1LL << 32);
   if (S > 1) {   // fp32 slabs, then (unless the consumer sums them) one reduce pass
-    if (variant == 5 && off32)   // the 4-wave h4 schedule per K slice
-      gemm_tile256_h4_kernel<kEpiPartial><<<dim3(nwg, S), 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy, P);
-    else
-      gemm_tile256_kernel<kEpiPartial><<<dim3(nwg, S), 512, 0, stream>>>(X, W, Y, bias, M, N, K, ldy, P);
+    gemm_tile256_kernel<kEpiPartial><<<dim3(nwg, S), 512, 0, stream>>>(X, W, Y, bias, M, N, K, ldy, P);
     OAMD_LAUNCH_CHECK();
     if (Y == nullptr) return 0;
     if (silu_gu) {
@@ -586,6 +573,7 @@ int gemm_tile(const bf16_t* X, const bf16_t* W, bf16_t* Y, const bf16_t* bias, i
     if (ldy != N) return -7;
     return splitk_reduce(P, Y, (int64_t)M * N, S, stream);
   }
+  const bool off32 = (int64_t)M * K * 2 < (1LL << 32) && (int64_t)N * K * 2 < (1LL << 32);
   if ((variant == 0 || variant == 1) && off32) {   // 4-wave, two 64 KiB buffers, four phases per K-tile
     if (silu_gu) gemm_tile256_h4_kernel<kEpiSilu><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
     else if (bias) gemm_tile256_h4_kernel<kEpiBias><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);

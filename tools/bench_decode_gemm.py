@@ -87,9 +87,6 @@ def main() -> int:
                     y2 = torch.empty(M, N // 2, dtype=torch.bfloat16, device="cuda")
                     cands[f"tile_s{S}"] = (lambda S=S, y2=y2: C.gemm_tile(x, nxt(), y2, None, True, 0, S,
                                                                          P if S > 1 else None))
-                    if 1 < S <= 4:   # the 4-wave h4 schedule per K slice (variant 5), then the SwiGLU reduce
-                        cands[f"h4_s{S}"] = (lambda S=S, y2=y2: C.gemm_tile(x, nxt(), y2, None, True, 5, S, P))
-                        cands[f"h4_s{S}_gemm_only"] = (lambda S=S: C.gemm_tile(x, nxt(), None, None, False, 5, S, P))
                 elif S == 1:
                     y1 = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
                     cands["tile_s1+norm"] = lambda y1=y1: (C.gemm_tile(x, nxt(), y1, None, False, 0, 1, None),
