@@ -478,9 +478,24 @@ def silu_quantize_fp8(gu, block: int | None = GU_BLOCK) -> tuple[torch.Tensor, t
     return quantize_fp8(silu_mul(gu, block=block))
 
 
+def _fp8_overrides() -> dict:
+    """OAMD_FP8_PLANS="NxK=bm,bn,S;..." (A/B of fp8 decode plans): (N, K) -> (bm, bn, S)."""
+    out = {}
+    for item in filter(None, os.environ.get("OAMD_FP8_PLANS", "").split(";")):
+        shape, plan = item.split("=")
+        n, k = (int(v) for v in shape.split("x"))
+        out[(n, k)] = tuple(int(v) for v in plan.split(","))
+    return out
+
+
+_FP8_OVERRIDES = _fp8_overrides()
+
+
 def fp8_plan(M: int, N: int, K: int) -> tuple[int, int, int]:
     """(bm, bn, splits) for gemm_fp8: row tile by M, 128-column tiles for wide N, and
     split-K until the blocks reach one per CU (K permitting)."""
+    if (N, K) in _FP8_OVERRIDES:
+        return _FP8_OVERRIDES[(N, K)]
     bm = 64 if M <= 64 else 128 if M <= 128 else 256
     bn = 128 if N % 128 == 0 and N // 128 >= 192 else 64
     mt = -(-M // bm)
