@@ -119,6 +119,19 @@ int rmsnorm(const bf16_t* x, bf16_t* residual, const bf16_t* w, bf16_t* y,
   const int nvec = hidden / 8;
   const int64_t slab = (int64_t)rows * hidden;
   const int sc = xp == nullptr ? 1 : S;
+  // split-K slab sums of rows up to 4096 wide: 512 threads, one vector each, so a row's
+  // slab loads all leave in one round (OAMD_RMS_WIDE=0: 256 threads x 2 vectors)
+  static const bool wide = [] { const char* e = getenv("OAMD_RMS_WIDE"); return !(e && e[0] == '0'); }();
+  if (wide && xp != nullptr && sc > 1 && nvec > NT && nvec <= 2 * NT) {
+    switch (sc) {
+      case 2: rmsnorm_kernel<2 * NT, 1, 2><<<rows, 2 * NT, 0, stream>>>(x, residual, w, y, hidden, x_stride, r_stride, y_stride, eps, xp, S, slab); break;
+      case 4: rmsnorm_kernel<2 * NT, 1, 4><<<rows, 2 * NT, 0, stream>>>(x, residual, w, y, hidden, x_stride, r_stride, y_stride, eps, xp, S, slab); break;
+      case 8: rmsnorm_kernel<2 * NT, 1, 8><<<rows, 2 * NT, 0, stream>>>(x, residual, w, y, hidden, x_stride, r_stride, y_stride, eps, xp, S, slab); break;
+      default: rmsnorm_kernel<2 * NT, 1, 0><<<rows, 2 * NT, 0, stream>>>(x, residual, w, y, hidden, x_stride, r_stride, y_stride, eps, xp, S, slab); break;
+    }
+    OAMD_LAUNCH_CHECK();
+    return 0;
+  }
 #define OAMD_RMS(MV, SCC) \
   rmsnorm_kernel<NT, MV, SCC><<<rows, NT, 0, stream>>>(x, residual, w, y, hidden, x_stride, r_stride, y_stride, eps, xp, S, slab)
 #define OAMD_RMS_S(MV)                  \

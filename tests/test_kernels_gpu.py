@@ -333,9 +333,10 @@ def test_gemm_fp8(M, N, K):
 
 
 @pytest.mark.parametrize("S", [1, 2, 3, 4, 8])
-def test_rmsnorm_sums_splitk_slabs(S):
+@pytest.mark.parametrize("N", [1024, 3072, 4096])   # 3072 / 4096: the 512-thread slab-sum path
+def test_rmsnorm_sums_splitk_slabs(S, N):
     torch.manual_seed(11)
-    M, N = 128, 1024
+    M = 128
     P = torch.randn(S * M * N, device=DEV, dtype=torch.float32)
     w = _rand(N)
     r1 = _rand(M, N)
