@@ -50,8 +50,8 @@ struct CacheStore<uint8_t> {
 
 // SC: compile-time split-K slab count (0: runtime S), so all S slab loads of a group
 // are issued before the first add (a runtime-trip-count loop waited for each in turn).
-template <int D, typename KV, int SC>
-__global__ void __launch_bounds__(kRopeItems) rope_kv_kernel(
+template <int D, typename KV, int SC, int NI = kRopeItems>
+__global__ void __launch_bounds__(NI) rope_kv_kernel(
     const bf16_t* __restrict__ qkv, int64_t qkv_stride, const int64_t* __restrict__ pos,
     const float* __restrict__ cos_t, const float* __restrict__ sin_t, int Hq, int Hkv,
     bf16_t* __restrict__ q_out, bf16_t* __restrict__ k_out, bf16_t* __restrict__ v_out,
@@ -132,7 +132,7 @@ __global__ void __launch_bounds__(kRopeItems) rope_kv_kernel(
   const int rot_items = (Hq + Hkv) * GPH;
   const int copy_items = Hkv * (D / 8);
   {
-    const int it = blockIdx.y * kRopeItems + threadIdx.x;
+    const int it = blockIdx.y * NI + threadIdx.x;
     if (it >= rot_items + copy_items) return;
     if (it < rot_items) {
       const int h = it / GPH, g = (it % GPH) * 8;
@@ -191,12 +191,18 @@ int rope_kv(const bf16_t* qkv, int64_t qkv_stride, const int64_t* pos, const flo
   if (head_dim != 128) return -1;
   const int64_t slab = (int64_t)tokens * (Hq + 2 * Hkv) * head_dim;
   const int items = (Hq + Hkv) * (head_dim / 16) + Hkv * (head_dim / 8);
-  const dim3 grid(tokens, (items + kRopeItems - 1) / kRopeItems);
+  static const int ni = [] { const char* e = getenv("OAMD_ROPE_ITEMS"); return e && e[0] == '6' ? 64 : 256; }();   // OAMD_ROPE_ITEMS=64: one-wave workgroups
+  const dim3 grid(tokens, (items + ni - 1) / ni);
   const int sc = xp == nullptr ? 1 : S;
 #define OAMD_ROPE(KVT, SCC, KI, VI)                                                                              \
-  rope_kv_kernel<128, KVT, SCC><<<grid, kRopeItems, 0, stream>>>(                                               \
-      qkv, qkv_stride, pos, cos_t, sin_t, Hq, Hkv, q_out, k_out, v_out, static_cast<KVT*>(k_cache),            \
-      static_cast<KVT*>(v_cache), slots, page_size, max_pos, xp, S, slab, bias, KI, VI)
+  if (ni == 256)                                                                                                 \
+    rope_kv_kernel<128, KVT, SCC, 256><<<grid, 256, 0, stream>>>(                                                \
+        qkv, qkv_stride, pos, cos_t, sin_t, Hq, Hkv, q_out, k_out, v_out, static_cast<KVT*>(k_cache),          \
+        static_cast<KVT*>(v_cache), slots, page_size, max_pos, xp, S, slab, bias, KI, VI);                      \
+  else                                                                                                           \
+    rope_kv_kernel<128, KVT, SCC><<<grid, kRopeItems, 0, stream>>>(                                             \
+        qkv, qkv_stride, pos, cos_t, sin_t, Hq, Hkv, q_out, k_out, v_out, static_cast<KVT*>(k_cache),          \
+        static_cast<KVT*>(v_cache), slots, page_size, max_pos, xp, S, slab, bias, KI, VI)
 #define OAMD_ROPE_S(KVT, KI, VI)                   \
   switch (sc) {                                    \
     case 1: OAMD_ROPE(KVT, 1, KI, VI); break;      \
