@@ -525,6 +525,347 @@ __global__ void __launch_bounds__(256) gemm_tile256_h4_kernel(const bf16_t* __re
   }
 }
 
+// Variant 5, the persistent "p5" schedule (round 6): the h4 tile (4 waves, 128 x 128 outputs
+// per wave in 256 tied AGPRs, BK = 64, two 64 KiB LDS buffers filled by 8-row x 128-B LDS-DMA
+// pieces with a source-side chunk swizzle), but
+//   * ONE workgroup per CU (grid = min(tiles, CUs)) walking its tiles in rounds: in round r
+//     block b takes linear tile r * G + xcd_remap(b, G), and the linear tile goes through the
+//     GROUP_M = 8 order, so the 32 tiles an XCD holds at once share X / W panels in its L2;
+//   * the LDS-DMA stream is continuous ACROSS tiles: K-step g issues the pieces of step g + 2
+//     of the block's flattened (tile, k) stream, so the last two steps of a tile already load
+//     the next tile's steps 0 and 1, whose first fragments are in registers when the previous
+//     tile's epilogue stores go out (no per-tile prologue fill, no workgroup relaunch);
+//   * two barriers and one counted vmcnt per K-step (the h4 loop had three and two):
+//       segment A: k-half 0 (64 MFMAs); the 16 fragment reads of k-half 1 ride on its first
+//         16 MFMAs; after 40 MFMAs lgkmcnt(0) + barrier (every wave is done with this buffer)
+//         and the 8 W pieces of step g + 2 go into it between the last 24;
+//       segment B: k-half 1 (64 MFMAs); the 8 X pieces of step g + 2 ride on its first 40;
+//         then vmcnt(16) + barrier (step g + 1 landed for every wave) and its k-half-0
+//         fragment reads ride on the last 24 MFMAs;
+//   * 16-B output stores: the two W fragments of a 32-feature block take interleaved feature
+//     rows (fragment jj, row m -> feature 8 (m / 4) + 4 jj + m % 4), so the lane holding
+//     accumulator rows 4q .. 4q+3 of both has features 8q .. 8q+7 -- one dwordx4 store per
+//     fragment pair, half the store instructions of the 8-B form: a tile's 128 KiB epilogue
+//     is bound by store ISSUE (cdna guide T21), and at the prefill shapes it was ~10 % of the
+//     kernel (K sweep, profiles/gemm_tile_p5_vs_hipblaslt_r6.jsonl). The chunk swizzle
+//     slot ^ (bit1(row) << 1 | bit3(row) << 2) keeps both fragment-read patterns conflict-free;
+//   * per-tile buffer resources (base = the tile's first row, num_records = its rows x K x 2):
+//     rows past M / N read as zeros, no clamps, no 32-bit limit on the operand size.
+// DEEP: which operand streams through THREE LDS buffers (its pieces issued 3 K-steps ahead, two steps
+// of flight) -- 0: neither (2 + 2 buffers, 128 KiB), 1: X (narrow N: the X panels come from HBM,
+// W stays in the Infinity Cache), 2: W (wide N: the W panels come from HBM); 160 KiB of LDS.
+// OPT (A/B arms): bit 0 = s_setprio 1 over the MFMA streams; bit 1 = MFMA groups over W fragments
+// (srcA fixed for 8 MFMAs, as hipBLASLt's MT256x256x64 loop issues them)
+template <int EPI, int DEEP = 0, int OPT = 0>
+__global__ void __launch_bounds__(256) gemm_tile256_p5_kernel(const bf16_t* __restrict__ X,
+                                                              const bf16_t* __restrict__ W, bf16_t* __restrict__ Y,
+                                                              const bf16_t* __restrict__ bias, int M, int N, int K,
+                                                              int ldy) {
+  constexpr int AUX = 16;
+  constexpr int kHalf = 32768;   // one operand of a K-step: 256 rows x 128 B
+  __shared__ __attribute__((aligned(1024))) char lds[DEEP ? 5 * kHalf : 4 * kHalf];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int mt = (M + kT - 1) / kT, nt = (N + kT - 1) / kT;
+  const int ntiles = mt * nt;
+  const int G = gridDim.x;
+  const int slot = xcd_remap(blockIdx.x, G);
+  const int T = K / kBK;
+  const int gsz = kGroupM * nt;
+  // linear tile of round r -> (m0, n0); false past the last tile
+  auto tile_rc = [&](int r, int& m0, int& n0) -> bool {
+    const int lid = r * G + slot;
+    if (lid >= ntiles) return false;
+    const int first_m = (lid / gsz) * kGroupM;
+    const int gm = min(mt - first_m, kGroupM);
+    m0 = (first_m + (lid % gsz) % gm) * kT;
+    n0 = ((lid % gsz) / gm) * kT;
+    return true;
+  };
+  // LDS byte offsets of an operand's buffer for K-step (parity p2 = g & 1, p3 = g % 3)
+  auto xoff = [&](int p2, int p3) -> int {
+    if constexpr (DEEP == 0) return p2 * 2 * kHalf;
+    else if constexpr (DEEP == 1) return 2 * kHalf + p3 * kHalf;
+    else return p2 * kHalf;
+  };
+  auto woff = [&](int p2, int p3) -> int {
+    if constexpr (DEEP == 0) return p2 * 2 * kHalf + kHalf;
+    else if constexpr (DEEP == 2) return 2 * kHalf + p3 * kHalf;
+    else return p2 * kHalf;
+  };
+  auto swz = [](int row) { return (((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2); };
+
+  // DMA piece q (0..7) of an operand for wave w = tile rows 8 (w + 4q) .. +7; lane l -> row + l/8,
+  // LDS slot l % 8, source chunk slot ^ swz(row). Same offsets for X and W (both K wide).
+  const int lrow = lane >> 3, lslot = lane & 7;
+  uint32_t vo[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int row = 8 * (w + 4 * q) + lrow;
+    vo[q] = ((uint32_t)row * (uint32_t)K + (uint32_t)((lslot ^ swz(row)) * 8)) * 2u;
+  }
+
+  // issue cursors: the (tile, k) step whose pieces go out next, per operand. A tile's operand is a
+  // buffer resource: base = its first row, num_records = its rows x K x 2 (rows past M / N read as
+  // zeros); the resource is rebuilt from (base, bytes) at each use
+  struct Cur { int r, kt; const bf16_t* p; int n; };
+  Cur cx{0, 0, nullptr, 0}, cw{0, 0, nullptr, 0};
+  {
+    int m0 = 0, n0 = 0;
+    if (!tile_rc(0, m0, n0)) return;   // grid <= tiles: never taken
+    cx.p = X + (int64_t)m0 * K;
+    cx.n = (int)((uint32_t)min(M - m0, kT) * (uint32_t)K * 2u);
+    cw.p = W + (int64_t)n0 * K;
+    cw.n = (int)((uint32_t)min(N - n0, kT) * (uint32_t)K * 2u);
+  }
+  auto advance = [&](Cur& c, bool isx) {
+    if (++c.kt == T) {
+      int m0n = 0, n0n = 0;
+      if (tile_rc(c.r + 1, m0n, n0n)) {
+        ++c.r;
+        c.kt = 0;
+        const int row0 = isx ? m0n : n0n;
+        c.p = (isx ? X : W) + (int64_t)row0 * K;
+        c.n = (int)((uint32_t)min((isx ? M : N) - row0, kT) * (uint32_t)K * 2u);
+      } else {
+        c.kt = T - 1;   // past the block's last tile: harmless re-loads of its last step
+      }
+    }
+  };
+  auto dma = [&](const Cur& c, int off, int q) {
+    char* dst = lds + off + (w + 4 * q) * 1024;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(__builtin_amdgcn_make_buffer_rsrc((void*)c.p, (short)0, c.n, 0x00020000),
+                                             (__attribute__((address_space(3))) void*)dst, 16, (int)vo[q],
+                                             c.kt * (kBK * 2), 0, AUX);
+  };
+
+  // fragments: X fragment i = tile rows wm*128 + 16 i + l15; W fragment j (f = j / 4, type =
+  // (j / 2) % 2, jj = j % 2) = rows f*128 + type*64 + wn*32 + 8 (l15 / 4) + 4 jj + l15 % 4; k-half h
+  // reads chunk 4h + lane/16 of the row at its swizzled slot (swz depends on the lane only)
+  const int l15 = lane & 15, lq = lane >> 4;
+  const int xs = swz(l15), wr = 8 * (l15 >> 2) + (l15 & 3), ws = swz(wr);
+  const int xo0 = (wm * 128 + l15) * 128 + ((lq ^ xs) << 4), xo1 = (wm * 128 + l15) * 128 + (((4 + lq) ^ xs) << 4);
+  const int wo0 = (wn * 32 + wr) * 128 + ((lq ^ ws) << 4), wo1 = (wn * 32 + wr) * 128 + (((4 + lq) ^ ws) << 4);
+  auto rdx = [&](int off, int h, u16x8 (&xf)[8], int i) {
+    xf[i] = *reinterpret_cast<const u16x8*>(lds + off + (h ? xo1 : xo0) + i * 2048);
+  };
+  auto rdw = [&](int off, int h, u16x8 (&wf)[8], int j) {
+    const int r = (j >> 2) * 128 + ((j >> 1) & 1) * 64 + (j & 1) * 4;
+    wf[j] = *reinterpret_cast<const u16x8*>(lds + off + (h ? wo1 : wo0) + r * 128);
+  };
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
+  asm volatile("s_nop 4");
+  u16x8 xa[8], wa[8], xb[8], wb[8];
+  constexpr bool kCols = (OPT & 2) != 0;
+  // one MFMA row: 8 MFMAs sharing fragment `u` of the per-row set (X fragment i = u, or with
+  // kCols W fragment j = u), op(v) after MFMA v
+  auto row = [&](const u16x8 (&xf)[8], const u16x8 (&wf)[8], int u, auto op) {
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {
+      if constexpr (kCols) mfma_tied(acc[v][u], wf[u], xf[v]);
+      else mfma_tied(acc[u][v], wf[v], xf[u]);
+      __builtin_amdgcn_sched_barrier(0);
+      op(v);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  // fragment reads in row order: the set every row needs (W, or X with kCols) first
+  auto rd_all = [&](int ox, int ow, int h, u16x8 (&xf)[8], u16x8 (&wf)[8], int v) {
+    if constexpr (kCols) rdx(ox, h, xf, v);
+    else rdw(ow, h, wf, v);
+  };
+  auto rd_row = [&](int ox, int ow, int h, u16x8 (&xf)[8], u16x8 (&wf)[8], int u) {
+    if constexpr (kCols) rdw(ow, h, wf, u);
+    else rdx(ox, h, xf, u);
+  };
+  auto none = [](int) {};
+
+  // prologue. DEEP == 0: steps 0 and 1 of both operands (W, X per step). DEEP != 0: shallow 0,
+  // deep 0, shallow 1, deep 1, deep 2 -- the order the loop keeps (shallow g+2, deep g+3 per step),
+  // so "step g+1 landed" is always "all but the 16 / 24 youngest pieces"
+  if constexpr (DEEP == 0) {
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) dma(cw, woff(st, 0), q);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) dma(cx, xoff(st, 0), q);
+      advance(cx, true);
+      advance(cw, false);
+    }
+    vm_wait<16>();
+  } else {
+    Cur& cs = DEEP == 1 ? cw : cx;   // shallow operand
+    Cur& cd = DEEP == 1 ? cx : cw;   // deep operand
+    auto soff = [&](int st) { return DEEP == 1 ? woff(st & 1, st % 3) : xoff(st & 1, st % 3); };
+    auto doff = [&](int st) { return DEEP == 1 ? xoff(st & 1, st % 3) : woff(st & 1, st % 3); };
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) dma(cs, soff(st), q);
+      advance(cs, DEEP == 2);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) dma(cd, doff(st), q);
+      advance(cd, DEEP == 1);
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) dma(cd, doff(2), q);
+    advance(cd, DEEP == 1);
+    vm_wait<24>();
+  }
+  seg_barrier();
+#pragma unroll
+  for (int v = 0; v < 8; ++v) rd_all(xoff(0, 0), woff(0, 0), 0, xa, wa, v);
+#pragma unroll
+  for (int u = 0; u < 8; ++u) rd_row(xoff(0, 0), woff(0, 0), 0, xa, wa, u);
+
+  int g = 0, p3 = 0;   // flattened step counter (buffer parity) and g % 3
+  int m0 = 0, n0 = 0;
+  for (int r = 0; tile_rc(r, m0, n0); ++r) {
+    for (int t = 0; t < T; ++t, ++g) {
+      const int p2 = g & 1, n2 = p2 ^ 1, n3 = p3 == 2 ? 0 : p3 + 1;
+      const int ox = xoff(p2, p3), ow = woff(p2, p3);          // this step's buffers
+      const int nox = xoff(n2, n3), now_ = woff(n2, n3);       // step g + 1's
+      // ---- segment A: k-half 0 from A; k-half 1 reads (row 0, row 1); this step's buffers released
+      if constexpr (OPT & 1) __builtin_amdgcn_s_setprio(1);
+      asm volatile("s_waitcnt lgkmcnt(7)" ::: "memory");   // the 8 shared + row 0's fragment
+      __builtin_amdgcn_sched_barrier(0);
+      row(xa, wa, 0, [&](int v) { rd_all(ox, ow, 1, xb, wb, v); });
+      asm volatile("s_waitcnt lgkmcnt(14)" ::: "memory");  // + row 1's
+      __builtin_amdgcn_sched_barrier(0);
+      row(xa, wa, 1, [&](int v) { rd_row(ox, ow, 1, xb, wb, v); });
+      asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory");  // every k-half-0 read of the step
+      __builtin_amdgcn_sched_barrier(0);
+      row(xa, wa, 2, none);
+      row(xa, wa, 3, none);
+      row(xa, wa, 4, none);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if constexpr (OPT & 1) __builtin_amdgcn_s_setprio(0);
+      seg_barrier();   // every wave is done reading this step's buffers
+      if constexpr (OPT & 1) __builtin_amdgcn_s_setprio(1);
+      // DEEP == 0: W of step g+2 here, X of step g+2 in segment B (both into this step's buffers);
+      // DEEP != 0: the shallow operand of step g+2 here, the deep one of step g+3 in segment B
+#pragma unroll
+      for (int i = 5; i < 8; ++i)
+        row(xa, wa, i, [&](int j) {
+          const int m = (i - 5) * 8 + j;
+          if (m % 3 == 0) {
+            if constexpr (DEEP == 1) dma(cw, ow, m / 3);
+            else if constexpr (DEEP == 2) dma(cx, ox, m / 3);
+            else dma(cw, ow, m / 3);
+          }
+        });
+      // ---- segment B: k-half 1 from B; then step g + 1 lands
+#pragma unroll
+      for (int i = 0; i < 5; ++i)
+        row(xb, wb, i, [&](int j) {
+          const int m = i * 8 + j;
+          if (m % 5 == 0) {
+            if constexpr (DEEP == 1) dma(cx, ox, m / 5);
+            else if constexpr (DEEP == 2) dma(cw, ow, m / 5);
+            else dma(cx, ox, m / 5);
+          }
+        });
+      advance(cx, true);
+      advance(cw, false);
+      if constexpr (DEEP == 0) vm_wait<16>();   // this wave's pieces of step g + 1
+      else vm_wait<24>();
+      if constexpr (OPT & 1) __builtin_amdgcn_s_setprio(0);
+      seg_barrier();   // ... every wave's
+      if constexpr (OPT & 1) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 5; i < 8; ++i)
+        row(xb, wb, i, [&](int j) {
+          const int m = (i - 5) * 8 + j;   // 16 reads on 24 MFMAs: the shared 8, then the per-row 8
+          if (m % 3 != 2) {
+            const int k = m - m / 3;
+            if (k < 8) rd_all(nox, now_, 0, xa, wa, k);
+            else rd_row(nox, now_, 0, xa, wa, k - 8);
+          }
+        });
+      p3 = n3;
+    }
+    if constexpr (OPT & 1) __builtin_amdgcn_s_setprio(0);
+
+    // ---- epilogue of the tile (the next tile's step 0 is in registers / flight); lane holds
+    // features 8 lq .. 8 lq + 7 of each 32-feature block (fragments jj = 0, 1) of token l15
+    asm volatile("s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
+    f32x4 bv[2][2][2];   // bias of this lane's features per (f, type, jj): independent of the token block
+    if constexpr (EPI == kEpiBias) {
+#pragma unroll
+      for (int f = 0; f < 2; ++f)
+#pragma unroll
+        for (int ty = 0; ty < 2; ++ty) {
+          const int col = min(n0 + f * 128 + ty * 64 + wn * 32 + 8 * lq, N - 8);
+          const uint4 bb = *reinterpret_cast<const uint4*>(bias + col);
+          bv[f][ty][0] = f32x4{__uint_as_float(bb.x << 16), __uint_as_float(bb.x & 0xffff0000u),
+                               __uint_as_float(bb.y << 16), __uint_as_float(bb.y & 0xffff0000u)};
+          bv[f][ty][1] = f32x4{__uint_as_float(bb.z << 16), __uint_as_float(bb.z & 0xffff0000u),
+                               __uint_as_float(bb.w << 16), __uint_as_float(bb.w & 0xffff0000u)};
+        }
+    }
+    auto store8 = [&](bf16_t* yrow, int col, bool ok, f32x4 v0, f32x4 v1) {
+      if (ok)
+        *reinterpret_cast<uint4*>(yrow + col) =
+            make_uint4(pack_bf2(v0[0], v0[1]), pack_bf2(v0[2], v0[3]), pack_bf2(v1[0], v1[1]), pack_bf2(v1[2], v1[3]));
+    };
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int tok = m0 + wm * 128 + i * 16 + l15;
+      bf16_t* yrow = Y + (int64_t)tok * ldy;
+#pragma unroll
+      for (int f = 0; f < 2; ++f) {
+        if constexpr (EPI == kEpiSilu) {
+          f32x4 o[2];
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) {
+            const f32x4 gt = acc[i][f * 4 + jj], up = acc[i][f * 4 + 2 + jj];
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+              const float gg = bf2f(f2bf(gt[rr]));
+              const float uu = bf2f(f2bf(up[rr]));
+              const float sg = bf2f(f2bf(gg / (1.f + __expf(-gg))));
+              o[jj][rr] = sg * uu;
+            }
+          }
+          const int col = (n0 >> 1) + f * 64 + wn * 32 + 8 * lq;
+          store8(yrow, col, tok < M && 2 * col < N, o[0], o[1]);
+        } else {
+#pragma unroll
+          for (int ty = 0; ty < 2; ++ty) {
+            f32x4 v0 = acc[i][f * 4 + ty * 2], v1 = acc[i][f * 4 + ty * 2 + 1];
+            if constexpr (EPI == kEpiBias) {
+              v0 += bv[f][ty][0];
+              v1 += bv[f][ty][1];
+            }
+            const int col = n0 + f * 128 + ty * 64 + wn * 32 + 8 * lq;
+            store8(yrow, col, tok < M && col < N, v0, v1);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        asm volatile("" : "+a"(acc[i][j]));
+      }
+    asm volatile("s_nop 4");
+  }
+  vm_wait<0>();   // the trailing re-loads land before the workgroup's LDS is released
+}
+
 // y[m, f] = SwiGLU of the split-K sums of the interleaved gate|up slabs (64-feature
 // blocks): g = bf16(sum_s P[s][m][128 b + j]), u = bf16(sum_s P[s][m][128 b + 64 + j]),
 // y = bf16(bf16(silu(g)) * u) — the numerics of the fused epilogue. 4 features per thread.
@@ -552,6 +893,19 @@ __global__ void splitk_silu_reduce_kernel(const float* __restrict__ P, bf16_t* _
   *reinterpret_cast<uint2*>(Y + (int64_t)m * ldy + f) = pack4(o);
 }
 
+// compute units of the current device (persistent grids), cached per device
+static int device_cus() {
+  static int cus[16] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) dev = 0;
+  if (cus[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cus[dev] = n;
+  }
+  return cus[dev];
+}
+
 int gemm_tile(const bf16_t* X, const bf16_t* W, bf16_t* Y, const bf16_t* bias, int M, int N, int K, int ldy,
               bool silu_gu, int variant, int S, float* P, hipStream_t stream) {
   if (M < 1 || N < 16 || N % 16 != 0 || K < kBK || K % kBK != 0) return -1;
@@ -574,7 +928,19 @@ int gemm_tile(const bf16_t* X, const bf16_t* W, bf16_t* Y, const bf16_t* bias, i
     return splitk_reduce(P, Y, (int64_t)M * N, S, stream);
   }
   const bool off32 = (int64_t)M * K * 2 < (1LL << 32) && (int64_t)N * K * 2 < (1LL << 32);
-  if ((variant == 0 || variant == 1) && off32) {   // 4-wave, two 64 KiB buffers, four phases per K-tile
+  const bool st16 = ldy % 8 == 0 && reinterpret_cast<uintptr_t>(Y) % 16 == 0;   // p5's 16-B stores
+  if (variant == 5 && K >= 2 * kBK && st16) {   // persistent, one workgroup per CU
+    const int grid = min(nwg, device_cus());
+    if (silu_gu) gemm_tile256_p5_kernel<kEpiSilu><<<grid, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+    else if (bias) gemm_tile256_p5_kernel<kEpiBias><<<grid, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+    else gemm_tile256_p5_kernel<kEpiStore><<<grid, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+  } else if (variant >= 6 && variant <= 9 && K >= 2 * kBK && !silu_gu && !bias && st16) {   // p5 A/B arms (timing)
+    const int grid = min(nwg, device_cus());
+    if (variant == 6) gemm_tile256_p5_kernel<kEpiStore, 0, 2><<<grid, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+    else if (variant == 7) gemm_tile256_p5_kernel<kEpiStore, 1><<<grid, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+    else if (variant == 8) gemm_tile256_p5_kernel<kEpiStore, 2><<<grid, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+    else gemm_tile256_p5_kernel<kEpiStore, 1, 2><<<grid, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+  } else if ((variant == 0 || variant == 1) && off32) {   // 4-wave, two 64 KiB buffers, four phases per K-tile
     if (silu_gu) gemm_tile256_h4_kernel<kEpiSilu><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
     else if (bias) gemm_tile256_h4_kernel<kEpiBias><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
     else gemm_tile256_h4_kernel<kEpiStore><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);

@@ -10,7 +10,8 @@ from operator_amd.ops import reference as ref
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-VARIANTS = (0, 1, 2, 3, 4)   # gemm_tile schedules: auto (default = 1), 4-wave two-buffer four-phase, 8-wave 2-segment, 8-wave 4-segment, 4-wave with W-fragment MFMA groups
+VARIANTS = (0, 1, 2, 3, 4, 5)   # gemm_tile schedules: auto, 4-wave two-buffer four-phase (h4), 8-wave 2-segment, 8-wave 4-segment,
+# 4-wave with W-fragment MFMA groups, persistent one-workgroup-per-CU p5 (variant 5 needs K >= 128)
 
 
 def _rand(*shape, scale=1.0):
@@ -96,6 +97,35 @@ def test_gemm_tile_split_k(S):
     ys = torch.empty(M, 256, dtype=torch.bfloat16, device=DEV)
     ops.kernels().gemm_tile(x, wgu, ys, None, True, 0, S, P)
     _close(ys, ref.silu_mul(torch.cat([gg, uu], 1), None), 3e-2)
+
+
+@pytest.mark.parametrize("M,N,K", [(8192 + 77, 2304, 192), (4096, 4096 + 16, 128), (2048, 16384, 320), (300, 1024, 4096)])
+@pytest.mark.parametrize("epi", ["store", "bias", "silu"])
+def test_gemm_tile_persistent_rounds(M, N, K, epi):
+    """Persistent p5 (variant 5): blocks walk several tiles (tiles > CUs), odd K-step
+    counts (the LDS buffer parity carries across tiles), M / N tails, grids below the CU
+    count -- every epilogue against the fp32 reference."""
+    torch.manual_seed(M + N + K)
+    x = _rand(M, K)
+    if epi == "silu":
+        if N % 128:
+            pytest.skip("the interleaved gate|up weight needs N % 128 == 0")
+        g, u = _rand(N // 2, K, scale=0.05), _rand(N // 2, K, scale=0.05)
+        w = ops.interleave_gate_up(g, u)
+        gg = (x.float() @ g.float().t()).to(torch.bfloat16)
+        uu = (x.float() @ u.float().t()).to(torch.bfloat16)
+        r = ref.silu_mul(torch.cat([gg, uu], 1), None)
+        y = torch.empty(M, N // 2, dtype=torch.bfloat16, device=DEV)
+        ops.kernels().gemm_tile(x, w, y, None, True, 5)
+        _close(y, r, 3e-2)
+        return
+    w = _rand(N, K, scale=0.05)
+    b = _rand(N, scale=0.5) if epi == "bias" else None
+    r = x.float() @ w.float().t() + (b.float() if b is not None else 0.0)
+    for v in ((5, 6, 7, 8, 9) if b is None else (5,)):   # 6-9: p5 schedule arms (store epilogue)
+        y = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        ops.kernels().gemm_tile(x, w, y, b, False, v)
+        _close(y, r)
 
 
 def test_gemm_tile_strided_output():
