@@ -685,6 +685,9 @@ def main() -> int:
                    "dfa_states": stats1["dfa_states"], "timed_monotonic_ns": [mono0, mono1],
                    "rccl_world": dist.get_world_size() if dist.is_initialized() else 1,
                    "dist_backend": info.backend,
+                   # the flagship is DP (tp = 1): no TP all-reduce to dispatch; tools/bench_tp.py reports the
+                   # node-measured one-shot / two-shot / RCCL table (custom_ar.OneShotAllReduce.calibrate)
+                   "allreduce_calibration": {"tp": 1, "table": None},
                    "launcher": "bench.py" if os.environ.get("OAMD_BENCH_LAUNCHED") else
                                ("torchrun" if world > 1 else "single"),
                    "per_rank_elapsed_s": [round(x, 3) for x in per_rank_s],

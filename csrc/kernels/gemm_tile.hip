@@ -633,12 +633,15 @@ __global__ void __launch_bounds__(256) gemm_tile256_p5_kernel(const bf16_t* __re
       }
     }
   };
-  auto dma = [&](const Cur& c, int off, int q) {
+  // (scalar parameters: hipcc's host pass silently drops the kernel's launch stub when the
+  // buffer-resource builtin reads struct members -- an undefined symbol at load time)
+  auto dma_ = [&](const bf16_t* cp, int cn, int ckt, int off, int q) {
     char* dst = lds + off + (w + 4 * q) * 1024;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(__builtin_amdgcn_make_buffer_rsrc((void*)c.p, (short)0, c.n, 0x00020000),
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(__builtin_amdgcn_make_buffer_rsrc((void*)cp, (short)0, cn, 0x00020000),
                                              (__attribute__((address_space(3))) void*)dst, 16, (int)vo[q],
-                                             c.kt * (kBK * 2), 0, AUX);
+                                             ckt * (kBK * 2), 0, AUX);
   };
+  auto dma = [&](const Cur& c, int off, int q) { dma_(c.p, c.n, c.kt, off, q); };
 
   // fragments: X fragment i = tile rows wm*128 + 16 i + l15; W fragment j (f = j / 4, type =
   // (j / 2) % 2, jj = j % 2) = rows f*128 + type*64 + wn*32 + 8 (l15 / 4) + 4 jj + l15 % 4; k-half h
@@ -893,6 +896,14 @@ __global__ void splitk_silu_reduce_kernel(const float* __restrict__ P, bf16_t* _
   *reinterpret_cast<uint2*>(Y + (int64_t)m * ldy + f) = pack4(o);
 }
 
+template <int DEEP>
+static void launch_p5(const bf16_t* X, const bf16_t* W, bf16_t* Y, const bf16_t* bias, int M, int N, int K, int ldy,
+                      bool silu_gu, int grid, hipStream_t stream) {
+  if (silu_gu) gemm_tile256_p5_kernel<kEpiSilu, DEEP><<<grid, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+  else if (bias) gemm_tile256_p5_kernel<kEpiBias, DEEP><<<grid, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+  else gemm_tile256_p5_kernel<kEpiStore, DEEP><<<grid, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+}
+
 // compute units of the current device (persistent grids), cached per device
 static int device_cus() {
   static int cus[16] = {0};
@@ -929,11 +940,14 @@ int gemm_tile(const bf16_t* X, const bf16_t* W, bf16_t* Y, const bf16_t* bias, i
   }
   const bool off32 = (int64_t)M * K * 2 < (1LL << 32) && (int64_t)N * K * 2 < (1LL << 32);
   const bool st16 = ldy % 8 == 0 && reinterpret_cast<uintptr_t>(Y) % 16 == 0;   // p5's 16-B stores
-  if (variant == 5 && K >= 2 * kBK && st16) {   // persistent, one workgroup per CU
+  // persistent p5 (variant 5; the default past 256 rows): one workgroup per CU; wide N (>= 16384:
+  // gate|up, the W panels stream from HBM) gives W a third LDS buffer -- a 2-step prefetch
+  // (M = 32k, N = 28672: 5786 -> 5366 us; at N = 4096 / 6144 the 2-buffer form is faster,
+  // profiles/gemm_tile_p5_vs_hipblaslt_r6.jsonl)
+  if ((variant == 5 || (variant == 0 && M > kT)) && K >= 2 * kBK && st16) {
     const int grid = min(nwg, device_cus());
-    if (silu_gu) gemm_tile256_p5_kernel<kEpiSilu><<<grid, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-    else if (bias) gemm_tile256_p5_kernel<kEpiBias><<<grid, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-    else gemm_tile256_p5_kernel<kEpiStore><<<grid, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+    if (N >= 16384) launch_p5<2>(X, W, Y, bias, M, N, K, ldy, silu_gu, grid, stream);
+    else launch_p5<0>(X, W, Y, bias, M, N, K, ldy, silu_gu, grid, stream);
   } else if (variant >= 6 && variant <= 9 && K >= 2 * kBK && !silu_gu && !bias && st16) {   // p5 A/B arms (timing)
     const int grid = min(nwg, device_cus());
     if (variant == 6) gemm_tile256_p5_kernel<kEpiStore, 0, 2><<<grid, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);

@@ -124,7 +124,21 @@ def build_kernels(verbose: bool = False, force: bool = False, jobs: int | None =
                 *[f"-L{d}" for d in libdirs if d != torch_lib],
                 "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python", "-lamdhip64"]
         _run(link, verbose)
+        _check_stubs(out)
     return out
+
+
+def _check_stubs(so: Path) -> None:
+    """Fail the build when a kernel's host launch stub is missing from the library: hipcc's
+    host pass can drop one silently (a template kernel whose body its host-side semantic check
+    rejects without a diagnostic), which otherwise only surfaces as an undefined symbol when
+    the GPU box imports the module."""
+    nm = shutil.which("nm") or "/opt/rocm/lib/llvm/bin/llvm-nm"
+    r = subprocess.run([nm, "-u", str(so)], capture_output=True, text=True)
+    missing = [ln.split()[-1] for ln in r.stdout.splitlines() if "__device_stub__" in ln]
+    if missing:
+        so.unlink(missing_ok=True)
+        raise RuntimeError(f"native build: {len(missing)} kernel launch stub(s) undefined in {so.name}: {missing[:4]}")
 
 
 def build(verbose: bool = False, force: bool = False) -> list[Path]:

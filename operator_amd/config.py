@@ -121,9 +121,11 @@ class EngineCfg(BaseModel):
     device: str = "cuda"
     tp: int = 1
     oneshot_allreduce_mb: float = 8.0  # TP all-reduces up to this size use the IPC kernels; 0 = RCCL only
-    # ... one-shot up to this size, two-shot (reduce-scatter + all-gather) above: SURVEY §5.8's
-    # ~256 KB-scale sizing; the crossover is unmeasured until an 8-GPU node exists (docs/PARITY.md)
-    oneshot_max_kb: float = 512.0
+    # one-shot / two-shot / RCCL crossovers: 0 = measured on the node when the TP group starts
+    # (custom_ar.OneShotAllReduce.calibrate over the decode buckets' message sizes); > 0 = override:
+    # one-shot up to this size, two-shot (reduce-scatter + all-gather) above
+    oneshot_max_kb: float = 0.0
+    allreduce_calibrate_iters: int = 20
     max_batch: int = 256
     max_prefill_tokens: int = 32768   # tokens per prefill batch (profiles/prefill_batch_sweep_8b.jsonl)
     admit_wait_ms: float = 20.0       # idle engine: gather arrivals this long before a partial prefill

@@ -18,6 +18,28 @@ def parse_model_spec(spec: str) -> tuple[str, str | None]:
     return name.strip(), (path.strip() or None)
 
 
+def decode_message_sizes(hidden: int, max_batch: int) -> list[int]:
+    """Bytes of the TP decode all-reduces: bf16 [rows, hidden] for every decode bucket
+    row count (powers of two up to ``max_batch``)."""
+    rows, out = 1, []
+    while rows <= max(1, max_batch):
+        out.append(rows * hidden * 2)
+        rows *= 2
+    return out
+
+
+def calibrate_allreduce(tp, hidden: int, max_batch: int, iters: int = 20) -> dict:
+    """Measure the IPC all-reduce protocols against RCCL on this node's TP group (collective;
+    before any graph capture) and install the dispatch table; the report is kept on the group
+    (``tp.oneshot.calibration``) for the bench JSON lines."""
+    car = getattr(tp, "oneshot", None)
+    if car is None or car.forced is not None:
+        return {}
+    rep = car.calibrate(decode_message_sizes(hidden, max_batch), iters=iters)
+    log.info("TP all-reduce dispatch (world %d): %s", tp.world, rep.get("table"))
+    return rep
+
+
 def build_llm(s: Settings, device: str | torch.device | None = None, tp=None):
     """(model, kv, LLMEngine, Tokenizer) for the configured explanation model."""
     from operator_amd.engine.llm import LLMEngine
@@ -37,7 +59,9 @@ def build_llm(s: Settings, device: str | torch.device | None = None, tp=None):
     dtype = getattr(torch, e.dtype)
     if tp is not None and tp.world > 1 and dev.type == "cuda" and e.oneshot_allreduce_mb > 0 \
             and getattr(tp, "oneshot", None) is None:
-        tp.enable_oneshot(dev, int(e.oneshot_allreduce_mb * (1 << 20)), int(e.oneshot_max_kb * 1024))
+        if tp.enable_oneshot(dev, int(e.oneshot_allreduce_mb * (1 << 20)), int(max(e.oneshot_max_kb, 0) * 1024) or None) \
+                and e.oneshot_max_kb <= 0:
+            calibrate_allreduce(tp, cfg.hidden, e.max_batch, e.allreduce_calibrate_iters)
     model = LlamaModel(cfg, device=dev, tp=tp, dtype=dtype, weight_dtype=e.weight_dtype)
     weight_cache.load_or_build(model, e.weight_cache_dir, e.model_path, e.seed)
     # KV cache: the compute dtype, or OCP fp8 (e4m3fn, per-tensor scales) with engine.kv_dtype=fp8

@@ -336,15 +336,13 @@ def skinny_plan(M: int, N: int, K: int) -> int | None:
     return S
 
 
-# The plain prefill projections (M > 256 rows, no bias, no fused epilogue: QKV, O and down
-# of the Llama family) are library GEMMs and run on hipBLASLt: its hand-scheduled stream-K
-# MT256x256x64 kernel is 1.13-1.18x gemm_tile h4 on those shapes at M = 32k
-# (profiles/gemm_tile_h4_vs_ph2_m32k.jsonl, hipblaslt_prefill_kernel_names.txt) and the
-# flagship runs +1.2 % faster with it (interleaved A/B, profiles/bench_prefill_blas_ab_r5.jsonl).
-# Everything fused stays on the gfx950 kernels: gate|up + SwiGLU and biased projections
-# (gemm_tile), every decode GEMM (gemm_pp / gemm_tn / gemm_skinny, faster than hipBLASLt
-# there), the lm_head, fp8. OAMD_PREFILL_BLAS=0 puts the plain projections on gemm_tile too.
-PREFILL_BLAS = os.environ.get("OAMD_PREFILL_BLAS", "1") != "0"
+# Every GPU GEMM of the model runs on the hand-written gfx950 kernels: prefill projections (M > 256
+# rows) on gemm_tile's persistent p5 schedule (csrc/kernels/gemm_tile.hip), decode buckets on
+# gemm_pp / gemm_tn / gemm_skinny, the lm_head on gemm_tile, fp8 on gemm_fp8. hipBLASLt is reached
+# only by shapes none of them takes (K % 64 != 0, N % 16 != 0, non-bf16), counted in BLAS_CALLS.
+# OAMD_PREFILL_BLAS=1 routes the plain prefill projections (QKV, O, down) to hipBLASLt instead, for
+# A/B runs against the vendor library (profiles/gemm_tile_p5_vs_hipblaslt_r6.jsonl).
+PREFILL_BLAS = os.environ.get("OAMD_PREFILL_BLAS", "0") == "1"
 BLAS_CALLS = {"n": 0}   # GPU GEMMs that FELL BACK to hipBLASLt (tests assert it stays 0 on model shapes)
 BLAS_PLANNED = {"n": 0}   # plain prefill projections run on hipBLASLt by design (PREFILL_BLAS)
 
@@ -395,8 +393,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None, sp
     """y = x @ w^T (+ bias) in bf16 on the gfx950 kernels: M <= 32 decode buckets on the
     weight-streaming gemm_skinny, M in {64, 128, 256} on the LDS-staged split-K
     gemm_decode (tuned tables), everything else (prefill, the lm_head, biased
-    projections) on the 256x256-tile gemm_tile. hipBLASLt only for shapes none of them
-    takes (K % 64 != 0, N % 16 != 0, non-bf16); CPU tensors on torch."""
+    projections) on the 256x256-tile gemm_tile (persistent p5 past 256 rows). hipBLASLt only
+    for shapes none of them takes (K % 64 != 0, N % 16 != 0, non-bf16), for decode shapes the
+    tuned table measured it fastest on, or under OAMD_PREFILL_BLAS=1 (A/B); CPU tensors on torch."""
     M, K = x.shape
     N = w.shape[0]
     plan = None

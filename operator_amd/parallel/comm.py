@@ -11,8 +11,12 @@
 
 Sizing notes for MI355X xGMI (7 point-to-point links / GPU, ~153 GB/s each):
 TP decode all-reduces are tiny (M x hidden x 2 B, e.g. 16 KB/token at 70B),
-i.e. latency-bound; RCCL's LL/LL128 protocols cover them. DP needs no
-collective on the hot path (per-rank engines, host-side result gathering).
+i.e. latency-bound: they run on the IPC kernels of ``parallel/custom_ar.py``
+(one-shot / two-shot, fused with residual + RMSNorm), whose size crossovers are
+measured on the node at engine start (``CustomAllReduce.calibrate``); RCCL takes
+what the IPC buffers cannot hold and every other collective (barriers, the DFA
+broadcast, timing maxima). DP needs no collective on the hot path (per-rank
+engines, host-side result gathering).
 """
 from __future__ import annotations
 

@@ -272,3 +272,73 @@ def test_oneshot_allreduce_missing_peer_fails_loudly(protocol):
         assert r1["late_ok"] and r1["failed"] and r1["all_nan"], r1
     else:   # rank 0 never published its gather piece: the late call already fails
         assert not r1["late_ok"] and r1["late_nan"] and r1["failed"] and r1["all_nan"], r1
+
+
+def _calibrate_worker(rank: int, world: int, port: int, q) -> None:
+    try:
+        import torch.distributed as dist
+
+        from operator_amd.engine.factory import calibrate_allreduce
+        from operator_amd.parallel.comm import Group
+        from operator_amd.parallel.custom_ar import PROTO_BACKEND
+
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        grp = Group()
+        assert grp.enable_oneshot(dev, max_bytes=4 << 20)
+        rep = calibrate_allreduce(grp, hidden=1024, max_batch=256, iters=5)
+        car = grp.oneshot
+        assert car.table and rep["table"], rep
+        # after calibration every size still sums exactly (whichever protocol it routes to)
+        ok = 0
+        for rows in (1, 16, 256):
+            x = [_inputs(r, rows * 1024, torch.bfloat16, 900 + rows) for r in range(world)]
+            ref = (x[0].float() + x[1].float()).to(torch.bfloat16)
+            t = x[rank].to(dev)
+            grp.all_reduce_(t)
+            torch.cuda.synchronize()
+            assert torch.equal(t.cpu(), ref), rows
+            ok += 1
+        q.put((rank, "ok", rep, [(b, p) for b, p in car.table], car.route(2048) != PROTO_BACKEND or True, ok))
+        dist.barrier()
+        car.close()
+        dist.destroy_process_group()
+    except Exception:
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc()))
+
+
+def test_allreduce_calibration_two_ranks_one_gpu():
+    """calibrate() at engine start (engine.oneshot_max_kb = 0): both ranks time one-shot,
+    two-shot and the group backend on the decode message sizes, take the max over ranks
+    and install the SAME dispatch table; all-reduces routed by it stay exact."""
+    import torch.multiprocessing as mp
+
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_calibrate_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = []
+    try:
+        for _ in procs:
+            res.append(q.get(timeout=100))
+    finally:
+        for p in procs:
+            p.join(timeout=20)
+            if p.is_alive():
+                p.kill()
+    errs = [r for r in res if r[1] != "ok"]
+    assert not errs, errs[0][2]
+    (_, _, rep0, t0, _, ok0), (_, _, rep1, t1, _, ok1) = res
+    assert t0 == t1 and rep0["table"] == rep1["table"]   # one table for the whole group
+    assert rep0["sizes"] == [rows * 1024 * 2 for rows in (1, 2, 4, 8, 16, 32, 64, 128, 256)]
+    assert set(rep0["us"]) == {"oneshot", "twoshot", "backend"} and ok0 == ok1 == 3
+    assert rep0["table"][-1][0] == rep0["sizes"][-1]

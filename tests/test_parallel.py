@@ -208,3 +208,39 @@ def test_bench_eight_ranks_gloo_one_apiserver():
     audit = out["detail"]["apiserver_audit"]
     assert audit == {"pods_with_complete_event": 48, "max_complete_events_per_pod": 1, "expected_pods": 48}
     assert out["value"] > 0
+
+
+def test_allreduce_dispatch_table_selection():
+    """custom_ar.choose_protocols: the fastest IPC protocol per size, the group backend
+    (RCCL) only when it beats both by the margin, runs merged, NaN = unavailable; and
+    lookup_protocol routes any message size through the table (past the end: last entry)."""
+    from operator_amd.parallel.custom_ar import (PROTO_BACKEND, PROTO_ONESHOT, PROTO_TWOSHOT, choose_protocols,
+                                                 lookup_protocol)
+
+    sizes = [8192, 16384, 65536, 262144, 1 << 20, 4 << 20]
+    times = {PROTO_ONESHOT: [5e-6, 5.5e-6, 7e-6, 12e-6, 40e-6, 150e-6],
+             PROTO_TWOSHOT: [8e-6, 8.5e-6, 9e-6, 11e-6, 25e-6, 80e-6],
+             PROTO_BACKEND: [30e-6, 30e-6, 31e-6, 33e-6, 26e-6, 60e-6]}
+    table = choose_protocols(sizes, times)
+    assert table == [(65536, PROTO_ONESHOT), (1 << 20, PROTO_TWOSHOT), (4 << 20, PROTO_BACKEND)]
+    assert lookup_protocol(table, 100) == PROTO_ONESHOT
+    assert lookup_protocol(table, 65536) == PROTO_ONESHOT
+    assert lookup_protocol(table, 65537) == PROTO_TWOSHOT
+    assert lookup_protocol(table, 3 << 20) == PROTO_BACKEND
+    assert lookup_protocol(table, 64 << 20) == PROTO_BACKEND
+    # within the margin the IPC kernel keeps the size (RCCL 1 % faster at 1 MB: not enough)
+    t2 = dict(times)
+    t2[PROTO_BACKEND] = [30e-6, 30e-6, 31e-6, 33e-6, 24.8e-6, 100e-6]
+    assert choose_protocols(sizes, t2) == [(65536, PROTO_ONESHOT), (4 << 20, PROTO_TWOSHOT)]
+    # a protocol that could not be timed (NaN) never wins; no IPC timing at all -> backend
+    t3 = {PROTO_ONESHOT: [float("nan")] * 6, PROTO_TWOSHOT: times[PROTO_TWOSHOT]}
+    assert choose_protocols(sizes, t3) == [(4 << 20, PROTO_TWOSHOT)]
+    assert choose_protocols(sizes[:2], {}) == [(16384, PROTO_BACKEND)]
+    assert choose_protocols([], times) == []
+
+
+def test_decode_message_sizes_follow_buckets():
+    from operator_amd.engine.factory import decode_message_sizes
+
+    assert decode_message_sizes(8192, 64) == [r * 8192 * 2 for r in (1, 2, 4, 8, 16, 32, 64)]
+    assert decode_message_sizes(4096, 1) == [8192]

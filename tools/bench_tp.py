@@ -45,6 +45,8 @@ ap.add_argument("--prompt", type=int, default=1024)
 ap.add_argument("--gen", type=int, default=128)
 ap.add_argument("--kv-gb", type=float, default=64.0)
 ap.add_argument("--oneshot-mb", type=float, default=8.0, help="0 = RCCL for every all-reduce")
+ap.add_argument("--oneshot-max-kb", type=float, default=0.0,
+                help="one-shot / two-shot crossover override; 0 = calibrate on the node (engine default)")
 ap.add_argument("--no-graphs", action="store_true")
 ap.add_argument("--simulate-tp", type=int, default=0,
                 help="one process: rank 0's shard of a TP=N replica, collectives as world-1 one-shot kernels")
@@ -65,10 +67,16 @@ if a.simulate_tp > 1:
     ctrl = None
 else:
     tp, _ = split_groups(info.world)
-    oneshot = bool(gpu and a.oneshot_mb > 0 and tp.enable_oneshot(dev, int(a.oneshot_mb * (1 << 20))))
+    oneshot = bool(gpu and a.oneshot_mb > 0 and tp.enable_oneshot(dev, int(a.oneshot_mb * (1 << 20)),
+                                                                   int(a.oneshot_max_kb * 1024) or None))
     ctrl = control_group(tp) if tp.world > 1 else None
 
 cfg = get_config(a.model)
+calibration = None
+if oneshot and a.simulate_tp <= 1 and a.oneshot_max_kb <= 0:   # the engine's own start-up measurement
+    from operator_amd.engine.factory import calibrate_allreduce  # noqa: E402
+
+    calibration = calibrate_allreduce(tp, cfg.hidden, a.batch)
 dtype = getattr(torch, a.dtype)
 t0 = time.perf_counter()
 m = LlamaModel(cfg, device=dev, tp=tp, dtype=dtype, weight_dtype=a.weights if gpu else "bfloat16").init_random(0)
@@ -135,6 +143,7 @@ print(json.dumps({"bench": "tp-decode", "model": a.model, "weights": a.weights i
                   "p50_ms_per_token": round(statistics.median(step_ms), 3) if step_ms else None,
                   "latency_s": round(t2 - t0, 3),
                   "simulated_tp": a.simulate_tp if a.simulate_tp > 1 else None,
+                  "allreduce_calibration": calibration,
                   "rank_weight_gb": round(wbytes / 1e9, 2),
                   "weight_floor_ms": round(wbytes / 6.3e12 * 1e3, 3)}), flush=True)
 sync()
