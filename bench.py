@@ -80,6 +80,10 @@ def parse_args():
                     help="operator.sink_concurrency: analyses writing results at once (0 = unbounded); a bound "
                          "keeps a finished wave's 256 result writers from starving the next wave's ramp "
                          "(GPU gap before its first prefill 230-440 -> 140-170 ms, profiles/wave_timeline_sinks_8b.jsonl)")
+    ap.add_argument("--ranks-per-apiserver", type=int, default=4,
+                    help="rest: ranks sharing one API server process (ranks g*R .. g*R+R-1 = the operator shards "
+                         "of server g). One Python API server costs ~2.8 ms of CPU per analysis (~357/s), below "
+                         "2x the ~260/s an 8-GPU node asks of it: 4 ranks per server keeps >= 2x headroom")
     ap.add_argument("--apiserver", choices=["auto", "inproc", "rest"], default="auto",
                     help="rest: ONE API server process (the REST FakeKube, kube/fake_server.py) that every rank's "
                          "operator shard talks to over HTTP, each rank owning the pods that hash to it "
@@ -186,13 +190,18 @@ def main() -> int:
     rest = a.mode == "pipeline" and (a.apiserver == "rest" or (a.apiserver == "auto" and world_env > 1))
     if rest and a.shards > 1:
         raise SystemExit("--apiserver rest runs one operator shard per rank (no --shards)")
-    apisrv = apiurl = None
+    apisrvs: list = []
+    apiurls: list = []
+    rpa = max(1, a.ranks_per_apiserver)
     if rest and int(os.environ.get("RANK", "0")) == 0:
-        # the one API server of the node: its own process, started before this rank
-        # touches the GPU; the URL reaches the other ranks over the process group
+        # the node's API servers (one per `rpa` ranks): their own processes, started before this
+        # rank touches the GPU; the URLs reach the other ranks over the process group
         from operator_amd.kube.fake_server import spawn as spawn_apiserver
 
-        apisrv, apiurl = spawn_apiserver(f"/tmp/oamd-bench-apiserver-{os.getpid()}.url")
+        for g in range(-(-world_env // rpa)):
+            p_, u_ = spawn_apiserver(f"/tmp/oamd-bench-apiserver-{os.getpid()}-{g}.url")
+            apisrvs.append(p_)
+            apiurls.append(u_)
     kids = spawn_shards(a) if (a.shards > 1 and not child) else []
     shard = a.shard_index or 0
     a.batch = max(1, a.batch // a.shards)   # this shard's wave (--batch is per GPU, over all shards)
@@ -278,12 +287,20 @@ def main() -> int:
     from operator_amd.utils.tracing import mark, trace_range
 
     s = settings(dev, a.max_batch, int(os.environ.get("OAMD_BENCH_WORLD", world)) if child else world)
-    if rest:   # rank r = operator shard r of `world` (run --shard-per-gpu), all on one API server
-        s.operator.shard_count, s.operator.shard_index = world, rank
+    # rest: rank r talks to API server g = r // rpa and is operator shard r - g*rpa of that server's
+    # group (run --shard-per-gpu against each server); a group's first rank creates its cluster state
+    grp, grp0, grp_n = 0, 0, 1
+    apiurl = None
+    if rest:
+        grp = rank // rpa
+        grp0 = grp * rpa
+        grp_n = min(rpa, world - grp0)
+        s.operator.shard_count, s.operator.shard_index = grp_n, rank - grp0
         if world > 1:
-            box = [apiurl]
+            box = [apiurls]
             dist.broadcast_object_list(box, src=0)
-            apiurl = box[0]
+            apiurls = box[0]
+        apiurl = apiurls[grp]
 
     def note(msg: str) -> None:   # stage progress on stderr (the JSON line stays alone on stdout)
         tag = f"rank {rank}" + (f" shard {shard}" if a.shards > 1 else "")
@@ -412,7 +429,7 @@ def main() -> int:
                 return self.inner.ready()
 
         op = Operator(fk, s, match_service=matcher, explain_service=CountingExplainer(explainer))
-        if not rest or rank == 0:   # cluster state, created once
+        if not rest or rank == grp0:   # cluster state, created once per API server
             fk.create(AIPROVIDERS, {"metadata": {"name": "local-llm", "namespace": "default"},
                                     "spec": {"providerId": "local", "modelId": a.model, "maxTokens": a.max_tokens,
                                              "temperature": 0.3, "cachingEnabled": False,
@@ -449,10 +466,10 @@ def main() -> int:
         def shard_name(base: str) -> str:
             """``base`` or the first ``base-xJ`` whose ns/name hash puts it in this rank's
             shard (rest: every rank's pods are the failures its own operator shard owns)."""
-            if not rest or world <= 1:
+            if not rest or grp_n <= 1:
                 return base
             j, name = 0, base
-            while not in_shard({"metadata": {"namespace": "default", "name": name}}, rank, world):
+            while not in_shard({"metadata": {"namespace": "default", "name": name}}, rank - grp0, grp_n):
                 j += 1
                 name = f"{base}-x{j}"
             return name
@@ -612,7 +629,7 @@ def main() -> int:
             for o, n in d.items():
                 job_outcomes[o] = job_outcomes.get(o, 0) + n
     audit = None
-    if a.mode == "pipeline" and (rank == 0 or not rest):
+    if a.mode == "pipeline" and (rank == grp0 or not rest):
         per_pod: dict[str, int] = {}
         for ev in fk.list(EVENTS, "default"):
             reg = ev.get("regarding") or {}
@@ -621,7 +638,14 @@ def main() -> int:
                 per_pod[reg["name"]] = per_pod.get(reg["name"], 0) + 1
         counts = list(per_pod.values())
         audit = {"pods_with_complete_event": len(per_pod), "max_complete_events_per_pod": max(counts, default=0),
-                 "expected_pods": a.batch * waves * (world if rest else 1)}   # inproc: this process's shard
+                 "expected_pods": a.batch * waves * (grp_n if rest else 1)}   # inproc: this process's shard
+    if rest and world > 1:   # every API server's own record, merged (group leaders audited theirs)
+        alla: list = [None] * world
+        dist.all_gather_object(alla, audit)
+        parts = [x for x in alla if x is not None]
+        audit = {"pods_with_complete_event": sum(x["pods_with_complete_event"] for x in parts),
+                 "max_complete_events_per_pod": max(x["max_complete_events_per_pod"] for x in parts),
+                 "expected_pods": sum(x["expected_pods"] for x in parts), "apiservers": len(parts)}
 
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev if info.backend == "nccl" else "cpu")
     p50_local = statistics.median(lat) if lat else float("nan")
@@ -656,7 +680,8 @@ def main() -> int:
                    "operator_shards_per_gpu": a.shards,
                    "kv_cache_dtype": "fp8_e4m3fn" if a.kv_dtype == "fp8" else "bf16",
                    "kv_page_tokens": a.page_size, "shared_prompt_prefix": not a.no_prefix_sharing,
-                   "apiserver": ("one REST API server process, rank r = operator shard r (run --shard-per-gpu)"
+                   "apiserver": (f"{-(-world // rpa)} REST API server process(es), {rpa} ranks each: rank r = "
+                                 f"operator shard r % {rpa} of server r // {rpa} (run --shard-per-gpu)"
                                  if rest else "in-process FakeKube per rank"),
                    "waves": "serial" if (a.serial_waves or a.mode != "pipeline") else "pipelined",
                    "wave_handoff": a.handoff},
@@ -714,9 +739,9 @@ def main() -> int:
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
-    if apisrv is not None:
-        apisrv.terminate()
-        apisrv.wait(30)
+    for p_ in apisrvs:
+        p_.terminate()
+        p_.wait(30)
     return 0
 
 

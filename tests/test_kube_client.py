@@ -297,6 +297,22 @@ def test_shard_per_gpu_topology_analyses_each_failure_exactly_once(tmp_path):
     assert r["complete_events_per_pod"] == {1: 2000}, r
 
 
+def test_shard_groups_on_two_apiservers_analyse_each_failure_exactly_once(tmp_path):
+    """bench.py's N = 8 layout (--ranks-per-apiserver 4): two API server processes, each
+    with its own 4-shard operator; 2000 failures split over them are each analysed exactly
+    once, and the two servers' CPU per analysis gives the node >= 2x the ~260 analyses/s
+    eight MI355X ranks ask of it (each server carries half the load)."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    from bench_plumbing import run_sharded
+
+    r = run_sharded(8, 2000, str(tmp_path), timeout_s=400, apiservers=2)
+    assert r["analysed"] == 2000, r
+    assert r["complete_events_per_pod"] == {1: 2000}, r
+    assert len(r["apiserver_cpu_ms_per_analysis"]) == 2
+    # capacity from the servers' own CPU time: each analysis costs one server a few ms
+    assert r["apiserver_capacity_analyses_per_s"] >= 520, r
+
+
 def test_shard_per_gpu_env_and_jittered_retrier():
     """--shard-per-gpu: shard i gets cuda:i (cpu stays cpu) and no engine pool; the
     shared status ring's 409 schedule is jittered and its delays stop doubling."""

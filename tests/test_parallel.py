@@ -180,9 +180,10 @@ def test_bench_two_ranks_gloo(shards, apiserver):
 
 def test_bench_eight_ranks_gloo_one_apiserver():
     """The N = 8 launch exactly as the driver starts it (torch.distributed.run, 8 ranks,
-    127.0.0.1 rendezvous), on the CPU tier: rank 0 starts ONE REST API server and
-    broadcasts its URL, every rank is one operator shard against it, the world is checked
-    against --gpus, and every failure of every rank is analysed exactly once."""
+    127.0.0.1 rendezvous), on the CPU tier: rank 0 starts the REST API servers (one per 4
+    ranks: 2) and broadcasts their URLs, every rank is one operator shard of its server's
+    group, the world is checked against --gpus, and every failure of every rank is analysed
+    exactly once (the servers' own Event records, merged)."""
     import json
     import subprocess
     import sys
@@ -200,13 +201,14 @@ def test_bench_eight_ranks_gloo_one_apiserver():
     out = json.loads(lines[0])
     assert out["n_gpus"] == 8 and out["config"]["parallelism"] == "dp8" and out["config"]["global_batch"] == 24
     assert out["detail"]["rccl_world"] == 8 and len(out["detail"]["per_rank_elapsed_s"]) == 8
-    assert out["config"]["apiserver"].startswith("one REST API server")
+    assert out["config"]["apiserver"].startswith("2 REST API server process(es), 4 ranks each")
     assert out["detail"]["outcomes"] == {"ai-complete": 3}              # rank 0's own timed wave
     assert out["detail"]["outcomes_all_ranks"] == {"ai-complete": 24}   # 8 ranks x 3 failures
     # the one API server's record: every pod of every rank (warmup waves too) has exactly one
     # PodmortemAnalysisComplete Event -- each failure analysed once, by one operator shard
     audit = out["detail"]["apiserver_audit"]
-    assert audit == {"pods_with_complete_event": 48, "max_complete_events_per_pod": 1, "expected_pods": 48}
+    assert audit == {"pods_with_complete_event": 48, "max_complete_events_per_pod": 1, "expected_pods": 48,
+                     "apiservers": 2}
     assert out["value"] > 0
 
 

@@ -81,50 +81,61 @@ def free_port_block(n: int) -> int:
     raise RuntimeError(f"no block of {n} free ports")
 
 
-def run_sharded(shards: int, failures: int, workdir: str, timeout_s: float = 600.0, log_kb: int = 0) -> dict:
-    """The production multi-GPU topology on the CPU: ONE API server process (the REST
-    FakeKube) and ``run --shard-per-gpu --gpus N`` (N operator shard processes, each
-    with its own stub log-parser + echo explainer, splitting the pods by hash). Fails
-    ``failures`` pods at once and waits until every one carries its analysis
-    annotation; returns the rate plus, per pod, how many PodmortemAnalysisComplete
-    Events it got (exactly one each = no double, no miss)."""
+def run_sharded(shards: int, failures: int, workdir: str, timeout_s: float = 600.0, log_kb: int = 0,
+                apiservers: int = 1) -> dict:
+    """The production multi-GPU topology on the CPU: ``apiservers`` API server processes (the
+    REST FakeKube), each with its own ``run --shard-per-gpu --gpus shards/apiservers`` operator
+    (the operator shard processes, each with its own stub log-parser + echo explainer,
+    splitting that server's pods by hash) -- bench.py's N-rank layout (``--ranks-per-apiserver``).
+    Fails ``failures`` pods at once (pod i on server i % apiservers) and waits until every one
+    carries its analysis annotation; returns the rate, each server's CPU time per analysis (its
+    capacity = 1000 / ms analyses/s) and, per pod, how many PodmortemAnalysisComplete Events it
+    got (exactly one each = no double, no miss)."""
     import signal
     import subprocess
     from collections import Counter
+    from concurrent.futures import ThreadPoolExecutor
 
     from operator_amd.kube.client import KubeClient, KubeConfig
     from operator_amd.kube.fake_server import spawn, write_kubeconfig
     from operator_amd.kube.resources import EVENTS
 
-    srv, url = spawn(os.path.join(workdir, "apiserver.url"))
-    kc = write_kubeconfig(url, os.path.join(workdir, "kubeconfig"))
-    port = free_port_block(shards)
+    if shards % apiservers:
+        raise ValueError("shards must split evenly over the API servers")
+    per = shards // apiservers
     env = dict(os.environ, PODMORTEM_LOG_LEVEL="WARNING")
-    op = None
-    kube = KubeClient(KubeConfig(url), 30.0)
+    srvs, kubes, ops = [], [], []
+    names = [f"p{i}" for i in range(failures)]
     try:
-        kube.create(AIPROVIDERS, {"metadata": {"name": "stub", "namespace": "default"},
-                                  "spec": {"providerId": "stub", "modelId": "echo"}})
-        kube.create(PODMORTEMS, {"metadata": {"name": "m0", "namespace": "default"},
-                                 "spec": {"podSelector": {"matchLabels": {"app": "demo"}},
-                                          "aiAnalysisEnabled": True, "aiProviderRef": {"name": "stub"}}})
-        log = LOG
-        if log_kb:
-            filler = b"INFO request served in 3 ms from cache shard 7\n"
-            log = filler * max(0, (log_kb * 1024 - len(LOG)) // len(filler)) + LOG
-        names = [f"p{i}" for i in range(failures)]
-        import httpx
+        for g in range(apiservers):
+            srv, url = spawn(os.path.join(workdir, f"apiserver{g}.url"))
+            srvs.append(srv)
+            kc = write_kubeconfig(url, os.path.join(workdir, f"kubeconfig{g}"))
+            kube = KubeClient(KubeConfig(url), 30.0)
+            kubes.append(kube)
+            kube.create(AIPROVIDERS, {"metadata": {"name": "stub", "namespace": "default"},
+                                      "spec": {"providerId": "stub", "modelId": "echo"}})
+            kube.create(PODMORTEMS, {"metadata": {"name": "m0", "namespace": "default"},
+                                     "spec": {"podSelector": {"matchLabels": {"app": "demo"}},
+                                              "aiAnalysisEnabled": True, "aiProviderRef": {"name": "stub"}}})
+            log = LOG
+            if log_kb:
+                filler = b"INFO request served in 3 ms from cache shard 7\n"
+                log = filler * max(0, (log_kb * 1024 - len(LOG)) // len(filler)) + LOG
+            import httpx
 
-        with httpx.Client(base_url=url, timeout=30) as h:
-            for n in names:
-                kube.create(PODS, running_pod(n, labels={"app": "demo"}))
-                h.put(f"/api/v1/namespaces/default/pods/{n}/log", content=log).raise_for_status()
-        op = subprocess.Popen([sys.executable, "-m", "operator_amd", "run", "--shard-per-gpu", "--gpus", str(shards),
-                               "--set", "engine.device=cpu", "--set", "services.match=stub",
-                               "--set", "services.explain=echo", "--set", "kube.mode=kubeconfig",
-                               "--set", f"kube.kubeconfig={kc}", "--set", f"health.port={port}",
-                               "--set", "health.host=127.0.0.1", "--set", f"patterns.cache_dir={workdir}/patterns",
-                               "--set", "operator.workers=64"], env=env)
+            with httpx.Client(base_url=url, timeout=30) as h:
+                for n in names[g::apiservers]:
+                    kube.create(PODS, running_pod(n, labels={"app": "demo"}))
+                    h.put(f"/api/v1/namespaces/default/pods/{n}/log", content=log).raise_for_status()
+            port = free_port_block(per)
+            ops.append((subprocess.Popen([sys.executable, "-m", "operator_amd", "run", "--shard-per-gpu", "--gpus", str(per),
+                                          "--set", "engine.device=cpu", "--set", "services.match=stub",
+                                          "--set", "services.explain=echo", "--set", "kube.mode=kubeconfig",
+                                          "--set", f"kube.kubeconfig={kc}", "--set", f"health.port={port}",
+                                          "--set", "health.host=127.0.0.1",
+                                          "--set", f"patterns.cache_dir={workdir}/patterns{g}",
+                                          "--set", "operator.workers=64"], env=env), port))
         import urllib.request
 
         def up(pt):
@@ -132,10 +143,8 @@ def run_sharded(shards: int, failures: int, workdir: str, timeout_s: float = 600
                 return urllib.request.urlopen(f"http://127.0.0.1:{pt}/q/health/ready", timeout=1).status == 200
             except OSError:
                 return False
-        assert wait(lambda: all(up(port + i) for i in range(shards)), 180), "shards did not come up"
+        assert wait(lambda: all(up(pt + i) for _, pt in ops for i in range(per)), 180), "shards did not come up"
         # the failures arrive as they would from many kubelets: concurrent status merge patches
-        from concurrent.futures import ThreadPoolExecutor
-
         st = failed_pod("x", finished_at="2025-08-29T10:00:00Z")["status"]
 
         def cpu_s(pid):   # user + system CPU seconds of a process (Linux /proc)
@@ -144,47 +153,53 @@ def run_sharded(shards: int, failures: int, workdir: str, timeout_s: float = 600
                 return (int(f[11]) + int(f[12])) / os.sysconf("SC_CLK_TCK")
             except OSError:
                 return float("nan")
-        c0 = cpu_s(srv.pid)
+        c0 = [cpu_s(p.pid) for p in srvs]
         t0 = time.perf_counter()
         with ThreadPoolExecutor(16) as ex:
-            list(ex.map(lambda n: kube.patch_status(PODS, n, "default", st), names))
+            list(ex.map(lambda i: kubes[i % apiservers].patch_status(PODS, names[i], "default", st), range(failures)))
         t_inj = time.perf_counter() - t0
 
         def analysed():
-            return sum(1 for p in kube.list(PODS, "default")
+            return sum(1 for k in kubes for p in k.list(PODS, "default")
                        if "podmortem.io/analysis" in ((p.get("metadata") or {}).get("annotations") or {}))
         end = time.perf_counter() + timeout_s
         n_done = 0
         while time.perf_counter() < end:
             # a LIST of every pod is the API server's most expensive request: poll it sparingly
-            # (the server is shared with the shards under test)
+            # (the servers are shared with the shards under test)
             time.sleep(0.5)
             n_done = analysed()
             if n_done >= failures:
                 break
         elapsed = time.perf_counter() - t0
-        srv_cpu = cpu_s(srv.pid) - c0
+        srv_cpu = [cpu_s(p.pid) - c for p, c in zip(srvs, c0)]
         time.sleep(2.0)   # let the last Events land before counting them
-        per_pod = Counter(e.get("regarding", {}).get("name") for e in kube.list(EVENTS, "default")
+        per_pod = Counter(e.get("regarding", {}).get("name") for k in kubes for e in k.list(EVENTS, "default")
                           if e.get("reason") == "PodmortemAnalysisComplete"
                           and e.get("regarding", {}).get("kind") == "Pod")
-        return {"topology": f"shard-per-gpu x{shards} on one REST API server (stub log-parser + echo explainer)",
+        ms = [1e3 * c / (failures / apiservers) for c in srv_cpu]
+        return {"topology": f"{apiservers} REST API server(s) x shard-per-gpu {per} (stub log-parser + echo explainer)",
                 "failures": failures, "analysed": n_done, "analyses_per_s": round(failures / elapsed, 1),
                 "inject_s": round(t_inj, 2), "elapsed_s": round(elapsed, 2),
-                # the API server's CPU time over the run: its ms per analysis bound the rate one
-                # server process can sustain (1000 / ms analyses/s)
-                "apiserver_cpu_s": round(srv_cpu, 2), "apiserver_cpu_ms_per_analysis": round(1e3 * srv_cpu / failures, 2),
+                # each API server's CPU time over the run: its ms per analysis bound the rate one
+                # server process can sustain (1000 / ms analyses/s); the servers add up
+                "apiserver_cpu_s": [round(c, 2) for c in srv_cpu],
+                "apiserver_cpu_ms_per_analysis": [round(m, 2) for m in ms],
+                "apiserver_capacity_analyses_per_s": round(sum(1e3 / m for m in ms if m > 0), 1),
                 "complete_events_per_pod": dict(Counter(per_pod.get(n, 0) for n in names))}
     finally:
-        if op is not None:
+        for op, _ in ops:
             op.send_signal(signal.SIGTERM)
+        for op, _ in ops:
             try:
                 op.wait(60)
             except subprocess.TimeoutExpired:
                 op.kill()
-        kube.close() if hasattr(kube, "close") else None
-        srv.terminate()
-        srv.wait(30)
+        for k in kubes:
+            k.close() if hasattr(k, "close") else None
+        for p in srvs:
+            p.terminate()
+            p.wait(30)
 
 
 def main():
@@ -198,15 +213,17 @@ def main():
                          "CPU matcher + echo explainer per worker) instead of in this process")
     ap.add_argument("--log-kb", type=int, default=0, help="pad every pod log to this size (KiB)")
     ap.add_argument("--shard-per-gpu", type=int, default=0,
-                    help="N operator shard processes (`run --shard-per-gpu --gpus N`, CPU stub engines) on ONE REST "
-                         "API server process, instead of everything in this process")
+                    help="N operator shard processes (`run --shard-per-gpu`, CPU stub engines) on REST API server "
+                         "processes (--apiservers), instead of everything in this process")
+    ap.add_argument("--apiservers", type=int, default=1, help="API server processes the shards split over")
     a = ap.parse_args()
     if a.shard_per_gpu:
         import tempfile
 
         with tempfile.TemporaryDirectory() as d:
             print(json.dumps({"bench": "plumbing (BASELINE config 1)", **run_sharded(a.shard_per_gpu, a.failures, d,
-                                                                                      log_kb=a.log_kb)}))
+                                                                                      log_kb=a.log_kb,
+                                                                                      apiservers=a.apiservers)}))
         return
     s = load_settings(env={}, overrides={"patterns.cache_dir": "/tmp/oamd-plumbing", "health.enabled": False,
                                          "operator.workers": a.workers})
