@@ -36,7 +36,7 @@ template <typename T>
 T* optr(const c10::optional<at::Tensor>& t) { return t.has_value() ? reinterpret_cast<T*>(t->data_ptr()) : nullptr; }
 
 void rmsnorm(const at::Tensor& x, const c10::optional<at::Tensor>& residual, const at::Tensor& w,
-             at::Tensor& y, double eps, const c10::optional<at::Tensor>& partial, int64_t splits) {
+             at::Tensor& y, double eps, const c10::optional<at::Tensor>& partial, int64_t splits, bool tiled_out) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(y); ROWMAJOR_VEC(x); ROWMAJOR_VEC(y);
   CHECK_CONTIG(w);
   const int64_t rows = x.size(0), hidden = x.size(1);
@@ -54,9 +54,53 @@ void rmsnorm(const at::Tensor& x, const c10::optional<at::Tensor>& residual, con
     TORCH_CHECK(residual->size(0) == rows && residual->size(1) == hidden, "residual shape mismatch");
     rstride = residual->stride(0);
   }
+  // tiled_out: y (contiguous, [rows, hidden] elements) receives the gemm_xr activation layout
+  TORCH_CHECK(!tiled_out || (rows % 16 == 0 && hidden % 64 == 0 && y.is_contiguous()),
+              "rmsnorm: tiled output needs rows % 16 == 0, hidden % 64 == 0 and a contiguous y");
   const c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   RC(oamd::rmsnorm(ptr<bf16_t>(x), optr<bf16_t>(residual), ptr<bf16_t>(w), ptr<bf16_t>(y), (int)rows,
-                   (int)hidden, x.stride(0), rstride, y.stride(0), (float)eps, xp, (int)splits, cur_stream()));
+                   (int)hidden, x.stride(0), rstride, tiled_out ? -1 : y.stride(0), (float)eps, xp, (int)splits,
+                   cur_stream()));
+}
+
+// gemm_xr (csrc/kernels/gemm_xr.hip): the 256-row decode GEMM with register-streamed activations.
+// xt: the activations [256, K] in the tiled layout (rmsnorm(tiled_out=True) / tile_rows / the SwiGLU
+// epilogue with epi 3); epi 0 = fp32 split-K slabs into p, 1 = bf16 y [256, N], 2 = SwiGLU y [256, N/2],
+// 3 = SwiGLU y [256, N/2] written tiled.
+void gemm_xr(const at::Tensor& xt, const at::Tensor& w, const c10::optional<at::Tensor>& y_opt,
+             const c10::optional<at::Tensor>& p, int64_t splits, int64_t epi) {
+  CHECK_DEV(xt); CHECK_BF16(xt); CHECK_BF16(w); CHECK_CONTIG(xt); CHECK_CONTIG(w);
+  TORCH_CHECK(xt.dim() == 2 && w.dim() == 2 && w.size(1) == xt.size(1), "gemm_xr: xt [256,K], w [N,K]");
+  const int64_t M = xt.size(0), K = xt.size(1), N = w.size(0);
+  TORCH_CHECK(M == 256 && N % 128 == 0 && K % 64 == 0, "gemm_xr: M == 256, N % 128 == 0, K % 64 == 0");
+  TORCH_CHECK(splits >= 1 && splits <= 16 && K % (64 * splits) == 0, "gemm_xr: K % (64 * splits) == 0");
+  TORCH_CHECK((epi >= 0 && epi <= 3) || (epi >= 10 && epi <= 12), "gemm_xr: epi in 0..3 (10..12: timing ablations)");
+  TORCH_CHECK(epi == 0 || epi >= 10 || splits == 1, "gemm_xr: bf16 / SwiGLU outputs need splits == 1");
+  bf16_t* yp = nullptr;
+  float* pp = nullptr;
+  if (epi == 0 || epi >= 10) {
+    TORCH_CHECK(p.has_value(), "gemm_xr: slabs need p");
+    CHECK_DT(*p, at::kFloat); CHECK_CONTIG(*p);
+    TORCH_CHECK(p->numel() >= splits * M * N, "gemm_xr: p too small");
+    pp = p->data_ptr<float>();
+  } else {
+    TORCH_CHECK(y_opt.has_value() && splits == 1, "gemm_xr: y needed (one K slice)");
+    CHECK_BF16(*y_opt); CHECK_CONTIG(*y_opt);
+    TORCH_CHECK(y_opt->numel() == M * (epi == 1 ? N : N / 2), "gemm_xr: y size");
+    yp = ptr<bf16_t>(*y_opt);
+  }
+  TORCH_CHECK(N * K < (1LL << 40), "gemm too large");
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(xt.device());
+  RC(oamd::gemm_xr(ptr<bf16_t>(xt), ptr<bf16_t>(w), yp, pp, (int)M, (int)N, (int)K, (int)splits, (int)epi,
+                   cur_stream()));
+}
+
+void tile_rows(const at::Tensor& x, at::Tensor& xt) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(xt); CHECK_CONTIG(x); CHECK_CONTIG(xt);
+  TORCH_CHECK(x.dim() == 2 && x.numel() == xt.numel() && x.size(0) % 16 == 0 && x.size(1) % 64 == 0,
+              "tile_rows: x [rows % 16, K % 64], xt of the same size");
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  RC(oamd::tile_rows(ptr<bf16_t>(x), ptr<bf16_t>(xt), (int)x.size(0), (int)x.size(1), cur_stream()));
 }
 
 void silu_mul(const at::Tensor& gu, at::Tensor& out, int64_t block) {
@@ -560,7 +604,10 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "operator_amd gfx950 kernels";
   m.def("rmsnorm", &rmsnorm, "RMSNorm with optional fused residual add (and split-K slab sum)", pybind11::arg("x"),
         pybind11::arg("residual"), pybind11::arg("w"), pybind11::arg("y"), pybind11::arg("eps"),
-        pybind11::arg("partial") = pybind11::none(), pybind11::arg("splits") = 1);
+        pybind11::arg("partial") = pybind11::none(), pybind11::arg("splits") = 1, pybind11::arg("tiled_out") = false);
+  m.def("gemm_xr", &gemm_xr, pybind11::arg("xt"), pybind11::arg("w"), pybind11::arg("y") = pybind11::none(),
+        pybind11::arg("p") = pybind11::none(), pybind11::arg("splits") = 1, pybind11::arg("epi") = 1);
+  m.def("tile_rows", &tile_rows, pybind11::arg("x"), pybind11::arg("xt"));
   m.def("silu_mul", &silu_mul, pybind11::arg("gu"), pybind11::arg("out"), pybind11::arg("block") = 0);
   m.def("embedding", &embedding);
   m.def("rope_kv", &rope_kv, pybind11::arg("qkv"), pybind11::arg("pos"), pybind11::arg("cos"),

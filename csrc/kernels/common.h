@@ -91,6 +91,15 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return base + orig / nx;
 }
 
+// Element offset of (row r, column c) in the fragment-major "tiled" activation layout that
+// gemm_xr reads: [K/64 step][rows/16 token block][2 k-half][64 lanes][8], lane = r % 16 +
+// 16 ((c % 32) / 8) -- one K-step of all rows is contiguous, each 1 KiB is one MFMA
+// B-fragment (rows % 16 == 0, K % 64 == 0).
+__device__ __forceinline__ int64_t xr_tiled_off(int r, int c, int rows) {
+  return ((((int64_t)(c >> 6) * (rows >> 4) + (r >> 4)) * 2 + ((c >> 5) & 1)) * 64 + (r & 15) + 16 * ((c & 31) >> 3)) * 8 +
+         (c & 7);
+}
+
 // Counter-based RNG for Gumbel sampling, so a captured graph replays deterministic
 // per (seed, step, row, col). The 64-bit finalizer runs once per row and yields two
 // 32-bit keys; the per-column hash is a 32-bit two-round mix with the second key

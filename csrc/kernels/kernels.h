@@ -45,6 +45,13 @@ int gemm_tile(const bf16_t* X, const bf16_t* W, bf16_t* Y, const bf16_t* bias, i
 // nullptr); silu_gu: fused SwiGLU (S == 1), Y [M, N/2]; nt: non-temporal weight loads.
 int gemm_pp(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, int N, int K, int S, int bm, bool silu_gu,
             bool nt, hipStream_t stream, bool one_seg = false);
+// 256-row decode GEMM with register-streamed activations (gemm_xr.hip): Xt = X [256, K] in the tiled
+// layout [16][K/32][64][8]; N % 128 == 0, K % (64 S) == 0; epi 0 = fp32 slabs P[S][256][N], 1 = bf16 Y,
+// 2 = SwiGLU (interleaved gate|up, S == 1) Y [256, N/2], 3 = the same written tiled.
+int gemm_xr(const bf16_t* Xt, const bf16_t* W, bf16_t* Y, float* P, int M, int N, int K, int S, int epi,
+            hipStream_t stream);
+// x [rows, K] row-major -> the tiled layout gemm_xr reads (rows % 16 == 0, K % 32 == 0).
+int tile_rows(const bf16_t* x, bf16_t* xt, int rows, int K, hipStream_t stream);
 // Y[M, N] = bf16(sum_s P[s][M][N]) (fp32 split-K slabs).
 int splitk_reduce(const float* P, bf16_t* Y, int64_t MN, int S, hipStream_t stream);
 // Skinny-M decode GEMM (M <= 32, gemm_skinny.hip): N % 16 == 0, K % (128 S) == 0; S-way split-K slabs P

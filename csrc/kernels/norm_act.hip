@@ -94,7 +94,10 @@ __global__ void __launch_bounds__(NT) rmsnorm_kernel(
   }
   const float tot = block_sum<NT>(ss, scratch);
   const float rs = rsqrtf(tot / static_cast<float>(hidden) + eps);
-  u16x8* yr = reinterpret_cast<u16x8*>(y + row * y_stride);
+  // y_stride < 0: y is written in the fragment-major tiled layout that gemm_xr reads its
+  // activations from (common.h xr_tiled_off; one block per row, rows % 16 == 0)
+  const bool tiled = y_stride < 0;
+  u16x8* yr = reinterpret_cast<u16x8*>(y + (tiled ? 0 : row * y_stride));
 #pragma unroll
   for (int i = 0; i < MAXV; ++i) {
     const int vi = threadIdx.x + i * NT;
@@ -106,7 +109,11 @@ __global__ void __launch_bounds__(NT) rmsnorm_kernel(
         // HF semantics: normalised value is rounded to bf16, then scaled by w
         o[j] = f2bf(bf2f(f2bf(v[i][j] * rs)) * bf2f(wv[j]));
       }
-      yr[vi] = o;
+      if (tiled) {
+        *reinterpret_cast<u16x8*>(y + xr_tiled_off(row, vi * 8, gridDim.x)) = o;
+      } else {
+        yr[vi] = o;
+      }
     }
   }
 }
