@@ -560,7 +560,7 @@ template <int EPI, int DEEP = 0, int OPT = 0>
 __global__ void __launch_bounds__(256) gemm_tile256_p5_kernel(const bf16_t* __restrict__ X,
                                                               const bf16_t* __restrict__ W, bf16_t* __restrict__ Y,
                                                               const bf16_t* __restrict__ bias, int M, int N, int K,
-                                                              int ldy) {
+                                                              int ldy, int group_m) {
   constexpr int AUX = 16;
   constexpr int kHalf = 32768;   // one operand of a K-step: 256 rows x 128 B
   __shared__ __attribute__((aligned(1024))) char lds[DEEP ? 5 * kHalf : 4 * kHalf];
@@ -572,13 +572,13 @@ __global__ void __launch_bounds__(256) gemm_tile256_p5_kernel(const bf16_t* __re
   const int G = gridDim.x;
   const int slot = xcd_remap(blockIdx.x, G);
   const int T = K / kBK;
-  const int gsz = kGroupM * nt;
+  const int gsz = group_m * nt;
   // linear tile of round r -> (m0, n0); false past the last tile
   auto tile_rc = [&](int r, int& m0, int& n0) -> bool {
     const int lid = r * G + slot;
     if (lid >= ntiles) return false;
-    const int first_m = (lid / gsz) * kGroupM;
-    const int gm = min(mt - first_m, kGroupM);
+    const int first_m = (lid / gsz) * group_m;
+    const int gm = min(mt - first_m, group_m);
     m0 = (first_m + (lid % gsz) % gm) * kT;
     n0 = ((lid % gsz) / gm) * kT;
     return true;
@@ -898,10 +898,10 @@ __global__ void splitk_silu_reduce_kernel(const float* __restrict__ P, bf16_t* _
 
 template <int DEEP>
 static void launch_p5(const bf16_t* X, const bf16_t* W, bf16_t* Y, const bf16_t* bias, int M, int N, int K, int ldy,
-                      bool silu_gu, int grid, hipStream_t stream) {
-  if (silu_gu) gemm_tile256_p5_kernel<kEpiSilu, DEEP><<<grid, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-  else if (bias) gemm_tile256_p5_kernel<kEpiBias, DEEP><<<grid, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-  else gemm_tile256_p5_kernel<kEpiStore, DEEP><<<grid, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+                      bool silu_gu, int grid, hipStream_t stream, int gm = kGroupM) {
+  if (silu_gu) gemm_tile256_p5_kernel<kEpiSilu, DEEP><<<grid, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy, gm);
+  else if (bias) gemm_tile256_p5_kernel<kEpiBias, DEEP><<<grid, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy, gm);
+  else gemm_tile256_p5_kernel<kEpiStore, DEEP><<<grid, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy, gm);
 }
 
 // compute units of the current device (persistent grids), cached per device
@@ -946,14 +946,16 @@ int gemm_tile(const bf16_t* X, const bf16_t* W, bf16_t* Y, const bf16_t* bias, i
   // profiles/gemm_tile_p5_vs_hipblaslt_r6.jsonl)
   if ((variant == 5 || (variant == 0 && M > kT)) && K >= 2 * kBK && st16) {
     const int grid = min(nwg, device_cus());
+    // GROUP_M 4 for the narrow projections (M = 32k, N = 6144: 1106 vs 1145 us at GROUP_M 8; N = 4096
+    // equal; 16 / 32 slower: profiles/gemm_tile_p5_vs_hipblaslt_r6.jsonl)
     if (N >= 16384) launch_p5<2>(X, W, Y, bias, M, N, K, ldy, silu_gu, grid, stream);
-    else launch_p5<0>(X, W, Y, bias, M, N, K, ldy, silu_gu, grid, stream);
-  } else if (variant >= 6 && variant <= 9 && K >= 2 * kBK && !silu_gu && !bias && st16) {   // p5 A/B arms (timing)
+    else launch_p5<0>(X, W, Y, bias, M, N, K, ldy, silu_gu, grid, stream, 4);
+  } else if (variant >= 6 && variant <= 9 && K >= 2 * kBK && st16) {   // p5 A/B arms (timing, same numerics)
     const int grid = min(nwg, device_cus());
-    if (variant == 6) gemm_tile256_p5_kernel<kEpiStore, 0, 2><<<grid, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-    else if (variant == 7) gemm_tile256_p5_kernel<kEpiStore, 1><<<grid, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-    else if (variant == 8) gemm_tile256_p5_kernel<kEpiStore, 2><<<grid, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
-    else gemm_tile256_p5_kernel<kEpiStore, 1, 2><<<grid, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
+    if (variant == 6) launch_p5<0>(X, W, Y, bias, M, N, K, ldy, silu_gu, grid, stream, 4);         // GROUP_M 4
+    else if (variant == 7) launch_p5<0>(X, W, Y, bias, M, N, K, ldy, silu_gu, grid, stream, 16);   // GROUP_M 16
+    else if (variant == 8) launch_p5<2>(X, W, Y, bias, M, N, K, ldy, silu_gu, grid, stream);       // W third buffer
+    else launch_p5<0>(X, W, Y, bias, M, N, K, ldy, silu_gu, grid, stream, 32);                      // GROUP_M 32
   } else if ((variant == 0 || variant == 1) && off32) {   // 4-wave, two 64 KiB buffers, four phases per K-tile
     if (silu_gu) gemm_tile256_h4_kernel<kEpiSilu><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
     else if (bias) gemm_tile256_h4_kernel<kEpiBias><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);
