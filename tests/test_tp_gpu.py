@@ -3,9 +3,10 @@ the box (cuda:0), the decode all-reduces through the IPC kernels between them (t
 all-reduce + residual + RMSNorm, and with fp8 weights its e4m3fn epilogue), gloo only
 for the handle exchange (RCCL refuses two ranks on one device). The sharded model's
 prefill logits and one paged decode step (the decode RoPE folded into attention, the
-per-rank kv-head shard) track the TP = 1 model run on the same kernels. The CPU tier
-pins TP = 4 / 8 to TP = 1 exactly in fp32 (tests/test_tp_scale.py); here bf16 / fp8 and
-a different reduction order allow a relative difference (SURVEY.md §4.2 "Distributed")."""
+per-rank kv-head shard) are checked against the fp32 PyTorch path of the same global
+weights on the host (as tests/test_llama_gpu.py does for TP = 1), with a bf16- / fp8-sized
+tolerance, and against the TP = 1 model on the same kernels. The CPU tier pins TP = 4 / 8
+to TP = 1 exactly in fp32 (tests/test_tp_scale.py) (SURVEY.md §4.2 "Distributed")."""
 import os
 import socket
 
@@ -31,14 +32,26 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _run(m, hkv: int):
+def _cpu_copy(m):
+    """The fp32 host model with the same (global, TP = 1) weights."""
+    from operator_amd.models.llama import LayerWeights, LlamaModel
+
+    c = LlamaModel(m.cfg, device="cpu", dtype=torch.float32)
+    c.embed, c.final_norm, c.lm_head = m.embed.float().cpu(), m.final_norm.float().cpu(), m.lm_head.float().cpu()
+    c.layers = [LayerWeights(*(t.float().cpu() for t in (l.wqkv, l.wo, l.wgu, l.wd, l.attn_norm, l.mlp_norm)))
+                for l in m.layers]
+    return c
+
+
+def _run(m, hkv: int, dev: str = "cuda"):
     """Prefill LENS, then one decode step: (last-token prefill logits, decode logits), the
     rank's vocab shard, on the CPU."""
     from operator_amd.models.kv_cache import PagedKVCache
     from operator_amd.models.llama import ForwardBatch
 
-    B, dev = len(LENS), "cuda"
-    kv = PagedKVCache(m.cfg.layers, B * PER, hkv, 128, P, device=dev)
+    B = len(LENS)
+    kv = PagedKVCache(m.cfg.layers, B * PER, hkv, 128, P, device=dev,
+                      **({} if dev == "cuda" else {"dtype": torch.float32}))
     bt = torch.arange(B * PER, dtype=torch.int32).reshape(B, PER)
     ids = [torch.randint(0, m.cfg.vocab_size, (L,), generator=torch.Generator().manual_seed(i))
            for i, L in enumerate(LENS)]
@@ -53,7 +66,8 @@ def _run(m, hkv: int):
     fb = ForwardBatch(nxt.to(dev), dpos.to(dev), dslots.to(dev), False, None, block_tables=bt.to(dev),
                       context_lens=(dpos + 1).int().to(dev), num_splits=1)
     dec = m.forward(fb, kv).float().cpu()
-    torch.cuda.synchronize()
+    if dev == "cuda":
+        torch.cuda.synchronize()
     return pre, dec
 
 
@@ -110,12 +124,29 @@ def test_tp_on_one_gpu_tracks_tp1(wdt, world):
     dec = torch.cat([got[r][1] for r in range(world)], dim=1)
     m1 = LlamaModel(_cfg(), device="cuda", weight_dtype=wdt).init_random(seed=7)
     pre1, dec1 = _run(m1, m1.hkv)
-    tol = 0.05 if wdt == "bfloat16" else 0.12   # fp8: per-shard channel scales of the row-parallel weights
-    for got_, want in ((pre, pre1), (dec, dec1)):
+    del m1
+    mb = LlamaModel(_cfg(), device="cuda").init_random(seed=7)   # the same global bf16 weights
+    with torch.inference_mode():
+        pref, decf = _run(_cpu_copy(mb), mb.hkv, dev="cpu")
+    del mb
+    # against the fp32 host path: bf16 rounding through 2 layers, or with fp8 weights the
+    # e4m3fn weight/activation quantization (per-shard channel scales of the row-parallel
+    # weights) on top
+    tol = 0.02 if wdt == "bfloat16" else 0.08   # measured: 0.0065 (TP=2, 4) and 0.056 (fp8)
+    errs = {}
+    for name, got_, want in (("prefill", pre, pref), ("decode", dec, decf)):
         assert got_.shape == want.shape
-        err = float((got_ - want).abs().max() / want.abs().max())
-        assert err < tol, err
-    # the decode step's greedy token agrees for rows whose top-2 logits are not a near tie
-    top2 = dec1.topk(2, dim=1).values
-    clear = (top2[:, 0] - top2[:, 1]) > 0.05 * dec1.abs().max()
-    assert torch.equal(dec.argmax(1)[clear], dec1.argmax(1)[clear])
+        errs[name] = float((got_ - want).abs().max() / want.abs().max())
+    errs1 = {n: float((a - b).abs().max() / b.abs().max()) for n, a, b in (("prefill", pre1, pref),
+                                                                        ("decode", dec1, decf))}
+    print(f"TP={world} {wdt}: max-logit error vs fp32 host {errs}; TP=1 on the same kernels {errs1}")
+    for n in errs:
+        assert errs[n] < tol, (n, errs, errs1)
+        # the sharding adds no error beyond what the kernels' precision already has at TP=1
+        assert errs[n] < 1.5 * errs1[n] + 0.005, (n, errs, errs1)
+    # the decode step's greedy token is the fp32 path's for rows whose top-2 logits are
+    # not a near tie
+    top2 = decf.topk(2, dim=1).values
+    clear = (top2[:, 0] - top2[:, 1]) > 0.02 * decf.abs().max()
+    assert torch.equal(dec.argmax(1)[clear], decf.argmax(1)[clear])
+    assert torch.equal(pre.argmax(1), pref.argmax(1)) or wdt == "fp8"
