@@ -19,12 +19,14 @@ int ac_scan(const uint8_t* text, int64_t n_segs, int seg_bytes, const uint8_t* c
             const uint16_t* table, int num_states, int log2_classes, int hot_states,
             const uint32_t* out_off, const uint32_t* out_ids, MatchRec* matches, uint32_t* match_count,
             uint32_t match_cap, uint32_t* seg_nl, int grid_blocks, const uint16_t* hot_table,
-            hipStream_t stream);
+            const uint8_t* chain, hipStream_t stream);
 
 // ac_scan v2's LDS image of the first min(num_states, 256) states: entry
 // [byte * kScanHotStride + state] = table[state][cls_map[byte]] (built on the host).
 constexpr int kScanHotStates = 256;
 constexpr int kScanHotStride = kScanHotStates + 2;
+// chain: per-state chain bytes of the exact re-walk (patterns.cpp dfa_chain), at least
+// round_up(num_states, 16) + 16 bytes.
 
 // seg_head: per-segment newline count of the part scanned by the stream that ends
 // inside the segment (ac_scan v2; the second half of its seg_nl buffer).

@@ -212,6 +212,8 @@ constexpr int kHotWide = kScanHotStates;
 constexpr int kWideStride = kScanHotStride;
 static_assert(kHotWideStates == kScanHotStates, "hot set sizes");
 constexpr int kWideLds = 256 + kHotWide * kWideStride * 2;
+constexpr int kScanLdsMax = 160 * 1024;
+constexpr int kChainLdsMax = (kScanLdsMax - kWideLds) / 16 * 16;   // chain bytes staged in LDS
 
 // 0x80 in each byte of w that is '\n' (exact: no carries between bytes)
 __device__ __forceinline__ uint32_t newline_bits(uint32_t w) {
@@ -219,22 +221,32 @@ __device__ __forceinline__ uint32_t newline_bits(uint32_t w) {
   return ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x | 0x7f7f7f7fu);
 }
 
-template <int NS, int CH, int NT = kScanThreads>
+// PROBE (timing probes, OAMD_SCAN_PROBE; results are NOT valid): 1 = every lookup on a
+// lane-private LDS bank (conflict-free, same dependent chain), 2 = real lookups without
+// the exact re-walk, 3 = a VALU-only chain (no LDS); 4 = the real kernel with per-wave
+// slow-path statistics, 5 = 4 + second-half-of-line text loads nontemporal, 6 = 4 +
+// the slow path at raised wave priority (s_setprio), 7 = 4 + the re-walk block entered
+// after every chunk (its non-walk code kept hot).
+template <int NS, int CH, int NT = kScanThreads, int PROBE = 0>
 __global__ void __launch_bounds__(NT) ac_scan_wide_kernel(
     const uint8_t* __restrict__ text, int64_t total, int64_t L, int64_t n_streams, int seg_shift,
     const uint8_t* __restrict__ cls_map, const uint16_t* __restrict__ tg, const uint16_t* __restrict__ hot_table,
     int log2C, int H, const uint32_t* __restrict__ out_off, const uint32_t* __restrict__ out_ids,
     MatchRec* __restrict__ matches, uint32_t* __restrict__ count, uint32_t cap, uint32_t* __restrict__ seg_nl,
-    uint32_t* __restrict__ seg_head) {
+    uint32_t* __restrict__ seg_head, const uint8_t* __restrict__ chain, uint32_t n_chain_lds) {
   constexpr int NV = CH / 16;  // 16-B loads per stream per chunk
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* cls = smem;
   uint16_t* tl = reinterpret_cast<uint16_t*>(smem + 256);
   const int tid = threadIdx.x;
-  // class map + the host-built [byte][state] hot table: plain 16-B copies
+  // class map + the host-built [byte][state] hot table + the first n_chain_lds chain
+  // bytes: plain 16-B copies
+  uint8_t* lchain = smem + 256 + kHotWide * kWideStride * 2;
   if (tid < 16) reinterpret_cast<uint4*>(cls)[tid] = reinterpret_cast<const uint4*>(cls_map)[tid];
   for (int i = tid; i < kHotWide * kWideStride * 2 / 16; i += NT)
     reinterpret_cast<uint4*>(tl)[i] = reinterpret_cast<const uint4*>(hot_table)[i];
+  for (int i = tid; i < static_cast<int>(n_chain_lds / 16); i += NT)
+    reinterpret_cast<uint4*>(lchain)[i] = reinterpret_cast<const uint4*>(chain)[i];
   __syncthreads();
 
   const int64_t k0 = NS * ((int64_t)blockIdx.x * NT + tid);
@@ -245,6 +257,9 @@ __global__ void __launch_bounds__(NT) ac_scan_wide_kernel(
 
   int64_t pos[NS], end[NS];
   uint32_t st[NS], nl[NS], mid = 0, act = 0;
+  uint64_t t_begin = 0, t_slow = 0, t_sub = 0;   // PROBE >= 4: per-wave slow-path statistics
+  uint32_t n_slow = 0, n_cold = 0, n_emit = 0, n_sub = 0, t_emit = 0, t_cold = 0;
+  if constexpr (PROBE >= 4) t_begin = clock64();
 #pragma unroll
   for (int k = 0; k < NS; ++k) {
     const int64_t b0 = (k0 + k) * L;
@@ -260,14 +275,19 @@ __global__ void __launch_bounds__(NT) ac_scan_wide_kernel(
   // a chunk per stream as consecutive 16-B loads (plain, not nontemporal: the other
   // half of each 128-B line is read by the next chunk, from L2; nt loads measured
   // 1.6x slower)
-  auto load = [&](u32x4_t (&dst)[NS][NV], int64_t delta) {
+  auto load = [&](u32x4_t (&dst)[NS][NV], int64_t delta, bool nt = false) {
 #pragma unroll
     for (int k = 0; k < NS; ++k) {
       const int64_t o = pos[k] + delta;
       if (o >= 0 && o < end[k] && (act >> k & 1u)) {
         const u32x4_t* p = reinterpret_cast<const u32x4_t*>(text + o);
+        if (nt) {
 #pragma unroll
-        for (int v = 0; v < NV; ++v) dst[k][v] = p[v];
+          for (int v = 0; v < NV; ++v) dst[k][v] = __builtin_nontemporal_load(p + v);
+        } else {
+#pragma unroll
+          for (int v = 0; v < NV; ++v) dst[k][v] = p[v];
+        }
       } else {
 #pragma unroll
         for (int v = 0; v < NV; ++v) dst[k][v] = u32x4_t{0u, 0u, 0u, 0u};
@@ -275,61 +295,106 @@ __global__ void __launch_bounds__(NT) ac_scan_wide_kernel(
     }
   };
 
-  // Exact walk of one chunk of stream k from state s (cold states through the
-  // global table) with match emission when `own`: the rare path. The chunk's bytes
-  // come from the registers the fast walk used (zeros outside the stream, as there);
-  // each byte step is one LDS read unless a lane of the wave is in a cold state
-  // (wave-uniform branch to the global table), and emission sits behind another.
-  // Rolled over the chunk's dwords (a dword picked by a 4-level select, no scratch),
-  // unrolled over the 4 bytes of each.
-  auto slow = [&](int k, const u32x4_t (&cu)[NV], int64_t at, uint32_t s, uint32_t nl_now, bool own) -> uint32_t {
+  // Exact walk of one 16-byte sub-chunk `q` of stream k from state s (cold states
+  // through the chain bytes / the global table) with match emission when `own`: the
+  // rare path, and issue-bound (it shares its SIMD with three fast-walking waves), so
+  // every byte costs few instructions: a byte step is its LDS read and one
+  // wave-uniform cold test; output entries are collected per dword and emitted behind
+  // one test per dword; newlines are counted per dword. Rolled over the 4 dwords
+  // (picked by a 2-level select), unrolled over their bytes.
+  auto slow_sub = [&](int k, const u32x4_t& q, int64_t at, uint32_t s, uint32_t nl_now, bool own) -> uint32_t {
 #pragma unroll 1
-    for (int d = 0; d < CH / 4; ++d) {
-      u32x4_t v4 = cu[0];
-      if constexpr (NV == 4) {
-        const u32x4_t v01 = (d & 4) ? cu[1] : cu[0];
-        const u32x4_t v23 = (d & 4) ? cu[3] : cu[2];
-        v4 = (d & 8) ? v23 : v01;
-      } else if constexpr (NV == 2) {
-        v4 = (d & 4) ? cu[1] : cu[0];
-      }
-      const uint32_t w01 = (d & 1) ? v4[1] : v4[0];
-      const uint32_t w23 = (d & 1) ? v4[3] : v4[2];
+    for (int d = 0; d < 4; ++d) {
+      const uint32_t w01 = (d & 1) ? q[1] : q[0];
+      const uint32_t w23 = (d & 1) ? q[3] : q[2];
       const uint32_t wv = (d & 2) ? w23 : w01;
+      uint32_t es[4], omask = 0;
 #pragma unroll
       for (int by = 0; by < 4; ++by) {
         const uint32_t b = (wv >> (8 * by)) & 0xffu;
         const uint32_t sk = s & 0x7fffu;
         uint32_t e = tl[b * kWideStride + (sk & 0xffu)];
         if (__ballot(sk >= Hs)) {
-          if (sk >= Hs) e = tg[(sk << log2C) | cls[b]];
+          uint64_t tc = 0;
+          if constexpr (PROBE >= 4) tc = clock64();
+          // A cold state is usually one step down a pattern literal's trie path, numbered
+          // so that the path's next state is sk + 1 (csrc/patterns/patterns.cpp
+          // reorder_dfa): the chain byte (LDS, the rest of the CU's 160 KB) says which
+          // class takes it there. Other transitions read the global table, as half of a
+          // 32-bit read: a uint16 load here is merged with the LDS read above into one
+          // flat_load through a selected address, and then EVERY byte of the re-walk
+          // waits on a flat load (vmcnt + lgkmcnt).
+          if (sk >= Hs) {
+            const uint32_t c = cls[b];
+            const uint32_t x = sk < n_chain_lds
+                                   ? static_cast<uint32_t>(lchain[sk])
+                                   : (reinterpret_cast<const uint32_t*>(chain)[sk >> 2] >> ((sk & 3u) * 8)) & 0xffu;
+            if ((x & 0x40u) && (x & 0x3fu) == c) {
+              e = (sk + 1) | ((x & 0x80u) << 8);
+            } else {
+              const uint32_t gi = (sk << log2C) | c;
+              e = (reinterpret_cast<const uint32_t*>(tg)[gi >> 1] >> ((gi & 1u) << 4)) & 0xffffu;
+            }
+          }
+          if constexpr (PROBE >= 4) {   // per lane: cold steps and their cycles
+            if (sk >= Hs) {
+              ++n_cold;
+              t_cold += static_cast<uint32_t>(clock64() - tc) + (e & 0u);
+            }
+          }
         }
-        if (__ballot(own && (e & 0x8000u))) {
-          const uint64_t p = static_cast<uint64_t>(at + 4 * d + by);
-          emit_matches_wave(own && (e & 0x8000u), e & 0x7fffu, static_cast<uint32_t>(p >> seg_shift),
-                            static_cast<uint32_t>(p) & seg_mask, nl_now | ((mid >> k & 1u) << 31), out_off, out_ids,
-                            matches, count, cap);
-        }
-        nl_now += (own && b == 10u);
+        es[by] = e;
+        omask |= ((e >> 15) & 1u) << by;
         s = e;
       }
+      const uint32_t nlb = newline_bits(wv);
+      if (__ballot(own && omask != 0)) {
+        uint64_t te = 0;
+        if constexpr (PROBE >= 4) te = clock64();
+#pragma unroll 1
+        for (int by = 0; by < 4; ++by) {
+          const bool hit = own && (omask >> by & 1u);
+          if (__ballot(hit)) {
+            const uint32_t e01 = (by & 1) ? es[1] : es[0];
+            const uint32_t e23 = (by & 1) ? es[3] : es[2];
+            const uint32_t e = (by & 2) ? e23 : e01;
+            const uint64_t p = static_cast<uint64_t>(at + 4 * d + by);
+            const uint32_t nl_at = nl_now + __builtin_popcount(nlb & ((1u << (8 * by)) - 1u));
+            emit_matches_wave(hit, e & 0x7fffu, static_cast<uint32_t>(p >> seg_shift),
+                              static_cast<uint32_t>(p) & seg_mask, nl_at | ((mid >> k & 1u) << 31), out_off,
+                              out_ids, matches, count, cap);
+          }
+        }
+        if constexpr (PROBE >= 4) {   // per lane (the emitting lanes)
+          if (own && omask != 0) {
+            t_emit += static_cast<uint32_t>(clock64() - te);
+            n_emit += __builtin_popcount(omask);
+          }
+        }
+      }
+      if (own) nl_now += __builtin_popcount(nlb);
     }
     return s;
   };
 
   // One chunk of every stream, the common case: one ds_read_u16 per byte and no
   // branch. The state register holds the raw entry (next | 0x8000 outputs), its low
-  // byte indexes the hot row; `acc` ORs every entry, so one test per chunk finds a
-  // stream that entered a cold state (>= 256: every later fast step was wrong) or
-  // an output state. Those chunks are re-walked exactly by `slow`. Bit k of `own`:
-  // stream k's own range (count newlines, emit) rather than its look-back.
+  // byte indexes the hot row; `acc` ORs every entry of a 16-byte sub-chunk, so one test
+  // per sub-chunk finds one that entered a cold state (>= 256: every later fast step
+  // was wrong) or an output state (bit v of fl[k]). The chunk is then re-walked exactly
+  // from its first flagged sub-chunk, one sub-chunk at a time, until the exact state
+  // meets the fast walk's state at a sub-chunk boundary again (from there the fast walk
+  // was exact; later flagged sub-chunks are re-walked from their saved start state).
+  // Bit k of `own`: stream k's own range (count newlines, emit) rather than its look-back.
   auto walk = [&](const u32x4_t (&cur)[NS][NV], uint32_t own, int64_t delta) {
-    uint32_t s0[NS], nl0[NS], acc[NS];
+    uint32_t sv[NS][NV], nl0[NS], acc[NS], fl[NS], m[NS];
 #pragma unroll
     for (int k = 0; k < NS; ++k) {
-      s0[k] = st[k];
+      sv[k][0] = st[k];
       nl0[k] = nl[k];
       acc[k] = st[k] & 0x7fffu;   // a chunk that STARTS in a cold state is re-walked too
+      fl[k] = 0;
+      m[k] = (own >> k & 1u) ? (cold_mask | 0x8000u) : cold_mask;
     }
 #pragma unroll
     for (int w = 0; w < CH / 4; ++w) {
@@ -341,27 +406,79 @@ __global__ void __launch_bounds__(NT) ac_scan_wide_kernel(
 #pragma unroll
         for (int k = 0; k < NS; ++k) {
           const uint32_t b = (wv[k] >> (8 * by)) & 0xffu;
-          st[k] = tl[b * kWideStride + (st[k] & 0xffu)];
+          if constexpr (PROBE == 1)
+            st[k] = tl[((((b ^ st[k]) & 0x7fu) << 5) | (threadIdx.x & 31u)) << 1];
+          else if constexpr (PROBE == 3)
+            st[k] = ((st[k] * 0x9e37u) ^ b) & 0xffffu;
+          else
+            st[k] = tl[b * kWideStride + (st[k] & 0xffu)];
           acc[k] |= st[k];
         }
       }
 #pragma unroll
       for (int k = 0; k < NS; ++k)
         if (own >> k & 1u) nl[k] += __builtin_popcount(newline_bits(wv[k]));
+      if ((w & 3) == 3) {   // sub-chunk boundary
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+          fl[k] |= (acc[k] & m[k]) ? (1u << (w >> 2)) : 0u;
+          acc[k] = st[k] & 0x7fffu;   // the next sub-chunk is re-walked if it starts cold
+          if ((w >> 2) + 1 < NV) sv[k][(w >> 2) + 1] = st[k];
+        }
+      }
       // keep the scheduler from hoisting the state-independent byte-offset math of
       // the whole chunk ahead of the chain (64 live VGPRs per stream, then spills)
       __builtin_amdgcn_sched_barrier(0);
     }
-    uint32_t flag = 0;
+    if constexpr (PROBE >= 1 && PROBE <= 3) {
 #pragma unroll
-    for (int k = 0; k < NS; ++k) {
-      const uint32_t m = (own >> k & 1u) ? (cold_mask | 0x8000u) : cold_mask;
-      flag |= (acc[k] & m) ? (1u << k) : 0u;
-    }
-    if (__ballot(flag != 0)) {
-#pragma unroll   // compile-time k: a runtime index would put st[]/pos[] in scratch
       for (int k = 0; k < NS; ++k)
-        if (flag >> k & 1u) st[k] = slow(k, cur[k], pos[k] + delta, s0[k], nl0[k], own >> k & 1u);
+        if (fl[k] == 0xfff0u + static_cast<uint32_t>(log2C) || sv[k][NV - 1] == 0xfff0u + static_cast<uint32_t>(log2C))
+          seg_head[0] = st[k];   // keep the walk live
+      return;
+    }
+    uint32_t any = PROBE == 7 ? 1u : 0u;
+#pragma unroll
+    for (int k = 0; k < NS; ++k) any |= fl[k];
+    if (__ballot(any != 0)) {
+      uint64_t t0 = 0;
+      if constexpr (PROBE >= 4) t0 = clock64();
+      if constexpr (PROBE == 6) __builtin_amdgcn_s_setprio(3);
+#pragma unroll   // compile-time k and v: a runtime index would put st[]/sv[] in scratch
+      for (int k = 0; k < NS; ++k) {
+        if (PROBE != 7 && !__ballot(fl[k] != 0)) continue;
+        const bool ownk = own >> k & 1u;
+        bool sync = true;          // the fast walk's state at this sub-chunk's start is exact
+        uint32_t s = 0, nlr = nl0[k];
+#pragma unroll   // compile-time v: selecting cur[k][v] / sv[k][v] at run time puts them in scratch
+        for (int v = 0; v < NV; ++v) {
+          const u32x4_t& q = cur[k][v];
+          const uint32_t sa = sv[k][v], sb = v + 1 < NV ? sv[k][v + 1 < NV ? v + 1 : v] : st[k];
+          const bool need = fl[k] != 0 && (!sync || (fl[k] >> v & 1u));
+          if (__ballot(need)) {
+            uint64_t tw = 0;
+            if constexpr (PROBE >= 4) {
+              ++n_sub;
+              tw = clock64();
+            }
+            if (need) {
+              s = slow_sub(k, q, pos[k] + delta + 16 * v, sync ? sa : s, nlr, ownk);
+              sync = s == sb;
+            }
+            if constexpr (PROBE >= 4) t_sub += __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(clock64() - tw));
+          }
+          if (ownk) {
+#pragma unroll
+            for (int d = 0; d < 4; ++d) nlr += __builtin_popcount(newline_bits(q[d]));
+          }
+        }
+        if (!sync) st[k] = s;
+      }
+      if constexpr (PROBE == 6) __builtin_amdgcn_s_setprio(0);
+      if constexpr (PROBE >= 4) {
+        t_slow += clock64() - t0;
+        ++n_slow;
+      }
     }
   };
 
@@ -377,7 +494,9 @@ __global__ void __launch_bounds__(NT) ac_scan_wide_kernel(
   load(cur, 0);
   const int64_t chunks = (L + CH - 1) / CH;
   for (int64_t c = 0; c < chunks; ++c) {
-    if (c + 1 < chunks) load(nxt, CH);
+    // PROBE 5: the chunk that reads the second half of each 128-B line (L % 128 == 0)
+    // loads it nontemporally: last use, so it is not kept in L2 over the DFA table
+    if (c + 1 < chunks) load(nxt, CH, PROBE == 5 && (c & 1) == 0);
     uint32_t own = 0;
 #pragma unroll
     for (int k = 0; k < NS; ++k) own |= ((act >> k & 1u) && pos[k] < end[k]) ? (1u << k) : 0u;
@@ -400,6 +519,35 @@ __global__ void __launch_bounds__(NT) ac_scan_wide_kernel(
       for (int k = 0; k < NS; ++k)
 #pragma unroll
         for (int v = 0; v < NV; ++v) cur[k][v] = nxt[k][v];
+    }
+  }
+  if constexpr (PROBE >= 4) {
+    // per-wave {cycles, slow-path cycles, slow-path entries, cold wave-steps, emission
+    // cycles, emissions, re-walked sub-chunks, sub-chunk walk cycles, cold-step cycles, 0, 0, 0}
+    // in the
+    // upper half of the match buffer (timing probe only)
+    // per-lane counters -> wave totals (counts) / the busiest lane (cycles)
+    for (int o = 32; o > 0; o >>= 1) {
+      n_cold += __shfl_xor(n_cold, o, 64);
+      n_emit += __shfl_xor(n_emit, o, 64);
+      t_cold = max(t_cold, (uint32_t)__shfl_xor(t_cold, o, 64));
+      t_emit = max(t_emit, (uint32_t)__shfl_xor(t_emit, o, 64));
+    }
+    if ((tid & 63) == 0) {
+      uint32_t* stats = reinterpret_cast<uint32_t*>(matches + cap / 2) +
+                        12 * ((int64_t)blockIdx.x * (NT / 64) + (tid >> 6));
+      stats[0] = static_cast<uint32_t>(clock64() - t_begin);
+      stats[1] = static_cast<uint32_t>(t_slow);
+      stats[2] = n_slow;
+      stats[3] = n_cold;
+      stats[4] = static_cast<uint32_t>(t_emit);
+      stats[5] = n_emit;
+      stats[6] = n_sub;
+      stats[7] = static_cast<uint32_t>(t_sub);
+      stats[8] = t_cold;
+      stats[9] = 0;
+      stats[10] = 0;
+      stats[11] = 0;
     }
   }
 }
@@ -426,10 +574,10 @@ static int num_cus() {
 int ac_scan(const uint8_t* text, int64_t n_segs, int seg_bytes, const uint8_t* cls_map, const uint16_t* table,
             int num_states, int log2_classes, int hot_states, const uint32_t* out_off, const uint32_t* out_ids,
             MatchRec* matches, uint32_t* match_count, uint32_t match_cap, uint32_t* seg_nl, int grid_blocks,
-            const uint16_t* hot_table, hipStream_t stream) {
+            const uint16_t* hot_table, const uint8_t* chain, hipStream_t stream) {
   if (n_segs == 0) return 0;
   if (!scan_v1_requested()) {
-    if (hot_table == nullptr) return -8;
+    if (hot_table == nullptr || chain == nullptr) return -8;
     if (seg_bytes < 64 || (seg_bytes & (seg_bytes - 1)) != 0) return -1;
     if (log2_classes < 3 || log2_classes > 8) return -2;
     if (num_states > 32768) return -3;
@@ -440,19 +588,37 @@ int ac_scan(const uint8_t* text, int64_t n_segs, int seg_bytes, const uint8_t* c
     // 2.32 TB/s; 2 streams x 32 B 2.02, 1 x 128 B and 2 x 64 B spill registers)
     constexpr int NSv = 1, CHv = 64;
     const int threads = kScanThreads;
-    const void* fn = reinterpret_cast<const void*>(ac_scan_wide_kernel<NSv, CHv>);
+    static const int probe = [] {
+      const char* e = getenv("OAMD_SCAN_PROBE");
+      return e ? atoi(e) : 0;
+    }();
+    const void* fn = probe == 1   ? reinterpret_cast<const void*>(ac_scan_wide_kernel<NSv, CHv, kScanThreads, 1>)
+                     : probe == 2 ? reinterpret_cast<const void*>(ac_scan_wide_kernel<NSv, CHv, kScanThreads, 2>)
+                     : probe == 3 ? reinterpret_cast<const void*>(ac_scan_wide_kernel<NSv, CHv, kScanThreads, 3>)
+                     : probe == 4 ? reinterpret_cast<const void*>(ac_scan_wide_kernel<NSv, CHv, kScanThreads, 4>)
+                     : probe == 5 ? reinterpret_cast<const void*>(ac_scan_wide_kernel<NSv, CHv, kScanThreads, 5>)
+                     : probe == 6 ? reinterpret_cast<const void*>(ac_scan_wide_kernel<NSv, CHv, kScanThreads, 6>)
+                     : probe == 7 ? reinterpret_cast<const void*>(ac_scan_wide_kernel<NSv, CHv, kScanThreads, 7>)
+                     : probe == 8 ? reinterpret_cast<const void*>(ac_scan_wide_kernel<2, 32>)
+                                  : reinterpret_cast<const void*>(ac_scan_wide_kernel<NSv, CHv>);
+    const int NSr = probe == 8 ? 2 : NSv, CHr = probe == 8 ? 32 : CHv;
     static bool attr_set = false;
     if (!attr_set) {
-      if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kWideLds) != hipSuccess) return -6;
+      if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kScanLdsMax) != hipSuccess) return -6;
       attr_set = true;
     }
+    // the chain bytes of the first n_chain states in LDS (the rest from global memory)
+    const int64_t n_chain_all = ((int64_t)num_states + 15) / 16 * 16;
+    const uint32_t n_chain = static_cast<uint32_t>(n_chain_all < kChainLdsMax ? n_chain_all : kChainLdsMax);
+    const int lds_bytes = kWideLds + static_cast<int>(n_chain);
     const int64_t total = n_segs * (int64_t)seg_bytes;
-    const int64_t streams = (int64_t)(grid_blocks > 0 ? grid_blocks : num_cus()) * threads * NSv;
+    const int64_t streams = (int64_t)(grid_blocks > 0 ? grid_blocks : num_cus()) * threads * NSr;
     int64_t L = (total + streams - 1) / streams;
-    L = ((L + CHv - 1) / CHv) * CHv;   // whole chunks (CH = 64 <= seg_bytes)
+    const int64_t Lq = probe == 5 ? 2 * CHr : CHr;
+    L = ((L + Lq - 1) / Lq) * Lq;   // whole chunks (CH = 64 <= seg_bytes)
     if (L < seg_bytes) L = seg_bytes;
     const int64_t n_streams = (total + L - 1) / L;
-    const int64_t per_block = (int64_t)threads * NSv;
+    const int64_t per_block = (int64_t)threads * NSr;
     const int64_t blocks = (n_streams + per_block - 1) / per_block;
     int shift = 0;
     while ((1 << shift) < seg_bytes) ++shift;
@@ -464,8 +630,9 @@ int ac_scan(const uint8_t* text, int64_t n_segs, int seg_bytes, const uint8_t* c
     int l2c = log2_classes;
     void* args[] = {&txt, (void*)&total, &L, (void*)&n_streams, &shift, (void*)&cls_map, &tgp, (void*)&hot_table,
                     &l2c, &H,
-                    (void*)&out_off, (void*)&out_ids, &matches, &match_count, &match_cap, &seg_nl, &seg_head};
-    if (hipLaunchKernel(fn, dim3(static_cast<unsigned>(blocks)), dim3(threads), args, kWideLds, stream) !=
+                    (void*)&out_off, (void*)&out_ids, &matches, &match_count, &match_cap, &seg_nl, &seg_head,
+                    (void*)&chain, (void*)&n_chain};
+    if (hipLaunchKernel(fn, dim3(static_cast<unsigned>(blocks)), dim3(threads), args, lds_bytes, stream) !=
         hipSuccess)
       return -7;
     OAMD_LAUNCH_CHECK();

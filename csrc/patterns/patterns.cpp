@@ -188,6 +188,49 @@ py::dict reorder_dfa(const std::string& table_b, const std::string& out_off_b, c
   for (int64_t i = 0; i < S; ++i) order[i] = static_cast<uint32_t>(i);
   // root first, then by visits (desc), ties in BFS order (stable)
   std::stable_sort(order.begin() + 1, order.end(), [&](uint32_t a, uint32_t b) { return visits[a] > visits[b]; });
+  // The cold states (past the hot prefix) in CHAIN order: a cold excursion is a log
+  // line matching a pattern literal, i.e. a walk down one trie path, one dependent
+  // global-table read per byte in the kernel's exact re-walk. Numbered so that each
+  // state's most-visited trie child (the goto edge: depth + 1) is the next state, the
+  // walk follows `dfa_chain` bytes (16 states per 16-byte read) instead of the table.
+  // Chains start at the shallowest unplaced state (depth = BFS distance from the root).
+  const int64_t H = std::min<int64_t>(std::max(hot, 0), S);
+  if (H < S) {
+    std::vector<int32_t> depth(S, -1);
+    std::vector<uint32_t> bfs;
+    bfs.reserve(S);
+    depth[0] = 0;
+    bfs.push_back(0);
+    for (size_t h = 0; h < bfs.size(); ++h) {
+      const uint32_t s = bfs[h];
+      for (int k = 0; k < C; ++k) {
+        const uint32_t t = tab[static_cast<size_t>(s) * C + k] & 0x7fffu;
+        if (depth[t] < 0) {
+          depth[t] = depth[s] + 1;
+          bfs.push_back(t);
+        }
+      }
+    }
+    std::vector<char> placed(S, 0);
+    for (int64_t i = 0; i < H; ++i) placed[order[i]] = 1;
+    std::vector<uint32_t> heads(order.begin() + H, order.end());
+    std::stable_sort(heads.begin(), heads.end(), [&](uint32_t a, uint32_t b) { return depth[a] < depth[b]; });
+    std::vector<uint32_t> chained(order.begin(), order.begin() + H);
+    for (uint32_t h : heads) {
+      for (uint32_t s = h; !placed[s];) {
+        placed[s] = 1;
+        chained.push_back(s);
+        int64_t best = -1;
+        for (int k = 0; k < C; ++k) {
+          const uint32_t t = tab[static_cast<size_t>(s) * C + k] & 0x7fffu;
+          if (!placed[t] && depth[t] == depth[s] + 1 && (best < 0 || visits[t] > visits[best])) best = t;
+        }
+        if (best < 0) break;
+        s = static_cast<uint32_t>(best);
+      }
+    }
+    order.swap(chained);
+  }
   std::vector<uint32_t> rank(S);
   for (int64_t i = 0; i < S; ++i) rank[order[i]] = static_cast<uint32_t>(i);
   std::string nt(S * C * 2, '\0');
@@ -218,6 +261,29 @@ py::dict reorder_dfa(const std::string& table_b, const std::string& out_off_b, c
   d["hot_after"] = total ? double(hot_after) / double(total) : 1.0;
   d["sampled"] = total;
   return d;
+}
+
+// Per-state chain byte for ac_scan's exact re-walk (csrc/kernels/scan.hip slow_sub):
+// chain[s] = 0x40 | k | (0x80 if s + 1 has outputs) when class k takes s to s + 1, else 0.
+// Only for <= 64 classes (all zero otherwise: the kernel then reads the table). Padded to
+// a multiple of 16 bytes plus 16, so the kernel's aligned 16-byte window reads stay inside.
+py::bytes dfa_chain(const std::string& table_b, int log2c, int64_t num_states) {
+  const int C = 1 << log2c;
+  const int64_t S = num_states;
+  if (static_cast<int64_t>(table_b.size()) != S * C * 2) throw std::invalid_argument("table size mismatch");
+  const auto* tab = reinterpret_cast<const uint16_t*>(table_b.data());
+  std::string ch(static_cast<size_t>((S + 15) / 16 * 16 + 16), '\0');
+  if (C <= 64) {
+    for (int64_t s = 0; s + 1 < S; ++s)
+      for (int k = 0; k < C; ++k) {
+        const uint16_t e = tab[static_cast<size_t>(s) * C + k];
+        if ((e & 0x7fffu) == static_cast<uint32_t>(s + 1)) {
+          ch[s] = static_cast<char>(0x40 | k | ((e & 0x8000u) ? 0x80 : 0));
+          break;
+        }
+      }
+  }
+  return py::bytes(ch);
 }
 
 // Layout: doc i occupies [first_seg[i]*seg, first_seg[i+1]*seg), content then NUL padding (>= 1 byte).
@@ -356,6 +422,7 @@ void register_verify(py::module_& m);   // verify.cpp (N3 / N4)
 PYBIND11_MODULE(_patterns, m) {
   m.doc() = "operator_amd host pattern compiler / packer / scorer";
   m.def("compile_dfa", &compile_dfa, py::arg("factors"));
+  m.def("dfa_chain", &dfa_chain, py::arg("table"), py::arg("log2_classes"), py::arg("num_states"));
   m.def("reorder_dfa", &reorder_dfa, py::arg("table"), py::arg("out_off"), py::arg("out_ids"), py::arg("log2_classes"),
         py::arg("num_states"), py::arg("cls_map"), py::arg("sample"), py::arg("hot"));
   m.def("plan_docs", &plan_docs, py::arg("lens"), py::arg("seg_bytes"));

@@ -13,7 +13,7 @@ namespace {
 void ac_scan(const at::Tensor& text, int64_t seg_bytes, const at::Tensor& cls_map, const at::Tensor& table,
              int64_t log2_classes, int64_t hot_states, const at::Tensor& out_off, const at::Tensor& out_ids,
              at::Tensor& matches, at::Tensor& match_count, at::Tensor& seg_nl, int64_t grid_blocks,
-             const at::Tensor& hot_table) {
+             const at::Tensor& hot_table, const at::Tensor& chain) {
   CHECK_T(text, at::kByte);
   CHECK_T(cls_map, at::kByte);
   CHECK_T(table, at::kShort);
@@ -23,6 +23,7 @@ void ac_scan(const at::Tensor& text, int64_t seg_bytes, const at::Tensor& cls_ma
   CHECK_T(match_count, at::kInt);
   CHECK_T(seg_nl, at::kInt);
   CHECK_T(hot_table, at::kShort);
+  CHECK_T(chain, at::kByte);
   TORCH_CHECK(hot_table.numel() == oamd::kScanHotStates * oamd::kScanHotStride,
               "hot_table must be [256 bytes x 258] (MatchEngine builds it)");
   TORCH_CHECK(seg_bytes >= 64 && (seg_bytes & (seg_bytes - 1)) == 0, "seg_bytes must be a power of two >= 64");
@@ -32,6 +33,8 @@ void ac_scan(const at::Tensor& text, int64_t seg_bytes, const at::Tensor& cls_ma
   TORCH_CHECK(table.dim() == 2 && table.size(1) == C, "table must be [states, 2^log2_classes]");
   const int64_t S = table.size(0);
   TORCH_CHECK(S >= 1 && S <= 32768, "DFA must have 1..32768 states");
+  TORCH_CHECK(chain.numel() >= (S + 15) / 16 * 16 + 16, "chain must have round_up(states, 16) + 16 bytes (dfa_chain)");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(chain.data_ptr()) % 16 == 0, "chain must be 16-byte aligned");
   TORCH_CHECK(out_off.numel() == S + 1, "out_off must have states+1 entries");
   TORCH_CHECK(hot_states >= 1 && hot_states <= S && hot_states <= oamd::max_hot_states((int)log2_classes),
               "hot_states out of range");
@@ -49,7 +52,8 @@ void ac_scan(const at::Tensor& text, int64_t seg_bytes, const at::Tensor& cls_ma
                                reinterpret_cast<oamd::MatchRec*>(matches.data_ptr()),
                                reinterpret_cast<uint32_t*>(match_count.data_ptr()), (uint32_t)matches.size(0),
                                reinterpret_cast<uint32_t*>(seg_nl.data_ptr()), (int)grid_blocks,
-                               reinterpret_cast<const uint16_t*>(hot_table.data_ptr()), c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream());
+                               reinterpret_cast<const uint16_t*>(hot_table.data_ptr()), chain.data_ptr<uint8_t>(),
+                               c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream());
   TORCH_CHECK(rc == 0, "ac_scan launch failed rc=", rc);
 }
 

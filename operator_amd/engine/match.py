@@ -272,8 +272,9 @@ class MatchEngine:
 
     def _build_hot_table(self, table: bytes) -> None:
         """ac_scan v2's LDS image: the first min(S, 256) states as full byte rows,
-        [byte][state] with a 258-entry row stride (csrc/kernels/scan.h)."""
-        from operator_amd.ops import kernels
+        [byte][state] with a 258-entry row stride (csrc/kernels/scan.h); and the per-state
+        chain bytes its exact re-walk follows through cold states (patterns.cpp dfa_chain)."""
+        from operator_amd.ops import kernels, patterns
 
         d = self.cp.dfa
         S, C = int(d["num_states"]), 1 << int(d["log2_classes"])
@@ -284,6 +285,8 @@ class MatchEngine:
         wide = np.zeros((256, stride), dtype=np.uint16)
         wide[:, :H] = tab[:H][:, cls].T
         self.hot_table = torch.from_numpy(wide.view(np.int16).reshape(-1).copy()).to(self.device)
+        chain = patterns().dfa_chain(table, int(d["log2_classes"]), S)
+        self.chain = torch.frombuffer(bytearray(chain), dtype=torch.uint8).to(self.device)
 
     def _profile_states(self, sample: bytes) -> None:
         """Renumber DFA states by how often a walk over ``sample`` visits them, so the
@@ -385,7 +388,7 @@ class MatchEngine:
                 setattr(self, "_count" + sfx, count)
             count.zero_()
             C.ac_scan(text[:total], seg, self.cls_map, self.table, self.log2c, self.hot_states, self.out_off,
-                      self.out_ids, matches, count, seg_nl, self.grid_blocks, self.hot_table)
+                      self.out_ids, matches, count, seg_nl, self.grid_blocks, self.hot_table, self.chain)
             C.line_prefix(seg_nl[:n_segs], excl, lp_state)
             C.scan_fixup(matches, count, excl[:n_segs], first_t, seg, seg_nl[n_segs:2 * n_segs])
             cnt = int(count.item())

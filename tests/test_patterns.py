@@ -174,6 +174,74 @@ def test_reorder_dfa_preserves_matches_and_raises_hot_coverage():
     assert ((t1[0] & 0x8000) == (t2[0] & 0x8000)).all()
 
 
+def _chain_scan(d, chain: bytes, text: bytes, hot: int):
+    """The kernel's exact re-walk (csrc/kernels/scan.hip slow_sub): cold states follow
+    the chain byte when its class matches, the table otherwise."""
+    C = 1 << d["log2_classes"]
+    tab = np.frombuffer(d["table"], dtype=np.uint16).reshape(-1, C)
+    cls = np.frombuffer(d["cls_map"], dtype=np.uint8)
+    ch = np.frombuffer(chain, dtype=np.uint8)
+    s, out, hits = 0, [], 0
+    for i, b in enumerate(text):
+        c = int(cls[b])
+        x = int(ch[s])
+        if s >= hot and (x & 0x40) and (x & 0x3F) == c:
+            e, hits = (s + 1) | ((x & 0x80) << 8), hits + 1
+        else:
+            e = int(tab[s, c])
+        s = e & 0x7FFF
+        if e & 0x8000:
+            out.append((i, s))
+    return out, hits
+
+
+def test_reorder_dfa_chains_cold_states_along_pattern_literals():
+    """Cold states are numbered along trie paths (a state's most-visited goto child is the
+    next state), and dfa_chain's bytes name the class of that step exactly: a walk that
+    follows them equals the table walk, and a failure line's excursion through cold states
+    is mostly chain steps (no table read)."""
+    ps = synthetic_library(200, seed=3)
+    cp = compile_patterns(ps)
+    d = cp.dfa
+    S, l2c = d["num_states"], d["log2_classes"]
+    fac = LogFactory(n_patterns=200, seed=5)
+    sample = b"".join(fac.batch(4, 16 * 1024, n_failures=3)[0])
+    hot = 64
+    r = native_patterns().reorder_dfa(d["table"], d["out_off"], d["out_ids"], l2c, S, d["cls_map"], sample, hot)
+    d2 = dict(d, table=r["table"], out_off=r["out_off"], out_ids=r["out_ids"])
+    chain = native_patterns().dfa_chain(r["table"], l2c, S)
+    assert len(chain) >= (S + 15) // 16 * 16 + 16 and len(chain) % 16 == 0
+    C = 1 << l2c
+    tab = np.frombuffer(r["table"], np.uint16).reshape(-1, C)
+    ch = np.frombuffer(chain, np.uint8)[:S]
+    v = np.nonzero(ch & 0x40)[0]
+    assert len(v) > S // 2
+    assert ((tab[v, ch[v] & 0x3F].astype(np.int64)) == ((v + 1) | ((ch[v].astype(np.int64) & 0x80) << 8))).all()
+    text = b"".join(LogFactory(n_patterns=200, seed=9).batch(3, 8 * 1024, n_failures=3)[0])
+    text += b" ".join(cp.factors[:50])
+    got, hits = _chain_scan(d2, chain, text, hot)
+    want = [(i, e & 0x7FFF) for i, e in ((i, int(x)) for i, x in enumerate(_table_entries(d2, text))) if e & 0x8000]
+    assert got == want
+    assert hits > 0
+    # the unprofiled (BFS) numbering gets valid, if few, chain bytes too
+    ch0 = np.frombuffer(native_patterns().dfa_chain(d["table"], l2c, S), np.uint8)[:S]
+    t0 = np.frombuffer(d["table"], np.uint16).reshape(-1, C)
+    v0 = np.nonzero(ch0 & 0x40)[0]
+    assert ((t0[v0, ch0[v0] & 0x3F] & 0x7FFF).astype(np.int64) == v0 + 1).all()
+
+
+def _table_entries(d, text: bytes):
+    C = 1 << d["log2_classes"]
+    tab = np.frombuffer(d["table"], dtype=np.uint16).reshape(-1, C)
+    cls = np.frombuffer(d["cls_map"], dtype=np.uint8)
+    s, out = 0, []
+    for b in text:
+        e = int(tab[s, cls[b]])
+        out.append(e)
+        s = e & 0x7FFF
+    return out
+
+
 def test_log_factory_injects_signatures_of_the_scanned_library_for_any_seed():
     """Benchmark workload invariance: whatever the factory's seed (bench.py seeds it per
     rank and shard), every injected failure is a signature of synthetic_library(n, 0),

@@ -69,7 +69,7 @@ def bench_scan(n_docs, doc_kb, n_patterns):
     for _ in range(5):
         eng._count.zero_()
         C.ac_scan(eng._text[:tot_pad], seg, eng.cls_map, eng.table, eng.log2c, eng.hot_states, eng.out_off,
-                  eng.out_ids, eng._matches, eng._count, eng._seg_nl, 0, eng.hot_table)
+                  eng.out_ids, eng._matches, eng._count, eng._seg_nl, 0, eng.hot_table, eng.chain)
     ev1.record()
     torch.cuda.synchronize()
     ms = ev0.elapsed_time(ev1) / 5

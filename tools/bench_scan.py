@@ -33,12 +33,12 @@ def kernel_ms(eng, docs, iters):
         for _ in range(2):
             eng._count.zero_()
             C.ac_scan(eng._text[:tot_pad], seg, eng.cls_map, eng.table, eng.log2c, eng.hot_states, eng.out_off,
-                      eng.out_ids, eng._matches, eng._count, eng._seg_nl, eng.grid_blocks, eng.hot_table)
+                      eng.out_ids, eng._matches, eng._count, eng._seg_nl, eng.grid_blocks, eng.hot_table, eng.chain)
         ev0.record()
         for _ in range(iters):
             eng._count.zero_()
             C.ac_scan(eng._text[:tot_pad], seg, eng.cls_map, eng.table, eng.log2c, eng.hot_states, eng.out_off,
-                      eng.out_ids, eng._matches, eng._count, eng._seg_nl, eng.grid_blocks, eng.hot_table)
+                      eng.out_ids, eng._matches, eng._count, eng._seg_nl, eng.grid_blocks, eng.hot_table, eng.chain)
         ev1.record()
     torch.cuda.synchronize()
     return ev0.elapsed_time(ev1) / iters, tot_pad, int(eng._count.item())
@@ -53,6 +53,7 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--arms", default="bfs,profiled")
     ap.add_argument("--pack-sweep", action="store_true")
+    ap.add_argument("--kernel-only", action="store_true", help="print the kernel timing and skip analyze()")
     ap.add_argument("--pipe-sweep", default="0,128,256,400,640",
                     help="MatchEngine.PIPE_SUB_BYTES values (MB; 0 = one batch) timed after the main arm")
     a = ap.parse_args()
@@ -70,6 +71,30 @@ def main():
         key = sorted(map(tuple, raw.tolist()))
         same = None if ref is None else (key == ref)
         ref = ref or key
+        probe_stats = None
+        if os.environ.get("OAMD_SCAN_PROBE") in ("4", "5", "6", "7"):
+            # per-wave {cycles, slow cycles, slow entries, cold wave-steps} (csrc/kernels/scan.hip)
+            cap = eng._matches.shape[0]
+            w = eng._matches[cap // 2: cap // 2 + 196608].cpu().view(torch.int32).numpy().view("uint32").reshape(-1, 12)
+            w = w[w[:, 0] > 0].astype("float64")
+            probe_stats = {"waves": int(w.shape[0]), "cycles_mean": round(float(w[:, 0].mean())),
+                           "cycles_max": round(float(w[:, 0].max())), "slow_cycles_mean": round(float(w[:, 1].mean())),
+                           "slow_cycles_max": round(float(w[:, 1].max())),
+                           "slow_entries_mean": round(float(w[:, 2].mean()), 2), "slow_entries_max": int(w[:, 2].max()),
+                           "cold_steps_mean": round(float(w[:, 3].mean()), 1),
+                           "cycles_per_slow_entry": round(float(w[:, 1].sum() / max(1.0, w[:, 2].sum()))),
+                           "emit_cycles_mean": round(float(w[:, 4].mean())), "emits_mean": round(float(w[:, 5].mean()), 2),
+                           "cycles_per_emit": round(float(w[:, 4].sum() / max(1.0, w[:, 5].sum()))),
+                           "subchunks_mean": round(float(w[:, 6].mean()), 2),
+                           "subchunk_walk_cycles_mean": round(float(w[:, 7].mean())),
+                           "cold_step_cycles_mean": round(float(w[:, 8].mean()))}
+        if a.kernel_only:
+            print(json.dumps({"probe_stats": probe_stats,"bench": "scan_kernel", "arm": arm, "probe": os.environ.get("OAMD_SCAN_PROBE", "0"),
+                              "padded_bytes": tot_pad, "kernel_ms": round(ms, 3),
+                              "kernel_GBps": round(tot_pad / ms / 1e6, 1), "raw_matches": cnt,
+                              "same_matches_as_first_arm": same}), flush=True)
+            del eng
+            continue
         t1 = time.perf_counter()
         res = eng.analyze(docs)
         t2 = time.perf_counter()
