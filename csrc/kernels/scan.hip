@@ -226,7 +226,8 @@ __device__ __forceinline__ uint32_t newline_bits(uint32_t w) {
 // the exact re-walk, 3 = a VALU-only chain (no LDS); 4 = the real kernel with per-wave
 // slow-path statistics, 5 = 4 + second-half-of-line text loads nontemporal, 6 = 4 +
 // the slow path at raised wave priority (s_setprio), 7 = 4 + the re-walk block entered
-// after every chunk (its non-walk code kept hot).
+// after every chunk (its non-walk code kept hot), 8 = two streams of 32-byte chunks per
+// lane, 9 = the real kernel with the slow path at raised wave priority.
 template <int NS, int CH, int NT = kScanThreads, int PROBE = 0>
 __global__ void __launch_bounds__(NT) ac_scan_wide_kernel(
     const uint8_t* __restrict__ text, int64_t total, int64_t L, int64_t n_streams, int seg_shift,
@@ -235,6 +236,7 @@ __global__ void __launch_bounds__(NT) ac_scan_wide_kernel(
     MatchRec* __restrict__ matches, uint32_t* __restrict__ count, uint32_t cap, uint32_t* __restrict__ seg_nl,
     uint32_t* __restrict__ seg_head, const uint8_t* __restrict__ chain, uint32_t n_chain_lds) {
   constexpr int NV = CH / 16;  // 16-B loads per stream per chunk
+  constexpr bool STATS = PROBE >= 4 && PROBE <= 7;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* cls = smem;
   uint16_t* tl = reinterpret_cast<uint16_t*>(smem + 256);
@@ -257,9 +259,9 @@ __global__ void __launch_bounds__(NT) ac_scan_wide_kernel(
 
   int64_t pos[NS], end[NS];
   uint32_t st[NS], nl[NS], mid = 0, act = 0;
-  uint64_t t_begin = 0, t_slow = 0, t_sub = 0;   // PROBE >= 4: per-wave slow-path statistics
+  uint64_t t_begin = 0, t_slow = 0, t_sub = 0;   // STATS (PROBE 4-7): per-wave slow-path statistics
   uint32_t n_slow = 0, n_cold = 0, n_emit = 0, n_sub = 0, t_emit = 0, t_cold = 0;
-  if constexpr (PROBE >= 4) t_begin = clock64();
+  if constexpr (STATS) t_begin = clock64();
 #pragma unroll
   for (int k = 0; k < NS; ++k) {
     const int64_t b0 = (k0 + k) * L;
@@ -316,7 +318,7 @@ __global__ void __launch_bounds__(NT) ac_scan_wide_kernel(
         uint32_t e = tl[b * kWideStride + (sk & 0xffu)];
         if (__ballot(sk >= Hs)) {
           uint64_t tc = 0;
-          if constexpr (PROBE >= 4) tc = clock64();
+          if constexpr (STATS) tc = clock64();
           // A cold state is usually one step down a pattern literal's trie path, numbered
           // so that the path's next state is sk + 1 (csrc/patterns/patterns.cpp
           // reorder_dfa): the chain byte (LDS, the rest of the CU's 160 KB) says which
@@ -336,7 +338,7 @@ __global__ void __launch_bounds__(NT) ac_scan_wide_kernel(
               e = (reinterpret_cast<const uint32_t*>(tg)[gi >> 1] >> ((gi & 1u) << 4)) & 0xffffu;
             }
           }
-          if constexpr (PROBE >= 4) {   // per lane: cold steps and their cycles
+          if constexpr (STATS) {   // per lane: cold steps and their cycles
             if (sk >= Hs) {
               ++n_cold;
               t_cold += static_cast<uint32_t>(clock64() - tc) + (e & 0u);
@@ -350,7 +352,7 @@ __global__ void __launch_bounds__(NT) ac_scan_wide_kernel(
       const uint32_t nlb = newline_bits(wv);
       if (__ballot(own && omask != 0)) {
         uint64_t te = 0;
-        if constexpr (PROBE >= 4) te = clock64();
+        if constexpr (STATS) te = clock64();
 #pragma unroll 1
         for (int by = 0; by < 4; ++by) {
           const bool hit = own && (omask >> by & 1u);
@@ -365,7 +367,7 @@ __global__ void __launch_bounds__(NT) ac_scan_wide_kernel(
                               out_ids, matches, count, cap);
           }
         }
-        if constexpr (PROBE >= 4) {   // per lane (the emitting lanes)
+        if constexpr (STATS) {   // per lane (the emitting lanes)
           if (own && omask != 0) {
             t_emit += static_cast<uint32_t>(clock64() - te);
             n_emit += __builtin_popcount(omask);
@@ -442,8 +444,8 @@ __global__ void __launch_bounds__(NT) ac_scan_wide_kernel(
     for (int k = 0; k < NS; ++k) any |= fl[k];
     if (__ballot(any != 0)) {
       uint64_t t0 = 0;
-      if constexpr (PROBE >= 4) t0 = clock64();
-      if constexpr (PROBE == 6) __builtin_amdgcn_s_setprio(3);
+      if constexpr (STATS) t0 = clock64();
+      if constexpr (PROBE == 6 || PROBE == 9) __builtin_amdgcn_s_setprio(3);
 #pragma unroll   // compile-time k and v: a runtime index would put st[]/sv[] in scratch
       for (int k = 0; k < NS; ++k) {
         if (PROBE != 7 && !__ballot(fl[k] != 0)) continue;
@@ -457,7 +459,7 @@ __global__ void __launch_bounds__(NT) ac_scan_wide_kernel(
           const bool need = fl[k] != 0 && (!sync || (fl[k] >> v & 1u));
           if (__ballot(need)) {
             uint64_t tw = 0;
-            if constexpr (PROBE >= 4) {
+            if constexpr (STATS) {
               ++n_sub;
               tw = clock64();
             }
@@ -465,7 +467,7 @@ __global__ void __launch_bounds__(NT) ac_scan_wide_kernel(
               s = slow_sub(k, q, pos[k] + delta + 16 * v, sync ? sa : s, nlr, ownk);
               sync = s == sb;
             }
-            if constexpr (PROBE >= 4) t_sub += __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(clock64() - tw));
+            if constexpr (STATS) t_sub += __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(clock64() - tw));
           }
           if (ownk) {
 #pragma unroll
@@ -474,8 +476,8 @@ __global__ void __launch_bounds__(NT) ac_scan_wide_kernel(
         }
         if (!sync) st[k] = s;
       }
-      if constexpr (PROBE == 6) __builtin_amdgcn_s_setprio(0);
-      if constexpr (PROBE >= 4) {
+      if constexpr (PROBE == 6 || PROBE == 9) __builtin_amdgcn_s_setprio(0);
+      if constexpr (STATS) {
         t_slow += clock64() - t0;
         ++n_slow;
       }
@@ -521,7 +523,7 @@ __global__ void __launch_bounds__(NT) ac_scan_wide_kernel(
         for (int v = 0; v < NV; ++v) cur[k][v] = nxt[k][v];
     }
   }
-  if constexpr (PROBE >= 4) {
+  if constexpr (STATS) {
     // per-wave {cycles, slow-path cycles, slow-path entries, cold wave-steps, emission
     // cycles, emissions, re-walked sub-chunks, sub-chunk walk cycles, cold-step cycles, 0, 0, 0}
     // in the
@@ -600,6 +602,7 @@ int ac_scan(const uint8_t* text, int64_t n_segs, int seg_bytes, const uint8_t* c
                      : probe == 6 ? reinterpret_cast<const void*>(ac_scan_wide_kernel<NSv, CHv, kScanThreads, 6>)
                      : probe == 7 ? reinterpret_cast<const void*>(ac_scan_wide_kernel<NSv, CHv, kScanThreads, 7>)
                      : probe == 8 ? reinterpret_cast<const void*>(ac_scan_wide_kernel<2, 32>)
+                     : probe == 9 ? reinterpret_cast<const void*>(ac_scan_wide_kernel<NSv, CHv, kScanThreads, 9>)
                                   : reinterpret_cast<const void*>(ac_scan_wide_kernel<NSv, CHv>);
     const int NSr = probe == 8 ? 2 : NSv, CHr = probe == 8 ? 32 : CHv;
     static bool attr_set = false;

@@ -142,6 +142,10 @@ def main():
         load += np.roll(colmass, bo)
     rb = rowbank
     run("perm", lambda b, s, l: b * 256 + ((rb[b] + (s >> 1)) % 32) + 32 * ((s >> 1) // 32))
+    cl = cls
+    fold = np.arange(256); fold[65:91] += 32
+    run("row_fold", lambda b, s, l: (fold[b] * 258 + s) >> 1)
+    run("row_class", lambda b, s, l: (cl[b] * 258 + s) >> 1)
     res["private"] = 0.0
     print(json.dumps(res))
 
