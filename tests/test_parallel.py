@@ -175,7 +175,7 @@ def test_bench_two_ranks_gloo(shards, apiserver):
     assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 6 * shards and out["config"]["parallelism"] == "dp2"
     assert out["config"]["operator_shards_per_gpu"] == shards
     assert out["detail"]["outcomes"] == {"ai-complete": 6 * shards} and out["value"] > 0
-    assert out["config"]["apiserver"].startswith("one REST API server" if apiserver == "auto" else "in-process")
+    assert out["config"]["apiserver"].startswith("1 REST API server process(es)" if apiserver == "auto" else "in-process")
 
 
 def test_bench_eight_ranks_gloo_one_apiserver():
