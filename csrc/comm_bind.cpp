@@ -128,7 +128,7 @@ class CustomAllReduce {
   void reset() {
     TORCH_CHECK(base_ != nullptr, "CustomAllReduce: closed");
     const c10::hip::HIPGuardMasqueradingAsCUDA g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device_));
-    TORCH_CHECK(oamd::car_reset(base_, herr_) == 0, "CustomAllReduce.reset failed");
+    TORCH_CHECK(oamd::car_reset(base_, oamd::car_buffer_bytes((size_t)cap_, (int)world_), herr_) == 0, "CustomAllReduce.reset failed");
   }
 
   void close() {

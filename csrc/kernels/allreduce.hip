@@ -180,6 +180,47 @@ __device__ __forceinline__ void sum_slots(float* a, __amdgpu_buffer_rsrc_t rm, i
   for (int p = 0; p < W; ++p) acc8(a, x[p], is_bf16);
 }
 
+// LL (flag-in-data) one-shot: a 16-B vector travels as two 16-B packets
+// {d0, round, d1, round}, {d2, round, d3, round}, so a consumer that sees the round in
+// both flag words of a packet has its data -- no store-completion wait, barrier, flag
+// store and flag poll between the push and the reduce (each 8-B half is written whole;
+// a torn packet shows a stale flag and is re-read). Packets 2v, 2v+1 of a slot hold
+// vector v, so a slot holds half as many vectors as with the flag protocol. Slots
+// alternate parity per round as before, so a stale packet carries round - 2.
+__device__ __forceinline__ void ll_st(__amdgpu_buffer_rsrc_t r, int par, int W, int src, int64_t capvec, int64_t v,
+                                      uint4 x, uint32_t round) {
+  car::st16(r, car::slot_off(par, W, src, capvec, 2 * v), make_uint4(x.x, round, x.y, round));
+  car::st16(r, car::slot_off(par, W, src, capvec, 2 * v + 1), make_uint4(x.z, round, x.w, round));
+}
+// Vector v of slot `src`, polled until both packets carry `round` (bounded: *err set and
+// whatever was read returned when the wall clock passes `deadline`).
+__device__ __forceinline__ uint4 ll_ld(__amdgpu_buffer_rsrc_t rm, int par, int W, int src, int64_t capvec, int64_t v,
+                                       uint32_t round, uint64_t deadline, uint32_t* err) {
+  uint4 a = car::ld16(rm, car::slot_off(par, W, src, capvec, 2 * v));
+  uint4 b = car::ld16(rm, car::slot_off(par, W, src, capvec, 2 * v + 1));
+  while ((a.y != round) | (a.w != round) | (b.y != round) | (b.w != round)) {
+    if ((uint64_t)wall_clock64() > deadline) {
+      *err = 1;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+    a = car::ld16(rm, car::slot_off(par, W, src, capvec, 2 * v));
+    b = car::ld16(rm, car::slot_off(par, W, src, capvec, 2 * v + 1));
+  }
+  return make_uint4(a.x, a.z, b.x, b.z);
+}
+template <int W>
+__device__ __forceinline__ void ll_sum_slots(float* a, __amdgpu_buffer_rsrc_t rm, int par, int64_t capvec, int64_t v,
+                                             bool is_bf16, uint32_t round, uint64_t deadline, uint32_t* err) {
+  uint4 x[W];
+#pragma unroll
+  for (int p = 0; p < W; ++p) x[p] = ll_ld(rm, par, W, p, capvec, v, round, deadline, err);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a[i] = 0.f;
+#pragma unroll
+  for (int p = 0; p < W; ++p) acc8(a, x[p], is_bf16);
+}
+
 // Call prologue shared by every kernel: this block's round, and whether an earlier
 // call left the sticky error.
 struct CarCall {
@@ -209,8 +250,9 @@ __device__ __forceinline__ void car_end(char* mine, int b, int tid, uint32_t rou
   if (tid == 0) reinterpret_cast<uint32_t*>(mine + car::kRoundsOff)[b] = round;
 }
 
-// Plain all-reduce, one 16-B vector = 8 bf16 or 4 fp32 elements. TWO: two-shot.
-template <int W, bool BF16, bool TWO, bool LIGHT>
+// Plain all-reduce, one 16-B vector = 8 bf16 or 4 fp32 elements. TWO: two-shot; LL:
+// one-shot with the flags in the data packets.
+template <int W, bool BF16, bool TWO, bool LIGHT, bool LL = false>
 __global__ void __launch_bounds__(car::kThreads) allreduce_kernel(const uint4* __restrict__ in,
                                                                   uint4* __restrict__ out, int64_t nvec,
                                                                   int64_t capvec, int rank, CarPeers peers,
@@ -231,6 +273,25 @@ __global__ void __launch_bounds__(car::kThreads) allreduce_kernel(const uint4* _
   for (int p = 0; p < W; ++p) rs[p] = car::rsrc(peers.base[p]);
   const __amdgpu_buffer_rsrc_t rm = car::rsrc(mine);
   const int64_t pq = (v1 - v0 + W - 1) / W;   // two-shot piece per owner
+  if constexpr (LL) {
+    const uint64_t deadline = (uint64_t)wall_clock64() + timeout_ticks;
+#pragma unroll
+    for (int p = 0; p < W; ++p)
+      for (int64_t v = v0 + tid; v < v1; v += car::kThreads) ll_st(rs[p], c.par, W, rank, capvec, v, in[v], c.round);
+    for (int64_t v = v0 + tid; v < v1; v += car::kThreads) {
+      float a[8];
+      ll_sum_slots<W>(a, rm, c.par, capvec, v, BF16, c.round, deadline, &s_err);
+      out[v] = pack8(a, BF16);
+    }
+    __syncthreads();
+    if (s_err) {
+      car_fail(mine, b, tid, c.round, herr);
+      poison<BF16>(out, v0, v1, tid);
+      return;
+    }
+    car_end(mine, b, tid, c.round);
+    return;
+  }
   // ---- push: one-shot: the whole range into slot [par][rank] of every rank;
   //      two-shot: piece q into rank q's slot [par][rank]
 #pragma unroll
@@ -287,7 +348,7 @@ __global__ void __launch_bounds__(car::kThreads) allreduce_kernel(const uint4* _
 // (bit-identical to splitk_reduce_fp32 + the bf16 path, one kernel fewer).
 // Q8: also emit the normalised rows as per-row e4m3fn (q8, sx) for the next fp8 GEMM,
 // bit-identical to quantize_fp8(y) — the activation quantization kernel disappears.
-template <int W, int MAXV, bool SLABS, bool Q8, bool TWO, bool LIGHT>
+template <int W, int MAXV, bool SLABS, bool Q8, bool TWO, bool LIGHT, bool LL = false>
 __global__ void __launch_bounds__(car::kThreads) ar_rmsnorm_kernel(
     const uint4* __restrict__ in, const float* __restrict__ slabs, int S, bf16_t* __restrict__ residual,
     const bf16_t* __restrict__ w, bf16_t* __restrict__ y, uint8_t* __restrict__ q8, float* __restrict__ sx,
@@ -352,10 +413,19 @@ __global__ void __launch_bounds__(car::kThreads) ar_rmsnorm_kernel(
     }
   };
   const int64_t pq = (v1 - v0 + W - 1) / W;
+  const uint64_t deadline = (uint64_t)wall_clock64() + timeout_ticks;   // LL polls
+  if constexpr (LL) {
+    for (int64_t v = v0 + tid; v < v1; v += car::kThreads) {
+      const uint4 x = load_x(v);
 #pragma unroll
-  for (int p = 0; p < W; ++p) {
-    const int64_t a = TWO ? min(v1, v0 + p * pq) : v0, e = TWO ? min(v1, a + pq) : v1;
-    for (int64_t v = a + tid; v < e; v += car::kThreads) car::st16(rs[p], car::slot_off(c.par, W, rank, capvec, v), load_x(v));
+      for (int p = 0; p < W; ++p) ll_st(rs[p], c.par, W, rank, capvec, v, x, c.round);
+    }
+  } else {
+#pragma unroll
+    for (int p = 0; p < W; ++p) {
+      const int64_t a = TWO ? min(v1, v0 + p * pq) : v0, e = TWO ? min(v1, a + pq) : v1;
+      for (int64_t v = a + tid; v < e; v += car::kThreads) car::st16(rs[p], car::slot_off(c.par, W, rank, capvec, v), load_x(v));
+    }
   }
   // the first row's residual and weight vectors, loaded while the hand-off is in flight
   // (they do not depend on it): one memory round trip off the critical path
@@ -372,12 +442,14 @@ __global__ void __launch_bounds__(car::kThreads) ar_rmsnorm_kernel(
       }
     }
   }
-  car::publish<W, LIGHT>(peers, car::kFlagsOff, b, rank, c.round, tid);
-  car::wait_all<W, LIGHT>(mine, car::kFlagsOff, b, c.round, timeout_ticks, tid, &s_err);
-  if (s_err) {
-    car_fail(mine, b, tid, c.round, herr);
-    fail_out();
-    return;
+  if constexpr (!LL) {
+    car::publish<W, LIGHT>(peers, car::kFlagsOff, b, rank, c.round, tid);
+    car::wait_all<W, LIGHT>(mine, car::kFlagsOff, b, c.round, timeout_ticks, tid, &s_err);
+    if (s_err) {
+      car_fail(mine, b, tid, c.round, herr);
+      fail_out();
+      return;
+    }
   }
   if constexpr (TWO) {
     const int64_t a0 = min(v1, v0 + rank * pq), e0 = min(v1, a0 + pq);
@@ -413,7 +485,10 @@ __global__ void __launch_bounds__(car::kThreads) ar_rmsnorm_kernel(
           for (int j = 0; j < 8; ++j) a[j] = 0.f;
           acc8(a, x, true);
         } else {
-          sum_slots<W>(a, rm, c.par, capvec, g, true);
+          if constexpr (LL)
+            ll_sum_slots<W>(a, rm, c.par, capvec, g, true, c.round, deadline, &s_err);
+          else
+            sum_slots<W>(a, rm, c.par, capvec, g, true);
 #pragma unroll
           for (int j = 0; j < 8; ++j) a[j] = bf2f(f2bf(a[j]));
         }
@@ -425,10 +500,29 @@ __global__ void __launch_bounds__(car::kThreads) ar_rmsnorm_kernel(
           v[i][j] = bf2f(s[j]);
           ss += v[i][j] * v[i][j];
         }
-        hr[vi] = s;
+        if constexpr (!LL) hr[vi] = s;
       }
     }
     const float tot = block_sum<car::kThreads>(ss, scratch);
+    if constexpr (LL) {
+      // a peer that never arrived: nothing of this row reaches the residual (the
+      // block's barrier in block_sum orders every lane's s_err write before this read)
+      if (s_err) {
+        car_fail(mine, b, tid, c.round, herr);
+        fail_out();
+        return;
+      }
+#pragma unroll
+      for (int i = 0; i < MAXV; ++i) {
+        const int vi = tid + i * car::kThreads;
+        if (vi < nvr) {
+          u16x8 s;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) s[j] = f2bf(v[i][j]);
+          hr[vi] = s;
+        }
+      }
+    }
     const float rs_ = rsqrtf(tot / static_cast<float>(hidden) + eps);
 #pragma unroll
     for (int i = 0; i < MAXV; ++i) {
@@ -524,11 +618,12 @@ void car_free_host_flag(uint32_t* host) {
 
 int car_error(const uint32_t* host) { return (int)__atomic_load_n(host, __ATOMIC_ACQUIRE); }
 
-int car_reset(void* base, uint32_t* host) {
+int car_reset(void* base, size_t bytes, uint32_t* host) {
   // flags, rounds and err back to zero; only meaningful when EVERY rank resets
-  // between two barriers with no call in flight (a collective restart)
+  // between two barriers with no call in flight (a collective restart). The data slots
+  // too: rounds restart at 1, and an LL packet left from before must not carry a live round.
   hipError_t e = hipDeviceSynchronize();
-  if (e == hipSuccess) e = hipMemset(base, 0, car::kDataOff);
+  if (e == hipSuccess) e = hipMemset(base, 0, bytes > car::kDataOff ? bytes : car::kDataOff);
   if (e == hipSuccess) e = hipDeviceSynchronize();
   if (host != nullptr) __atomic_store_n(host, 0u, __ATOMIC_RELEASE);
   return (int)e;
@@ -543,20 +638,22 @@ int car_all_reduce(const void* in, void* out, int64_t bytes, bool bf16, int rank
   if (bytes % 16 != 0 || (size_t)bytes > cap_bytes || cap_bytes % 16 != 0) return -2;
   if (blocks < 1 || blocks > car::kMaxBlocks) return -3;
   if ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15) return -4;
-  if (proto < kCarOneShot || proto > kCarOneShotFence) return -6;
+  if (proto < kCarOneShot || proto > kCarLL) return -6;
   if (world == 1 && proto == kCarTwoShot) proto = kCarOneShot;
+  if (proto == kCarLL && (size_t)bytes * 2 > cap_bytes) return -7;   // LL packets: twice the bytes
   CarPeers peers{};
   for (int p = 0; p < world; ++p) peers.base[p] = static_cast<char*>(bases[p]);
   const int64_t nvec = bytes / 16, capvec = cap_bytes / 16;
   const uint4* i4 = static_cast<const uint4*>(in);
   uint4* o4 = static_cast<uint4*>(out);
   const uint64_t ticks = timeout_s > 0 ? (uint64_t)(timeout_s * 1e8) : car::kDefaultTimeoutTicks;
-#define OAMD_CARP(W, B, T, L) \
-  allreduce_kernel<W, B, T, L><<<blocks, car::kThreads, 0, stream>>>(i4, o4, nvec, capvec, rank, peers, herr_dev, ticks)
+#define OAMD_CARP(W, B, T, L, LLP) \
+  allreduce_kernel<W, B, T, L, LLP><<<blocks, car::kThreads, 0, stream>>>(i4, o4, nvec, capvec, rank, peers, herr_dev, ticks)
 #define OAMD_CARD(W, B)                                    \
-  if (proto == kCarTwoShot) OAMD_CARP(W, B, (W > 1), true); \
-  else if (proto == kCarOneShot) OAMD_CARP(W, B, false, true); \
-  else OAMD_CARP(W, B, false, false);
+  if (proto == kCarTwoShot) OAMD_CARP(W, B, (W > 1), true, false); \
+  else if (proto == kCarOneShot) OAMD_CARP(W, B, false, true, false); \
+  else if (proto == kCarLL) OAMD_CARP(W, B, false, true, true); \
+  else OAMD_CARP(W, B, false, false, false);
 #define OAMD_CAR(W)                 \
   case W:                           \
     if (bf16) { OAMD_CARD(W, true) } \
@@ -593,8 +690,9 @@ int car_all_reduce_rmsnorm(const void* in, const float* slabs, int S, bf16_t* re
   if ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(slabs) | reinterpret_cast<uintptr_t>(residual) |
        reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(y) | reinterpret_cast<uintptr_t>(q8)) & 15)
     return -4;
-  if (proto < kCarOneShot || proto > kCarOneShotFence) return -6;
+  if (proto < kCarOneShot || proto > kCarLL) return -6;
   if (world == 1 && proto == kCarTwoShot) proto = kCarOneShot;
+  if (proto == kCarLL && (size_t)rows * hidden * 2 * 2 > cap_bytes) return -7;   // LL packets: twice the bytes
   CarPeers peers{};
   for (int p = 0; p < world; ++p) peers.base[p] = static_cast<char*>(bases[p]);
   const int64_t capvec = cap_bytes / 16;
@@ -602,13 +700,14 @@ int car_all_reduce_rmsnorm(const void* in, const float* slabs, int S, bf16_t* re
   const uint64_t ticks = timeout_s > 0 ? (uint64_t)(timeout_s * 1e8) : car::kDefaultTimeoutTicks;
   const bool big = hidden > car::kThreads * 8 * 2;
   const int mode = (slabs != nullptr ? 1 : 0) | (q8 != nullptr ? 2 : 0);
-#define OAMD_CARK(W, MV, SL, Q, T, L)                                                                          \
-  ar_rmsnorm_kernel<W, MV, SL, Q, T, L><<<blocks, car::kThreads, 0, stream>>>(                                 \
+#define OAMD_CARK(W, MV, SL, Q, T, L, LLP)                                                                     \
+  ar_rmsnorm_kernel<W, MV, SL, Q, T, L, LLP><<<blocks, car::kThreads, 0, stream>>>(                            \
       i4, slabs, S, residual, w, y, q8, sx, rows, hidden, eps, capvec, rank, peers, herr_dev, ticks)
 #define OAMD_CARP(W, MV, SL, Q)                                                                                \
-  if (proto == kCarTwoShot) OAMD_CARK(W, MV, SL, Q, (W > 1), true);                                            \
-  else if (proto == kCarOneShot) OAMD_CARK(W, MV, SL, Q, false, true);                                         \
-  else OAMD_CARK(W, MV, SL, Q, false, false);
+  if (proto == kCarTwoShot) OAMD_CARK(W, MV, SL, Q, (W > 1), true, false);                                     \
+  else if (proto == kCarOneShot) OAMD_CARK(W, MV, SL, Q, false, true, false);                                  \
+  else if (proto == kCarLL) OAMD_CARK(W, MV, SL, Q, false, true, true);                                        \
+  else OAMD_CARK(W, MV, SL, Q, false, false, false);
 #define OAMD_CARM(W, MV)                                                                                       \
   switch (mode) {                                                                                              \
     case 0: { OAMD_CARP(W, MV, false, false) } break;                                                          \

@@ -127,14 +127,14 @@ int car_free(void* base);
 int car_host_flag(uint32_t** host, uint32_t** dev);   // host-mapped error word (read without a device sync)
 void car_free_host_flag(uint32_t* host);
 int car_error(const uint32_t* host);
-int car_reset(void* base, uint32_t* host);
+int car_reset(void* base, size_t bytes, uint32_t* host);
 // Fused one-shot all-reduce + residual add + RMSNorm (bf16 rows of `hidden`, hidden % 8 == 0, <= 16384):
 // residual += bf16(sum over ranks of in); y = rmsnorm(residual) * w. Exactly one of `in` (bf16 rows) and
 // `slabs` (S fp32 split-K slabs [S, rows, hidden], summed then bf16-rounded) is non-null; q8/sx non-null
 // also emit per-row e4m3fn of y (== quantize_fp8_rows(y)).
 // all-reduce protocols (allreduce.hip): one-shot / two-shot (reduce-scatter + all-gather)
 // with sc0 sc1 hand-offs, and the original system-fence one-shot (A/B)
-constexpr int kCarOneShot = 0, kCarTwoShot = 1, kCarOneShotFence = 2;
+constexpr int kCarOneShot = 0, kCarTwoShot = 1, kCarOneShotFence = 2, kCarLL = 3;
 int car_all_reduce_rmsnorm(const void* in, const float* slabs, int S, bf16_t* residual, const bf16_t* w, bf16_t* y,
                            uint8_t* q8, float* sx, int rows, int hidden, float eps, int rank, int world,
                            void* const* bases, size_t cap_bytes, int blocks, uint32_t* herr_dev, double timeout_s,

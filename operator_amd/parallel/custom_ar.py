@@ -23,8 +23,13 @@ same table on every rank, which the protocol choice must be (a rank on RCCL whil
 waits in a one-shot kernel is a deadlock). Without calibration (``engine.oneshot_max_kb`` > 0
 as an override, or a forced protocol) messages up to ``oneshot_max_bytes`` go one-shot,
 larger ones two-shot, up to ``max_bytes`` (``engine.oneshot_allreduce_mb``); above that
-``Group.all_reduce_`` keeps using RCCL. OAMD_CAR_PROTOCOL = oneshot / twoshot / fence forces
+``Group.all_reduce_`` keeps using RCCL. OAMD_CAR_PROTOCOL = oneshot / twoshot / fence / ll forces
 one protocol (fence: the original system-fence one-shot hand-off, for A/B).
+
+* LL (flag-in-data one-shot): each 16-B vector travels as two packets that carry the call's
+  round in their flag words, so the consumer polls the data itself -- no store-completion
+  wait, barrier, flag store and flag poll between push and reduce; twice the bytes on the
+  link, so it competes for the small decode messages (up to half the buffer capacity).
 
 Set-up exchanges the 64-byte hipIpc handles over the process group (any
 backend: gloo in tests, RCCL in production).
@@ -46,9 +51,10 @@ class CollectiveTimeout(RuntimeError):
 
 DEFAULT_MAX_BYTES = 8 << 20   # 256 tokens x 8192 x 2 B (70B hidden) = 4 MB, with room
 DEFAULT_ONESHOT_MAX_BYTES = 512 << 10   # uncalibrated: one-shot up to here, two-shot above
-PROTO_ONESHOT, PROTO_TWOSHOT, PROTO_FENCE = 0, 1, 2   # csrc/kernels/kernels.h kCar*
+PROTO_ONESHOT, PROTO_TWOSHOT, PROTO_FENCE, PROTO_LL = 0, 1, 2, 3   # csrc/kernels/kernels.h kCar*
 PROTO_BACKEND = -1   # the group's own all-reduce (RCCL): the IPC kernels step aside
-PROTO_NAMES = {PROTO_ONESHOT: "oneshot", PROTO_TWOSHOT: "twoshot", PROTO_FENCE: "fence", PROTO_BACKEND: "backend"}
+PROTO_NAMES = {PROTO_ONESHOT: "oneshot", PROTO_TWOSHOT: "twoshot", PROTO_FENCE: "fence", PROTO_LL: "ll",
+               PROTO_BACKEND: "backend"}
 
 
 def choose_protocols(sizes: list[int], times: dict[int, list[float]], margin: float = 0.03) -> list[tuple[int, int]]:
@@ -64,7 +70,7 @@ def choose_protocols(sizes: list[int], times: dict[int, list[float]], margin: fl
     table: list[tuple[int, int]] = []
     for k, size in enumerate(sizes):
         best, best_t = None, float("inf")
-        for p in (PROTO_ONESHOT, PROTO_TWOSHOT):
+        for p in (PROTO_LL, PROTO_ONESHOT, PROTO_TWOSHOT):
             t = times.get(p, [float("inf")] * len(sizes))[k]
             if t == t and t < best_t:   # skips NaN
                 best, best_t = p, t
@@ -87,7 +93,7 @@ def lookup_protocol(table: list[tuple[int, int]], nbytes: int) -> int:
         if nbytes <= bound:
             return p
     return table[-1][1]
-_FORCED = {"oneshot": PROTO_ONESHOT, "twoshot": PROTO_TWOSHOT, "fence": PROTO_FENCE}
+_FORCED = {"oneshot": PROTO_ONESHOT, "twoshot": PROTO_TWOSHOT, "fence": PROTO_FENCE, "ll": PROTO_LL}
 # workgroups of every one-shot call (fixed per group: each block keeps its own round
 # counter and data-slot parity, so every call of a group must use the same count)
 DEFAULT_BLOCKS = int(os.environ.get("OAMD_CAR_BLOCKS", "64"))   # 64 vs 32: 7.15 vs 7.63 ms TP8-sim step (profiles/tp8_car_blocks_r5.jsonl)
@@ -129,10 +135,14 @@ class OneShotAllReduce:
         """Protocol for a message of ``nbytes``: the forced one, the calibrated table's, or
         one-shot up to ``oneshot_max_bytes`` and two-shot above. PROTO_BACKEND = RCCL."""
         if self.forced is not None:
-            return self.forced
-        if self.table:
-            return lookup_protocol(self.table, nbytes)
-        return PROTO_ONESHOT if nbytes <= self.oneshot_max_bytes else PROTO_TWOSHOT
+            p = self.forced
+        elif self.table:
+            p = lookup_protocol(self.table, nbytes)
+        else:
+            p = PROTO_ONESHOT if nbytes <= self.oneshot_max_bytes else PROTO_TWOSHOT
+        if p == PROTO_LL and 2 * nbytes > self.max_bytes:   # LL packets carry half their bytes as flags
+            p = PROTO_ONESHOT
+        return p
 
     def fits(self, t: torch.Tensor) -> bool:
         nbytes = t.numel() * t.element_size()
@@ -157,7 +167,7 @@ class OneShotAllReduce:
         if not sizes:
             return {}
         forced, self.forced = self.forced, None
-        protos = [PROTO_ONESHOT, PROTO_TWOSHOT] + ([PROTO_BACKEND] if backend and self.world > 1 else [])
+        protos = [PROTO_LL, PROTO_ONESHOT, PROTO_TWOSHOT] + ([PROTO_BACKEND] if backend and self.world > 1 else [])
         res = torch.full((len(protos), len(sizes)), float("nan"), dtype=torch.float64)
         buf = torch.zeros(sizes[-1] // 2, dtype=torch.bfloat16, device=self.device)
 
@@ -168,6 +178,8 @@ class OneShotAllReduce:
         for k, size in enumerate(sizes):
             t = buf[: size // 2]
             for pi, p in enumerate(protos):
+                if p == PROTO_LL and 2 * size > self.max_bytes:
+                    continue   # beyond LL capacity: stays NaN (unavailable)
                 if p == PROTO_BACKEND:
                     call = (lambda t=t: dist.all_reduce(t, group=self.group.pg))
                 else:

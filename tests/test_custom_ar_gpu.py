@@ -140,11 +140,12 @@ def _worker(rank: int, world: int, port: int, q, protocol: str = "auto") -> None
         q.put((rank, "error", traceback.format_exc()))
 
 
-@pytest.mark.parametrize("protocol", ["auto", "oneshot", "twoshot", "fence"])
+@pytest.mark.parametrize("protocol", ["auto", "oneshot", "twoshot", "fence", "ll"])
 def test_oneshot_allreduce_two_ranks_one_gpu(protocol):
     """Every protocol (auto: one-shot up to 512 KB, two-shot above; each forced; the
-    original system-fence one-shot) gives the exact fp32-in-rank-order sums, fused
-    epilogues included, interleaved on the same per-block round counters."""
+    original system-fence one-shot; LL flag-in-data packets, one-shot past their half-
+    capacity limit) gives the exact fp32-in-rank-order sums, fused epilogues included,
+    interleaved on the same per-block round counters."""
     import torch.multiprocessing as mp
 
     if not torch.cuda.is_available():
@@ -237,9 +238,9 @@ def _missing_peer_worker(rank: int, world: int, port: int, q, protocol: str = "o
         q.put((rank, "error", traceback.format_exc()))
 
 
-@pytest.mark.parametrize("protocol", ["oneshot", "twoshot"])
+@pytest.mark.parametrize("protocol", ["oneshot", "twoshot", "ll"])
 def test_oneshot_allreduce_missing_peer_fails_loudly(protocol):
-    """One-shot: rank 1's late call still completes (rank 0 pushed before timing out),
+    """One-shot and LL: rank 1's late call still completes (rank 0 pushed before timing out),
     its next one times out. Two-shot: rank 0 never reaches the all-gather phase, so rank
     1's late call already times out. Either way: NaN, never a partial sum, and sticky."""
     import torch.multiprocessing as mp
@@ -268,7 +269,7 @@ def test_oneshot_allreduce_missing_peer_fails_loudly(protocol):
     assert r0["failed"] and r0["raised"] and r0["all_nan"], r0
     assert 0.15 < r0["wait_s"] < 5.0, r0
     assert r0["sticky_nan"] and r0["sticky_s"] < 0.1, r0
-    if protocol == "oneshot":
+    if protocol in ("oneshot", "ll"):
         assert r1["late_ok"] and r1["failed"] and r1["all_nan"], r1
     else:   # rank 0 never published its gather piece: the late call already fails
         assert not r1["late_ok"] and r1["late_nan"] and r1["failed"] and r1["all_nan"], r1
@@ -340,5 +341,5 @@ def test_allreduce_calibration_two_ranks_one_gpu():
     (_, _, rep0, t0, _, ok0), (_, _, rep1, t1, _, ok1) = res
     assert t0 == t1 and rep0["table"] == rep1["table"]   # one table for the whole group
     assert rep0["sizes"] == [rows * 1024 * 2 for rows in (1, 2, 4, 8, 16, 32, 64, 128, 256)]
-    assert set(rep0["us"]) == {"oneshot", "twoshot", "backend"} and ok0 == ok1 == 3
+    assert set(rep0["us"]) == {"ll", "oneshot", "twoshot", "backend"} and ok0 == ok1 == 3
     assert rep0["table"][-1][0] == rep0["sizes"][-1]
