@@ -28,8 +28,9 @@ namespace oamd {
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 
 constexpr int kBK = 64;     // K per stage: one 128-B line per row
-constexpr int kStages = 3;  // default LDS ring depth (2: two blocks per CU for the smaller tiles; 4: three
-                            // stages in flight for tiles with BM + BN <= 320 rows, 160 KB of LDS at most)
+constexpr int kStages = 3;  // default LDS ring depth (2: two blocks per CU for the smaller tiles; 4 / 5 / 6:
+                            // three / four / five stages in flight for tiles with BM + BN <= 320 / 256 /
+                            // 192 rows, 160 KB of LDS at most)
 
 // 8 waves (2 per SIMD: one wave's LDS-read latency hides under the other's
 // MFMAs) laid out 4 (M) x 2 (N).
@@ -155,12 +156,16 @@ __global__ void __launch_bounds__(kWaves * 64, NS == 2 ? 2 : 1) gemm_tn_kernel(c
   // prologue: stages 0 .. NS-2 in flight; iteration t issues stage t + NS - 1
   // into the buffer compute(t - 1) just released (fenced by the barrier)
   issue(0, 0);
-  if (NS >= 3 && T > 1) issue(1, 1);
-  if (NS >= 4 && T > 2) issue(2, 2);
+#pragma unroll
+  for (int st = 1; st < NS - 1; ++st)
+    if (T > st) issue(st, st);
   for (int t = 0; t < T; ++t) {
     // stages issued so far: min(T, t + NS - 1); leave all but stage t in flight
-    if (NS >= 4 && t + 2 < T) wait_vmcnt<2 * C::GL>();
-    else if (NS >= 3 && t + 1 < T) wait_vmcnt<C::GL>();
+    const int rem = min(T - 1 - t, NS - 2);   // stages younger than t in flight
+    if (NS >= 6 && rem >= 4) wait_vmcnt<4 * C::GL>();
+    else if (NS >= 5 && rem >= 3) wait_vmcnt<3 * C::GL>();
+    else if (NS >= 4 && rem >= 2) wait_vmcnt<2 * C::GL>();
+    else if (NS >= 3 && rem >= 1) wait_vmcnt<C::GL>();
     else wait_vmcnt<0>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -276,6 +281,10 @@ int gemm_decode(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, in
     OAMD_GEMM3(BM, BNN, 2);                                    \
   } else if (stages == 4 && BM + BNN <= 320) {                 \
     OAMD_GEMM3(BM, BNN, (BM + BNN <= 320 ? 4 : 3));            \
+  } else if (stages == 5 && BM + BNN <= 256) {                 \
+    OAMD_GEMM3(BM, BNN, (BM + BNN <= 256 ? 5 : 3));            \
+  } else if (stages == 6 && BM + BNN <= 192) {                 \
+    OAMD_GEMM3(BM, BNN, (BM + BNN <= 192 ? 6 : 3));            \
   } else {                                                     \
     OAMD_GEMM3(BM, BNN, 3);                                    \
   }
