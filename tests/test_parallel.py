@@ -239,6 +239,25 @@ def test_allreduce_dispatch_table_selection():
     assert choose_protocols(sizes, t3) == [(4 << 20, PROTO_TWOSHOT)]
     assert choose_protocols(sizes[:2], {}) == [(16384, PROTO_BACKEND)]
     assert choose_protocols([], times) == []
+    # the LL protocol competes where it was timed (NaN past its half-capacity limit)
+    from operator_amd.parallel.custom_ar import PROTO_LL
+
+    t4 = dict(times)
+    t4[PROTO_LL] = [3e-6, 3.5e-6, 6e-6, float("nan"), float("nan"), float("nan")]
+    assert choose_protocols(sizes, t4) == [(65536, PROTO_LL), (1 << 20, PROTO_TWOSHOT), (4 << 20, PROTO_BACKEND)]
+
+
+def test_allreduce_route_keeps_ll_within_capacity():
+    """route(): a forced or tabled LL protocol falls back to one-shot for messages whose
+    LL packets (twice the bytes) would not fit the receive slots."""
+    from operator_amd.parallel.custom_ar import PROTO_LL, PROTO_ONESHOT, OneShotAllReduce
+
+    car = OneShotAllReduce.__new__(OneShotAllReduce)
+    car.max_bytes, car.oneshot_max_bytes, car.forced, car.table = 8 << 20, 512 << 10, PROTO_LL, None
+    assert car.route(4 << 20) == PROTO_LL
+    assert car.route((4 << 20) + 16) == PROTO_ONESHOT
+    car.forced, car.table = None, [(8 << 20, PROTO_LL)]
+    assert car.route(1 << 20) == PROTO_LL and car.route(6 << 20) == PROTO_ONESHOT
 
 
 def test_decode_message_sizes_follow_buckets():
