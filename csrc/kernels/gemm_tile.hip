@@ -950,7 +950,7 @@ int gemm_tile(const bf16_t* X, const bf16_t* W, bf16_t* Y, const bf16_t* bias, i
     // equal; 16 / 32 slower: profiles/gemm_tile_p5_vs_hipblaslt_r6.jsonl)
     if (N >= 16384) launch_p5<2>(X, W, Y, bias, M, N, K, ldy, silu_gu, grid, stream, 4);   // GROUP_M 4: -1.1 / -1.4 % at M = 12k / 32k
     else launch_p5<0>(X, W, Y, bias, M, N, K, ldy, silu_gu, grid, stream, 4);
-  } else if (variant >= 6 && variant <= 12 && K >= 2 * kBK && st16) {   // p5 A/B arms (timing, same numerics)
+  } else if (variant >= 6 && variant <= 14 && K >= 2 * kBK && st16) {   // p5 A/B arms (timing, same numerics)
     const int grid = min(nwg, device_cus());
     if (variant == 6) launch_p5<0>(X, W, Y, bias, M, N, K, ldy, silu_gu, grid, stream, 4);         // GROUP_M 4
     else if (variant == 7) launch_p5<0>(X, W, Y, bias, M, N, K, ldy, silu_gu, grid, stream, 16);   // GROUP_M 16
@@ -958,6 +958,8 @@ int gemm_tile(const bf16_t* X, const bf16_t* W, bf16_t* Y, const bf16_t* bias, i
     else if (variant == 10) launch_p5<2>(X, W, Y, bias, M, N, K, ldy, silu_gu, grid, stream, 4);   // W third, GROUP_M 4
     else if (variant == 11) launch_p5<2>(X, W, Y, bias, M, N, K, ldy, silu_gu, grid, stream, 16);  // W third, GROUP_M 16
     else if (variant == 12) launch_p5<2>(X, W, Y, bias, M, N, K, ldy, silu_gu, grid, stream, 2);   // W third, GROUP_M 2
+    else if (variant == 13) launch_p5<1>(X, W, Y, bias, M, N, K, ldy, silu_gu, grid, stream, 4);   // X third, GROUP_M 4
+    else if (variant == 14) launch_p5<0>(X, W, Y, bias, M, N, K, ldy, silu_gu, grid, stream, 2);   // GROUP_M 2
     else launch_p5<0>(X, W, Y, bias, M, N, K, ldy, silu_gu, grid, stream, 32);                      // GROUP_M 32
   } else if ((variant == 0 || variant == 1) && off32) {   // 4-wave, two 64 KiB buffers, four phases per K-tile
     if (silu_gu) gemm_tile256_h4_kernel<kEpiSilu><<<nwg, 256, 0, stream>>>(X, W, Y, bias, M, N, K, ldy);

@@ -122,7 +122,7 @@ def test_gemm_tile_persistent_rounds(M, N, K, epi):
     w = _rand(N, K, scale=0.05)
     b = _rand(N, scale=0.5) if epi == "bias" else None
     r = x.float() @ w.float().t() + (b.float() if b is not None else 0.0)
-    for v in ((5, 6, 7, 8, 9, 10, 11, 12) if b is None else (5,)):   # 6-12: p5 schedule arms (store epilogue)
+    for v in ((5, 6, 7, 8, 9, 10, 11, 12, 13, 14) if b is None else (5,)):   # 6-14: p5 schedule arms (store epilogue)
         y = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
         ops.kernels().gemm_tile(x, w, y, b, False, v)
         _close(y, r)
