@@ -233,7 +233,7 @@ void gemm_decode(const at::Tensor& x, const at::Tensor& w, const c10::optional<a
   if (bm == 0) bm = std::min<int64_t>(M, 256);
   TORCH_CHECK((bm == 64 || bm == 128 || bm == 256) && M % bm == 0, "gemm_decode: M % bm, bm in {64,128,256}");
   TORCH_CHECK((bn == 64 || bn == 128) && N % bn == 0, "gemm_decode: N % bn, bn in {64, 128}");
-  TORCH_CHECK(splits >= 1 && 8 % splits == 0 && K % (64 * splits) == 0, "gemm_decode: bad split count");
+  TORCH_CHECK(splits >= 1 && splits <= 16 && K % 64 == 0 && K / 64 >= splits, "gemm_decode: bad split count");
   float* pp = nullptr;
   if (splits > 1) {
     TORCH_CHECK(p.has_value(), "split-K needs a partial buffer");
@@ -291,7 +291,8 @@ void gemm_tile(const at::Tensor& x, const at::Tensor& w, const c10::optional<at:
 }
 
 void gemm_pp(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& y_opt,
-             const c10::optional<at::Tensor>& p, int64_t splits, int64_t bm, bool silu_gu, bool nt, bool one_seg) {
+             const c10::optional<at::Tensor>& p, int64_t splits, int64_t bm, bool silu_gu, bool nt, bool one_seg,
+             const c10::optional<at::Tensor>& sk_ws, const c10::optional<at::Tensor>& sk_flags) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && w.size(1) == x.size(1), "x [M,K], w [N,K]");
   const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
@@ -316,8 +317,18 @@ void gemm_pp(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::T
   }
   TORCH_CHECK(M * K < (1LL << 40) && N * K < (1LL << 40), "gemm too large");
   const c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  float* wsp = nullptr;
+  int* flp = nullptr;
+  if (sk_ws.has_value() || sk_flags.has_value()) {   // stream-K workspace: fp32 partials + zeroed int flags
+    TORCH_CHECK(sk_ws.has_value() && sk_flags.has_value(), "gemm_pp: stream-K needs sk_ws and sk_flags");
+    CHECK_DEV(*sk_ws); CHECK_DEV(*sk_flags); CHECK_CONTIG(*sk_ws); CHECK_CONTIG(*sk_flags);
+    CHECK_DT(*sk_ws, at::kFloat); CHECK_DT(*sk_flags, at::kInt);
+    TORCH_CHECK(sk_ws->numel() >= (N / 128) * 32768 && sk_flags->numel() >= N / 128, "gemm_pp: stream-K workspace too small");
+    wsp = sk_ws->data_ptr<float>();
+    flp = sk_flags->data_ptr<int>();
+  }
   RC(oamd::gemm_pp(ptr<bf16_t>(x), ptr<bf16_t>(w), yp, pp, (int)M, (int)N, (int)K, (int)splits, (int)bm, silu_gu, nt,
-                   cur_stream(), one_seg));
+                   cur_stream(), one_seg, wsp, flp));
 }
 
 void gemm_skinny(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& y_opt,
@@ -641,7 +652,9 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("splits") = 1, pybind11::arg("partial") = pybind11::none());
   m.def("gemm_pp", &gemm_pp, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"),
         pybind11::arg("p") = pybind11::none(), pybind11::arg("splits") = 1, pybind11::arg("bm") = 256,
-        pybind11::arg("silu_gu") = false, pybind11::arg("nt") = true, pybind11::arg("one_seg") = false);
+        pybind11::arg("silu_gu") = false, pybind11::arg("nt") = true, pybind11::arg("one_seg") = false,
+        pybind11::arg("sk_ws") = pybind11::none(), pybind11::arg("sk_flags") = pybind11::none());
+  m.def("gemm_pp_sk_grid", &oamd::gemm_pp_sk_grid, pybind11::arg("tiles"), pybind11::arg("steps"));
   m.def("gemm_skinny", &gemm_skinny, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"),
         pybind11::arg("p") = pybind11::none(), pybind11::arg("splits") = 1, pybind11::arg("silu_gu") = false);
   m.def("attn_prefill", &attn_prefill, pybind11::arg("q"), pybind11::arg("k"), pybind11::arg("v"),

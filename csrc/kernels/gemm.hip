@@ -18,7 +18,8 @@
 //     column tiles alone cannot fill 256 CUs. Split-K partials are fp32 slabs
 //     [S][M][N] summed by gemm_splitk_reduce (or by a consumer kernel). With
 //     S | 8 the blocks of one K-slice share an XCD (block id % 8), so each
-//     XCD's L2 holds only its slice of X.
+//     XCD's L2 holds only its slice of X; other S (<= 16) cut K into slices
+//     that differ by at most one 64-column step.
 // MFMA v_mfma_f32_16x16x32_bf16; fragment maps as in attn_decode.hip.
 #include "common.h"
 #include "kernels.h"
@@ -78,9 +79,12 @@ __global__ void __launch_bounds__(kWaves * 64, NS == 2 ? 2 : 1) gemm_tn_kernel(c
   const int n0 = nt * BN;
   const int m0 = blockIdx.y * BM;  // row tile (M may be split into BM-row tiles)
   X += (int64_t)m0 * K;
-  const int Kc = K / S;
-  const int kbase = kz * Kc;
-  const int T = Kc / kBK;
+  // K-slice kz = K-steps [kz * TK / S, (kz + 1) * TK / S): slices differ by at most one step
+  // when S does not divide TK (S = 5 puts 240 workgroups of the 48-tile qkv on 256 CUs)
+  const int TK = K / kBK;
+  const int t0 = kz * TK / S;
+  const int kbase = t0 * kBK;
+  const int T = (kz + 1) * TK / S - t0;
 
   // ---- LDS-DMA issue of one stage: instruction q covers rows 8q..8q+7 of the
   // stage (A rows [0, BM), then B rows [BM, BM + BN)); lane l -> row 8q + l/8,
@@ -269,7 +273,7 @@ int gemm_decode(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, in
     return 0;
   }
   if ((BN != 64 && BN != 128) || N % BN != 0) return -2;
-  if (S < 1 || 8 % S != 0 || K % (kBK * S) != 0) return -3;
+  if (S < 1 || S > 16 || K % kBK != 0 || K / kBK < S) return -3;
   if (S > 1 && P == nullptr) return -4;
   const dim3 grid((N / BN) * S, M / BM);
 #define OAMD_GEMM3(BM, BNN, NSS)                                                                               \

@@ -23,6 +23,17 @@
 //     (rmsnorm / rope_kv) or gemm_splitk_reduce.
 // LDS image: lane-linear LDS-DMA rows of 128 B with the chunk ^ ((row >> 1) & 7)
 // swizzle applied on the source and the read (conflict-free ds_read_b128).
+//
+// SK (stream-K, 256-row tiles, one K slice): the 224 column tiles of the 8B gate|up
+// projection leave 32 of 256 CUs idle, and at M = 256 the kernel is bound per CU (MFMA
+// issue and LDS-DMA ingest, profiles/decode_gemm_xr_vs_table_m256_r6.jsonl ablations), so
+// grid = one block per CU, and block b runs K-steps [b F / G, (b + 1) F / G) of the
+// flattened (tile, k) stream -- 7/8 of a tile each -- with ONE continuous LDS-DMA stream
+// across its tile boundary. A tile cut in two: the block holding its END (which runs it
+// first) stores the fp32 partial in a lane-linear workspace slot; the block holding its
+// START (which runs it last) adds that partial and runs the epilogue. The partial's flag is
+// raised only after the block's last K-step (so no block waits on a chain: every block
+// raises before it waits), and the waiting block polls with a bounded spin.
 #include "common.h"
 #include "kernels.h"
 
@@ -57,22 +68,30 @@ __device__ __forceinline__ uint2 pack4(f32x4 v) { return make_uint2(pack_bf2(v[0
 // ONE (XH == 2): the K-tile in ONE barrier segment per wave group (both X halves' 32
 // MFMAs behind one pair of barriers, all three regions of tile t+2 issued together) —
 // the XH == 1 schedule with a second X fragment set, half the barriers of two phases.
-template <int XH, int EPI, bool NT, bool ONE = false>
+template <int XH, int EPI, bool NT, bool ONE = false, bool SK = false>
 __global__ void __launch_bounds__(512) gemm_pp_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
                                                       bf16_t* __restrict__ Y, float* __restrict__ P, int M, int N,
-                                                      int K) {
+                                                      int K, float* __restrict__ ws, int* __restrict__ flags) {
   constexpr int NR = XH + 1;               // regions per K-tile
   constexpr int BUF = NR * kRegion;
   constexpr int GL = 2;                    // DMA instructions per wave per region
+  static_assert(!SK || (XH == 2 && !ONE), "stream-K runs the two-phase 256-row schedule");
   __shared__ __attribute__((aligned(1024))) char lds[kNBuf * BUF];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = w >> 2, wc = w & 3;
-  const int n0 = blockIdx.x * 128;
-  const int m0 = blockIdx.z * (128 * XH);
-  const int S = gridDim.y, kz = blockIdx.y;
+  const int m0 = SK ? 0 : blockIdx.z * (128 * XH);
+  const int S = SK ? 1 : gridDim.y, kz = SK ? 0 : blockIdx.y;
   const int Kc = K / S;
-  const int T = Kc / kBK;
+  const int TT = Kc / kBK;                 // K-steps per tile
+  // this block's K-steps: [F0, F0 + T) of the flattened (tile, k) stream (SK), else its tile's T
+  int F0 = 0, T = TT;
+  if constexpr (SK) {
+    const int64_t Ft = (int64_t)(N / 128) * TT;
+    F0 = (int)((int64_t)blockIdx.x * Ft / gridDim.x);
+    T = (int)((int64_t)(blockIdx.x + 1) * Ft / gridDim.x) - F0;
+  }
+  const int n0 = SK ? 0 : blockIdx.x * 128;   // SK: per K-step (tile * 128 rows of W)
 
   // region r: 0 = X rows 0-127, 1 = W rows 0-127, 2 = X rows 128-255 (XH == 2)
   const int lrow = lane >> 3, lslot = lane & 7;
@@ -90,15 +109,25 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const bf16_t* __restrict__
       if (r == 1) src[r][i] = W + (int64_t)(n0 + row) * K + koff;
       else src[r][i] = X + (int64_t)min(m0 + (r == 2 ? 128 : 0) + row, M - 1) * K + koff;
     }
+  // element offset of local K-step j in region r's source (SK: tile-major flattened stream)
+  auto step_off = [&](int r, int j) -> int64_t {
+    if constexpr (SK) {
+      const int F = F0 + j, tile = F / TT;
+      return (int64_t)(F - tile * TT) * kBK + (r == 1 ? (int64_t)tile * 128 * K : 0);
+    } else {
+      return (int64_t)j * kBK;
+    }
+  };
   auto issue = [&](int r, int buf, int kt) {
     char* dst = lds + buf * BUF + r * kRegion;
+    const int64_t off = step_off(r, kt);
 #pragma unroll
     for (int i = 0; i < GL; ++i) {
       if (NT && r == 1)
-        __builtin_amdgcn_global_load_lds(src[r][i] + kt * kBK,
+        __builtin_amdgcn_global_load_lds(src[r][i] + off,
                                          (__attribute__((address_space(3))) void*)(dst + (w + 8 * i) * 1024), 16, 0, 2);
       else
-        __builtin_amdgcn_global_load_lds(src[r][i] + kt * kBK,
+        __builtin_amdgcn_global_load_lds(src[r][i] + off,
                                          (__attribute__((address_space(3))) void*)(dst + (w + 8 * i) * 1024), 16, 0, 0);
     }
   };
@@ -170,6 +199,73 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const bf16_t* __restrict__
     __builtin_amdgcn_sched_barrier(0);
   };
 
+  // bf16 / SwiGLU / slab stores of the accumulators for the tile at column n0t
+  auto epilogue = [&](int n0t) {
+#pragma unroll
+    for (int h = 0; h < XH; ++h)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int tok = m0 + h * 128 + g * 64 + b * 16 + l15;
+        if (tok >= M) continue;
+        if constexpr (EPI == kSilu) {
+          const int col = (n0t >> 1) + wc * 16 + 4 * lq;
+          const f32x4 gt = acc[h][b][0], up = acc[h][b][1];
+          f32x4 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float gg = bf2f(f2bf(gt[r]));
+            const float uu = bf2f(f2bf(up[r]));
+            o[r] = bf2f(f2bf(gg / (1.f + __expf(-gg)))) * uu;
+          }
+          *reinterpret_cast<uint2*>(Y + (int64_t)tok * (N >> 1) + col) = pack4(o);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int col = n0t + e * 64 + wc * 16 + 4 * lq;
+            if constexpr (EPI == kPartial)
+              *reinterpret_cast<f32x4*>(P + ((int64_t)kz * M + tok) * N + col) = acc[h][b][e];
+            else
+              *reinterpret_cast<uint2*>(Y + (int64_t)tok * N + col) = pack4(acc[h][b][e]);
+          }
+        }
+      }
+  };
+  // SK partial of a cut tile: slot (h, b, e) of thread tid, lane-linear (both blocks of the
+  // tile map threads to accumulators identically)
+  auto ws_at = [&](int tile, int h, int b, int e) {
+    return reinterpret_cast<f32x4*>(ws) + ((int64_t)tile * (XH * 8) + (h * 4 + b) * 2 + e) * 512 + tid;
+  };
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int h = 0; h < XH; ++h)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[h][b][0] = acc[h][b][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  int tail_tile = -1, head_tile = -1;   // SK: the cut tiles this block ends / starts
+  // SK, after local K-step t (every wave has run its MFMAs of it; no barrier in here)
+  auto seg_end = [&](int t) {
+    if constexpr (SK) {
+      const int F = F0 + t, tile = F / TT;
+      if (F + 1 != (tile + 1) * TT && t != T - 1) return;   // the tile goes on in this block
+      const bool has_start = tile * TT >= F0, has_end = (tile + 1) * TT <= F0 + T;
+      if (has_start && has_end) {
+        epilogue(tile * 128);
+        zero_acc();
+      } else if (has_end) {   // the tile's end: its partial, for the block holding its start
+#pragma unroll
+        for (int h = 0; h < XH; ++h)
+#pragma unroll
+          for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int e = 0; e < 2; ++e) *ws_at(tile, h, b, e) = acc[h][b][e];
+        zero_acc();
+        tail_tile = tile;
+      } else {
+        head_tile = tile;   // the block's last K-step: finished after the stream
+      }
+    }
+  };
+
   // prologue: K-tiles 0 and 1 in flight; tile 0's first phase regions (X0, W) retired
 #pragma unroll
   for (int r = 0; r < NR; ++r) issue(r, 0, 0);
@@ -213,6 +309,7 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const bf16_t* __restrict__
       mfma_q(acc[1]);
       if (g == 0) { if (m2) vmw<GL * 4>(); else if (m1) vmw<GL * 1>(); }
       seg();
+      seg_end(t);
     } else {
       // one phase (X0, W): issue both regions of tile t+2; retire tile t+1 first.
       // Buffer (t+2) % 3 held tile t-1, whose LAST reader is the partner group one
@@ -239,38 +336,75 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const bf16_t* __restrict__
   }
   if (g == 0) seg();
 
-#pragma unroll
-  for (int h = 0; h < XH; ++h)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int tok = m0 + h * 128 + g * 64 + b * 16 + l15;
-      if (tok >= M) continue;
-      if constexpr (EPI == kSilu) {
-        const int col = (n0 >> 1) + wc * 16 + 4 * lq;
-        const f32x4 gt = acc[h][b][0], up = acc[h][b][1];
-        f32x4 o;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float gg = bf2f(f2bf(gt[r]));
-          const float uu = bf2f(f2bf(up[r]));
-          o[r] = bf2f(f2bf(gg / (1.f + __expf(-gg)))) * uu;
-        }
-        *reinterpret_cast<uint2*>(Y + (int64_t)tok * (N >> 1) + col) = pack4(o);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const int col = n0 + e * 64 + wc * 16 + 4 * lq;
-          if constexpr (EPI == kPartial)
-            *reinterpret_cast<f32x4*>(P + ((int64_t)kz * M + tok) * N + col) = acc[h][b][e];
-          else
-            *reinterpret_cast<uint2*>(Y + (int64_t)tok * N + col) = pack4(acc[h][b][e]);
-        }
-      }
+  if constexpr (SK) {
+    // raise the flag of the partial stored at the tile end (every thread's stores written back
+    // to agent scope first), THEN wait for the partial of the tile this block started
+    // (one wave fences for the block: every wave's stores have landed in the XCD's L2 at its
+    // vmcnt(0), and an agent-scope fence writes back / invalidates the whole L2 -- an acquire in
+    // the poll loop itself would invalidate it per poll under the blocks still streaming)
+    if (tail_tile >= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tail_tile >= 0 && tid == 0) {
+      __threadfence();
+      __hip_atomic_store(flags + tail_tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (head_tile >= 0) {
+      if (tid == 0) {
+        // bounded: the block holding the tile's end raises the flag right after its last
+        // K-step, before it waits for anything
+        int n = 0;
+        while (__hip_atomic_load(flags + head_tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 && ++n < (1 << 22))
+          __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      }
+      __syncthreads();
+      f32x4 pt[XH][4][2];
+#pragma unroll
+      for (int h = 0; h < XH; ++h)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+          for (int e = 0; e < 2; ++e) pt[h][b][e] = *ws_at(head_tile, h, b, e);
+#pragma unroll
+      for (int h = 0; h < XH; ++h)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+          for (int e = 0; e < 2; ++e) acc[h][b][e] += pt[h][b][e];
+      epilogue(head_tile * 128);
+      if (tid == 0) __hip_atomic_store(flags + head_tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  } else {
+    epilogue(n0);
+  }
+}
+
+static int pp_device_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  }
+  return n;
+}
+
+// Stream-K grid for `tiles` column tiles of `steps` K-steps: one block per CU when that is
+// more blocks than tiles, every block at least 2 K-steps, and no block strictly inside one
+// tile (a tile is cut at most once, so it has at most one partial); else 0 (plain launch)
+int gemm_pp_sk_grid(int tiles, int steps) {
+  const int64_t Ft = (int64_t)tiles * steps;
+  const int G = pp_device_cus();
+  if (G <= tiles || Ft < 2LL * G) return 0;
+  for (int b = 0; b < G; ++b) {
+    const int64_t f0 = (int64_t)b * Ft / G, f1 = (int64_t)(b + 1) * Ft / G;
+    if (f0 % steps != 0 && f1 < (f0 / steps + 1) * steps) return 0;
+  }
+  return G;
 }
 
 int gemm_pp(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, int N, int K, int S, int bm, bool silu_gu,
-            bool nt, hipStream_t stream, bool one_seg) {
+            bool nt, hipStream_t stream, bool one_seg, float* ws, int* flags) {
   if (M < 1 || N % 128 != 0 || S < 1 || S > 32 || K % (kBK * S) != 0) return -1;
   if (bm != 128 && bm != 256) return -2;
   if (silu_gu && S != 1) return -3;
@@ -278,12 +412,24 @@ int gemm_pp(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, int N,
   if (S == 1 && Y == nullptr) return -5;
   const dim3 grid(N / 128, S, (M + bm - 1) / bm);
   const int epi = silu_gu ? kSilu : (S > 1 ? kPartial : kStore);
-#define OAMD_PP(XH, E, NTB) gemm_pp_kernel<XH, E, NTB><<<grid, 512, 0, stream>>>(X, W, Y, P, M, N, K)
+  // stream-K: 256-row tile (M <= 256), one K slice, workspace ((N / 128) x 128 KiB fp32) and
+  // zeroed flags (N / 128 ints; the kernel leaves them zero) given
+  const int skg = (ws != nullptr && flags != nullptr && bm == 256 && M <= 256 && S == 1 && !one_seg && nt)
+                      ? gemm_pp_sk_grid(N / 128, K / kBK) : 0;
+  if (skg > 0) {
+    if (epi == kSilu)
+      gemm_pp_kernel<2, kSilu, true, false, true><<<skg, 512, 0, stream>>>(X, W, Y, P, M, N, K, ws, flags);
+    else
+      gemm_pp_kernel<2, kStore, true, false, true><<<skg, 512, 0, stream>>>(X, W, Y, P, M, N, K, ws, flags);
+    OAMD_LAUNCH_CHECK();
+    return 0;
+  }
+#define OAMD_PP(XH, E, NTB) gemm_pp_kernel<XH, E, NTB><<<grid, 512, 0, stream>>>(X, W, Y, P, M, N, K, nullptr, nullptr)
 #define OAMD_PP_E(XH, NTB)                  \
   if (epi == kSilu) OAMD_PP(XH, kSilu, NTB); \
   else if (epi == kPartial) OAMD_PP(XH, kPartial, NTB); \
   else OAMD_PP(XH, kStore, NTB)
-#define OAMD_PP1(E) gemm_pp_kernel<2, E, true, true><<<grid, 512, 0, stream>>>(X, W, Y, P, M, N, K)
+#define OAMD_PP1(E) gemm_pp_kernel<2, E, true, true><<<grid, 512, 0, stream>>>(X, W, Y, P, M, N, K, nullptr, nullptr)
   if (bm == 256 && one_seg) {   // one barrier segment per K-tile (nt weights)
     if (epi == kSilu) OAMD_PP1(kSilu);
     else if (epi == kPartial) OAMD_PP1(kPartial);

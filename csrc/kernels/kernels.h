@@ -43,8 +43,11 @@ int gemm_tile(const bf16_t* X, const bf16_t* W, bf16_t* Y, const bf16_t* bias, i
 // Decode-bucket GEMM on the ping-pong schedule (gemm_pp.hip): Y[M,N] = X[M,K] W[N,K]^T, bm-row tiles
 // (128 / 256), 128-column tiles (N % 128 == 0), S-way split-K slabs P (S > 1; reduced into Y unless Y is
 // nullptr); silu_gu: fused SwiGLU (S == 1), Y [M, N/2]; nt: non-temporal weight loads.
+// ws / flags (both given): the stream-K form for bm 256, S 1, nt (gemm_pp.hip SK): ws >= (N / 128) x 32768
+// floats, flags >= N / 128 ints, zero (left zero). gemm_pp_sk_grid: its block count, 0 = plain launch.
 int gemm_pp(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* P, int M, int N, int K, int S, int bm, bool silu_gu,
-            bool nt, hipStream_t stream, bool one_seg = false);
+            bool nt, hipStream_t stream, bool one_seg = false, float* ws = nullptr, int* flags = nullptr);
+int gemm_pp_sk_grid(int tiles, int steps);
 // 256-row decode GEMM with register-streamed activations (gemm_xr.hip): Xt = X [256, K] in the tiled
 // layout [16][K/32][64][8]; N % 128 == 0, K % (64 S) == 0; epi 0 = fp32 slabs P[S][256][N], 1 = bf16 Y,
 // 2 = SwiGLU (interleaved gate|up, S == 1) Y [256, N/2], 3 = the same written tiled.

@@ -208,6 +208,7 @@ int rope_kv(const bf16_t* qkv, int64_t qkv_stride, const int64_t* pos, const flo
     case 1: OAMD_ROPE(KVT, 1, KI, VI); break;      \
     case 2: OAMD_ROPE(KVT, 2, KI, VI); break;      \
     case 4: OAMD_ROPE(KVT, 4, KI, VI); break;      \
+    case 5: OAMD_ROPE(KVT, 5, KI, VI); break;      \
     case 8: OAMD_ROPE(KVT, 8, KI, VI); break;      \
     default: OAMD_ROPE(KVT, 0, KI, VI); break;     \
   }

@@ -108,7 +108,9 @@ def gate_up_silu(x: torch.Tensor, wgu: torch.Tensor, block: int | None) -> torch
         t = _gemm_table_get().get(("silu", M, N, K))
         if isinstance(t, str) and t.startswith("pp"):   # ping-pong kernel, nt weight loads (bm 128 / 256)
             y = torch.empty(M, N // 2, dtype=x.dtype, device=x.device)
-            kernels().gemm_pp(x, wgu, y, None, 1, int(t[2:]), True, True)
+            bm = int(t[2:])
+            ws, fl = _pp_sk_workspace(x.device, N // 128) if (bm == 256 and PP_STREAM_K) else (None, None)
+            kernels().gemm_pp(x, wgu, y, None, 1, bm, True, True, False, ws, fl)
             return y
         if t != "blas":
             bm = t[0] if t else row_tile(M)
@@ -119,6 +121,26 @@ def gate_up_silu(x: torch.Tensor, wgu: torch.Tensor, block: int | None) -> torch
     if block == 64 and tile_ok(x, wgu) and N % 128 == 0:
         return linear_tile(x, wgu, silu_gu=True)   # prefill: SwiGLU fused into the tile epilogue
     return silu_mul(linear(x, wgu), block=block)
+
+
+# Stream-K form of the 256-row gate|up+SwiGLU decode GEMM (csrc/kernels/gemm_pp.hip SK): one block per
+# CU over the flattened (tile, K-step) stream instead of one block per 128-feature tile (224 of 256 CUs
+# busy at the 8B shape). OAMD_PP_STREAM_K=1 turns it on (A/B runs).
+PP_STREAM_K = os.environ.get("OAMD_PP_STREAM_K", "0") == "1"
+_PP_SK_WS: dict = {}
+
+
+def _pp_sk_workspace(device, tiles: int):
+    """(fp32 partials, zeroed int flags) for the stream-K gate|up kernel, one pair per (device,
+    tile count), kept for the life of the process: captured decode graphs hold the pointers, and the
+    kernel leaves the flags zero. A stream runs one such GEMM at a time (the engine's decode stream)."""
+    key = (str(device), tiles)
+    ws = _PP_SK_WS.get(key)
+    if ws is None:
+        ws = (torch.empty(tiles * 32768, dtype=torch.float32, device=device),
+              torch.zeros(tiles, dtype=torch.int32, device=device))
+        _PP_SK_WS[key] = ws
+    return ws
 
 
 def embedding(ids: torch.Tensor, table: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:

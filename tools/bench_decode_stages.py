@@ -37,8 +37,8 @@ def plans(N: int, K: int):
                 if ns * stage > LDS or (ns == 4 and bm + bn > 320) or (ns == 5 and bm + bn > 256) \
                         or (ns == 6 and bm + bn > 192):
                     continue
-                for S in (1, 2, 4, 8):
-                    if K % (64 * S):
+                for S in (1, 2, 3, 4, 5, 6, 8):
+                    if K // 64 < S:
                         continue
                     wgs = (N // bn) * S * (256 // bm)
                     if wgs < 128 or wgs > 1024:
