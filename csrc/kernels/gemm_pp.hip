@@ -24,16 +24,13 @@
 // LDS image: lane-linear LDS-DMA rows of 128 B with the chunk ^ ((row >> 1) & 7)
 // swizzle applied on the source and the read (conflict-free ds_read_b128).
 //
-// SK (stream-K, 256-row tiles, one K slice): the 224 column tiles of the 8B gate|up
-// projection leave 32 of 256 CUs idle, and at M = 256 the kernel is bound per CU (MFMA
-// issue and LDS-DMA ingest, profiles/decode_gemm_xr_vs_table_m256_r6.jsonl ablations), so
-// grid = one block per CU, and block b runs K-steps [b F / G, (b + 1) F / G) of the
-// flattened (tile, k) stream -- 7/8 of a tile each -- with ONE continuous LDS-DMA stream
-// across its tile boundary. A tile cut in two: the block holding its END (which runs it
-// first) stores the fp32 partial in a lane-linear workspace slot; the block holding its
-// START (which runs it last) adds that partial and runs the epilogue. The partial's flag is
-// raised only after the block's last K-step (so no block waits on a chain: every block
-// raises before it waits), and the waiting block polls with a bounded spin.
+// SK (stream-K, 256-row tiles, one K slice; an A/B arm, not the default): the 224 column
+// tiles of the 8B gate|up projection leave 32 of 256 CUs idle, so grid = one block per CU,
+// each running 7/8 of a tile's K-steps with ONE continuous LDS-DMA stream across its tile
+// boundary; a cut tile's first block stores an fp32 partial that its second block adds before
+// the epilogue. Measured SLOWER than the per-tile launch (profiles/gemm_pp_stream_k_r6.jsonl):
+// even with the hand-off removed, 256 blocks x 7/8 of a tile take 75 us against 73 for 224
+// blocks x 1 tile, so the M = 256 GEMM is not bound per CU; the hand-off adds 12 us more.
 #include "common.h"
 #include "kernels.h"
 
@@ -84,12 +81,26 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const bf16_t* __restrict__
   const int S = SK ? 1 : gridDim.y, kz = SK ? 0 : blockIdx.y;
   const int Kc = K / S;
   const int TT = Kc / kBK;                 // K-steps per tile
-  // this block's K-steps: [F0, F0 + T) of the flattened (tile, k) stream (SK), else its tile's T
-  int F0 = 0, T = TT;
+  // SK: logical block lb (XCD-grouped: the blocks one XCD runs -- block ids = x mod 8 -- hold
+  // consecutive ranges, so both blocks of a cut tile normally share an L2) owns the K-steps
+  // [F0, F0 + T) of the flattened (tile, k) stream. It runs them as segment A = the piece of
+  // the LAST tile it touches (from k = 0), then segment B = the piece of the first one (to the
+  // tile's end): at local step j every block reads K-step j or j + TT - T, so all blocks walk X
+  // in step and its panel stays in L2 (tile-major order scattered them over 8 phases, 85 vs
+  // 73 us with no hand-off at all).
+  int T = TT, tA = 0, kA = 0, nA = TT, tB = 0, kB = 0;
   if constexpr (SK) {
+    const int G = gridDim.x;
+    const int lb = (G % 8 == 0) ? (int)(blockIdx.x % 8) * (G / 8) + (int)blockIdx.x / 8 : (int)blockIdx.x;
     const int64_t Ft = (int64_t)(N / 128) * TT;
-    F0 = (int)((int64_t)blockIdx.x * Ft / gridDim.x);
-    T = (int)((int64_t)(blockIdx.x + 1) * Ft / gridDim.x) - F0;
+    const int F0 = (int)((int64_t)lb * Ft / G), F1 = (int)((int64_t)(lb + 1) * Ft / G);
+    T = F1 - F0;
+    const int tf = F0 / TT, tl = (F1 - 1) / TT;   // host: at most two tiles, never strictly inside one
+    if (tf == tl) {
+      tA = tf; kA = F0 - tf * TT; nA = T;
+    } else {
+      tA = tl; kA = 0; nA = F1 - tl * TT; tB = tf; kB = F0 - tf * TT;
+    }
   }
   const int n0 = SK ? 0 : blockIdx.x * 128;   // SK: per K-step (tile * 128 rows of W)
 
@@ -109,11 +120,12 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const bf16_t* __restrict__
       if (r == 1) src[r][i] = W + (int64_t)(n0 + row) * K + koff;
       else src[r][i] = X + (int64_t)min(m0 + (r == 2 ? 128 : 0) + row, M - 1) * K + koff;
     }
-  // element offset of local K-step j in region r's source (SK: tile-major flattened stream)
+  // element offset of local K-step j in region r's source (SK: segment A, then B)
   auto step_off = [&](int r, int j) -> int64_t {
     if constexpr (SK) {
-      const int F = F0 + j, tile = F / TT;
-      return (int64_t)(F - tile * TT) * kBK + (r == 1 ? (int64_t)tile * 128 * K : 0);
+      const bool a = j < nA;
+      const int tile = a ? tA : tB, k = a ? kA + j : kB + j - nA;
+      return (int64_t)k * kBK + (r == 1 ? (int64_t)tile * 128 * K : 0);
     } else {
       return (int64_t)j * kBK;
     }
@@ -241,17 +253,18 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const bf16_t* __restrict__
 #pragma unroll
       for (int b = 0; b < 4; ++b) acc[h][b][0] = acc[h][b][1] = f32x4{0.f, 0.f, 0.f, 0.f};
   };
-  int tail_tile = -1, head_tile = -1;   // SK: the cut tiles this block ends / starts
+  int part_tile = -1, fin_tile = -1;   // SK: the cut tile this block starts (partial) / ends (finishes)
   // SK, after local K-step t (every wave has run its MFMAs of it; no barrier in here)
   auto seg_end = [&](int t) {
     if constexpr (SK) {
-      const int F = F0 + t, tile = F / TT;
-      if (F + 1 != (tile + 1) * TT && t != T - 1) return;   // the tile goes on in this block
-      const bool has_start = tile * TT >= F0, has_end = (tile + 1) * TT <= F0 + T;
-      if (has_start && has_end) {
+      int tile, k0, n;
+      if (t == nA - 1) { tile = tA; k0 = kA; n = nA; }
+      else if (t == T - 1) { tile = tB; k0 = kB; n = T - nA; }
+      else return;
+      if (k0 == 0 && n == TT) {
         epilogue(tile * 128);
         zero_acc();
-      } else if (has_end) {   // the tile's end: its partial, for the block holding its start
+      } else if (k0 == 0) {   // the tile's start: its partial, for the block running its end (lb + 1)
 #pragma unroll
         for (int h = 0; h < XH; ++h)
 #pragma unroll
@@ -259,9 +272,9 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const bf16_t* __restrict__
 #pragma unroll
             for (int e = 0; e < 2; ++e) *ws_at(tile, h, b, e) = acc[h][b][e];
         zero_acc();
-        tail_tile = tile;
+        part_tile = tile;
       } else {
-        head_tile = tile;   // the block's last K-step: finished after the stream
+        fin_tile = tile;   // the tile's end = the block's last K-step: finished after the stream
       }
     }
   };
@@ -337,25 +350,26 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const bf16_t* __restrict__
   if (g == 0) seg();
 
   if constexpr (SK) {
-    // raise the flag of the partial stored at the tile end (every thread's stores written back
-    // to agent scope first), THEN wait for the partial of the tile this block started
-    // (one wave fences for the block: every wave's stores have landed in the XCD's L2 at its
-    // vmcnt(0), and an agent-scope fence writes back / invalidates the whole L2 -- an acquire in
-    // the poll loop itself would invalidate it per poll under the blocks still streaming)
-    if (tail_tile >= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // Hand-off: every wave's partial stores have reached L2 at its vmcnt(0); after the barrier one
+    // thread writes the XCD's L2 back (agent-scope fence: the reader may sit on another XCD) and
+    // raises the flag with the writer's XCC id. The reader invalidates its own L2 only when that
+    // id differs from its own (never, with the XCD-grouped order): an invalidate per block under
+    // the blocks still streaming cost them their X panel (profiles/gemm_pp_stream_k_r6.jsonl).
+    const int xcc = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (3 << 11)) & 15;   // HW_REG_XCC_ID
+    if (part_tile >= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tail_tile >= 0 && tid == 0) {
+    if (part_tile >= 0 && tid == 0) {
       __threadfence();
-      __hip_atomic_store(flags + tail_tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(flags + part_tile, 1 + xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (head_tile >= 0) {
+    if (fin_tile >= 0) {
       if (tid == 0) {
-        // bounded: the block holding the tile's end raises the flag right after its last
+        // bounded: the block holding the tile's start raises the flag right after its last
         // K-step, before it waits for anything
-        int n = 0;
-        while (__hip_atomic_load(flags + head_tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 && ++n < (1 << 22))
+        int n = 0, f = 0;
+        while ((f = __hip_atomic_load(flags + fin_tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0 && ++n < (1 << 22))
           __builtin_amdgcn_s_sleep(2);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (f != 1 + xcc) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       }
       __syncthreads();
       f32x4 pt[XH][4][2];
@@ -364,15 +378,15 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(const bf16_t* __restrict__
 #pragma unroll
         for (int b = 0; b < 4; ++b)
 #pragma unroll
-          for (int e = 0; e < 2; ++e) pt[h][b][e] = *ws_at(head_tile, h, b, e);
+          for (int e = 0; e < 2; ++e) pt[h][b][e] = __builtin_nontemporal_load(ws_at(fin_tile, h, b, e));
 #pragma unroll
       for (int h = 0; h < XH; ++h)
 #pragma unroll
         for (int b = 0; b < 4; ++b)
 #pragma unroll
           for (int e = 0; e < 2; ++e) acc[h][b][e] += pt[h][b][e];
-      epilogue(head_tile * 128);
-      if (tid == 0) __hip_atomic_store(flags + head_tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      epilogue(fin_tile * 128);
+      if (tid == 0) __hip_atomic_store(flags + fin_tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   } else {
     epilogue(n0);
@@ -398,7 +412,8 @@ int gemm_pp_sk_grid(int tiles, int steps) {
   if (G <= tiles || Ft < 2LL * G) return 0;
   for (int b = 0; b < G; ++b) {
     const int64_t f0 = (int64_t)b * Ft / G, f1 = (int64_t)(b + 1) * Ft / G;
-    if (f0 % steps != 0 && f1 < (f0 / steps + 1) * steps) return 0;
+    if (f0 % steps != 0 && f1 < (f0 / steps + 1) * steps) return 0;   // strictly inside a tile
+    if ((f1 - 1) / steps > f0 / steps + 1) return 0;                    // three tiles
   }
   return G;
 }
