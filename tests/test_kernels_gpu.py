@@ -405,9 +405,10 @@ def test_deferred_splitk_decode_matches_plain():
     torch.testing.assert_close(a.float(), b.float(), atol=3e-2, rtol=3e-2)
 
 
-def test_rope_kv_from_splitk_slabs():
+@pytest.mark.parametrize("S", [4, 5, 3])   # 4 / 5: compiled slab counts (5 = the 8B qkv plan), 3: runtime S
+def test_rope_kv_from_splitk_slabs(S):
     torch.manual_seed(12)
-    T, Hq, Hkv, D, S = 64, 8, 2, 128, 4
+    T, Hq, Hkv, D = 64, 8, 2, 128
     W = (Hq + 2 * Hkv) * D
     P = torch.randn(S * T * W, device=DEV, dtype=torch.float32)
     sk = ops.SplitK(P, S, T, W)
