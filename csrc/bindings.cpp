@@ -409,7 +409,7 @@ void gemm_fp8(const at::Tensor& x8, const at::Tensor& w8, const at::Tensor& sx, 
               "gemm_fp8 shapes");
   TORCH_CHECK((bn == 64 || bn == 128) && N % bn == 0, "gemm_fp8: N % bn");
   TORCH_CHECK(bm == 64 || bm == 128 || bm == 256, "gemm_fp8: bm in {64,128,256}");
-  TORCH_CHECK(splits >= 1 && 8 % splits == 0 && K % (128 * splits) == 0, "gemm_fp8: K % (128 * splits)");
+  TORCH_CHECK(splits >= 1 && splits <= 16 && K % 128 == 0 && K / 128 >= splits, "gemm_fp8: K % 128, 1 <= splits <= min(16, K / 128)");
   float* pp = nullptr;
   if (splits > 1) {
     TORCH_CHECK(p.has_value() && p->scalar_type() == at::kFloat && p->numel() >= splits * M * N,

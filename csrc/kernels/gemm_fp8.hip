@@ -64,7 +64,8 @@ __global__ void __launch_bounds__(f8::kWaves * 64, 1)
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int kz = blockIdx.x % S, nt = blockIdx.x / S;
   const int n0 = nt * BN, m0 = blockIdx.y * BM;
-  const int Kc = K / S, kbase = kz * Kc, T = Kc / f8::kBK;
+  // K-slice kz = K-steps [kz * TK / S, (kz + 1) * TK / S) (uneven when S does not divide TK)
+  const int TK = K / f8::kBK, t0 = kz * TK / S, kbase = t0 * f8::kBK, T = (kz + 1) * TK / S - t0;
 
   const int lrow = lane >> 3, lslot = lane & 7;
   auto issue = [&](int t, int buf) {
@@ -332,7 +333,7 @@ int gemm_fp8(const uint8_t* X, const uint8_t* W, const float* sx, const float* s
   if (M <= 0) return 0;
   if (BM != 64 && BM != 128 && BM != 256) return -1;
   if ((BN != 64 && BN != 128) || N % BN != 0) return -2;
-  if (S < 1 || 8 % S != 0 || K % (f8::kBK * S) != 0) return -3;
+  if (S < 1 || S > 16 || K % f8::kBK != 0 || K / f8::kBK < S) return -3;
   if (S > 1 && P == nullptr) return -4;
   const dim3 grid((N / BN) * S, (M + BM - 1) / BM);
   static const int wnt = [] { const char* e = getenv("OAMD_FP8_WNT"); return e && e[0] == '0' ? 0 : 1; }();
