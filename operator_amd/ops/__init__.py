@@ -28,6 +28,9 @@ DECODE_MIN_SPLIT_TOKENS = int(os.environ.get("OAMD_DECODE_MIN_SPLIT", "256"))
 # one workgroup per CU: the best split count at every measured (B, group, ctx) of
 # profiles/attn_decode_splits_sweep_r5.jsonl lands at B x Hkv x splits ~ 256
 DECODE_TARGET_BLOCKS = int(os.environ.get("OAMD_DECODE_TARGET_BLOCKS", "256"))
+# attn_decode schedule bits (csrc/kernels/attn_decode.hip): 2 = NT 2 (two 16-token tiles per wave),
+# 4 = one kv-head across all sequences first (else a sequence's kv-heads back to back)
+DECODE_ATTN_VARIANT = int(os.environ.get("OAMD_DECODE_ATTN_VARIANT", "0"))
 
 
 class SplitK:
@@ -576,7 +579,7 @@ def decode_workspace(B: int, Hq: int, num_splits: int, device, D: int = 128):
 
 def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
                 seq_lens: torch.Tensor, scale: float, num_splits: int, out: torch.Tensor | None = None,
-                workspace: tuple[torch.Tensor, torch.Tensor] | None = None, variant: int = 0,
+                workspace: tuple[torch.Tensor, torch.Tensor] | None = None, variant: int | None = None,
                 k_scale: float = 1.0, v_scale: float = 1.0, quant: bool = False):
     """Paged decode attention; ``num_splits`` workgroups per (sequence, kv-head)
     (``decode_splits``). Any value >= 1 is correct; it only changes the schedule.
@@ -590,6 +593,7 @@ def attn_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, b
             r = out
         return quantize_fp8(r.reshape(r.shape[0], -1)) if quant else r
     B, Hq, D = q.shape
+    variant = DECODE_ATTN_VARIANT if variant is None else variant
     o = out if out is not None else torch.empty_like(q)
     if workspace is None:
         workspace = decode_workspace(B, Hq, num_splits, q.device)
@@ -615,7 +619,7 @@ def attn_decode_rope(qkv, pos: torch.Tensor, cos: torch.Tensor, sin: torch.Tenso
                      v_cache: torch.Tensor, slots: torch.Tensor, block_tables: torch.Tensor, seq_lens: torch.Tensor,
                      scale: float, num_splits: int, workspace: tuple[torch.Tensor, torch.Tensor] | None = None,
                      bias: torch.Tensor | None = None, k_scale: float = 1.0, v_scale: float = 1.0,
-                     quant: bool = False, variant: int = 0):
+                     quant: bool = False, variant: int | None = None):
     """One decode step's ``rope_kv`` (want_kv=False) + ``attn_decode`` as ONE kernel: every
     attention workgroup rotates its q from the QKV projection (``qkv``: bf16 rows or the
     GEMM's :class:`SplitK` slabs, + the Qwen2 bias), and the workgroup holding each
@@ -630,6 +634,7 @@ def attn_decode_rope(qkv, pos: torch.Tensor, cos: torch.Tensor, sin: torch.Tenso
                            variant=variant, k_scale=k_scale, v_scale=v_scale, quant=quant)
     B = qkv.shape[0]
     D = cos.shape[1] * 2
+    variant = DECODE_ATTN_VARIANT if variant is None else variant
     o = torch.empty(B, Hq, D, dtype=torch.bfloat16, device=qkv.device)
     if workspace is None:
         workspace = decode_workspace(B, Hq, num_splits, qkv.device)
