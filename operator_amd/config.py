@@ -128,7 +128,7 @@ class EngineCfg(BaseModel):
     allreduce_calibrate_iters: int = 20
     max_batch: int = 256
     max_prefill_tokens: int = 32768   # tokens per prefill batch (profiles/prefill_batch_sweep_8b.jsonl)
-    admit_wait_ms: float = 20.0       # idle engine: gather arrivals this long before a partial prefill
+    admit_wait_ms: float = 5.0        # idle engine: gather arrivals this long before a partial prefill (5 vs 20: +0.9 %, profiles/admit_wait_ab_r6.jsonl)
     max_context: int = 4096
     max_prompt_tokens: int = 1536
     kv_cache_gb: float = 64.0
