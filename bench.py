@@ -244,7 +244,7 @@ def main() -> int:
             "engine.prefix_sharing": not a.no_prefix_sharing,
             "engine.seed": 0, "health.enabled": False, "operator.workers": 2 * a.batch + 16, "operator.io_workers": 16,
             "operator.sink_concurrency": a.sink_concurrency,
-            "patterns.cache_dir": f"/tmp/oamd-bench-{os.getpid()}", "services.match_max_batch": 64,
+            "patterns.cache_dir": f"/tmp/oamd-bench-{os.getpid()}", "services.match_max_batch": int(os.environ.get("OAMD_BENCH_MATCH_MAX_BATCH", "64")),
             "services.match_batch_wait_ms": float(os.environ.get("OAMD_BENCH_MATCH_WAIT_MS", "15"))})
 
     patset = synthetic_library(a.patterns, seed=0)
